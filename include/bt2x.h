@@ -1,0 +1,241 @@
+/*
+ * bt2x.h — C-ABI of the MI355X-native Bowtie 2 hot path (seed search + DP).
+ *
+ * This is the drop-in boundary for sfiligoi/omp-bowtie2-prime's two data-parallel
+ * hot loops.  Plain pointers and sizes only; no C++ or torch
+ * types cross it.  Every entry point cites the reference interface it replaces.
+ *
+ *   bt2x_index_load / bt2x_index_free   Ebwt::readIntoMemory (bt2_io.cpp:39-560): parse a
+ *                                       forward .1/.2.bt2l pair into host arrays.
+ *   bt2x_open / bt2x_close              one context per GPU; uploads the index arrays
+ *                                       (Ebwt::_ebwt/_ftab/_eftab/_fchr, bt2_idx.h:2617-2639).
+ *   bt2x_seed_search                    MultiSeedAligner::searchAllSeedsDoAll(doExtend)
+ *                                       (aligner_seed.cpp:674-725): exact backward search of
+ *                                       every seed (searchSeedBi<8>, :820-957) and the
+ *                                       left extension (MultiSeedAligner::extend, :603-672).
+ *   bt2x_dp_align                       SwAligner::align (aligner_sw.cpp:235 ->
+ *                                       alignEnd2EndSseU8, aligner_swsse_ee_u8.cpp:542) followed
+ *                                       by every SwAligner::nextAlignment call until done()
+ *                                       (aligner_sw.cpp:252-375, backtrace u8.cpp:746-1352).
+ *
+ * Conventions: return 0 on success, negative BT2X_E_* on error, never
+ * throw.  Host buffers are caller-owned, device buffers are context-owned.  Calls on one
+ * context are serialised.  The *_dev variants take device pointers (inputs already resident
+ * in HBM) and a hipStream_t passed as void*; they are asynchronous on that stream.
+ * The product path has no CPU fallback: without a usable GPU bt2x_open fails with
+ * BT2X_E_NODEVICE.
+ */
+#ifndef BT2X_H_
+#define BT2X_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BT2X_ABI_VERSION 1
+
+enum {
+	BT2X_OK = 0,
+	BT2X_E_ARG = -1,        /* bad argument / shape outside the reference's limits */
+	BT2X_E_IO = -2,         /* index file missing or malformed */
+	BT2X_E_NODEVICE = -3,   /* no HIP device / HIP call failed */
+	BT2X_E_OVERFLOW = -4,   /* result arena too small; required sizes reported */
+	BT2X_E_NOMEM = -5
+};
+
+/* Reference limits that are part of the observable behaviour. */
+#define BT2X_MAX_ROWS 160      /* ALN_MAX_ROWS, aligner_result.h:42 */
+#define BT2X_MAX_COLS 200      /* ALN_MAX_COLS, aligner_result.h:43 (rflen+1 <= 200) */
+#define BT2X_SIDE_BYTES 128    /* .bt2l side: 96 B of BWT + 4 x u64 occ (bt2_idx.h:134-165) */
+#define BT2X_SIDE_CHARS 384    /* 48 * OFF_SIZE (bt2_idx.h:377) */
+
+/* ------------------------------------------------------------------ index */
+
+/* In-memory forward index, the arrays Ebwt holds after loadIntoMemory(). */
+typedef struct {
+	uint64_t len;            /* _eh._len: length of the joined text              */
+	uint64_t zoff;           /* _zOff: BWT row whose L char is '$'                */
+	uint64_t fchr[5];        /* _fchr                                             */
+	int32_t  ftab_chars;     /* _eh._ftabChars (10)                               */
+	int32_t  off_rate;       /* _eh._offRate (4)                                  */
+	int32_t  line_rate;      /* _eh._lineRate (7 => 128-byte sides)               */
+	int32_t  flags;
+	const uint8_t*  ebwt;    uint64_t ebwt_bytes;  /* _ebwt, numSides * 128       */
+	const uint64_t* ftab;    uint64_t ftab_len;    /* _ftab, 4^ftabChars + 1      */
+	const uint64_t* eftab;   uint64_t eftab_len;   /* _eftab, 2 * ftabChars       */
+	const uint64_t* offs;    uint64_t offs_len;    /* _offs (SA sample, .2.bt2l)  */
+	const uint64_t* plen;    uint64_t npat;        /* _plen: reference lengths    */
+	const uint64_t* rstarts; uint64_t nfrag;       /* _rstarts: 3 words/fragment  */
+	void* owner;             /* loader-owned storage (bt2x_index_free) */
+} bt2x_index_desc;
+
+/* Parse <base>.1.bt2l (+ <base>.2.bt2l when load_offs) like Ebwt::readIntoMemory. */
+int  bt2x_index_load(const char* basename, int load_offs, bt2x_index_desc* out);
+void bt2x_index_free(bt2x_index_desc* idx);
+
+/* ---------------------------------------------------------------- scoring */
+
+/* Scoring scheme (scoring.h:28-132).  Defaults: bt2x_scoring_default(). */
+typedef struct {
+	int32_t mm_max, mm_min;          /* --mp MX,MN  (6,2), COST_MODEL_QUAL          */
+	int32_t n_pen;                   /* --np (1), COST_MODEL_CONSTANT               */
+	int32_t rdg_const, rdg_linear;   /* --rdg (5,3): open = const+linear, ext = lin  */
+	int32_t rfg_const, rfg_linear;   /* --rfg (5,3)                                  */
+	int32_t gapbar;                  /* --gbar (4)                                   */
+	int32_t mmpens[256];             /* filled by bt2x_scoring_init (initPens)       */
+	int32_t npens[256];
+} bt2x_scoring;
+
+void bt2x_scoring_default(bt2x_scoring* sc);
+/* Recompute the per-quality tables from the scalar fields (Scoring::initPens). */
+void bt2x_scoring_init(bt2x_scoring* sc);
+
+/* ---------------------------------------------------------------- context */
+
+typedef struct bt2x_ctx bt2x_ctx;
+
+int  bt2x_open(int hip_device, const bt2x_index_desc* idx, const bt2x_scoring* sc, bt2x_ctx** out);
+void bt2x_close(bt2x_ctx* ctx);
+/* Last kernel's duration in ms (HIP events on the launching stream), by kernel id. */
+enum { BT2X_K_SEED = 0, BT2X_K_DP = 1, BT2X_K_COUNT = 2 };
+double bt2x_last_kernel_ms(const bt2x_ctx* ctx, int kernel);
+/* Algorithmic bytes / counters of the last call, by kernel id. */
+typedef struct {
+	uint64_t n_bilf;      /* mapBiLFEx calls (2 sides each)   */
+	uint64_t n_lf1;       /* mapLF1 calls (1 side)            */
+	uint64_t n_ftab;      /* ftab lookups (16 B)              */
+	uint64_t dp_cells;    /* R*C summed over DP problems      */
+	uint64_t dp_cols;     /* C summed                         */
+	uint64_t bt_cells;    /* backtrace cells visited          */
+	uint64_t n_problems;
+	uint64_t alg_bytes;   /* algorithmic HBM bytes of the launch */
+} bt2x_counters;
+int bt2x_last_counters(const bt2x_ctx* ctx, int kernel, bt2x_counters* out);
+
+/* ------------------------------------------------------------ seed search */
+
+/* One exact seed (SeedAlignerSearchParams, aligner_seed.cpp:81-171).  The oriented read
+ * (patFw for fw seeds, patRc for rc seeds; codes 0-3, 4 = N) starts at reads[read_off].
+ * The seed is read[seed_off .. seed_off+seed_len); extension walks left over
+ * read[seed_off-1] .. read[0] (SeedResults::get_rel_offs, aligner_seed.h:1155). */
+typedef struct {
+	uint64_t read_off;
+	uint8_t  seed_off;       /* < 256 (uint8_t in the reference)          */
+	uint8_t  seed_len;       /* n_seed_steps, 1..32                       */
+	uint8_t  pad[6];
+} bt2x_seed_in;
+
+/* SeedAlignerSearchData (aligner_seed.cpp:173-202). */
+typedef struct {
+	uint64_t topf, botf;     /* last BW range set (valid when need_reporting) */
+	uint8_t  nlex;           /* left-extension length, <= 255                */
+	uint8_t  need_reporting; /* 1 = seed matched exactly over all its steps  */
+	uint8_t  pad[6];
+} bt2x_seed_out;
+
+int bt2x_seed_search(bt2x_ctx* ctx, const uint8_t* reads, uint64_t reads_bytes,
+                     const bt2x_seed_in* in, uint32_t n, int do_extend, bt2x_seed_out* out);
+int bt2x_seed_search_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const bt2x_seed_in* d_in,
+                         uint32_t n, int do_extend, bt2x_seed_out* d_out, void* stream);
+
+/* -------------------------------------------------------------------- DP */
+
+/* One end-to-end DP problem, i.e. SwAligner state after initRead + initRef
+ * (aligner_sw.cpp:35-229): oriented read codes/qualities (rd_/qu_), reference window
+ * codes (0-4; rf_ before the 1<<c mask step) of ncol columns, DPRect fields. */
+typedef struct {
+	uint64_t read_off;       /* reads[read_off .. +rdlen): codes 0-4            */
+	uint64_t qual_off;       /* quals[qual_off .. +rdlen): Phred+33 characters  */
+	uint64_t ref_off;        /* refs[ref_off .. +ncol): codes 0-4               */
+	int64_t  refl;           /* rect.refl; reported offset = col + refl         */
+	uint16_t rdlen;          /* rows, 1..BT2X_MAX_ROWS                          */
+	uint16_t ncol;           /* rflen_, ncol + 1 <= BT2X_MAX_COLS               */
+	int16_t  minsc;          /* clamped to >= -254 (aligner_sw.cpp:77-83)       */
+	int16_t  nceil;          /* max Ns in the reference portion                 */
+	uint16_t triml, corel, corer;
+	uint8_t  fw;             /* orientation: rc results get invertEdits()       */
+	uint8_t  pad;
+} bt2x_dp_in;
+
+/* Result of align() for one problem.  Its nextAlignment() call sequence is
+ * recs[rec_off .. rec_off + nrec). */
+typedef struct {
+	int32_t  status;         /* align() return value                            */
+	int32_t  best;           /* best score out of align(); INT32_MIN if saturated */
+	uint16_t ncand;          /* btncand_.size()                                  */
+	uint16_t nrec;
+	uint32_t rec_off;
+} bt2x_dp_out;
+
+/* One nextAlignment(res, minsc, rnd) call.  ntries = candidates backtraced during the
+ * call; the caller replays the RNG as ntries x {reseed = rnd.nextU32()+1;
+ * rnd.init(reseed+1);} (aligner_sw.cpp:324-336). */
+typedef struct {
+	uint16_t ntries;
+	uint8_t  ok;             /* 1: an alignment was returned; 0: call returned false */
+	uint8_t  pad0;
+	int16_t  score;          /* AlnScore::score_                                 */
+	uint16_t ns;             /* AlnScore::ns_                                    */
+	uint16_t gaps;           /* AlnScore::gaps_                                  */
+	uint16_t nedit;          /* edits_ = ned().size()                             */
+	uint16_t bases_aligned;  /* basesAligned_                                    */
+	uint16_t refns;          /* AlnRes::refns_                                   */
+	int64_t  refoff;         /* refcoord_.off() = col + rect.refl                */
+	uint32_t edit_off;       /* edits[edit_off .. +nedit), final order of ned()  */
+	uint32_t pad1;
+} bt2x_aln_rec;
+
+/* Packed Edit (edit.h:58-310): pos in bits 0-9, type (EDIT_TYPE_*) 12-14,
+ * chr 16-23, qchr 24-31 (ASCII, as in Edit::chr/qchr). */
+#define BT2X_EDIT_POS(e)  ((uint32_t)(e) & 0x3ffu)
+#define BT2X_EDIT_TYPE(e) (((uint32_t)(e) >> 12) & 7u)
+#define BT2X_EDIT_CHR(e)  ((char)(((uint32_t)(e) >> 16) & 0xffu))
+#define BT2X_EDIT_QCHR(e) ((char)(((uint32_t)(e) >> 24) & 0xffu))
+
+/* Optional debug outputs (may be NULL): per-problem order-independent digests of the
+ * filled E, F, H matrices (bt2x_cell_digest) and the sorted candidate list
+ * (DpBtCandidate order, aligner_sw_nuc.h:149), BT2X_MAX_COLS entries per problem,
+ * each (col << 16) | (row << 8)... see bt2x_cand_pack. */
+#define BT2X_CAND_PACK(row, col, score) (((uint32_t)(col) << 16) | ((uint32_t)(row) << 8) | (uint32_t)(score))
+typedef struct {
+	uint64_t* digests;       /* 3 per problem: E, F, H                       */
+	uint32_t* cands;         /* BT2X_MAX_COLS per problem                    */
+} bt2x_dp_debug;
+
+/* Arena capacities are caller-given; on BT2X_E_OVERFLOW *nrec_used / *nedit_used hold
+ * the required sizes and the call may be repeated with larger arenas. */
+int bt2x_dp_align(bt2x_ctx* ctx,
+                  const uint8_t* reads, uint64_t reads_bytes,
+                  const uint8_t* quals, uint64_t quals_bytes,
+                  const uint8_t* refs, uint64_t refs_bytes,
+                  const bt2x_dp_in* in, uint32_t n,
+                  bt2x_dp_out* out,
+                  bt2x_aln_rec* recs, uint32_t rec_cap, uint32_t* nrec_used,
+                  uint32_t* edits, uint32_t edit_cap, uint32_t* nedit_used,
+                  bt2x_dp_debug* debug);
+
+/* Device-pointer variant: all buffers in HBM; counters (2 x u32: recs, edits) in HBM. */
+int bt2x_dp_align_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const uint8_t* d_quals,
+                      const uint8_t* d_refs, const bt2x_dp_in* d_in, uint32_t n,
+                      bt2x_dp_out* d_out, bt2x_aln_rec* d_recs, uint32_t rec_cap,
+                      uint32_t* d_edits, uint32_t edit_cap, uint32_t* d_counters,
+                      bt2x_dp_debug* d_debug, void* stream);
+
+/* Order-independent digest of one matrix cell (shared by oracle, kernel and harness). */
+static inline uint64_t bt2x_cell_digest(uint32_t row, uint32_t col, uint32_t mat, uint32_t val) {
+	uint64_t z = ((uint64_t)row << 40) ^ ((uint64_t)col << 20) ^ ((uint64_t)mat << 16) ^ (uint64_t)val;
+	z += 0x9e3779b97f4a7c15ULL;
+	z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+	z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+	return z ^ (z >> 31);
+}
+
+const char* bt2x_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BT2X_H_ */

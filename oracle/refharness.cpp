@@ -1,0 +1,326 @@
+// oracle/refharness.cpp — TEST INFRASTRUCTURE ONLY (never shipped, never on the GPU box).
+//
+// Golden-vector dumper.  Compiles the reference aligner's own translation units
+// in place (-I/root/reference, the same list bowtie2-align.cpp:1-38 includes,
+// minus bowtie_main.cpp) and drives its hot-path classes directly:
+//
+//   seeds : MultiSeedResults::prepareOneSeed / instantiateSeeds
+//           (aligner_seed.cpp:411), MultiSeedAligner::searchAllSeedsDoAll(true)
+//           (aligner_seed.cpp:674) -> per-seed (topf, botf, need_reporting, nlex)
+//   dp    : DynProgFramer::frameSeedExtensionRect (dp_framer.cpp:81),
+//           SwAligner::initRead/initRef/align/nextAlignment (aligner_sw.cpp:35-375)
+//           -> rectangle, reference window, E/F/H digests, sorted candidates and
+//           the full sequence of nextAlignment() results with RNG state.
+//
+// Options (scoring, seed length, --dpad, ...) are parsed by the reference's own
+// parseOptions() (bt2_search.cpp:1578) so every default is the reference's.
+// Private members are opened with a preprocessor switch purely to read results.
+#include <algorithm>
+#include <atomic>
+#include <cassert>
+#include <cmath>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <limits>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <queue>
+#include <set>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+#include <getopt.h>
+#include <pthread.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/time.h>
+#include <time.h>
+#include <unistd.h>
+#include <zlib.h>
+#include <omp.h>
+#include "../include/bt2x.h"
+
+#define private public
+#define protected public
+#include "edit.cpp"
+#include "ds.cpp"
+#include "ccnt_lut.cpp"
+#include "ref_read.cpp"
+#include "alphabet.cpp"
+#include "shmem.cpp"
+#include "bt2_locks.cpp"
+#include "bt2_idx.cpp"
+#include "bt2_io.cpp"
+#include "bt2_util.cpp"
+#include "reference.cpp"
+#include "multikey_qsort.cpp"
+#include "random_source.cpp"
+#include "qual.cpp"
+#include "pat.cpp"
+#include "sam.cpp"
+#include "read_qseq.cpp"
+#include "aligner_seed_policy.cpp"
+#include "aligner_cache.cpp"
+#include "aligner_result.cpp"
+#include "ref_coord.cpp"
+#include "mask.cpp"
+#include "pe.cpp"
+#include "aln_sink.cpp"
+#include "dp_framer.cpp"
+#include "scoring.cpp"
+#include "presets.cpp"
+#include "unique.cpp"
+#include "simple_func.cpp"
+#include "outq.cpp"
+#include "aligner_swsse_ee_u8.cpp"
+#include "aligner_sw.cpp"
+#include "aligner_sw_driver.cpp"
+#include "aligner_seed.cpp"
+#include "bt2_search.cpp"
+#undef private
+#undef protected
+
+namespace harness {
+
+struct Fq { std::string name, seq, qual; };
+
+static bool readFq(std::istream& in, Fq& r) {
+	std::string plus;
+	if(!std::getline(in, r.name)) return false;
+	if(!std::getline(in, r.seq)) return false;
+	if(!std::getline(in, plus)) return false;
+	if(!std::getline(in, r.qual)) return false;
+	if(!r.name.empty() && r.name[0] == '@') r.name = r.name.substr(1);
+	return true;
+}
+
+static void parseRefOptions(const std::string& idx, const std::string& reads,
+                            int nextra, char** extra) {
+	std::vector<const char*> av;
+	av.push_back("bowtie2-align-l");
+	av.push_back("-x"); av.push_back(idx.c_str());
+	av.push_back("-U"); av.push_back(reads.c_str());
+	for(int i = 0; i < nextra; i++) av.push_back(extra[i]);
+	resetOptions();
+	parseOptions((int)av.size(), av.data());
+}
+
+static Ebwt* loadEbwt(const std::string& idx) {
+	Ebwt* e = new Ebwt(idx, 0, -1, true, -1, 0, false, false, false,
+	                   true, true, true, true, false, false, false, false);
+	e->loadIntoMemory(0, -1, true, true, true, true, false);
+	return e;
+}
+
+static const char* DNA = "ACGTN";
+
+// -------------------------------------------------------------------- seeds
+static int cmdSeeds(int argc, char** argv) {
+	if(argc < 4) { fprintf(stderr, "seeds <idx> <reads.fq> <out> [bt2 opts]\n"); return 2; }
+	std::string idx = argv[1], fq = argv[2], out = argv[3];
+	parseRefOptions(idx, fq, argc - 4, argv + 4);
+	Ebwt* ebwt = loadEbwt(idx);
+	FILE* fo = fopen(out.c_str(), "w");
+	fprintf(fo, "# seeds idx=%s reads=%s seedlen=%d rounds=%d\n", idx.c_str(), fq.c_str(),
+	        (int)multiseedLen, (int)nSeedRounds);
+	MultiSeedResults srs(1, multiseedLen, gNofw, gNorc);
+	MultiSeedAligner als(ebwt, srs);
+	std::ifstream in(fq);
+	Fq r; size_t ridx = 0, nseeds = 0;
+	while(readFq(in, r)) {
+		Read rd(r.name.c_str(), r.seq.c_str(), r.qual.c_str());
+		const size_t rdlen = rd.length();
+		size_t myidx = ridx++;
+		if(rdlen >= 256 || rdlen < 1) continue;      // bt2_search.cpp:2495 (rdlen<256)
+		const int interval = std::max((int)msIval.f<int>((double)rdlen), 1);
+		const uint32_t nrounds = std::min<uint16_t>(nSeedRounds, interval);
+		for(uint32_t roundi = 0; roundi < nrounds; roundi++) {
+			const uint32_t offset = (interval * roundi) / nrounds;
+			if(offset > 0 && multiseedLen + offset > rdlen) break;   // bt2_search.cpp:2575
+			srs.clearSeeds();
+			srs.prepareOneSeed(0, offset, interval, &rd);
+			Read* rds[1] = { &rd };
+			srs.instantiateSeeds(rds);
+			als.reserveBuffers();
+			als.prepareSearchAllSeedsOne(0);
+			als.searchAllSeedsDoAll(true);
+			for(size_t k = 0; k < als._bufVec_filled; k++) {
+				const SeedAlignerSearchParams& p = als._paramVec[k];
+				const SeedAlignerSearchData& d = als._dataVec[k];
+				const char* base = p.fw ? rd.patFw.buf() : rd.patRc.buf();
+				long seqoff = (long)(p.cs.seq - base);
+				fprintf(fo, "S %zu %u %d %d %ld %d %llu %llu %d %d\n", myidx, roundi,
+				        (int)p.fw, (int)p.seedoffidx, seqoff, (int)p.cs.n_seed_steps,
+				        (unsigned long long)d.bwt.topf, (unsigned long long)d.bwt.botf,
+				        (int)d.need_reporting, (int)d.nlex);
+				nseeds++;
+			}
+		}
+	}
+	fclose(fo);
+	fprintf(stderr, "seeds: %zu reads, %zu seed searches\n", ridx, nseeds);
+	return 0;
+}
+
+// ----------------------------------------------------------------------- dp
+static uint64_t digestMat(const SSEMatrix<false, ALN_MAX_ROWS, ALN_MAX_COLS>& m,
+                          size_t nrow, size_t ncol, int mat) {
+	uint64_t h = 0;   // order-independent: sum of bt2x_cell_digest over cells
+	for(size_t i = 0; i < nrow; i++)
+		for(size_t j = 0; j < ncol; j++)
+			h += bt2x_cell_digest((uint32_t)i, (uint32_t)j, (uint32_t)mat, (uint32_t)(m.elt(i, j, mat) & 0xff));
+	return h;
+}
+
+// Read names of simulated reads: "<anything>:<refidx>:<off>:<fw>"; off = leftmost
+// reference offset of the read's true alignment, fw = 1 if forward strand.
+static bool parseOrigin(const std::string& nm, long& tidx, long& off, int& fw) {
+	std::vector<std::string> f; std::string cur;
+	for(char c : nm) { if(c == ':' || c == ' ') { f.push_back(cur); cur.clear(); } else cur += c; }
+	f.push_back(cur);
+	if(f.size() < 4) return false;
+	tidx = atol(f[f.size()-3].c_str()); off = atol(f[f.size()-2].c_str()); fw = atoi(f.back().c_str());
+	return true;
+}
+
+static int cmdDp(int argc, char** argv) {
+	if(argc < 5) { fprintf(stderr, "dp <idx> <reads.fq> <out> <seed> [bt2 opts]\n"); return 2; }
+	std::string idx = argv[1], fq = argv[2], out = argv[3];
+	uint32_t seed = (uint32_t)atol(argv[4]);
+	parseRefOptions(idx, fq, argc - 5, argv + 5);
+	Ebwt* ebwt = loadEbwt(idx);
+	BitPairReference ref(idx, false, false, NULL, NULL, false, false, false, false, false, false);
+	if(!ref.loaded()) { fprintf(stderr, "reference not loaded\n"); return 1; }
+	Scoring sc(bonusMatch, penMmcType, penMmcMax, penMmcMin, scoreMin, nCeil, penNType, penN,
+	           penNCatPair, penRdGapConst, penRfGapConst, penRdGapLinear, penRfGapLinear, gGapBarrier);
+	FILE* fo = fopen(out.c_str(), "w");
+	fprintf(fo, "# dp idx=%s reads=%s maxhalf=%zu gapbar=%d mmp=%d,%d np=%d rdg=%d,%d rfg=%d,%d\n",
+	        idx.c_str(), fq.c_str(), (size_t)maxhalf, (int)gGapBarrier, (int)penMmcMax, (int)penMmcMin,
+	        (int)penN, (int)penRdGapConst, (int)penRdGapLinear, (int)penRfGapConst, (int)penRfGapLinear);
+	SwAligner* swap = new SwAligner();
+	SwAligner& swa = *swap;
+	RandomSource jrnd; jrnd.init(seed);
+	std::ifstream in(fq);
+	Fq r; size_t ridx = 0, nprob = 0;
+	DynProgFramer dpframe(!gReportOverhangs);
+	while(readFq(in, r)) {
+		size_t myidx = ridx++;
+		long tidx, off; int fwTrue;
+		if(!parseOrigin(r.name, tidx, off, fwTrue)) continue;
+		Read rd(r.name.c_str(), r.seq.c_str(), r.qual.c_str());
+		const size_t rdlen = rd.length();
+		if(rdlen >= 256 || rdlen < 2) continue;
+		TAlScore minsc = scoreMin.f<TAlScore>((double)rdlen);
+		if(minsc > 0) minsc = 0;
+		if(minsc < -254) minsc = -254;
+		int nceil = std::min((int)nCeil.f<int>((double)rdlen), (int)rdlen);
+		swa.reset();
+		if(!swa.initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, rdlen, sc)) {
+			fprintf(fo, "R %zu initRead-fail %zu\n", myidx, rdlen);
+			continue;
+		}
+		const int64_t tlen = (int64_t)ebwt->plen()[tidx];
+		// Diagonals: the true one, small shifts, band-edge shifts and one on the
+		// opposite strand, the way distinct seed hits reach extendSeeds.
+		std::vector<std::pair<long,int> > probs;
+		probs.push_back(std::make_pair(off, fwTrue));
+		probs.push_back(std::make_pair(off + 1 + (long)(jrnd.nextU32() % 4), fwTrue));
+		probs.push_back(std::make_pair(off - 1 - (long)(jrnd.nextU32() % 16), fwTrue));
+		if(jrnd.nextU32() % 4 == 0) probs.push_back(std::make_pair(off, 1 - fwTrue));
+		for(size_t pi = 0; pi < probs.size(); pi++) {
+			int64_t refoff = probs[pi].first;
+			bool fw = probs[pi].second != 0;
+			int readGaps = sc.maxReadGaps(minsc, rdlen);
+			int refGaps  = sc.maxRefGaps(minsc, rdlen);
+			DPRect rect;
+			bool found = dpframe.frameSeedExtensionRect(refoff, rdlen, tlen, readGaps, refGaps,
+			                                            (size_t)nceil, maxhalf, rect);
+			if(!found) { fprintf(fo, "F %zu %ld %d frame-trimmed\n", myidx, (long)refoff, (int)fw); continue; }
+			size_t nwindow = 0;
+			if(refoff >= rect.refl) nwindow = (size_t)(refoff - rect.refl);
+			size_t nsInLeftShift = 0;
+			swa.reset();
+			swa.initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, rdlen, sc);
+			bool okRef = swa.initRef(fw, (TRefId)tidx, rect, ref, tlen, minsc, true, true,
+			                         nwindow, nsInLeftShift);
+			if(!okRef) { fprintf(fo, "F %zu %ld %d initRef-fail\n", myidx, (long)refoff, (int)fw); continue; }
+			std::string win;
+			for(size_t i = 0; i < swa.rflen_; i++) win += DNA[firsts5[(int)swa.rf_[i]]];
+			uint32_t rseed = jrnd.nextU32();
+			fprintf(fo, "P %zu %zu %d %s %s %s %lld %lld %zu %zu %zu %lld %d %u\n", nprob, myidx, (int)fw,
+			        r.seq.c_str(), r.qual.c_str(), win.c_str(), (long long)rect.refl, (long long)rect.refr,
+			        (size_t)rect.triml, (size_t)rect.corel, (size_t)rect.corer, (long long)minsc, nceil, rseed);
+			nprob++;
+			TAlScore best = std::numeric_limits<TAlScore>::min();
+			bool ok = swa.align(best);
+			auto& d = fw ? swa.sseU8fw_ : swa.sseU8rc_;
+			fprintf(fo, "A %d %lld %zu %016llx %016llx %016llx\n", (int)ok, (long long)best,
+			        (size_t)swa.btncand_.size(),
+			        (unsigned long long)digestMat(d.mat_, rdlen, swa.rflen_, SSEMatrixConsts::E),
+			        (unsigned long long)digestMat(d.mat_, rdlen, swa.rflen_, SSEMatrixConsts::F),
+			        (unsigned long long)digestMat(d.mat_, rdlen, swa.rflen_, SSEMatrixConsts::H));
+			if(getenv("HARNESS_DUMP") && nprob == 1) {
+				for(size_t i = 0; i < rdlen; i++) for(size_t j = 0; j < swa.rflen_; j++)
+					fprintf(stderr, "M %zu %zu %d %d %d\n", i, j, d.mat_.elt(i, j, 0), d.mat_.elt(i, j, 1), d.mat_.elt(i, j, 2));
+			}
+			fprintf(fo, "C");
+			for(size_t c = 0; c < swa.btncand_.size(); c++)
+				fprintf(fo, " %zu,%zu,%lld", swa.btncand_[c].row, swa.btncand_[c].col,
+				        (long long)swa.btncand_[c].score);
+			fprintf(fo, "\n");
+			if(ok) {
+				RandomSource rnd; rnd.init(rseed);
+				SwResult res;
+				while(!swa.done()) {
+					res.reset();
+					swa.nextAlignment(res, minsc, rnd);
+					if(res.empty()) { fprintf(fo, "N 0 %u\n", rnd.last); break; }
+					AlnRes& a = res.alres;
+					fprintf(fo, "N 1 %u %lld %lld %lld %d %d %lld %zu %zu", rnd.last,
+					        (long long)a.score_.score_, (long long)a.score_.ns_, (long long)a.score_.gaps_,
+					        a.score_.edits_, a.score_.basesAligned_, (long long)a.refcoord_.off(),
+					        (size_t)a.refns_, (size_t)a.ned_.size());
+					for(size_t e = 0; e < a.ned_.size(); e++) {
+						const Edit& ed = a.ned_[e];
+						fprintf(fo, " %u,%d,%c,%c", ed.pos, (int)ed.type, (char)ed.chr, (char)ed.qchr);
+					}
+					fprintf(fo, "\n");
+				}
+			}
+			fprintf(fo, "E\n");
+		}
+	}
+	fclose(fo);
+	fprintf(stderr, "dp: %zu reads, %zu problems\n", ridx, nprob);
+	delete swap;
+	return 0;
+}
+
+} // namespace harness
+
+int main(int argc, char** argv) {
+	if(argc < 2) { fprintf(stderr, "usage: refharness seeds|dp ...\n"); return 2; }
+	std::string cmd = argv[1];
+	try {
+		if(cmd == "seeds") return harness::cmdSeeds(argc - 1, argv + 1);
+		if(cmd == "dp") return harness::cmdDp(argc - 1, argv + 1);
+	} catch(int e) {
+		fprintf(stderr, "reference threw %d\n", e);
+		return 1;
+	}
+	fprintf(stderr, "unknown command %s\n", cmd.c_str());
+	return 2;
+}

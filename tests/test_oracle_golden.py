@@ -1,0 +1,62 @@
+"""Pin the CPU restatement (oracle/bt2x_oracle.c) against golden vectors dumped by the
+reference's own code (oracle/refharness.cpp via tools/make_golden.py).
+
+The oracle must be bit-exact here before it is trusted as the checker of the HIP
+kernels on the GPU box (where the reference does not exist)."""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io as g
+import oracle_lib as ol
+
+SEED_SETS = [("lambda_virus", "lambda_longreads.fq.xz", "seeds_lambda.txt.xz"),
+             ("rep", "rep_reads.fq.xz", "seeds_rep.txt.xz")]
+DP_SETS = ["dp_rep.txt.xz", "dp_rep_dpad12.txt.xz", "dp_rep_alt.txt.xz"]
+
+
+def scoring_for(golden):
+    sc = ol.default_scoring()
+    for k, v in g.dp_header_scoring(golden).items():
+        setattr(sc, k, v)
+    ol.lib().bt2o_scoring_init.argtypes = [ol.ctypes.POINTER(g.abi.Scoring)]
+    ol.lib().bt2o_scoring_init(ol.ctypes.byref(sc))
+    return sc
+
+
+@pytest.mark.parametrize("name,fq,gold", SEED_SETS)
+def test_seed_search_matches_reference(golden_dir, name, fq, gold):
+    base = g.materialize_index(name, str(golden_dir))
+    idx = ol.OracleIndex(base)
+    case = g.SeedCase(os.path.join(g.GOLDEN, fq), os.path.join(g.GOLDEN, gold))
+    assert case.n > 20000
+    out, ctr = ol.seed_search(idx, case.reads, case.inp, do_extend=True)
+    np.testing.assert_array_equal(out["need_reporting"], case.exp_rep)
+    np.testing.assert_array_equal(out["topf"], case.exp_topf)
+    np.testing.assert_array_equal(out["botf"], case.exp_botf)
+    np.testing.assert_array_equal(out["nlex"], case.exp_nlex)
+    assert ctr["n_lf1"] > 0
+
+
+def test_rep_set_covers_multi_row_ranges(golden_dir):
+    case = g.SeedCase(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), os.path.join(g.GOLDEN, "seeds_rep.txt.xz"))
+    rep = case.exp_rep == 1
+    assert ((case.exp_botf - case.exp_topf)[rep] > 1).sum() > 1000      # mapBiLFEx path
+    assert (case.exp_nlex[rep] > 0).sum() > 1000                        # extension path
+    assert (case.exp_rep == 0).sum() > 1000                             # failing seeds
+
+
+@pytest.mark.parametrize("gold", DP_SETS)
+def test_dp_matches_reference(gold):
+    path = os.path.join(g.GOLDEN, gold)
+    case = g.DpCase(path)
+    assert case.n > 5000
+    sc = scoring_for(path)
+    out, recs, edits, dig, cands, ctr = ol.dp_align(sc, case.reads, case.quals, case.refs, case.inp)
+    bad = g.compare_dp(case, out, recs, edits, dig, cands)
+    assert not bad, "\n".join(bad)
+    # the golden set exercises successes, failures, gaps, Ns and multiple calls
+    assert (out["status"] == 1).sum() > 1000 and (out["status"] == 0).sum() > 100
+    assert (recs["gaps"] > 0).sum() > 100 and (recs["ns"] > 0).sum() > 10
+    assert (out["nrec"] > 1).sum() > 100

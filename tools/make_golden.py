@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/ from the reference itself (run in the dev container,
+where /root/reference exists; never on the GPU box).
+
+Steps (all outputs xz-compressed under tests/golden/):
+  1. make -C oracle ref          -> oracle/_ref/{bowtie2-build-l,refharness}
+  2. lambda: index built by the reference's bowtie2-build-l from
+     example/reference/lambda_virus.fa; reads = first 2000 records of the shipped
+     example/reads/longreads.fq; seeds golden = refharness seeds.
+  3. rep: seeded synthetic 300 kbp genome with repeat families / low complexity / N
+     runs (tools/simdata.py), reference-built index, simulated reads of several
+     lengths (and an N-rich set); seeds golden + DP golden at the reference defaults,
+     DP golden at --dpad 12 (config C3's setting) and DP golden under a non-default
+     scoring scheme.
+Each golden file starts with a '#' header naming the command that produced it.
+"""
+from __future__ import annotations
+
+import lzma
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+REF = os.environ.get("BT2X_REFERENCE", "/root/reference")
+GOLD = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, HERE)
+import simdata as sd  # noqa: E402
+
+BUILD = os.path.join(ROOT, "oracle", "_ref", "bowtie2-build-l")
+HARN = os.path.join(ROOT, "oracle", "_ref", "refharness")
+
+# non-default scoring variant used by dp_rep_alt (must match tests/test_oracle_golden.py)
+ALT_OPTS = ["--mp", "5,1", "--np", "2", "--rdg", "4,2", "--rfg", "6,3", "--gbar", "2"]
+
+
+def xz_copy(src: str, dst: str) -> None:
+    with open(src, "rb") as fi, lzma.open(dst, "wb", preset=9 | lzma.PRESET_EXTREME) as fo:
+        shutil.copyfileobj(fi, fo)
+
+
+def run(cmd, **kw):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, **kw)
+
+
+def main() -> None:
+    run(["make", "-C", os.path.join(ROOT, "oracle"), "ref", "oracle"])
+    os.makedirs(GOLD, exist_ok=True)
+    tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
+    try:
+        # ---------------- lambda (the reference's own example data)
+        lam = os.path.join(tmp, "lambda_virus")
+        run([BUILD, os.path.join(REF, "example/reference/lambda_virus.fa"), lam],
+            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        for k in "1234":
+            xz_copy(f"{lam}.{k}.bt2l", os.path.join(GOLD, f"lambda_virus.{k}.bt2l.xz"))
+        fq = os.path.join(tmp, "lambda_longreads.fq")
+        with open(os.path.join(REF, "example/reads/longreads.fq")) as fi, open(fq, "w") as fo:
+            for i, line in enumerate(fi):
+                if i >= 4 * 2000:
+                    break
+                fo.write(line)
+        xz_copy(fq, os.path.join(GOLD, "lambda_longreads.fq.xz"))
+        out = os.path.join(tmp, "seeds_lambda.txt")
+        run([HARN, "seeds", lam, fq, out])
+        xz_copy(out, os.path.join(GOLD, "seeds_lambda.txt.xz"))
+
+        # ---------------- rep (synthetic, repeat-rich)
+        g = sd.gen_genome(300000, nchrom=3, seed=7, repeat_frac=0.3, n_runs_per_mb=20,
+                          lowcomp_per_mb=40)
+        fa = os.path.join(tmp, "rep.fa")
+        sd.write_fasta(fa, g)
+        rep = os.path.join(tmp, "rep")
+        run([BUILD, fa, rep], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        for k in "1234":
+            xz_copy(f"{rep}.{k}.bt2l", os.path.join(GOLD, f"rep.{k}.bt2l.xz"))
+        xz_copy(fa, os.path.join(GOLD, "rep.fa.xz"))
+        reads = (sd.sim_reads(g, 1500, 100, seed=11) + sd.sim_reads(g, 1000, 150, seed=12)
+                 + sd.sim_reads(g, 300, 40, seed=13)
+                 + sd.sim_reads(g, 200, 160, seed=14, allow_ref_n=True)
+                 + sd.sim_reads(g, 100, 20, seed=15)
+                 + sd.sim_reads(g, 300, 100, seed=16, n_rate=0.03, sub_rate=0.03)
+                 + sd.sim_reads(g, 100, 139, seed=17) + sd.sim_reads(g, 60, 12, seed=18))
+        rfq = os.path.join(tmp, "rep_reads.fq")
+        sd.write_fastq(rfq, reads)
+        xz_copy(rfq, os.path.join(GOLD, "rep_reads.fq.xz"))
+        out = os.path.join(tmp, "seeds_rep.txt")
+        run([HARN, "seeds", rep, rfq, out])
+        xz_copy(out, os.path.join(GOLD, "seeds_rep.txt.xz"))
+        for name, opts in (("dp_rep", []), ("dp_rep_dpad12", ["--dpad", "12"]),
+                           ("dp_rep_alt", ALT_OPTS)):
+            out = os.path.join(tmp, name + ".txt")
+            run([HARN, "dp", rep, rfq, out, "1234"] + opts)
+            xz_copy(out, os.path.join(GOLD, name + ".txt.xz"))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    for f in sorted(os.listdir(GOLD)):
+        print(f"{os.path.getsize(os.path.join(GOLD, f)):>10}  {f}")
+
+
+if __name__ == "__main__":
+    main()

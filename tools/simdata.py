@@ -1,0 +1,151 @@
+"""Deterministic synthetic genomes and reads (test and bench inputs).
+
+The reference ships one real genome (lambda, example/reference/lambda_virus.fa) and
+no simulator usable offline (its scripts/sim needs Math::Random), so the
+synthetic inputs for BASELINE.json's configs are generated here, seeded:
+
+* genome: uniform random ACGT per chromosome, plus (a) interspersed repeat
+  families -- a few hundred bp element copied many times with ~2% divergence, which
+  gives seed ranges > 1 and multi-hit DP work, (b) low-complexity stretches
+  (homopolymers / dinucleotides), (c) N runs, which the index excludes from the
+  joined text and the DP pads (aligner_sw.cpp:148-184).
+* reads: error model of BASELINE.md ("1 % substitutions, 10 % of reads carry one
+  indel, 50 % reverse-complemented, Phred uniform 2-40"), plus a small rate of read
+  Ns.  The read name encodes the true origin as ``r<i>:<chrom>:<leftmost offset>:<fw>``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ACGT = np.frombuffer(b"ACGTN", dtype=np.uint8)
+_COMP = np.zeros(256, dtype=np.uint8)
+for a, b in zip(b"ACGTN", b"TGCAN"):
+    _COMP[a] = b
+
+
+def gen_genome(total_len: int, nchrom: int = 1, seed: int = 0, repeat_frac: float = 0.05,
+               repeat_len: int = 300, n_runs_per_mb: float = 2.0,
+               lowcomp_per_mb: float = 5.0) -> list[tuple[str, bytes]]:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    per = total_len // nchrom
+    out = []
+    fam = [rng.integers(0, 4, size=repeat_len, dtype=np.uint8) for _ in range(8)]
+    for c in range(nchrom):
+        s = rng.integers(0, 4, size=per, dtype=np.uint8)
+        # interspersed repeat copies with ~2% divergence
+        ncopies = int(per * repeat_frac / repeat_len)
+        if ncopies and per > 4 * repeat_len:
+            pos = rng.integers(0, per - repeat_len, size=ncopies)
+            which = rng.integers(0, len(fam), size=ncopies)
+            for p, w in zip(pos.tolist(), which.tolist()):
+                el = fam[w].copy()
+                mut = rng.random(repeat_len) < 0.02
+                el[mut] = rng.integers(0, 4, size=int(mut.sum()), dtype=np.uint8)
+                s[p:p + repeat_len] = el
+        # low-complexity stretches
+        nlow = int(per / 1e6 * lowcomp_per_mb) + (1 if per >= 20000 else 0)
+        for _ in range(nlow):
+            ln = int(rng.integers(20, 200))
+            p = int(rng.integers(0, max(1, per - ln)))
+            unit = rng.integers(0, 4, size=int(rng.integers(1, 3)), dtype=np.uint8)
+            s[p:p + ln] = np.resize(unit, ln)
+        seq = ACGT[s]
+        # N runs (excluded from the joined text by the index builder)
+        nn = int(per / 1e6 * n_runs_per_mb) + (1 if per >= 20000 else 0)
+        for _ in range(nn):
+            ln = int(rng.integers(1, 600))
+            p = int(rng.integers(0, max(1, per - ln)))
+            seq[p:p + ln] = ord("N")
+        out.append((f"chr{c + 1}", seq.tobytes()))
+    return out
+
+
+def write_fasta(path: str, chroms: list[tuple[str, bytes]], width: int = 60) -> None:
+    with open(path, "wb") as f:
+        for name, seq in chroms:
+            f.write(b">" + name.encode() + b"\n")
+            for i in range(0, len(seq), width):
+                f.write(seq[i:i + width] + b"\n")
+
+
+def read_fasta(path: str) -> list[tuple[str, bytes]]:
+    out, name, cur = [], None, []
+    with open(path, "rb") as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith(b">"):
+                if name is not None:
+                    out.append((name, b"".join(cur)))
+                name, cur = line[1:].split()[0].decode(), []
+            elif line:
+                cur.append(line.upper())
+    if name is not None:
+        out.append((name, b"".join(cur)))
+    return out
+
+
+def revcomp(s: bytes) -> bytes:
+    return _COMP[np.frombuffer(s, dtype=np.uint8)[::-1]].tobytes()
+
+
+def sim_reads(chroms: list[tuple[str, bytes]], n: int, rdlen: int, seed: int,
+              sub_rate: float = 0.01, indel_frac: float = 0.10, rc_frac: float = 0.5,
+              qmin: int = 2, qmax: int = 40, n_rate: float = 0.001,
+              allow_ref_n: bool = False) -> list[tuple[str, bytes, bytes]]:
+    """Return [(name, seq, qual)].  Origins avoid reference N runs unless allowed."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lens = np.array([len(s) for _, s in chroms], dtype=np.int64)
+    cum = np.cumsum(lens)
+    reads = []
+    i = 0
+    tries = 0
+    while len(reads) < n:
+        tries += 1
+        g = int(rng.integers(0, int(cum[-1])))
+        c = int(np.searchsorted(cum, g, side="right"))
+        ref = chroms[c][1]
+        if len(ref) < rdlen + 2:
+            continue
+        p = int(rng.integers(0, len(ref) - rdlen - 1))
+        frag = bytearray(ref[p:p + rdlen + 1])
+        if not allow_ref_n and b"N" in frag:
+            continue
+        s = np.frombuffer(bytes(frag[:rdlen]), dtype=np.uint8).copy()
+        mut = rng.random(rdlen) < sub_rate
+        s[mut] = ACGT[rng.integers(0, 4, size=int(mut.sum()))]
+        if rdlen > 24 and rng.random() < indel_frac:
+            k = int(rng.integers(10, rdlen - 10))
+            if rng.random() < 0.5:      # deletion from the read
+                s = np.concatenate([s[:k], s[k + 1:], np.frombuffer(bytes(frag[rdlen:rdlen + 1]), np.uint8)])
+            else:                       # insertion into the read
+                s = np.concatenate([s[:k], ACGT[rng.integers(0, 4, size=1)], s[k:-1]])
+        nm = rng.random(rdlen) < n_rate
+        s[nm] = ord("N")
+        fw = rng.random() >= rc_frac
+        seq = s.tobytes()
+        if not fw:
+            seq = revcomp(seq)
+        q = (rng.integers(qmin, qmax + 1, size=rdlen) + 33).astype(np.uint8).tobytes()
+        reads.append((f"r{i}:{c}:{p}:{int(fw)}", seq, q))
+        i += 1
+    return reads
+
+
+def write_fastq(path: str, reads) -> None:
+    with open(path, "wb") as f:
+        for name, seq, q in reads:
+            f.write(b"@" + name.encode() + b"\n" + seq + b"\n+\n" + q + b"\n")
+
+
+def read_fastq(path: str) -> list[tuple[str, bytes, bytes]]:
+    out = []
+    with open(path, "rb") as f:
+        while True:
+            h = f.readline()
+            if not h:
+                break
+            s = f.readline().strip()
+            f.readline()
+            q = f.readline().strip()
+            out.append((h.strip()[1:].decode(), s, q))
+    return out
