@@ -234,6 +234,9 @@ static inline uint64_t bt2x_cell_digest(uint32_t row, uint32_t col, uint32_t mat
 }
 
 const char* bt2x_version(void);
+/* sizeof of the ABI structs (seed_in, seed_out, dp_in, dp_out, aln_rec, scoring,
+ * index_desc, counters), for binding self-checks; returns the count. */
+int bt2x_abi_sizes(uint32_t* out, int n);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,195 @@
+"""ctypes binding of libbt2x.so (the product library: gfx950 kernels + C-ABI).
+
+There is deliberately no CPU fallback: if the shared library is missing, or no HIP
+device is present, every entry point raises.  The CPU restatement in oracle/ is a test
+checker and is never imported from here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbt2x.so")
+_LIB = None
+
+FUNCS = {
+    "bt2x_index_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(abi.IndexDesc)]),
+    "bt2x_index_free": (None, [ctypes.POINTER(abi.IndexDesc)]),
+    "bt2x_scoring_default": (None, [ctypes.POINTER(abi.Scoring)]),
+    "bt2x_scoring_init": (None, [ctypes.POINTER(abi.Scoring)]),
+    "bt2x_open": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(abi.IndexDesc),
+                                 ctypes.POINTER(abi.Scoring), ctypes.POINTER(ctypes.c_void_p)]),
+    "bt2x_close": (None, [ctypes.c_void_p]),
+    "bt2x_last_kernel_ms": (ctypes.c_double, [ctypes.c_void_p, ctypes.c_int]),
+    "bt2x_last_counters": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(abi.Counters)]),
+    "bt2x_seed_search": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]),
+    "bt2x_seed_search_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p]),
+    "bt2x_dp_align": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p,
+                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                     ctypes.POINTER(abi.DpDebug)]),
+    "bt2x_dp_align_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                         ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.POINTER(abi.DpDebug), ctypes.c_void_p]),
+    "bt2x_version": (ctypes.c_char_p, []),
+    "bt2x_abi_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
+}
+
+
+class Bt2xError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libbt2x.so (built in-tree by __graft_entry__.build()); raise if absent."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise Bt2xError(f"{LIB_PATH} is missing: build it with "
+                            "`make -C omp-bowtie2-prime_amd/csrc` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in FUNCS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise Bt2xError(f"{what} failed with bt2x error {rc}")
+
+
+def default_scoring(**overrides) -> abi.Scoring:
+    sc = abi.Scoring()
+    L = load()
+    L.bt2x_scoring_default(ctypes.byref(sc))
+    if overrides:
+        for k, v in overrides.items():
+            setattr(sc, k, int(v))
+        L.bt2x_scoring_init(ctypes.byref(sc))
+    return sc
+
+
+class Index:
+    """Host image of a forward .bt2l index (Ebwt::readIntoMemory)."""
+
+    def __init__(self, basename: str, load_offs: bool = False):
+        self.desc = abi.IndexDesc()
+        check(load().bt2x_index_load(basename.encode(), int(load_offs), ctypes.byref(self.desc)),
+              f"bt2x_index_load({basename})")
+        self.basename = basename
+
+    def close(self):
+        if self.desc.owner:
+            load().bt2x_index_free(ctypes.byref(self.desc))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One GPU context (bt2x_open): uploaded index + scoring + kernel launch state."""
+
+    def __init__(self, index: Index, device: int = 0, scoring: abi.Scoring | None = None):
+        self.index = index
+        self.scoring = scoring if scoring is not None else default_scoring()
+        h = ctypes.c_void_p()
+        check(load().bt2x_open(device, ctypes.byref(index.desc), ctypes.byref(self.scoring),
+                               ctypes.byref(h)), "bt2x_open")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            load().bt2x_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- seeds
+    def seed_search(self, reads: np.ndarray, inp: np.ndarray, do_extend: bool = True) -> np.ndarray:
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        inp = np.ascontiguousarray(inp, dtype=abi.SEED_IN)
+        out = np.zeros(len(inp), dtype=abi.SEED_OUT)
+        check(load().bt2x_seed_search(self.h, abi.ptr(reads), reads.nbytes, abi.ptr(inp), len(inp),
+                                      int(do_extend), abi.ptr(out)), "bt2x_seed_search")
+        return out
+
+    def seed_search_dev(self, d_reads: int, d_in: int, n: int, d_out: int, do_extend=True, stream=0):
+        check(load().bt2x_seed_search_dev(self.h, d_reads, d_in, n, int(do_extend), d_out, stream),
+              "bt2x_seed_search_dev")
+
+    # ----------------------------------------------------------------- DP
+    def dp_align(self, reads, quals, refs, inp, debug=False, rec_cap=None, edit_cap=None):
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        quals = np.ascontiguousarray(quals, dtype=np.uint8)
+        refs = np.ascontiguousarray(refs, dtype=np.uint8)
+        inp = np.ascontiguousarray(inp, dtype=abi.DP_IN)
+        n = len(inp)
+        rec_cap = rec_cap or max(64, 4 * n)
+        edit_cap = edit_cap or max(1024, 32 * n)
+        out = np.zeros(n, dtype=abi.DP_OUT)
+        recs = np.zeros(rec_cap, dtype=abi.ALN_REC)
+        edits = np.zeros(edit_cap, dtype=np.uint32)
+        nrec, nedit = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        dig = np.zeros((n, 3), dtype=np.uint64) if debug else None
+        cands = np.zeros((n, abi.MAX_COLS), dtype=np.uint32) if debug else None
+        dbg = abi.DpDebug(abi.ptr(dig).value, abi.ptr(cands).value) if debug else None
+        rc = load().bt2x_dp_align(self.h, abi.ptr(reads), reads.nbytes, abi.ptr(quals), quals.nbytes,
+                                  abi.ptr(refs), refs.nbytes, abi.ptr(inp), n, abi.ptr(out),
+                                  abi.ptr(recs), rec_cap, ctypes.byref(nrec), abi.ptr(edits),
+                                  edit_cap, ctypes.byref(nedit),
+                                  ctypes.byref(dbg) if dbg is not None else None)
+        if rc == abi.E_OVERFLOW:
+            return self.dp_align(reads, quals, refs, inp, debug, nrec.value + 64, nedit.value + 1024)
+        check(rc, "bt2x_dp_align")
+        return out, recs[: nrec.value], edits[: nedit.value], dig, cands
+
+    def dp_align_dev(self, d_reads, d_quals, d_refs, d_in, n, d_out, d_recs, rec_cap, d_edits,
+                     edit_cap, d_counters, stream=0):
+        check(load().bt2x_dp_align_dev(self.h, d_reads, d_quals, d_refs, d_in, n, d_out, d_recs,
+                                       rec_cap, d_edits, edit_cap, d_counters, None, stream),
+              "bt2x_dp_align_dev")
+
+    def device_name(self) -> str:
+        try:
+            import torch
+            return torch.cuda.get_device_name(0)
+        except Exception:
+            return "hip device"
+
+    # ------------------------------------------------------------ metrics
+    def last_kernel_ms(self, kernel: int) -> float:
+        return float(load().bt2x_last_kernel_ms(self.h, kernel))
+
+    def last_counters(self, kernel: int) -> dict:
+        c = abi.Counters()
+        check(load().bt2x_last_counters(self.h, kernel, ctypes.byref(c)), "bt2x_last_counters")
+        return c.as_dict()
+
+
+def abi_sizes() -> list[int]:
+    buf = (ctypes.c_uint32 * 16)()
+    n = load().bt2x_abi_sizes(buf, 16)
+    return list(buf[:n])

@@ -1,0 +1,376 @@
+// bt2x_api.cpp — host side of the C-ABI (include/bt2x.h): index loader, scoring
+// tables, per-GPU context, staging and launches.  No CPU compute path exists: every
+// seed search and DP goes through the gfx950 kernels, and without a HIP device
+// bt2x_open fails with BT2X_E_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "bt2x_device.h"
+
+size_t bt2x_dp_slot_bytes();
+
+#define HIPCHK(x) do { if((x) != hipSuccess) return BT2X_E_NODEVICE; } while(0)
+
+// ----------------------------------------------------------------- index load
+namespace {
+struct IndexOwner { std::vector<std::vector<uint8_t>> blocks; };
+
+bool read_exact(FILE* f, void* p, size_t n) { return n == 0 || fread(p, 1, n, f) == n; }
+
+template<typename T> T* take(IndexOwner* o, size_t n) {
+	o->blocks.emplace_back(n * sizeof(T) + 16);
+	return reinterpret_cast<T*>(o->blocks.back().data());
+}
+}
+
+// Ebwt::readIntoMemory (bt2_io.cpp:39-560) for the 64-bit (.bt2l) forward index.
+extern "C" int bt2x_index_load(const char* base, int load_offs, bt2x_index_desc* o) {
+	if(!base || !o) return BT2X_E_ARG;
+	std::memset(o, 0, sizeof(*o));
+	std::string p1 = std::string(base) + ".1.bt2l";
+	FILE* f = fopen(p1.c_str(), "rb");
+	if(!f) return BT2X_E_IO;
+	std::unique_ptr<IndexOwner> own(new IndexOwner());
+	uint32_t one = 0; uint64_t len = 0; int32_t lineRate, lps, offRate, ftabChars, flags;
+	bool ok = read_exact(f, &one, 4) && read_exact(f, &len, 8) && read_exact(f, &lineRate, 4) &&
+	          read_exact(f, &lps, 4) && read_exact(f, &offRate, 4) && read_exact(f, &ftabChars, 4) &&
+	          read_exact(f, &flags, 4);
+	// only the fork's build is supported: little-endian, lineRate 7 (128-B sides)
+	if(!ok || one != 1 || lineRate != 7 || ftabChars < 1 || ftabChars > 16) { fclose(f); return BT2X_E_IO; }
+	uint64_t npat = 0, nfrag = 0;
+	ok = read_exact(f, &npat, 8);
+	uint64_t* plen = take<uint64_t>(own.get(), npat + 1);
+	ok = ok && read_exact(f, plen, 8 * npat) && read_exact(f, &nfrag, 8);
+	uint64_t* rstarts = take<uint64_t>(own.get(), 3 * nfrag + 1);
+	ok = ok && read_exact(f, rstarts, 24 * nfrag);
+	const uint64_t sideSz = 1ULL << lineRate, sideBwtSz = sideSz - 32;    // EbwtParams::init
+	const uint64_t numSides = (len / 4 + 1 + sideBwtSz - 1) / sideBwtSz;
+	const uint64_t ebwtTot = numSides * sideSz;
+	uint8_t* ebwt = take<uint8_t>(own.get(), ebwtTot);
+	uint64_t zoff = 0;
+	ok = ok && read_exact(f, ebwt, ebwtTot) && read_exact(f, &zoff, 8) && read_exact(f, o->fchr, 40);
+	const uint64_t ftabLen = (1ULL << (2 * ftabChars)) + 1, eftabLen = 2ULL * ftabChars;
+	uint64_t* ftab = take<uint64_t>(own.get(), ftabLen);
+	uint64_t* eftab = take<uint64_t>(own.get(), eftabLen);
+	ok = ok && read_exact(f, ftab, 8 * ftabLen) && read_exact(f, eftab, 8 * eftabLen);
+	fclose(f);
+	if(!ok) return BT2X_E_IO;
+	o->len = len; o->zoff = zoff; o->ftab_chars = ftabChars; o->off_rate = offRate;
+	o->line_rate = lineRate; o->flags = flags;
+	o->ebwt = ebwt; o->ebwt_bytes = ebwtTot;
+	o->ftab = ftab; o->ftab_len = ftabLen; o->eftab = eftab; o->eftab_len = eftabLen;
+	o->plen = plen; o->npat = npat; o->rstarts = rstarts; o->nfrag = nfrag;
+	if(load_offs) {
+		std::string p2 = std::string(base) + ".2.bt2l";
+		f = fopen(p2.c_str(), "rb");
+		if(!f) return BT2X_E_IO;
+		const uint64_t offsLen = (len + 1 + (1ULL << offRate) - 1) >> offRate;
+		uint64_t* offs = take<uint64_t>(own.get(), offsLen);
+		ok = read_exact(f, &one, 4) && read_exact(f, offs, 8 * offsLen);
+		fclose(f);
+		if(!ok) return BT2X_E_IO;
+		o->offs = offs; o->offs_len = offsLen;
+	}
+	o->owner = own.release();
+	return BT2X_OK;
+}
+
+extern "C" void bt2x_index_free(bt2x_index_desc* o) {
+	if(!o) return;
+	delete reinterpret_cast<IndexOwner*>(o->owner);
+	std::memset(o, 0, sizeof(*o));
+}
+
+// -------------------------------------------------------------------- scoring
+extern "C" void bt2x_scoring_init(bt2x_scoring* sc) {
+	// Scoring::initPens (scoring.h:94-132): COST_MODEL_QUAL mismatches, constant N
+	for(int i = 0; i < 256; i++) {
+		const int ii = i < 40 ? i : 40;
+		const float frac = (float)ii / 40.0f;
+		sc->mmpens[i] = sc->mm_min + (int)(frac * (float)(sc->mm_max - sc->mm_min));
+		sc->npens[i] = sc->n_pen;
+	}
+}
+
+extern "C" void bt2x_scoring_default(bt2x_scoring* sc) {
+	std::memset(sc, 0, sizeof(*sc));
+	sc->mm_max = 6; sc->mm_min = 2; sc->n_pen = 1;      // scoring.h:38-50
+	sc->rdg_const = 5; sc->rdg_linear = 3;              // scoring.h:70-79
+	sc->rfg_const = 5; sc->rfg_linear = 3;
+	sc->gapbar = 4;                                     // bt2_search.cpp:374
+	bt2x_scoring_init(sc);
+}
+
+extern "C" const char* bt2x_version(void) { return "bt2x 0.1 (gfx950; abi 1)"; }
+
+// -------------------------------------------------------------------- context
+struct DevBuf {
+	void* p = nullptr; size_t cap = 0;
+	int ensure(size_t n) {
+		if(n <= cap) return 0;
+		if(p) (void)hipFree(p);
+		p = nullptr; cap = 0;
+		size_t want = n + n / 4 + 4096;
+		if(hipMalloc(&p, want) != hipSuccess) return BT2X_E_NOMEM;
+		cap = want;
+		return 0;
+	}
+	void release() { if(p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct bt2x_ctx {
+	int device = 0;
+	hipStream_t stream = nullptr;
+	hipEvent_t ev[BT2X_K_COUNT][2];
+	bool ev_valid[BT2X_K_COUNT] = {false, false};
+	DevIndex ix{};
+	DevScoring sc{};
+	void* d_ebwt = nullptr; void* d_ftab = nullptr; void* d_eftab = nullptr;
+	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
+	DevBuf scratch;
+	uint32_t nslots = 0;
+	unsigned long long* d_stats = nullptr;     // [0..2] seed, [4..6] dp
+	uint32_t* d_counters = nullptr;
+	uint64_t n_seed_last = 0, n_dp_last = 0;
+};
+
+namespace {
+DevScoring to_dev(const bt2x_scoring& s) {
+	DevScoring d{};
+	d.rdo = s.rdg_const + s.rdg_linear; d.rde = s.rdg_linear;
+	d.rfo = s.rfg_const + s.rfg_linear; d.rfe = s.rfg_linear;
+	d.gapbar = s.gapbar; d.npen = s.npens[0];
+	for(int i = 0; i < 256; i++) d.mmpen[i] = (uint8_t)(s.mmpens[i] < 0 ? 0 : s.mmpens[i] > 255 ? 255 : s.mmpens[i]);
+	return d;
+}
+}
+
+extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scoring* sc, bt2x_ctx** out) {
+	if(!idx || !out) return BT2X_E_ARG;
+	*out = nullptr;
+	int ndev = 0;
+	if(hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return BT2X_E_NODEVICE;
+	std::unique_ptr<bt2x_ctx> c(new bt2x_ctx());
+	c->device = device;
+	HIPCHK(hipSetDevice(device));
+	HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	for(int k = 0; k < BT2X_K_COUNT; k++) {
+		HIPCHK(hipEventCreate(&c->ev[k][0]));
+		HIPCHK(hipEventCreate(&c->ev[k][1]));
+	}
+	HIPCHK(hipMalloc(&c->d_ebwt, idx->ebwt_bytes + 256));
+	HIPCHK(hipMemcpy(c->d_ebwt, idx->ebwt, idx->ebwt_bytes, hipMemcpyHostToDevice));
+	HIPCHK(hipMalloc(&c->d_ftab, 8 * idx->ftab_len));
+	HIPCHK(hipMemcpy(c->d_ftab, idx->ftab, 8 * idx->ftab_len, hipMemcpyHostToDevice));
+	HIPCHK(hipMalloc(&c->d_eftab, 8 * (idx->eftab_len + 1)));
+	HIPCHK(hipMemcpy(c->d_eftab, idx->eftab, 8 * idx->eftab_len, hipMemcpyHostToDevice));
+	c->ix.ebwt = (const uint8_t*)c->d_ebwt;
+	c->ix.ftab = (const uint64_t*)c->d_ftab;
+	c->ix.eftab = (const uint64_t*)c->d_eftab;
+	c->ix.len = idx->len;
+	c->ix.zoff = idx->zoff;
+	const uint64_t zs = idx->zoff / BT2X_SIDE_CHARS, zc = idx->zoff % BT2X_SIDE_CHARS;
+	c->ix.zbyte = zs * BT2X_SIDE_BYTES + (zc >> 2);          // Ebwt::postReadInit
+	c->ix.zbp = (int32_t)(zc & 3);
+	for(int k = 0; k < 5; k++) c->ix.fchr[k] = idx->fchr[k];
+	c->ix.ftab_chars = idx->ftab_chars;
+	bt2x_scoring s;
+	if(sc) s = *sc; else bt2x_scoring_default(&s);
+	c->sc = to_dev(s);
+	HIPCHK(hipMalloc((void**)&c->d_stats, 16 * sizeof(unsigned long long)));
+	HIPCHK(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
+	HIPCHK(hipMalloc((void**)&c->d_counters, 16 * sizeof(uint32_t)));
+	hipDeviceProp_t prop;
+	HIPCHK(hipGetDeviceProperties(&prop, device));
+	// one 64-lane wave per workgroup, LDS-bound to 4 per CU (40 KiB each)
+	c->nslots = (uint32_t)prop.multiProcessorCount * 4;
+	*out = c.release();
+	return BT2X_OK;
+}
+
+extern "C" void bt2x_close(bt2x_ctx* c) {
+	if(!c) return;
+	(void)hipSetDevice(c->device);
+	(void)hipStreamSynchronize(c->stream);
+	for(DevBuf* b : {&c->b_reads, &c->b_quals, &c->b_refs, &c->b_in, &c->b_out, &c->b_recs,
+	                 &c->b_edits, &c->b_dbg_dig, &c->b_dbg_cand, &c->scratch}) b->release();
+	(void)hipFree(c->d_ebwt); (void)hipFree(c->d_ftab); (void)hipFree(c->d_eftab);
+	(void)hipFree(c->d_stats); (void)hipFree(c->d_counters);
+	for(int k = 0; k < BT2X_K_COUNT; k++) { (void)hipEventDestroy(c->ev[k][0]); (void)hipEventDestroy(c->ev[k][1]); }
+	(void)hipStreamDestroy(c->stream);
+	delete c;
+}
+
+extern "C" double bt2x_last_kernel_ms(const bt2x_ctx* c, int k) {
+	if(!c || k < 0 || k >= BT2X_K_COUNT || !c->ev_valid[k]) return -1.0;
+	float ms = -1.0f;
+	if(hipEventSynchronize(c->ev[k][1]) != hipSuccess) return -1.0;
+	if(hipEventElapsedTime(&ms, c->ev[k][0], c->ev[k][1]) != hipSuccess) return -1.0;
+	return (double)ms;
+}
+
+extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) {
+	if(!c || !out || k < 0 || k >= BT2X_K_COUNT) return BT2X_E_ARG;
+	unsigned long long st[16];
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(hipMemcpy(st, c->d_stats, sizeof st, hipMemcpyDeviceToHost));
+	std::memset(out, 0, sizeof(*out));
+	if(k == BT2X_K_SEED) {
+		out->n_bilf = st[0]; out->n_lf1 = st[1]; out->n_ftab = st[2];
+		out->n_problems = c->n_seed_last;
+		out->alg_bytes = 128 * (2 * out->n_bilf + out->n_lf1) + 16 * out->n_ftab;
+	} else {
+		out->dp_cells = st[4]; out->dp_cols = st[5]; out->bt_cells = st[6];
+		out->n_problems = c->n_dp_last;
+		// traceback byte per cell written + reference window + read codes/quals
+		out->alg_bytes = out->dp_cells + out->dp_cols;
+	}
+	return BT2X_OK;
+}
+
+// ------------------------------------------------------------- seed search
+extern "C" int bt2x_seed_search_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt2x_seed_in* d_in,
+                                    uint32_t n, int do_extend, bt2x_seed_out* d_out, void* stream) {
+	if(!c) return BT2X_E_ARG;
+	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipMemsetAsync(c->d_stats, 0, 3 * sizeof(unsigned long long), s));
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][0], s));
+	int rc = bt2x_launch_seed(c->ix, d_reads, d_in, n, do_extend, d_out, c->d_stats, s);
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][1], s));
+	c->ev_valid[BT2X_K_SEED] = true;
+	c->n_seed_last = n;
+	return rc;
+}
+
+extern "C" int bt2x_seed_search(bt2x_ctx* c, const uint8_t* reads, uint64_t reads_bytes,
+                                const bt2x_seed_in* in, uint32_t n, int do_extend, bt2x_seed_out* out) {
+	if(!c || (n && (!reads || !in || !out))) return BT2X_E_ARG;
+	if(n == 0) return BT2X_OK;
+	for(uint32_t i = 0; i < n; i++)
+		if(in[i].seed_len < 1 || in[i].seed_len > 32 || in[i].read_off + in[i].seed_off + in[i].seed_len > reads_bytes)
+			return BT2X_E_ARG;
+	HIPCHK(hipSetDevice(c->device));
+	int rc;
+	if((rc = c->b_reads.ensure(reads_bytes)) || (rc = c->b_in.ensure(sizeof(bt2x_seed_in) * n)) ||
+	   (rc = c->b_out.ensure(sizeof(bt2x_seed_out) * n))) return rc;
+	HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->b_in.p, in, sizeof(bt2x_seed_in) * n, hipMemcpyHostToDevice, c->stream));
+	rc = bt2x_seed_search_dev(c, (const uint8_t*)c->b_reads.p, (const bt2x_seed_in*)c->b_in.p, n,
+	                          do_extend, (bt2x_seed_out*)c->b_out.p, c->stream);
+	if(rc) return rc;
+	HIPCHK(hipMemcpyAsync(out, c->b_out.p, sizeof(bt2x_seed_out) * n, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return BT2X_OK;
+}
+
+// ---------------------------------------------------------------------- DP
+static int ensure_scratch(bt2x_ctx* c) {
+	return c->scratch.ensure(bt2x_dp_slot_bytes() * c->nslots);
+}
+
+extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint8_t* d_quals,
+                                 const uint8_t* d_refs, const bt2x_dp_in* d_in, uint32_t n,
+                                 bt2x_dp_out* d_out, bt2x_aln_rec* d_recs, uint32_t rec_cap,
+                                 uint32_t* d_edits, uint32_t edit_cap, uint32_t* d_counters,
+                                 bt2x_dp_debug* d_debug, void* stream) {
+	if(!c || !d_counters) return BT2X_E_ARG;
+	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+	HIPCHK(hipSetDevice(c->device));
+	int rc = ensure_scratch(c);
+	if(rc) return rc;
+	HIPCHK(hipMemsetAsync(d_counters, 0, 2 * sizeof(uint32_t), s));
+	HIPCHK(hipMemsetAsync(c->d_stats + 4, 0, 3 * sizeof(unsigned long long), s));
+	DpLaunch a{};
+	a.reads = d_reads; a.quals = d_quals; a.refs = d_refs; a.in = d_in; a.n = n; a.out = d_out;
+	a.recs = d_recs; a.rec_cap = rec_cap; a.edits = d_edits; a.edit_cap = edit_cap;
+	a.counters = d_counters; a.stats = c->d_stats + 4;
+	a.digests = d_debug ? d_debug->digests : nullptr;
+	a.cands = d_debug ? d_debug->cands : nullptr;
+	a.scratch = (uint8_t*)c->scratch.p; a.nslots = c->nslots;
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
+	rc = bt2x_launch_dp(c->sc, a, s);
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));
+	c->ev_valid[BT2X_K_DP] = true;
+	c->n_dp_last = n;
+	return rc;
+}
+
+extern "C" int bt2x_dp_align(bt2x_ctx* c,
+                             const uint8_t* reads, uint64_t reads_bytes,
+                             const uint8_t* quals, uint64_t quals_bytes,
+                             const uint8_t* refs, uint64_t refs_bytes,
+                             const bt2x_dp_in* in, uint32_t n,
+                             bt2x_dp_out* out,
+                             bt2x_aln_rec* recs, uint32_t rec_cap, uint32_t* nrec_used,
+                             uint32_t* edits, uint32_t edit_cap, uint32_t* nedit_used,
+                             bt2x_dp_debug* debug) {
+	if(!c || (n && (!reads || !quals || !refs || !in || !out))) return BT2X_E_ARG;
+	if(nrec_used) *nrec_used = 0;
+	if(nedit_used) *nedit_used = 0;
+	if(n == 0) return BT2X_OK;
+	// shape checks: the kernel trusts these (reference limits)
+	for(uint32_t i = 0; i < n; i++) {
+		const bt2x_dp_in& p = in[i];
+		if(p.rdlen < 1 || p.rdlen > BT2X_MAX_ROWS || p.ncol < 1 || p.ncol + 1 > BT2X_MAX_COLS ||
+		   p.read_off + p.rdlen > reads_bytes || p.qual_off + p.rdlen > quals_bytes ||
+		   p.ref_off + p.ncol > refs_bytes || p.minsc < -254 || p.minsc > 0)
+			return BT2X_E_ARG;
+	}
+	HIPCHK(hipSetDevice(c->device));
+	int rc;
+	if((rc = c->b_reads.ensure(reads_bytes)) || (rc = c->b_quals.ensure(quals_bytes)) ||
+	   (rc = c->b_refs.ensure(refs_bytes)) || (rc = c->b_in.ensure(sizeof(bt2x_dp_in) * n)) ||
+	   (rc = c->b_out.ensure(sizeof(bt2x_dp_out) * n)) ||
+	   (rc = c->b_recs.ensure(sizeof(bt2x_aln_rec) * (size_t)(rec_cap ? rec_cap : 1))) ||
+	   (rc = c->b_edits.ensure(sizeof(uint32_t) * (size_t)(edit_cap ? edit_cap : 1)))) return rc;
+	bt2x_dp_debug dd{nullptr, nullptr};
+	if(debug && debug->digests) {
+		if((rc = c->b_dbg_dig.ensure(sizeof(uint64_t) * 3 * n))) return rc;
+		dd.digests = (uint64_t*)c->b_dbg_dig.p;
+	}
+	if(debug && debug->cands) {
+		if((rc = c->b_dbg_cand.ensure(sizeof(uint32_t) * BT2X_MAX_COLS * n))) return rc;
+		dd.cands = (uint32_t*)c->b_dbg_cand.p;
+	}
+	HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->b_quals.p, quals, quals_bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->b_refs.p, refs, refs_bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->b_in.p, in, sizeof(bt2x_dp_in) * n, hipMemcpyHostToDevice, c->stream));
+	rc = bt2x_dp_align_dev(c, (const uint8_t*)c->b_reads.p, (const uint8_t*)c->b_quals.p,
+	                       (const uint8_t*)c->b_refs.p, (const bt2x_dp_in*)c->b_in.p, n,
+	                       (bt2x_dp_out*)c->b_out.p, (bt2x_aln_rec*)c->b_recs.p, rec_cap,
+	                       (uint32_t*)c->b_edits.p, edit_cap, c->d_counters,
+	                       (dd.digests || dd.cands) ? &dd : nullptr, c->stream);
+	if(rc) return rc;
+	uint32_t used[2] = {0, 0};
+	HIPCHK(hipMemcpyAsync(used, c->d_counters, sizeof used, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipMemcpyAsync(out, c->b_out.p, sizeof(bt2x_dp_out) * n, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if(nrec_used) *nrec_used = used[0];
+	if(nedit_used) *nedit_used = used[1];
+	if(used[0] > rec_cap || used[1] > edit_cap) return BT2X_E_OVERFLOW;
+	if(used[0]) HIPCHK(hipMemcpy(recs, c->b_recs.p, sizeof(bt2x_aln_rec) * used[0], hipMemcpyDeviceToHost));
+	if(used[1]) HIPCHK(hipMemcpy(edits, c->b_edits.p, sizeof(uint32_t) * used[1], hipMemcpyDeviceToHost));
+	if(dd.digests) HIPCHK(hipMemcpy(debug->digests, dd.digests, sizeof(uint64_t) * 3 * n, hipMemcpyDeviceToHost));
+	if(dd.cands) HIPCHK(hipMemcpy(debug->cands, dd.cands, sizeof(uint32_t) * BT2X_MAX_COLS * n, hipMemcpyDeviceToHost));
+	return BT2X_OK;
+}
+
+// Struct sizes, so bindings can check their mirrors of bt2x.h.
+extern "C" int bt2x_abi_sizes(uint32_t* out, int n) {
+	const uint32_t s[] = {(uint32_t)sizeof(bt2x_seed_in), (uint32_t)sizeof(bt2x_seed_out),
+	                      (uint32_t)sizeof(bt2x_dp_in), (uint32_t)sizeof(bt2x_dp_out),
+	                      (uint32_t)sizeof(bt2x_aln_rec), (uint32_t)sizeof(bt2x_scoring),
+	                      (uint32_t)sizeof(bt2x_index_desc), (uint32_t)sizeof(bt2x_counters)};
+	const int m = (int)(sizeof s / sizeof s[0]);
+	for(int i = 0; i < n && i < m; i++) out[i] = s[i];
+	return m;
+}

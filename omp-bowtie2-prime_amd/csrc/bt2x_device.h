@@ -1,0 +1,49 @@
+// bt2x_device.h — device-side types shared by the gfx950 kernels and the host API.
+//
+// MI355X layout of the FM index (SURVEY §3.4, bt2_idx.h:2617-2639): the .bt2l side
+// array is uploaded verbatim (128-byte sides, 128-byte aligned in HBM, so one side is
+// exactly one L2 line), ftab/eftab/fchr as-is.  Nothing is re-packed: the reference's
+// own layout is already one cache line per LF step.
+#pragma once
+#include <stdint.h>
+#include "../../include/bt2x.h"
+
+struct DevIndex {
+	const uint8_t* ebwt;      // numSides * 128 bytes
+	const uint64_t* ftab;     // 4^ftabChars + 1
+	const uint64_t* eftab;    // 2 * ftabChars
+	uint64_t len;             // joined text length
+	uint64_t zoff;            // '$' row
+	uint64_t zbyte;           // byte offset of '$' in ebwt (Ebwt::postReadInit, bt2_idx.h:1684)
+	uint64_t fchr[5];
+	int32_t zbp;              // bit-pair of '$' within zbyte
+	int32_t ftab_chars;
+};
+
+struct DevScoring {
+	int32_t rdo, rde, rfo, rfe;   // read/ref gap open (const+linear) and extend (linear)
+	int32_t gapbar;
+	int32_t npen;                 // constant N penalty (COST_MODEL_CONSTANT)
+	uint8_t mmpen[256];           // mismatch penalty by (qual-33), COST_MODEL_QUAL
+};
+
+// Launch helpers implemented in the kernel translation units.
+int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
+                     uint32_t n, int do_extend, bt2x_seed_out* d_out,
+                     unsigned long long* d_ctr, void* stream);
+
+struct DpLaunch {
+	const uint8_t* reads; const uint8_t* quals; const uint8_t* refs;
+	const bt2x_dp_in* in; uint32_t n;
+	bt2x_dp_out* out;
+	bt2x_aln_rec* recs; uint32_t rec_cap;
+	uint32_t* edits; uint32_t edit_cap;
+	uint32_t* counters;            // [0] recs used, [1] edits used, [2..] stats (u32 pairs)
+	unsigned long long* stats;     // dp_cells, dp_cols, bt_cells
+	uint64_t* digests;             // optional, 3 per problem
+	uint32_t* cands;               // optional, BT2X_MAX_COLS per problem
+	uint8_t* scratch;              // per resident wave: BT2X_DP_SCRATCH_PER_LANE * 64
+	uint32_t nslots;               // resident wave slots backed by scratch
+};
+#define BT2X_DP_SCRATCH_PER_LANE (32768u + 8192u)
+int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream);

@@ -260,9 +260,10 @@ static int cmdDp(int argc, char** argv) {
 			std::string win;
 			for(size_t i = 0; i < swa.rflen_; i++) win += DNA[firsts5[(int)swa.rf_[i]]];
 			uint32_t rseed = jrnd.nextU32();
-			fprintf(fo, "P %zu %zu %d %s %s %s %lld %lld %zu %zu %zu %lld %d %u\n", nprob, myidx, (int)fw,
+			fprintf(fo, "P %zu %zu %d %s %s %s %lld %lld %zu %zu %zu %lld %d %u %lld %ld %lld\n", nprob, myidx, (int)fw,
 			        r.seq.c_str(), r.qual.c_str(), win.c_str(), (long long)rect.refl, (long long)rect.refr,
-			        (size_t)rect.triml, (size_t)rect.corel, (size_t)rect.corer, (long long)minsc, nceil, rseed);
+			        (size_t)rect.triml, (size_t)rect.corel, (size_t)rect.corer, (long long)minsc, nceil, rseed,
+			        (long long)refoff, tidx, (long long)tlen);
 			nprob++;
 			TAlScore best = std::numeric_limits<TAlScore>::min();
 			bool ok = swa.align(best);

@@ -120,6 +120,7 @@ class DpCase:
                            "win": t[6].encode(), "refl": int(t[7]), "refr": int(t[8]),
                            "triml": int(t[9]), "corel": int(t[10]), "corer": int(t[11]),
                            "minsc": int(t[12]), "nceil": int(t[13]), "rseed": int(t[14]),
+                           "refoff": int(t[15]), "tidx": int(t[16]), "tlen": int(t[17]),
                            "cands": [], "calls": []}
                     probs.append(cur)
                 elif t[0] == "A":

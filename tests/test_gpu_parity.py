@@ -1,0 +1,131 @@
+"""Parity of the gfx950 kernels (through the C-ABI, libbt2x.so) with the reference's
+golden vectors and with the CPU oracle.  Integer/byte/index work: bit-exact."""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io as g
+import oracle_lib as ol
+from bt2x import abi, framing, lib
+
+pytestmark = pytest.mark.gpu
+
+SEED_SETS = [("lambda_virus", "lambda_longreads.fq.xz", "seeds_lambda.txt.xz"),
+             ("rep", "rep_reads.fq.xz", "seeds_rep.txt.xz")]
+DP_SETS = ["dp_rep.txt.xz", "dp_rep_dpad12.txt.xz", "dp_rep_alt.txt.xz"]
+
+
+@pytest.fixture(scope="module")
+def ctxs(golden_dir):
+    out = {}
+    for name in ("lambda_virus", "rep"):
+        base = g.materialize_index(name, str(golden_dir))
+        idx = lib.Index(base)
+        out[name] = (lib.Context(idx), ol.OracleIndex(base))
+    return out
+
+
+@pytest.mark.parametrize("name,fq,gold", SEED_SETS)
+def test_seed_kernel_matches_reference_golden(ctxs, name, fq, gold):
+    ctx, _ = ctxs[name]
+    case = g.SeedCase(os.path.join(g.GOLDEN, fq), os.path.join(g.GOLDEN, gold))
+    out = ctx.seed_search(case.reads, case.inp, do_extend=True)
+    np.testing.assert_array_equal(out["need_reporting"], case.exp_rep)
+    np.testing.assert_array_equal(out["topf"], case.exp_topf)
+    np.testing.assert_array_equal(out["botf"], case.exp_botf)
+    np.testing.assert_array_equal(out["nlex"], case.exp_nlex)
+    ms = ctx.last_kernel_ms(abi.K_SEED)
+    assert ms > 0
+    c = ctx.last_counters(abi.K_SEED)
+    _, oc = ol.seed_search(ctxs[name][1], case.reads, case.inp)
+    assert (c["n_bilf"], c["n_lf1"], c["n_ftab"]) == (oc["n_bilf"], oc["n_lf1"], oc["n_ftab"])
+
+
+def test_seed_kernel_without_extension(ctxs):
+    ctx, oidx = ctxs["rep"]
+    case = g.SeedCase(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), os.path.join(g.GOLDEN, "seeds_rep.txt.xz"))
+    out = ctx.seed_search(case.reads, case.inp, do_extend=False)
+    exp, _ = ol.seed_search(oidx, case.reads, case.inp, do_extend=False)
+    np.testing.assert_array_equal(out, exp)
+    assert (out["nlex"] == 0).all()
+
+
+def scoring_pair(path):
+    kv = g.dp_header_scoring(path)
+    return lib.default_scoring(**kv), kv
+
+
+@pytest.mark.parametrize("gold", DP_SETS)
+def test_dp_kernel_matches_reference_golden(ctxs, gold):
+    path = os.path.join(g.GOLDEN, gold)
+    case = g.DpCase(path)
+    sc, kv = scoring_pair(path)
+    ctx = lib.Context(ctxs["rep"][0].index, scoring=sc)
+    out, recs, edits, dig, cands = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=True)
+    bad = g.compare_dp(case, out, recs, edits, dig, cands)
+    assert not bad, "\n".join(bad)
+    c = ctx.last_counters(abi.K_DP)
+    assert c["dp_cells"] == int((case.inp["rdlen"].astype(np.int64) * case.inp["ncol"]).sum())
+    ctx.close()
+
+
+def test_dp_kernel_matches_oracle_at_scale(ctxs):
+    """40k framed problems on the repeat-rich genome, incl. shifted diagonals, N-rich reads
+    and both strands: HIP vs the C oracle, every output field."""
+    import lzma
+    import simdata as sd
+    with lzma.open(os.path.join(g.GOLDEN, "rep.fa.xz"), "rb") as f:
+        tmp = f.read()
+    chroms, cur, name = [], [], None
+    for line in tmp.split(b"\n"):
+        if line.startswith(b">"):
+            if name is not None:
+                chroms.append((name, b"".join(cur)))
+            name, cur = line[1:].decode(), []
+        elif line:
+            cur.append(line)
+    chroms.append((name, b"".join(cur)))
+    ref = [g.codes(s) for _, s in chroms]
+    reads = (sd.sim_reads(chroms, 16000, 100, seed=101) + sd.sim_reads(chroms, 8000, 139, seed=102)
+             + sd.sim_reads(chroms, 4000, 60, seed=103, n_rate=0.05, sub_rate=0.05)
+             + sd.sim_reads(chroms, 4000, 30, seed=104))
+    rng = np.random.default_rng(5)
+    tidx, off, fw, rc, qc = [], [], [], [], []
+    for nm, s, q in reads:
+        _, c, o, f = nm.split(":")
+        shift = int(rng.choice([0, 0, 1, -1, 3, -7, 15]))
+        tidx.append(int(c)); off.append(int(o) + shift); fw.append(bool(int(f)) ^ (rng.random() < 0.1))
+        rc.append(g.codes(s)); qc.append(np.frombuffer(q, np.uint8))
+    # framing takes the read as sequenced; for rc-strand reads the oriented read is patRc
+    rd, qu, rf, dp, keep = framing.build_dp_batch(ref, tidx, off, fw, rc, qc)
+    assert keep.sum() > 30000
+    ctx = ctxs["rep"][0]
+    out, recs, edits, dig, cands = ctx.dp_align(rd, qu, rf, dp, debug=True)
+    sc = ol.default_scoring()
+    eo, erecs, eedits, edig, ecands, _ = ol.dp_align(sc, rd, qu, rf, dp)
+    np.testing.assert_array_equal(out[["status", "best", "ncand", "nrec"]], eo[["status", "best", "ncand", "nrec"]])
+    np.testing.assert_array_equal(dig, edig)
+    np.testing.assert_array_equal(cands, ecands)
+    # records: compare per problem (arena order differs)
+    for i in np.nonzero(out["nrec"])[0]:
+        a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
+        b = erecs[eo["rec_off"][i]: eo["rec_off"][i] + eo["nrec"][i]]
+        fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff"]
+        assert (a[fields] == b[fields]).all(), i
+        for ra, rb in zip(a, b):
+            np.testing.assert_array_equal(edits[ra["edit_off"]: ra["edit_off"] + ra["nedit"]],
+                                          eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
+    assert (out["status"] == 1).sum() > 20000
+
+
+def test_dp_rejects_shapes_outside_reference_limits(ctxs):
+    ctx = ctxs["rep"][0]
+    dp = np.zeros(1, dtype=abi.DP_IN)
+    dp["rdlen"], dp["ncol"], dp["minsc"] = 161, 100, -60           # > ALN_MAX_ROWS
+    z = np.zeros(400, np.uint8)
+    with pytest.raises(lib.Bt2xError):
+        ctx.dp_align(z, z + 40, z, dp)
+    dp["rdlen"], dp["ncol"] = 100, 200                               # ncol+1 > ALN_MAX_COLS
+    with pytest.raises(lib.Bt2xError):
+        ctx.dp_align(z, z + 40, z, dp)
