@@ -155,37 +155,39 @@ seed_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* 
 		}
 		int nlex = 0;
 		if(report && do_extend) {
+			// extend() works on copies; the seed's own range is reported unchanged
+			uint64_t etop = top, ebot = bot;
 			// MultiSeedAligner::extend: walk left over read[seed_off-1 .. 0]
 			const int lim = p.seed_off;
 			for(int ii = 0; ii < lim; ii++) {
 				const int rdc = seq[-1 - ii];
-				if(bot - top > 1) {
+				if(ebot - etop > 1) {
 					n_bilf++;
 					uint64_t t[4], b[4];
-					load_side(ix, top, st);
-					load_side(ix, bot, sb);
+					load_side(ix, etop, st);
+					load_side(ix, ebot, sb);
 					count_all(ix, st, t);
 					count_all(ix, sb, b);
 					int nonz = -1; bool abort_ = false;
-					const uint64_t orig = bot - top;
+					const uint64_t orig = ebot - etop;
 #pragma unroll
 					for(int j = 0; j < 4; j++) {
 						if(!abort_ && b[j] > t[j]) {
 							if(nonz >= 0) abort_ = true;
-							else { nonz = j; top = t[j]; bot = b[j]; }
+							else { nonz = j; etop = t[j]; ebot = b[j]; }
 						}
 					}
-					if(abort_ || (nonz != rdc && rdc <= 3) || bot - top < orig) break;
+					if(abort_ || (nonz != rdc && rdc <= 3) || ebot - etop < orig) break;
 				} else {
 					n_lf1++;
 					int c = -1;
-					if(top != ix.zoff) {
-						load_side(ix, top, st);
+					if(etop != ix.zoff) {
+						load_side(ix, etop, st);
 						c = row_l(st);
-						top = count_one(ix, st, c);
+						etop = count_one(ix, st, c);
 					}
 					if(c != rdc && rdc <= 3) break;
-					bot = top + 1;
+					ebot = etop + 1;
 				}
 				if(++nlex == 255) break;
 			}
