@@ -102,3 +102,45 @@ def build_dp_batch(ref_codes: list[np.ndarray], tidx, off, fw, read_codes: list[
         pr += len(c); pq += len(q); pf += len(w)
     cat = lambda parts: np.ascontiguousarray(np.concatenate(parts)) if parts else np.zeros(1, np.uint8)
     return cat(rd_parts), cat(q_parts), cat(rf_parts), dp, keep
+
+
+def build_dp_batch_fixed(genome: np.ndarray, chrom_starts: np.ndarray, chrom_lens: np.ndarray,
+                         chrom, off, fw, reads: np.ndarray, quals: np.ndarray,
+                         maxhalf: int = 15, ref_stride: int = abi.MAX_COLS):
+    """Vectorised build_dp_batch for equal-length reads over a concatenated genome.
+    Oriented reads/quals are laid out with stride rdlen, windows with stride ref_stride.
+    Returns (reads_buf, quals_buf, refs_buf, dp_in, keep)."""
+    n, R = reads.shape
+    chrom = np.asarray(chrom, dtype=np.int64)
+    fw = np.asarray(fw, dtype=bool)
+    minsc = min_score(np.full(n, R))
+    nceil = n_ceil(np.full(n, R))
+    rect = frame_rect(off, np.full(n, R), chrom_lens[chrom], max_read_gaps(minsc, R),
+                      max_ref_gaps(minsc, R), maxhalf)
+    ncol = rect["refr"] - rect["refl"] + 1
+    keep = rect["found"] & (R <= abi.MAX_ROWS) & (ncol + 1 <= abi.MAX_COLS)
+    idx = np.nonzero(keep)[0]
+    m = len(idx)
+    rc = np.where(reads < 4, 3 - reads, 4).astype(np.uint8)[:, ::-1]
+    ord_reads = np.where(fw[:, None], reads, rc)[idx]
+    ord_quals = np.where(fw[:, None], quals, quals[:, ::-1])[idx]
+    gstart = chrom_starts[chrom[idx]] + rect["refl"][idx]
+    cols = np.arange(ref_stride)[None, :]
+    gi = np.minimum(gstart[:, None] + cols, len(genome) - 1)
+    win = np.where(cols < ncol[idx][:, None], genome[gi], 4).astype(np.uint8)
+    dp = np.zeros(m, dtype=abi.DP_IN)
+    k = np.arange(m, dtype=np.int64)
+    dp["read_off"] = k * R
+    dp["qual_off"] = k * R
+    dp["ref_off"] = k * ref_stride
+    dp["refl"] = rect["refl"][idx]
+    dp["rdlen"] = R
+    dp["ncol"] = ncol[idx]
+    dp["minsc"] = minsc[idx]
+    dp["nceil"] = nceil[idx]
+    dp["triml"] = rect["triml"][idx]
+    dp["corel"] = rect["corel"][idx]
+    dp["corer"] = rect["corer"][idx]
+    dp["fw"] = fw[idx].astype(np.uint8)
+    return (np.ascontiguousarray(ord_reads).reshape(-1), np.ascontiguousarray(ord_quals).reshape(-1),
+            np.ascontiguousarray(win).reshape(-1), dp, keep)

@@ -14,6 +14,7 @@
 #include "bt2x_device.h"
 
 size_t bt2x_dp_slot_bytes();
+int bt2x_dp_blocks_per_cu();
 
 #define HIPCHK(x) do { if((x) != hipSuccess) return BT2X_E_NODEVICE; } while(0)
 
@@ -188,8 +189,8 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	HIPCHK(hipMalloc((void**)&c->d_counters, 16 * sizeof(uint32_t)));
 	hipDeviceProp_t prop;
 	HIPCHK(hipGetDeviceProperties(&prop, device));
-	// one 64-lane wave per workgroup, LDS-bound to 4 per CU (40 KiB each)
-	c->nslots = (uint32_t)prop.multiProcessorCount * 4;
+	// one 64-lane wave per workgroup; as many as are co-resident (register-bound)
+	c->nslots = (uint32_t)prop.multiProcessorCount * (uint32_t)bt2x_dp_blocks_per_cu();
 	*out = c.release();
 	return BT2X_OK;
 }
@@ -295,6 +296,7 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	a.digests = d_debug ? d_debug->digests : nullptr;
 	a.cands = d_debug ? d_debug->cands : nullptr;
 	a.scratch = (uint8_t*)c->scratch.p; a.nslots = c->nslots;
+	{ const char* ab = getenv("BT2X_DP_ABLATE"); a.ablate = (ab && *ab == '1') ? 1u : 0u; }
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));

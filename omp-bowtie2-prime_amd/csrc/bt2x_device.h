@@ -44,6 +44,7 @@ struct DpLaunch {
 	uint32_t* cands;               // optional, BT2X_MAX_COLS per problem
 	uint8_t* scratch;              // per resident wave: BT2X_DP_SCRATCH_PER_LANE * 64
 	uint32_t nslots;               // resident wave slots backed by scratch
+	uint32_t ablate;               // profiling only: 1 = stop after the fill (outputs invalid)
 };
 #define BT2X_DP_SCRATCH_PER_LANE (32768u + 8192u)
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream);

@@ -72,10 +72,23 @@ struct BtResult {
 	int score, ns, gaps, nedit, bases, refns, off;
 };
 
+__device__ __forceinline__ int wave_max(int v) {
+	for(int d = 32; d > 0; d >>= 1) { const int o = __shfl_xor(v, d); v = v > o ? v : o; }
+	return v;
+}
+
+// Per-row info byte kept in LDS during the fill: read code (3 bits), gap-barrier flag
+// (bit 3), mismatch penalty for the row's quality (bits 4-7; Scoring::mmpens <= 15).
+__device__ __forceinline__ uint32_t row_info(int rdc, bool gbar, int mm) {
+	return (uint32_t)rdc | (gbar ? 8u : 0u) | ((uint32_t)mm << 4);
+}
+
 template<bool kDebug>
 __global__ void __launch_bounds__(64)
 dp_kernel(DevScoring sc, DpLaunch a) {
-	__shared__ uint32_t rowst[kRows * 64];       // per row: H | E<<8 | rdc<<16 | mmpen<<24
+	// LDS, reused: during the fill the row-info bytes (4 rows per dword), afterwards the
+	// last DP row (4 columns per dword) for candidate enumeration.  12.8 KiB per wave.
+	__shared__ uint32_t lds[(kCols / 4) * 64];
 	const int lane = threadIdx.x;
 	uint8_t* slot = a.scratch + (size_t)blockIdx.x * kSlotBytes;
 	uint32_t* dir = reinterpret_cast<uint32_t*>(slot + kDirOff);
@@ -83,72 +96,122 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 	uint32_t* stage_ed = reinterpret_cast<uint32_t*>(slot + kEditOff);
 	bt2x_aln_rec* stage_rec = reinterpret_cast<bt2x_aln_rec*>(slot + kRecOff);
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0;
+	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 
 	for(uint32_t chunk = blockIdx.x; (uint64_t)chunk * 64 < a.n; chunk += gridDim.x) {
 		const uint32_t pi = chunk * 64 + lane;
-		if(pi >= a.n) continue;
-		const bt2x_dp_in p = a.in[pi];
+		const bool active = pi < a.n;
+		bt2x_dp_in p;
+		if(active) p = a.in[pi];
+		else { p.read_off = p.qual_off = p.ref_off = 0; p.refl = 0; p.rdlen = 0; p.ncol = 0;
+		       p.minsc = 0; p.nceil = 0; p.triml = p.corel = p.corer = 0; p.fw = 1; p.pad = 0; }
 		const int R = p.rdlen, C = p.ncol;
+		const int Rmax = wave_max(R), Cmax = wave_max(C);
 		const uint8_t* rd = a.reads + p.read_off;
 		const uint8_t* qu = a.quals + p.qual_off;
 		const uint8_t* rf = a.refs + p.ref_off;
 		const int thr = (int)p.minsc + 0xff;
-		for(int i = 0; i < R; i++) {
-			const int rdc = rd[i];
-			int q = (int)qu[i] - 33;
-			q = q < 0 ? 0 : (q > 255 ? 255 : q);
-			rowst[i * 64 + lane] = ((uint32_t)rdc << 16) | ((uint32_t)sc.mmpen[q] << 24);
+		// ------------- row info (rows >= R: N, barred, no penalty) ----------------
+		// 4 rows per dword, held in VGPRs for the whole fill (constant per problem)
+		uint32_t Info[kRowWords];
+#pragma unroll
+		for(int blk = 0; blk < kRowWords; blk++) {
+			uint32_t w = row_info(4, true, 0) * 0x01010101u;
+			if(blk * 4 < Rmax) {
+				w = 0;
+#pragma unroll
+				for(int r = 0; r < 4; r++) {
+					const int i = blk * 4 + r;
+					uint32_t b = row_info(4, true, 0);
+					if(i < R) {
+						int q = (int)qu[i] - 33;
+						q = q < 0 ? 0 : (q > 255 ? 255 : q);
+						const bool gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
+						b = row_info(rd[i], gbar, sc.mmpen[q]);
+					}
+					w |= b << (8 * r);
+				}
+			}
+			Info[blk] = w;
 		}
+		// ------------- fill: column-major, per-row state in VGPRs --------------
+		// H and E of the previous column, 4 rows per dword (40 dwords each for 160 rows).
+		uint32_t Hs[kRowWords], Es[kRowWords];
+#pragma unroll
+		for(int b = 0; b < kRowWords; b++) { Hs[b] = 0; Es[b] = 0; }
 		uint64_t dg0 = 0, dg1 = 0, dg2 = 0;
 		int lrmax = 0, ncand = 0;
-		// ---------------- fill: column-major exact recurrence ----------------
-		for(int j = 0; j < C; j++) {
-			const int refc = rf[j];
-			int hdiag = 0xff;           // H[-1][j-1] = 0xff: alignment may start anywhere
-			int hup = 0, fup = 0, h = 0;
-			uint32_t dword = 0;
-			for(int i = 0; i < R; i++) {
-				const uint32_t w = rowst[i * 64 + lane];
-				const int hl = (int)(w & 0xff), el = (int)((w >> 8) & 0xff);
-				const int rdc = (int)((w >> 16) & 0xff), mm = (int)(w >> 24);
-				const bool gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
-				const int e = imax(sat(el - sc.rde), gbar ? 0 : sat(hl - sc.rdo));
-				const int f = (i == 0 || gbar) ? 0 : imax(sat(fup - sc.rfe), sat(hup - sc.rfo));
-				const int pen = (rdc > 3 || refc > 3) ? sc.npen : (rdc == refc ? 0 : mm);
-				const int d = (i == 0) ? 0xff : hdiag;
-				h = imax(sat(d - pen), imax(e, f));
-				uint32_t tb = 0;
-				if(i > 0) {
-					const bool ga = !gbar;
-					int hd = H_NONE;
-					if(j > 0 && hdiag - pen == h) hd = H_DIAG;
-					else if(ga && hup - sc.rfo == h) hd = H_REF_OPEN;
-					else if(ga && fup - sc.rfe == h) hd = H_RFGAP_EXT;
-					else if(ga && j > 0 && hl - sc.rdo == h) hd = H_READ_OPEN;
-					else if(ga && j > 0 && el - sc.rde == h) hd = H_RDGAP_EXT;
-					int ed = 0;
-					if(j > 0) ed = (hl - sc.rdo == e) ? 1 : ((el - sc.rde == e) ? 2 : 0);
-					const int fd = (hup - sc.rfo == f) ? 1 : ((fup - sc.rfe == f) ? 2 : 0);
-					tb = (uint32_t)hd | ((uint32_t)ed << 3) | ((uint32_t)fd << 5);
+		const int lastblk = (R - 1) >> 2, lastsh = 8 * ((R - 1) & 3);
+		int refn = (C > 0) ? rf[0] : 4;
+		for(int j = 0; j < Cmax; j++) {
+			const int refc = refn;
+			if(j + 1 < C) refn = rf[j + 1];            // prefetch next column's base
+			const bool colok = j < C;
+			const bool refamb = refc > 3;
+			int hdiag = 0xff, hup = 0, fup = 0;        // H[-1][j-1] = 0xff: start anywhere
+			uint32_t lrw = 0;
+#pragma unroll
+			for(int blk = 0; blk < kRowWords; blk++) {
+				if(blk * 4 < Rmax) {                     // wave-uniform
+				uint32_t info = Info[blk];
+				asm volatile("" : "+v"(info));      // keep the per-row fields from being hoisted (VGPR blow-up)
+				const uint32_t hw = Hs[blk], ew = Es[blk];
+				uint32_t nh = 0, ne = 0, tbw = 0;
+#pragma unroll
+				for(int r = 0; r < 4; r++) {
+					const int i = blk * 4 + r;
+					const int hl = (int)((hw >> (8 * r)) & 0xffu);
+					const int el = (int)((ew >> (8 * r)) & 0xffu);
+					const uint32_t inf = (info >> (8 * r)) & 0xffu;
+					const int rdc = (int)(inf & 7u);
+					const bool gb = (inf & 8u) != 0;
+					const int mm = (int)(inf >> 4);
+					const int pen = (refamb || rdc > 3) ? npen : (rdc == refc ? 0 : mm);
+					// E[i][j] = max(E[i][j-1] - rde, H[i][j-1] - rdo (barred rows: none)), >= 0
+					const int hl_o = hl - rdo, el_e = el - rde;
+					const int e = imax(imax(el_e, gb ? 0 : hl_o), 0);
+					// F[i][j] = max(F[i-1][j] - rfe, H[i-1][j] - rfo), barred rows 0, row 0 = 0
+					const int hu_o = hup - rfo, fu_e = fup - rfe;
+					const int f = (i == 0 || gb) ? 0 : imax(imax(hu_o, fu_e), 0);
+					const int d = ((i == 0) ? 0xff : hdiag) - pen;
+					const int h = imax(imax(d, e), f);
+					uint32_t tb = 0;
+					if(i > 0) {
+						// Traceback choice of backtraceNucleotidesEnd2EndSseU8 for each cell type.
+						// Exact for every cell a backtrace can reach (value >= 1).
+						// branch-free: 0/1 flags combined arithmetically
+						const uint32_t f_open = hu_o == f, f_ext = (fu_e == f) & !f_open;
+						const uint32_t e_open = hl_o == e, e_ext = (el_e == e) & !e_open;
+						const uint32_t fd = f_open | (f_ext << 1), ed = e_open | (e_ext << 1);
+						const uint32_t isd = d == h;
+						const uint32_t isf = (f == h) & !isd;
+						const uint32_t ise = (e == h) & !isd & !isf;
+						const uint32_t hd = isd | (isf * (fd + 1)) | (ise * (ed + 3));
+						tb = hd | (ed << 3) | (fd << 5);
+					}
+					if(kDebug && a.digests && colok && i < R) {
+						dg0 += cell_digest(i, j, 0, e);
+						dg1 += cell_digest(i, j, 1, f);
+						dg2 += cell_digest(i, j, 2, h);
+					}
+					nh |= (uint32_t)h << (8 * r);
+					ne |= (uint32_t)e << (8 * r);
+					tbw |= tb << (8 * r);
+					hdiag = hl; hup = h; fup = f;
 				}
-				dword |= tb << (8 * (i & 3));
-				if((i & 3) == 3 || i == R - 1) {
-					dir[((size_t)j * kRowWords + (i >> 2)) * 64 + lane] = dword;
-					dword = 0;
+				Hs[blk] = nh; Es[blk] = ne;
+				lrw = (blk == lastblk) ? nh : lrw;
+				if(colok) dir[((size_t)j * kRowWords + blk) * 64 + lane] = tbw;
 				}
-				if(kDebug && a.digests) {
-					dg0 += cell_digest(i, j, 0, e);
-					dg1 += cell_digest(i, j, 1, f);
-					dg2 += cell_digest(i, j, 2, h);
-				}
-				rowst[i * 64 + lane] = (w & 0xffff0000u) | (uint32_t)h | ((uint32_t)e << 8);
-				hdiag = hl;
-				hup = h; fup = f;
 			}
-			lastrow[(size_t)j * 64 + lane] = (uint8_t)h;
-			lrmax = imax(lrmax, h);
-			ncand += (h >= thr);
+			if(colok) {
+				const int lr = (int)((lrw >> lastsh) & 0xffu);
+				lastrow[(size_t)j * 64 + lane] = (uint8_t)lr;
+				lrmax = imax(lrmax, lr);
+				ncand += (lr >= thr);
+			}
 		}
+		if(!active || a.ablate) continue;
 		st_cells += (unsigned long long)R * C;
 		st_cols += C;
 		if(kDebug && a.digests) {
@@ -169,11 +232,16 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 		o.status = ncand > 0 ? 1 : 0; o.best = score; o.ncand = (uint16_t)ncand;
 		// ------------- nextAlignment() sequence until done() -----------------
 		// move the last row into LDS (the row state is no longer needed)
-		uint8_t* lr8 = reinterpret_cast<uint8_t*>(rowst);
-		for(int j = 0; j < C; j++) lr8[(j >> 2) * 256 + lane * 4 + (j & 3)] = lastrow[(size_t)j * 64 + lane];
+		for(int q = 0; q < (C + 3) >> 2; q++) {
+			uint32_t w4 = 0;
+			for(int r = 0; r < 4; r++) {
+				const int j = q * 4 + r;
+				if(j < C) w4 |= (uint32_t)lastrow[(size_t)j * 64 + lane] << (8 * r);
+			}
+			lds[q * 64 + lane] = w4;
+		}
 		int cur_key = 0x7fffffff, ndone = 0, nrec = 0;
 		const int row0 = R - 1;
-		const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 		while(ndone < ncand) {
 			int ntries = 0;
 			bool found = false;
@@ -181,11 +249,18 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 			res.nedit = 0;
 			while(ndone < ncand) {
 				// next candidate in DpBtCandidate order: largest key = score*256+col below cur_key
+				// (4 columns per LDS dword; columns >= C hold 0 and never qualify)
 				int best = -1;
-				for(int j = 0; j < C; j++) {
-					const int s = lr8[(j >> 2) * 256 + lane * 4 + (j & 3)];
-					const int key = s * 256 + j;
-					if(s >= thr && key < cur_key && key > best) best = key;
+				const int nw = (C + 3) >> 2;
+#pragma unroll 2
+				for(int q = 0; q < nw; q++) {
+					const uint32_t w4 = lds[q * 64 + lane];
+#pragma unroll
+					for(int r = 0; r < 4; r++) {
+						const int s = (int)((w4 >> (8 * r)) & 0xffu);
+						const int key = s * 256 + q * 4 + r;
+						best = (s >= thr && key < cur_key && key > best) ? key : best;
+					}
 				}
 				if(best < 0) { ndone = ncand; break; }   // unreachable: ncand counted above
 				cur_key = best;
@@ -203,12 +278,16 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 				int row = row0, col = col0, ct = 2 /*H*/, bscore = 0, ns = 0, gaps = 0, ne = 0;
 				bool over_core = false, ok = true;
 				int trimBeg = 0;
+				// One dependent load round trip per step: the next cell's traceback byte and
+				// its read/ref/quality bytes are issued before this cell's stores (the mark
+				// byte and the staged edit), so the in-order vmcnt never waits on a store.
+				const uint8_t* dir8 = reinterpret_cast<const uint8_t*>(dir);
+				uint8_t* dirw8 = reinterpret_cast<uint8_t*>(dir);
+				size_t bi = (((size_t)col * kRowWords + (row >> 2)) * 64 + lane) * 4 + (row & 3);
+				uint32_t tb = dir8[bi];
+				int rdc = rd[row], refc = rf[col], qch = qu[row];
 				while(true) {
 					st_bt++;
-					const size_t wi = ((size_t)col * kRowWords + (row >> 2)) * 64 + lane;
-					uint32_t w = dir[wi];
-					const int sh = 8 * (row & 3);
-					const uint32_t tb = (w >> sh) & 0xffu;
 					if(tb & 0x80u) { ok = false; break; }          // reportedThrough
 					int move = H_NONE;
 					bool empty = false;
@@ -218,43 +297,53 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 						else { const int fd = (int)((tb >> 5) & 3u); move = fd == 1 ? H_REF_OPEN : fd == 2 ? H_RFGAP_EXT : H_NONE; }
 						empty = (move == H_NONE);
 					}
-					dir[wi] = w | (0x80u << sh);                   // setReportedThrough
 					const int diag = col - row + (int)p.triml;
 					if(diag >= 0 && diag >= (int)p.corel && diag <= (int)p.corer) over_core = true;
-					if(empty || row == 0) { trimBeg = row; break; }
-					const int rdc = rd[row];
+					const size_t cur_bi = bi;
+					const uint32_t cur_tb = tb;
+					if(empty || row == 0) {
+						dirw8[cur_bi] = (uint8_t)(cur_tb | 0x80u);  // setReportedThrough
+						trimBeg = row;
+						break;
+					}
+					const int crow = row, ccol = col, crdc = rdc, crefc = refc, cq = qch;
+					// next cell
+					if(move == H_DIAG) { row--; col--; ct = 2; }
+					else if(move == H_REF_OPEN || move == H_RFGAP_EXT) { row--; ct = (move == H_REF_OPEN) ? 2 : 1; }
+					else { col--; ct = (move == H_READ_OPEN) ? 2 : 0; }
+					bi = (((size_t)col * kRowWords + (row >> 2)) * 64 + lane) * 4 + (row & 3);
+					tb = dir8[bi];
+					rdc = rd[row]; refc = rf[col]; qch = qu[row];
+					// stores for the cell just left
+					dirw8[cur_bi] = (uint8_t)(cur_tb | 0x80u);      // setReportedThrough
 					if(move == H_DIAG) {
-						const int refc = rf[col];
-						const bool amb = rdc > 3 || refc > 3;
-						if(amb || rdc != refc) {
-							const int q0 = (int)qu[row] - 33;
+						const bool amb = crdc > 3 || crefc > 3;
+						if(amb || crdc != crefc) {
+							const int q0 = cq - 33;
 							const int q = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
-							stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
+							stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(crefc), acgtn(crdc));
 							ne++;
 							bscore -= amb ? sc.npen : (int)sc.mmpen[q];
 						}
 						if(amb) ns++;
-						row--; col--; ct = 2;
 					} else if(move == H_REF_OPEN || move == H_RFGAP_EXT) {
-						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)row, EDIT_REF_GAP, '-', acgtn(rdc));
+						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(crdc));
 						ne++;
 						bscore -= (move == H_REF_OPEN) ? rfo : rfe;
-						ct = (move == H_REF_OPEN) ? 2 : 1;
-						row--; gaps++;
+						gaps++;
 					} else {
-						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)row + 1, EDIT_READ_GAP, mask_chr(rf[col]), '-');
+						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(crefc), '-');
 						ne++;
 						bscore -= (move == H_READ_OPEN) ? rdo : rde;
-						ct = (move == H_READ_OPEN) ? 2 : 0;
-						col--; gaps++;
+						gaps++;
 					}
+					(void)ccol;
 				}
 				if(!ok || !over_core) continue;
 				{
-					const int rdc = rd[row], refc = rf[col];
 					const bool amb = rdc > 3 || refc > 3;
 					if(amb || rdc != refc) {
-						const int q0 = (int)qu[row] - 33;
+						const int q0 = qch - 33;
 						const int q = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
 						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
 						ne++;
@@ -326,6 +415,14 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 } // namespace
 
 size_t bt2x_dp_slot_bytes() { return kSlotBytes; }
+
+// Resident 64-lane workgroups per CU for the DP kernel (VGPR/LDS-limited), so the
+// persistent grid fills the chip exactly once.
+int bt2x_dp_blocks_per_cu() {
+	int nb = 0;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dp_kernel<false>, 64, 0) != hipSuccess || nb < 1) nb = 4;
+	return nb;
+}
 
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream) {
 	if(a.n == 0) return 0;

@@ -18,7 +18,8 @@
 namespace {
 
 struct Side {
-	uint64_t w[16];          // 12 words of packed BWT (384 chars) + occ[A,C,G,T]
+	uint64_t w[12];          // 12 words of packed BWT (384 chars); constant indices only
+	uint64_t o0, o1, o2, o3; // occ[A,C,G,T] at the side start (named: selected, not indexed)
 	uint64_t byte_off;       // side byte offset in ebwt
 	int charoff;             // row % 384
 };
@@ -29,11 +30,16 @@ __device__ __forceinline__ void load_side(const DevIndex& ix, uint64_t row, Side
 	s.byte_off = side * BT2X_SIDE_BYTES;
 	const uint4* p = reinterpret_cast<const uint4*>(ix.ebwt + s.byte_off);
 #pragma unroll
-	for(int k = 0; k < 8; k++) {
+	for(int k = 0; k < 6; k++) {
 		uint4 v = p[k];
 		s.w[2 * k] = ((uint64_t)v.y << 32) | v.x;
 		s.w[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
 	}
+	const uint4 v6 = p[6], v7 = p[7];
+	s.o0 = ((uint64_t)v6.y << 32) | v6.x;
+	s.o1 = ((uint64_t)v6.w << 32) | v6.z;
+	s.o2 = ((uint64_t)v7.y << 32) | v7.x;
+	s.o3 = ((uint64_t)v7.w << 32) | v7.z;
 }
 
 // Bit-pair matches of character c in word w, on the low bit of each pair (countInU64,
@@ -64,7 +70,12 @@ __device__ __forceinline__ uint64_t count_one(const DevIndex& ix, const Side& s,
 #pragma unroll
 	for(int k = 0; k < 12; k++) cnt += __popcll(match_c(s.w[k], c) & prefix_mask(s.charoff, k));
 	if(c == 0 && dollar_before(ix, s)) cnt--;
-	return s.w[12 + c] + cnt + ix.fchr[c];
+	// mask-select (a ?: chain gets folded into an indexed, i.e. scratch, load)
+	const uint64_t m0 = 0ULL - (uint64_t)(c == 0), m1 = 0ULL - (uint64_t)(c == 1);
+	const uint64_t m2 = 0ULL - (uint64_t)(c == 2), m3 = 0ULL - (uint64_t)(c == 3);
+	const uint64_t occ = (s.o0 & m0) | (s.o1 & m1) | (s.o2 & m2) | (s.o3 & m3);
+	const uint64_t fc = (ix.fchr[0] & m0) | (ix.fchr[1] & m1) | (ix.fchr[2] & m2) | (ix.fchr[3] & m3);
+	return occ + cnt + fc;
 }
 
 // Ebwt::countBt2SideEx (bt2_idx.h:1940-1972)
@@ -79,14 +90,22 @@ __device__ __forceinline__ void count_all(const DevIndex& ix, const Side& s, uin
 		t += __popcll(match_c(w, 3) & m);
 	}
 	if(dollar_before(ix, s)) a--;
-	o[0] = s.w[12] + a + ix.fchr[0];
-	o[1] = s.w[13] + cc + ix.fchr[1];
-	o[2] = s.w[14] + g + ix.fchr[2];
-	o[3] = s.w[15] + t + ix.fchr[3];
+	o[0] = s.o0 + a + ix.fchr[0];
+	o[1] = s.o1 + cc + ix.fchr[1];
+	o[2] = s.o2 + g + ix.fchr[2];
+	o[3] = s.o3 + t + ix.fchr[3];
 }
 
 __device__ __forceinline__ int row_l(const Side& s) {
-	return (int)((s.w[s.charoff >> 5] >> (2 * (s.charoff & 31))) & 3);
+	// select the word without a dynamic register index (that would spill Side to scratch)
+	const int k = s.charoff >> 5, sh = 2 * (s.charoff & 31);
+	int c = 0;
+#pragma unroll
+	for(int q = 0; q < 12; q++) {
+		const int cq = (int)((s.w[q] >> sh) & 3);   // computed per word, then selected
+		c = (q == k) ? cq : c;
+	}
+	return c;
 }
 
 __device__ __forceinline__ uint64_t ftab_hi(const DevIndex& ix, uint64_t i) {

@@ -149,3 +149,57 @@ def read_fastq(path: str) -> list[tuple[str, bytes, bytes]]:
             q = f.readline().strip()
             out.append((h.strip()[1:].decode(), s, q))
     return out
+
+
+def sim_reads_fixed(genome_codes: np.ndarray, chrom_starts: np.ndarray, n: int, rdlen: int,
+                    seed: int, sub_rate: float = 0.01, indel_frac: float = 0.10,
+                    rc_frac: float = 0.5, qmin: int = 2, qmax: int = 40, n_rate: float = 0.001):
+    """Vectorised fixed-length read simulator over a concatenated genome (codes 0-4).
+
+    Same error model as sim_reads; origins avoid N and chromosome boundaries.
+    Returns (reads (n, rdlen) u8 codes as sequenced, quals (n, rdlen) u8 Phred+33,
+    chrom (n,), off (n,) leftmost 0-based offset within the chromosome, fw (n,) bool)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    G = len(genome_codes)
+    ends = np.append(chrom_starts[1:], G)
+    over = int(n * 1.3) + 64
+    out_pos = np.empty(0, dtype=np.int64)
+    isn = (genome_codes > 3).astype(np.int32)
+    csum = np.concatenate([[0], np.cumsum(isn)])
+    while len(out_pos) < n:
+        p = rng.integers(0, G - rdlen - 2, size=over)
+        c = np.searchsorted(chrom_starts, p, side="right") - 1
+        ok = (p + rdlen + 1 < ends[c]) & (csum[p + rdlen + 1] - csum[p] == 0)
+        out_pos = np.concatenate([out_pos, p[ok]])
+    p = out_pos[:n]
+    chrom = np.searchsorted(chrom_starts, p, side="right") - 1
+    j = np.arange(rdlen)[None, :]
+    idx = np.broadcast_to(p[:, None] + j, (n, rdlen)).copy()
+    indel = rng.random(n) < indel_frac
+    k = rng.integers(10, rdlen - 10, size=n)[:, None]
+    dele = indel & (rng.random(n) < 0.5)
+    ins = indel & ~dele
+    idx = np.where(dele[:, None] & (j >= k), idx + 1, idx)
+    idx = np.where(ins[:, None] & (j > k), idx - 1, idx)
+    reads = genome_codes[idx].astype(np.uint8)
+    insmask = ins[:, None] & (j == k)
+    reads = np.where(insmask, rng.integers(0, 4, size=(n, rdlen)).astype(np.uint8), reads)
+    sub = rng.random((n, rdlen)) < sub_rate
+    reads = np.where(sub, rng.integers(0, 4, size=(n, rdlen)).astype(np.uint8), reads)
+    reads = np.where(rng.random((n, rdlen)) < n_rate, np.uint8(4), reads)
+    fw = rng.random(n) >= rc_frac
+    rc = np.where(reads < 4, 3 - reads, 4).astype(np.uint8)[:, ::-1]
+    reads = np.where(fw[:, None], reads, rc)
+    quals = (rng.integers(qmin, qmax + 1, size=(n, rdlen)) + 33).astype(np.uint8)
+    return np.ascontiguousarray(reads), quals, chrom, p - chrom_starts[chrom], fw
+
+
+def concat_genome(chroms):
+    """[(name, ACGTN bytes)] -> (codes u8 concatenated, chrom start offsets)."""
+    lut = np.full(256, 4, dtype=np.uint8)
+    for i, ch in enumerate(b"ACGT"):
+        lut[ch] = i
+        lut[ch + 32] = i
+    parts = [lut[np.frombuffer(s, dtype=np.uint8)] for _, s in chroms]
+    starts = np.cumsum([0] + [len(x) for x in parts[:-1]]).astype(np.int64)
+    return np.concatenate(parts), starts
