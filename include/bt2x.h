@@ -76,6 +76,11 @@ typedef struct {
 int  bt2x_index_load(const char* basename, int load_offs, bt2x_index_desc* out);
 void bt2x_index_free(bt2x_index_desc* idx);
 
+/* Build <outbase>.{1,2,3,4}.bt2l from a FASTA file, byte-identical to the reference's
+ * bowtie2-build-l (bt2_build.cpp / Ebwt::buildToDisk, bt2_idx.h:2922) for lineRate 7.
+ * Host-only (SA-IS suffix sorting); used to index synthetic genomes on the GPU box. */
+int  bt2x_build_index(const char* fasta, const char* outbase, int off_rate, int ftab_chars);
+
 /* ---------------------------------------------------------------- scoring */
 
 /* Scoring scheme (scoring.h:28-132).  Defaults: bt2x_scoring_default(). */

@@ -45,6 +45,7 @@ FUNCS = {
                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                          ctypes.POINTER(abi.DpDebug), ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
+    "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
     "bt2x_abi_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
 }
 
@@ -187,6 +188,13 @@ class Context:
         c = abi.Counters()
         check(load().bt2x_last_counters(self.h, kernel, ctypes.byref(c)), "bt2x_last_counters")
         return c.as_dict()
+
+
+def build_index(fasta: str, outbase: str, off_rate: int = 4, ftab_chars: int = 10) -> str:
+    """Write <outbase>.{1,2,3,4}.bt2l (bt2x_build_index); returns outbase."""
+    check(load().bt2x_build_index(fasta.encode(), outbase.encode(), off_rate, ftab_chars),
+          f"bt2x_build_index({fasta})")
+    return outbase
 
 
 def abi_sizes() -> list[int]:

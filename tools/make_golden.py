@@ -96,6 +96,17 @@ def main() -> None:
             out = os.path.join(tmp, name + ".txt")
             run([HARN, "dp", rep, rfq, out, "1234"] + opts)
             xz_copy(out, os.path.join(GOLD, name + ".txt.xz"))
+        # ---------------- builder known answers: tricky FASTA (empty/all-N/unnamed records,
+        # IUPAC, lowercase, gaps) indexed by the reference builder
+        import hashlib
+        import json
+        tri = os.path.join(GOLD, "tricky.fa")
+        tb = os.path.join(tmp, "tricky")
+        run([BUILD, tri, tb], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        md5 = {k: hashlib.md5(open(f"{tb}.{k}.bt2l", "rb").read()).hexdigest() for k in "1234"}
+        with open(os.path.join(GOLD, "builder_md5.json"), "w") as f:
+            json.dump({"tricky": md5, "_note": "md5 of oracle/_ref/bowtie2-build-l tests/golden/tricky.fa "
+                       "output (tools/make_golden.py)"}, f, indent=1)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     for f in sorted(os.listdir(GOLD)):
