@@ -41,27 +41,61 @@ def parse():
     ap.add_argument("--reads", type=int, default=1 << 20, help="reads per step per GPU")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--dpad", type=int, default=12, help="--dpad (maxhalf); 12 fits 150 bp in ALN_MAX_COLS")
-    ap.add_argument("--genome", default="rep", help="'rep' (fixture) or 'synthetic'")
-    ap.add_argument("--genome-mb", type=float, default=64.0)
+    ap.add_argument("--genome", default="synthetic", help="'synthetic' (default) or 'rep' (fixture)")
+    ap.add_argument("--genome-mb", type=float, default=1000.0)
+    ap.add_argument("--genome-seed", type=int, default=2024)
     ap.add_argument("--cpu-sample", type=int, default=50000, help="reads timed on the CPU oracle")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def load_genome(args, workdir):
+def load_genome(args, workdir, rank=0, dist=None):
+    """-> (chroms, index basename, description).  'synthetic' (default): a seeded
+    genome-scale reference (tools/simdata.gen_genome: 24 chromosomes, interspersed
+    repeat families, low-complexity stretches, N runs) indexed here -- suffix array
+    by prefix doubling on the GPU (tools/gpu_sa.py), files by bt2x_build_index_sa
+    (byte-identical to the reference's bowtie2-build-l, tests/test_builder.py).
+    Index building is setup, outside the timed region."""
     import golden_io as g
     import simdata as sd
     if args.genome == "rep":
         import lzma
         with lzma.open(os.path.join(g.GOLDEN, "rep.fa.xz"), "rb") as f:
             raw = f.read()
-        path = os.path.join(workdir, "rep.fa")
+        path = os.path.join(workdir, f"rep{rank}.fa")
         with open(path, "wb") as f:
             f.write(raw)
         chroms = sd.read_fasta(path)
-        base = g.materialize_index("rep", workdir)
+        base = g.materialize_index("rep", os.path.join(workdir, f"r{rank}"))
         return chroms, base, "rep (300 kbp repeat-rich fixture)"
-    raise SystemExit("only --genome rep is available in this build")
+    if args.genome != "synthetic":
+        raise SystemExit("--genome must be 'synthetic' or 'rep'")
+    import gpu_sa
+    from bt2x import lib
+    total = int(args.genome_mb * 1e6)
+    tag = f"syn{total}_s{args.genome_seed}"
+    base = os.path.join(workdir, tag)
+    fa = base + ".fa"
+    t0 = time.perf_counter()
+    chroms = sd.gen_genome(total, nchrom=24, seed=args.genome_seed)
+    # rank 0 builds (ranks share the node's /tmp); the others wait at the barrier
+    if rank == 0 and not all(os.path.exists(f"{base}.{k}.bt2l") for k in "1234"):
+        sd.write_fasta(fa, chroms)
+        codes, _ = sd.concat_genome(chroms)
+        sa, bwt, keys = gpu_sa.suffix_array(codes[codes < 4], device="cuda")
+        lib.build_index_sa(fa, base + ".tmp", sa, bwt=bwt, keys=keys)
+        for k in "1234":
+            os.replace(f"{base}.tmp.{k}.bt2l", f"{base}.{k}.bt2l")
+        del sa, bwt, keys, codes
+        os.unlink(fa)
+        import torch
+        torch.cuda.empty_cache()
+    if dist:
+        dist.barrier()
+    print(f"# genome {tag}: {total / 1e6:.0f} Mbp, index ready in {time.perf_counter() - t0:.1f} s",
+          file=sys.stderr, flush=True)
+    return chroms, base, f"synthetic {total / 1e6:.0f} Mbp (seed {args.genome_seed}, 24 chromosomes, " \
+                         f"5% repeat families, low-complexity, N runs)"
 
 
 def main():
@@ -79,9 +113,9 @@ def main():
     from bt2x import abi, framing, lib, seeds
     import simdata as sd
 
-    workdir = os.path.join("/tmp", f"bt2x_bench_{os.getuid()}_{rank}")
+    workdir = os.path.join("/tmp", f"bt2x_bench_{os.getuid()}")
     os.makedirs(workdir, exist_ok=True)
-    chroms, base, gdesc = load_genome(args, workdir)
+    chroms, base, gdesc = load_genome(args, workdir, rank, dist)
     genome, starts = sd.concat_genome(chroms)
     lens = np.array([len(s) for _, s in chroms], dtype=np.int64)
 

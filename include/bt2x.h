@@ -81,6 +81,15 @@ void bt2x_index_free(bt2x_index_desc* idx);
  * Host-only (SA-IS suffix sorting); used to index synthetic genomes on the GPU box. */
 int  bt2x_build_index(const char* fasta, const char* outbase, int off_rate, int ftab_chars);
 
+/* Same, with the suffix array of the joined text supplied by the caller (n = joined
+ * length + 1, '$' row last: sa[n-1] == n-1), e.g. sorted on the GPU for genome-scale
+ * synthetic indexes.  Optional per-row gathers computed alongside it (NULL = derive
+ * from the text): bwt[i] = text[sa[i]-1] (any value where sa[i] == 0) and keys[i] =
+ * the ftab_chars-mer at sa[i], 2 bits/char MSB-first (any value for suffixes shorter
+ * than ftab_chars).  Cheap consistency checks only; BT2X_E_ARG if they fail. */
+int  bt2x_build_index_sa(const char* fasta, const char* outbase, int off_rate, int ftab_chars,
+                         const uint64_t* sa, uint64_t n, const uint8_t* bwt, const uint32_t* keys);
+
 /* ---------------------------------------------------------------- scoring */
 
 /* Scoring scheme (scoring.h:28-132).  Defaults: bt2x_scoring_default(). */

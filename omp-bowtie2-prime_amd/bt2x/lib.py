@@ -46,6 +46,9 @@ FUNCS = {
                                          ctypes.POINTER(abi.DpDebug), ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
     "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
+    "bt2x_build_index_sa": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
     "bt2x_abi_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
 }
 
@@ -194,6 +197,26 @@ def build_index(fasta: str, outbase: str, off_rate: int = 4, ftab_chars: int = 1
     """Write <outbase>.{1,2,3,4}.bt2l (bt2x_build_index); returns outbase."""
     check(load().bt2x_build_index(fasta.encode(), outbase.encode(), off_rate, ftab_chars),
           f"bt2x_build_index({fasta})")
+    return outbase
+
+
+def build_index_sa(fasta: str, outbase: str, sa, off_rate: int = 4, ftab_chars: int = 10,
+                   bwt=None, keys=None) -> str:
+    """bt2x_build_index_sa with a caller-sorted suffix array (uint64 numpy array, len+1)
+    and optional per-row gathers bwt (uint8) / keys (uint32)."""
+    import numpy as np
+    sa = np.ascontiguousarray(sa, dtype=np.uint64)
+    if bwt is not None:
+        bwt = np.ascontiguousarray(bwt, dtype=np.uint8)
+        assert len(bwt) == len(sa)
+    if keys is not None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        assert len(keys) == len(sa)
+    check(load().bt2x_build_index_sa(fasta.encode(), outbase.encode(), off_rate, ftab_chars,
+                                     sa.ctypes.data, len(sa),
+                                     None if bwt is None else bwt.ctypes.data,
+                                     None if keys is None else keys.ctypes.data),
+          f"bt2x_build_index_sa({fasta})")
     return outbase
 
 

@@ -203,7 +203,8 @@ bool write_file(const std::string& path, const std::vector<uint8_t>& data) {
 
 } // namespace
 
-extern "C" int bt2x_build_index(const char* fasta, const char* outbase, int off_rate, int ftab_chars) {
+static int build_impl(const char* fasta, const char* outbase, int off_rate, int ftab_chars,
+                      const uint64_t* sa_in, uint64_t sa_n, const uint8_t* bwt_in, const uint32_t* key_in) {
 	if(!fasta || !outbase || off_rate < 0 || off_rate > 16 || ftab_chars < 1 || ftab_chars > 16) return BT2X_E_ARG;
 	Parsed P;
 	if(!parse_fasta(fasta, P)) return BT2X_E_IO;
@@ -223,8 +224,16 @@ extern "C" int bt2x_build_index(const char* fasta, const char* outbase, int off_
 	}
 	// ---------------- suffix array (rows 0..len; '$' sorts last)
 	const uint64_t n = len + 1;
-	std::vector<uint64_t> SA(n);
-	{
+	if(sa_in) {
+		// caller-supplied suffix array (e.g. sorted on the GPU): cheap consistency checks --
+		// '$' row last, entries in range, first characters non-decreasing
+		if(sa_n != n || sa_in[len] != len) return BT2X_E_ARG;
+		if(!bwt_in)
+			for(uint64_t k = 0; k + 1 < len; k++)
+				if(sa_in[k] >= len || P.text[sa_in[k]] > P.text[sa_in[k + 1]]) return BT2X_E_ARG;
+	}
+	std::vector<uint64_t> SA(sa_in ? 0 : n);
+	if(!sa_in) {
 		std::vector<uint8_t> Tc(n);
 		for(uint64_t k = 0; k < len; k++) Tc[k] = (uint8_t)(4 - P.text[k]);   // 3-c, shifted by 1
 		Tc[len] = 0;                                                          // sentinel
@@ -262,12 +271,13 @@ extern "C" int bt2x_build_index(const char* fasta, const char* outbase, int off_
 				int bwtChar = 0;
 				bool count = true;
 				if(si <= len) {
-					const uint64_t saElt = SA[si];
+					const uint64_t saElt = sa_in ? sa_in[si] : SA[si];
 					if(saElt == 0) { bwtChar = 0; count = false; zOff = si; }
-					else { bwtChar = P.text[saElt - 1]; fchr[bwtChar]++; }
+					else { bwtChar = bwt_in ? bwt_in[si] : P.text[saElt - 1]; fchr[bwtChar]++; }
 					if(len - saElt >= (uint64_t)ftab_chars) {
 						uint64_t sufInt = 0;
-						for(int k = 0; k < ftab_chars; k++) sufInt = (sufInt << 2) | P.text[saElt + k];
+						if(key_in) sufInt = key_in[si];
+						else for(int k = 0; k < ftab_chars; k++) sufInt = (sufInt << 2) | P.text[saElt + k];
 						ftab[sufInt + 1]++;
 						if(absorbCnt > 0) { absorb[sufInt] = absorbCnt; absorbCnt = 0; }
 					} else {
@@ -359,4 +369,14 @@ extern "C" int bt2x_build_index(const char* fasta, const char* outbase, int off_
 		if(!write_file(base + ".2.bt2l", o2)) return BT2X_E_IO;
 	}
 	return BT2X_OK;
+}
+
+extern "C" int bt2x_build_index(const char* fasta, const char* outbase, int off_rate, int ftab_chars) {
+	return build_impl(fasta, outbase, off_rate, ftab_chars, nullptr, 0, nullptr, nullptr);
+}
+
+extern "C" int bt2x_build_index_sa(const char* fasta, const char* outbase, int off_rate, int ftab_chars,
+                                   const uint64_t* sa, uint64_t n, const uint8_t* bwt, const uint32_t* keys) {
+	if(!sa || (keys && ftab_chars > 16)) return BT2X_E_ARG;
+	return build_impl(fasta, outbase, off_rate, ftab_chars, sa, n, bwt, keys);
 }

@@ -1,0 +1,74 @@
+"""Suffix array of a joined reference text by prefix doubling on the GPU (torch sorts).
+
+Bench-input tooling, not the measured path: it lets bench.py index a genome-scale
+synthetic reference on the GPU box in seconds, then bt2x_build_index_sa writes the
+.bt2l files from it (byte-identical to bt2x_build_index / the reference's builder,
+tests/test_builder.py).  Order is the reference's: '$' (end of text) sorts after every
+base, so shorter suffixes sort after longer ones that share their prefix
+(Ebwt::buildToDisk's SA, bt2_idx.h:2922).
+
+Round 0 sorts 21-character keys (3 bits/char: A,C,G,T = 0..3, '$' = 4); round k
+sorts (rank[i], rank[i + h]) pairs packed into one int64 (ranks < n+1 <= 2^31), h
+doubling from 21 until every rank is unique.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def suffix_array(codes: np.ndarray, device="cuda", max_rounds: int = 40, ftab_chars: int = 10):
+    """codes: uint8 joined text (values 0..3).  Returns (sa, bwt, keys): uint64 SA of
+    length len+1 plus the per-row gathers bt2x_build_index_sa accepts (bwt[i] =
+    text[sa[i]-1], keys[i] = ftab_chars-mer at sa[i])."""
+    import torch
+    n = len(codes)
+    N = n + 1
+    if N >= (1 << 31):
+        raise ValueError("gpu_sa: text too long for 31-bit ranks")
+    dev = torch.device(device)
+    t = torch.zeros(N + 21, dtype=torch.int64, device=dev)
+    t[:n] = torch.from_numpy(np.ascontiguousarray(codes)).to(dev)
+    t[n] = 4
+    key = torch.zeros(N, dtype=torch.int64, device=dev)
+    for k in range(21):
+        key.bitwise_left_shift_(3).bitwise_or_(t[k:k + N])
+    del t
+    h = 21
+    ar = torch.arange(N, dtype=torch.int64, device=dev)
+    rank = None
+    for _ in range(max_rounds):
+        vals, sa = torch.sort(key)
+        del key
+        head = torch.ones(N, dtype=torch.bool, device=dev)
+        head[1:] = vals[1:] != vals[:-1]
+        del vals
+        done = bool(head.all())
+        gstart = torch.where(head, ar, torch.zeros_like(ar))
+        del head
+        gstart = torch.cummax(gstart, 0).values
+        rank = torch.empty(N, dtype=torch.int64, device=dev)
+        rank[sa] = gstart
+        del gstart
+        if done:
+            del rank
+            return _finish(codes, sa, dev, ftab_chars)
+        del sa
+        key = rank * N
+        key[: N - h] += rank[h:]
+        h *= 2
+    raise RuntimeError("gpu_sa: prefix doubling did not converge")
+
+
+def _finish(codes, sa, dev, ftab_chars):
+    import torch
+    n = len(codes)
+    c = torch.from_numpy(np.ascontiguousarray(codes)).to(dev)
+    bwt = c[(sa - 1).clamp_(min=0)]
+    km = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+    m = n - ftab_chars + 1
+    if m > 0:
+        for k in range(ftab_chars):
+            km[:m].bitwise_left_shift_(2).bitwise_or_(c[k:k + m].to(torch.int32))
+    keys = km[sa]
+    return (sa.cpu().numpy().view(np.uint64), bwt.cpu().numpy(),
+            keys.cpu().numpy().view(np.uint32))
