@@ -37,3 +37,26 @@ def test_builder_record_edge_cases(tmp_path):
     mine = lib.build_index(os.path.join(g.GOLDEN, "tricky.fa"), str(tmp_path / "tricky"))
     for k in "1234":
         assert md5(f"{mine}.{k}.bt2l") == exp[k], k
+
+
+def test_builder_with_supplied_sa(tmp_path):
+    """bench.py's path: prefix-doubling SA (tools/gpu_sa.py, run on the CPU here) +
+    bt2x_build_index_sa -> the same bytes as the reference-built rep index."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(g.HERE), "tools"))
+    import gpu_sa
+    import simdata as sd
+    fa = str(tmp_path / "in.fa")
+    with lzma.open(os.path.join(g.GOLDEN, "rep.fa.xz"), "rb") as fi, open(fa, "wb") as fo:
+        fo.write(fi.read())
+    codes, _ = sd.concat_genome(sd.read_fasta(fa))
+    sa, bwt, keys = gpu_sa.suffix_array(codes[codes < 4], device="cpu")
+    ref = g.materialize_index("rep", str(tmp_path / "ref"))
+    mine = lib.build_index_sa(fa, str(tmp_path / "mine"), sa, bwt=bwt, keys=keys)
+    for k in "1234":
+        assert md5(f"{mine}.{k}.bt2l") == md5(f"{ref}.{k}.bt2l"), k
+    # a corrupted SA is rejected
+    bad = sa.copy()
+    bad[-1] = 0
+    with pytest.raises(lib.Bt2xError):
+        lib.build_index_sa(fa, str(tmp_path / "bad"), bad)
