@@ -44,9 +44,31 @@ def parse():
     ap.add_argument("--genome", default="synthetic", help="'synthetic' (default) or 'rep' (fixture)")
     ap.add_argument("--genome-mb", type=float, default=1000.0)
     ap.add_argument("--genome-seed", type=int, default=2024)
-    ap.add_argument("--cpu-sample", type=int, default=50000, help="reads timed on the CPU oracle")
+    ap.add_argument("--cpu-sample", type=int, default=200000,
+                    help="reads timed on the reference's CPU path (oracle/_ref/refharness bench)")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
+                    help="OpenMP threads for the reference CPU baseline (the box's CPU share)")
+    ap.add_argument("--port-sample", type=int, default=20000, help="reads timed on the 1-thread C port")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
+
+
+def workload_key(args) -> str:
+    g = f"synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}" if args.genome == "synthetic" else args.genome
+    return f"{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}"
+
+
+def pmc_traffic(args, kernel: str):
+    """Per-launch HBM bytes of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>_traffic.json, tools/pmc_traffic.py) taken on this same workload;
+    (None, None) if there is none."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == workload_key(args) and kernel in t.get("kernels", {}):
+            return t["kernels"][kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def load_genome(args, workdir, rank=0, dist=None):
@@ -191,6 +213,7 @@ def main():
     kern = {"seed": (seed_avg, fm_bytes), "dp": (dp_avg, dp_bytes)}
     dom = max(kern, key=lambda k: kern[k][0])
     ach = kern[dom][1] / (kern[dom][0] / 1e3) / 1e9
+    traffic, traffic_src = pmc_traffic(args, dom)
     line = {
         "metric": "M reads/s aligned (150 bp SE vs hg38) at 1/2/4/8 MI355X; % HBM-roofline",
         "value": round(value, 4), "unit": "M reads/s", "n_gpus": world, "steps": args.steps,
@@ -199,9 +222,11 @@ def main():
         "data": "synthetic (seeded genome + simulated 150 bp reads, BASELINE.md error model)",
         "config": {"workload": f"C3 stand-in: {R} bp SE, --dpad {args.dpad}, genome {gdesc}; "
                                f"step = seed search+extend ({nseed} seeds) + DP ({ndp} problems)",
-                   "reads_per_gpu_step": n, "read_len": R, "parallelism": f"dp{world} (read shards)"},
+                   "reads_per_gpu_step": n, "read_len": R, "parallelism": f"dp{world} (read shards)",
+                   "key": workload_key(args)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None},
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "alg_bytes": kern[dom][1], "traffic_src": traffic_src},
         "kernels": {"seed_ms": round(seed_avg, 3), "dp_ms": round(dp_avg, 3),
                     "seed_alg_bytes": fm_bytes, "dp_alg_bytes": dp_bytes,
                     "dp_traceback_bytes": cd["dp_cells"], "counters_seed": cs, "counters_dp": cd},
@@ -209,17 +234,55 @@ def main():
                    "seed_reported_frac": round(float(sout["need_reporting"].mean()), 4)},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(args, sbuf, sin, drd, dqu, drf, dpin, base, n)
+        ref = cpu_baseline_reference(args, reads, quals, chrom, off, fw, base, workdir)
+        port = cpu_baseline_port(args, sbuf, sin, drd, dqu, drf, dpin, base, n)
+        line["cpu_baseline"] = ref if ref is not None else port
+        if ref is not None:
+            line["cpu_port"] = port
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, sbuf, sin, drd, dqu, drf, dpin, base, n):
+def cpu_baseline_reference(args, reads, quals, chrom, off, fw, base, workdir):
+    """The reference's own seed search + DP (oracle/_ref/refharness bench: its
+    MultiSeedAligner::searchAllSeedsDoAll and SwAligner::align/nextAlignment, OpenMP
+    over --cpu-threads host cores) on the first --cpu-sample reads of this batch.
+    None when the reference build did not travel with the snapshot."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "refharness")
+    if not os.access(exe, os.X_OK):
+        return None
+    m = min(args.cpu_sample, len(reads))
+    fq = os.path.join(workdir, "cpu_sample.fq")
+    alpha = np.frombuffer(b"ACGTN", dtype=np.uint8)
+    with open(fq, "wb") as f:
+        seqs, qs = alpha[reads[:m]], quals[:m]
+        for i in range(m):
+            f.write(b"@r%d:%d:%d:%d\n%s\n+\n%s\n" % (i, chrom[i], off[i], int(fw[i]),
+                                                        seqs[i].tobytes(), qs[i].tobytes()))
+    env = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY="ACTIVE")
+    out = subprocess.run([exe, "bench", base, fq, "--dpad", str(args.dpad)], env=env,
+                         capture_output=True, text=True, timeout=900)
+    if out.returncode != 0:
+        print(out.stderr[-2000:], file=sys.stderr)
+        return None
+    kv = dict(t.split("=") for t in out.stdout.split("BENCH", 1)[1].split())
+    dt = float(kv["seed_s"]) + float(kv["dp_s"])
+    return {"value": round(m / dt / 1e6, 6), "unit": "M reads/s", "cores": int(kv["threads"]),
+            "kind": "reference",
+            "sample": f"{m} reads of this batch: {kv['seeds']} seeds searched+extended "
+                      f"({float(kv['seed_s']):.2f} s) + {kv['dp_probs']} DP problems, "
+                      f"{kv['dp_alns']} alignments ({float(kv['dp_s']):.2f} s); reference "
+                      f"searchAllSeedsDoAll + SwAligner (oracle/_ref/refharness bench), "
+                      f"OpenMP {kv['threads']} threads"}
+
+
+def cpu_baseline_port(args, sbuf, sin, drd, dqu, drf, dpin, base, n):
     """The oracle ("port", 1 thread) on a bounded sample of the same workload."""
     import oracle_lib as ol
-    m = min(args.cpu_sample, n)
+    m = min(args.port_sample, n)
     spr = len(sin) / n
     sseeds = sin[: int(round(spr * m))]
     sdp = dpin[: int(round(len(dpin) / n * m))]

@@ -310,6 +310,113 @@ static int cmdDp(int argc, char** argv) {
 	return 0;
 }
 
+
+// -------------------------------------------------------------------- bench
+// CPU baseline for bench.py: the reference's own hot path, OpenMP-parallel the way
+// bt2_search.cpp drives it, over a FASTQ sample whose names carry the true origin.
+//   seeds: batches of 4096 reads -> prepareOneSeed (round 0) -> instantiateSeeds ->
+//          prepareSearchAllSeedsOne -> searchAllSeedsDoAll(extend)   (bt2_search.cpp:2572-2640)
+//   dp:    omp parallel over reads, one SwAligner per thread: frameSeedExtensionRect at
+//          the true origin, initRead, initRef, align, nextAlignment until done
+//          (SwDriver::extendSeeds' per-DP sequence, aligner_sw_driver.cpp:481-538)
+// Only the two compute phases are timed.
+static double nowSec() { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + 1e-9 * t.tv_nsec; }
+
+static int cmdBench(int argc, char** argv) {
+	if(argc < 3) { fprintf(stderr, "bench <idx> <reads.fq> [bt2 opts]\n"); return 2; }
+	std::string idx = argv[1], fq = argv[2];
+	parseRefOptions(idx, fq, argc - 3, argv + 3);
+	Ebwt* ebwt = loadEbwt(idx);
+	BitPairReference ref(idx, false, false, NULL, NULL, false, false, false, false, false, false);
+	if(!ref.loaded()) { fprintf(stderr, "reference not loaded\n"); return 1; }
+	Scoring sc(bonusMatch, penMmcType, penMmcMax, penMmcMin, scoreMin, nCeil, penNType, penN,
+	           penNCatPair, penRdGapConst, penRfGapConst, penRdGapLinear, penRfGapLinear, gGapBarrier);
+	std::vector<Read*> reads; std::vector<long> tids, offs; std::vector<int> fws;
+	{
+		std::ifstream in(fq); Fq r;
+		while(readFq(in, r)) {
+			long tidx, off; int fw;
+			if(!parseOrigin(r.name, tidx, off, fw)) continue;
+			Read* rd = new Read(r.name.c_str(), r.seq.c_str(), r.qual.c_str());
+			if(rd->length() < 2 || rd->length() >= 256) { delete rd; continue; }
+			reads.push_back(rd); tids.push_back(tidx); offs.push_back(off); fws.push_back(fw);
+		}
+	}
+	const size_t n = reads.size();
+	const int nthr = omp_get_max_threads();
+	// ---- seeds
+	const uint32_t B = 4096;
+	MultiSeedResults srs(B, multiseedLen, gNofw, gNorc);
+	MultiSeedAligner als(ebwt, srs);
+	std::vector<const Read*> rds(B);
+	size_t nseeds = 0;
+	double t0 = nowSec();
+	for(size_t b0 = 0; b0 < n; b0 += B) {
+		const uint32_t m = (uint32_t)std::min<size_t>(B, n - b0);
+		srs.clearSeeds();
+		for(uint32_t k = 0; k < B; k++) {
+			const Read* rd = reads[b0 + std::min<uint32_t>(k, m - 1)];
+			rds[k] = rd;
+			if(k < m) {
+				const int interval = std::max((int)msIval.f<int>((double)rd->length()), 1);
+				srs.prepareOneSeed(k, 0, interval, rd);
+			}
+		}
+		srs.instantiateSeeds(rds.data());
+		als.reserveBuffers();
+#pragma omp parallel for schedule(dynamic, 64)
+		for(uint32_t k = 0; k < m; k++) als.prepareSearchAllSeedsOne(k);
+		als.searchAllSeedsDoAll(true);
+		nseeds += als._bufVec_filled;
+	}
+	const double tSeed = nowSec() - t0;
+	// ---- dp
+	size_t nprob = 0, naln = 0;
+	t0 = nowSec();
+#pragma omp parallel reduction(+:nprob,naln)
+	{
+		SwAligner* swa = new SwAligner();
+		DynProgFramer dpframe(!gReportOverhangs);
+#pragma omp for schedule(dynamic, 64)
+		for(size_t i = 0; i < n; i++) {
+			const Read& rd = *reads[i];
+			const size_t rdlen = rd.length();
+			TAlScore minsc = scoreMin.f<TAlScore>((double)rdlen);
+			if(minsc > 0) minsc = 0;
+			if(minsc < -254) minsc = -254;
+			const int nceil = std::min((int)nCeil.f<int>((double)rdlen), (int)rdlen);
+			const int64_t tlen = (int64_t)ebwt->plen()[tids[i]];
+			DPRect rect;
+			if(!dpframe.frameSeedExtensionRect(offs[i], rdlen, tlen, sc.maxReadGaps(minsc, rdlen),
+			                                   sc.maxRefGaps(minsc, rdlen), (size_t)nceil, maxhalf, rect)) continue;
+			const size_t nwindow = offs[i] >= rect.refl ? (size_t)(offs[i] - rect.refl) : 0;
+			size_t nsInLeftShift = 0;
+			swa->reset();
+			if(!swa->initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, rdlen, sc)) continue;
+			if(!swa->initRef(fws[i] != 0, (TRefId)tids[i], rect, ref, tlen, minsc, true, true,
+			                 nwindow, nsInLeftShift)) continue;
+			nprob++;
+			TAlScore best = std::numeric_limits<TAlScore>::min();
+			if(!swa->align(best)) continue;
+			RandomSource rnd; rnd.init((uint32_t)i * 2654435761u + 1);
+			SwResult res;
+			while(!swa->done()) {
+				res.reset();
+				swa->nextAlignment(res, minsc, rnd);
+				if(res.empty()) break;
+				naln++;
+			}
+		}
+		delete swa;
+	}
+	const double tDp = nowSec() - t0;
+	printf("BENCH threads=%d reads=%zu seeds=%zu seed_s=%.6f dp_probs=%zu dp_alns=%zu dp_s=%.6f\n",
+	       nthr, n, nseeds, tSeed, nprob, naln, tDp);
+	for(Read* r : reads) delete r;
+	delete ebwt;
+	return 0;
+}
+
 } // namespace harness
 
 int main(int argc, char** argv) {
@@ -318,6 +425,7 @@ int main(int argc, char** argv) {
 	try {
 		if(cmd == "seeds") return harness::cmdSeeds(argc - 1, argv + 1);
 		if(cmd == "dp") return harness::cmdDp(argc - 1, argv + 1);
+		if(cmd == "bench") return harness::cmdBench(argc - 1, argv + 1);
 	} catch(int e) {
 		fprintf(stderr, "reference threw %d\n", e);
 		return 1;

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 output of tools/profile_r01.sh into committed profile summaries.
+
+Inputs (a gpurun_out/ tree): prof_kt/run_kernel_stats.csv (+ run_kernel_trace.csv),
+prof_fetch/run_counter_collection.csv (--pmc FETCH_SIZE), prof_write/... (WRITE_SIZE).
+Outputs under profiles/: <tag>_kernel_stats.csv (verbatim), <tag>_bt2x_trace.csv (our
+kernels' dispatches), <tag>_pmc.csv (our kernels' counter rows) and <tag>_traffic.json:
+per-launch HBM traffic per kernel, corrected as MI355X_MICROARCH.md prescribes for
+gfx950 (FETCH_SIZE, reported in KiB, counts half the bytes of wide reads -> x2;
+WRITE_SIZE in KiB taken as is).  bench.py reads <tag>_traffic.json for
+roofline.traffic when the workload key matches its own run.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import shutil
+from collections import defaultdict
+
+KERNELS = {"seed": "seed_kernel", "dp": "dp_kernel"}
+
+
+def short(name: str) -> str | None:
+    for k, pat in KERNELS.items():
+        if pat in name:
+            return k
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--src", default="gpurun_out")
+    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--workload", required=True, help="bench.py workload key of the profiled run")
+    ap.add_argument("--cmd", default="python3 bench.py --steps 5 --warmup 2 --no-cpu")
+    a = ap.parse_args()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = os.path.join(root, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(a.src, "prof_kt", "run_kernel_stats.csv"),
+                os.path.join(out, f"{a.tag}_kernel_stats.csv"))
+    dur = defaultdict(list)
+    with open(os.path.join(a.src, "prof_kt", "run_kernel_trace.csv")) as f, \
+            open(os.path.join(out, f"{a.tag}_bt2x_trace.csv"), "w", newline="") as g:
+        rd = csv.DictReader(f)
+        wr = csv.DictWriter(g, fieldnames=rd.fieldnames)
+        wr.writeheader()
+        for r in rd:
+            k = short(r["Kernel_Name"])
+            if k:
+                wr.writerow(r)
+                dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    ctr = defaultdict(lambda: defaultdict(list))
+    rows = []
+    for sub in ("prof_fetch", "prof_write"):
+        p = os.path.join(a.src, sub, "run_counter_collection.csv")
+        with open(p) as f:
+            rd = csv.DictReader(f)
+            for r in rd:
+                k = short(r["Kernel_Name"])
+                if k:
+                    rows.append(r)
+                    ctr[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if rows:
+        with open(os.path.join(out, f"{a.tag}_pmc.csv"), "w", newline="") as g:
+            wr = csv.DictWriter(g, fieldnames=list(rows[0].keys()))
+            wr.writeheader()
+            wr.writerows(rows)
+    res = {"workload": a.workload, "command": a.cmd,
+           "correction": "traffic = 2 x FETCH_SIZE(KiB) x 1024 + WRITE_SIZE(KiB) x 1024 per launch "
+                         "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM section); Infinity-Cache "
+                         "hits are included by the counters",
+           "kernels": {}}
+    for k in KERNELS:
+        f = ctr[k].get("FETCH_SIZE", [])
+        w = ctr[k].get("WRITE_SIZE", [])
+        d = dur.get(k, [])
+        if not f or not w:
+            continue
+        fetch = sum(f) / len(f) * 1024 * 2
+        write = sum(w) / len(w) * 1024
+        res["kernels"][k] = {"fetch_bytes": round(fetch), "write_bytes": round(write),
+                             "traffic_bytes": round(fetch + write), "launches_fetch": len(f),
+                             "launches_write": len(w),
+                             "avg_duration_ms": round(sum(d) / len(d) / 1e6, 4) if d else None}
+    with open(os.path.join(out, f"{a.tag}_traffic.json"), "w") as g:
+        json.dump(res, g, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
