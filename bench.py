@@ -123,9 +123,8 @@ def load_genome(args, workdir, rank=0, dist=None):
 def main():
     args = parse()
     import torch
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from bt2x import dist as bdist
+    rank, world, local = bdist.world()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -143,7 +142,7 @@ def main():
 
     R = args.read_len
     n = args.reads
-    reads, quals, chrom, off, fw = sd.sim_reads_fixed(genome, starts, n, R, seed=3 + 7919 * rank)
+    reads, quals, chrom, off, fw = sd.sim_reads_fixed(genome, starts, n, R, seed=bdist.rank_seed(3, rank))
     # host prep (untimed): seeds and DP problems
     sbuf, sin, _ = seeds.batch_fixed_length(reads)
     drd, dqu, drf, dpin, keep = framing.build_dp_batch_fixed(genome, starts, lens, chrom, off, fw,
@@ -191,9 +190,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = bdist.max_over_ranks(elapsed, dist, dev)
     used = d_cnt[:2].cpu().numpy()
     if used[0] > rec_cap or used[1] > edit_cap:
         raise SystemExit(f"result arena overflow {used} vs {(rec_cap, edit_cap)}")
