@@ -129,3 +129,67 @@ def test_dp_rejects_shapes_outside_reference_limits(ctxs):
     dp["rdlen"], dp["ncol"] = 100, 200                               # ncol+1 > ALN_MAX_COLS
     with pytest.raises(lib.Bt2xError):
         ctx.dp_align(z, z + 40, z, dp)
+
+
+SHIM = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "test_shims")
+
+
+def _golden_records(gold):
+    """Per problem: (P fields, [A line tokens], [N lines]) straight from the golden text."""
+    out = []
+    with g.open_text(os.path.join(g.GOLDEN, gold)) as f:
+        for line in f:
+            t = line.split()
+            if not t:
+                continue
+            if t[0] == "P":
+                out.append((t, None, []))
+            elif t[0] == "A":
+                out[-1] = (out[-1][0], t, out[-1][2])
+            elif t[0] == "N":
+                out[-1][2].append(line.strip())
+    return out
+
+
+@pytest.mark.parametrize("gold,mode,limit", [("dp_rep.txt.xz", "batch", None),
+                                             ("dp_rep_alt.txt.xz", "batch", None),
+                                             ("dp_rep_dpad12.txt.xz", "single", 400)])
+def test_cpp_host_shims_match_golden(golden_dir, tmp_path, gold, mode, limit):
+    """include/bt2x_shims.hpp driven like SwDriver drives SwAligner (initRead, initRef,
+    align, nextAlignment until done, the caller's RandomSource advanced by the shim)
+    reproduces the reference's records line for line."""
+    import subprocess
+    assert os.access(SHIM, os.X_OK), "tests/cpp/test_shims not built (__graft_entry__.build())"
+    recs = _golden_records(gold)[:limit]
+    pf = tmp_path / "probs.txt"
+    with open(pf, "w") as f:
+        for t, _, _ in recs:
+            # fw seq qual win refl refr triml corel corer minsc nceil rseed tlen
+            f.write(" ".join([t[3], t[4], t[5], t[6], t[7], t[8], t[9], t[10], t[11], t[12], t[13],
+                              t[14], t[17]]) + "\n")
+    s = g.dp_header_scoring(os.path.join(g.GOLDEN, gold))
+    args = [str(s[k]) for k in ("gapbar", "mm_max", "mm_min", "n_pen", "rdg_const", "rdg_linear",
+                                "rfg_const", "rfg_linear")]
+    base = g.materialize_index("rep", str(golden_dir))
+    r = subprocess.run([SHIM, base, str(pf), mode] + args, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = {}
+    cur = None
+    for line in r.stdout.splitlines():
+        t = line.split()
+        if t[0] == "P":
+            cur = int(t[1])
+            got[cur] = (None, [])
+        elif t[0] == "A":
+            got[cur] = (t, got[cur][1])
+        elif t[0] == "N":
+            got[cur][1].append(line.strip())
+    assert len(got) == len(recs)
+    ncalls = 0
+    for i, (_, a, ns) in enumerate(recs):
+        ga, gn = got[i]
+        k = 4 if mode == "batch" else 3
+        assert ga[:k] == a[:k], (i, ga, a)
+        assert gn == ns, (i, gn, ns)
+        ncalls += len(ns)
+    assert ncalls > 0
