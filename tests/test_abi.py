@@ -82,3 +82,14 @@ def test_no_cpu_fallback_without_gpu(golden_dir):
     base = g.materialize_index("lambda_virus", str(golden_dir))
     with pytest.raises(lib.Bt2xError):
         lib.Context(lib.Index(base))
+
+
+def test_cpp_shim_binary_links_and_runs_without_gpu_work():
+    """include/bt2x_shims.hpp compiles against bt2x.h and the test binary resolves
+    libbt2x.so (usage path only: no device call)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "test_shims")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.dirname(exe)], check=True, capture_output=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
