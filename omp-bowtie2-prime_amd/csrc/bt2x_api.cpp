@@ -136,6 +136,7 @@ struct bt2x_ctx {
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
 	DevBuf scratch;
 	uint32_t nslots = 0;
+	int ncu = 0;
 	unsigned long long* d_stats = nullptr;     // [0..2] seed, [4..6] dp
 	uint32_t* d_counters = nullptr;
 	uint64_t n_seed_last = 0, n_dp_last = 0;
@@ -190,6 +191,7 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	hipDeviceProp_t prop;
 	HIPCHK(hipGetDeviceProperties(&prop, device));
 	// one 64-lane wave per workgroup; as many as are co-resident (register-bound)
+	c->ncu = prop.multiProcessorCount;
 	c->nslots = (uint32_t)prop.multiProcessorCount * (uint32_t)bt2x_dp_blocks_per_cu();
 	*out = c.release();
 	return BT2X_OK;
@@ -244,7 +246,7 @@ extern "C" int bt2x_seed_search_dev(bt2x_ctx* c, const uint8_t* d_reads, const b
 	HIPCHK(hipSetDevice(c->device));
 	HIPCHK(hipMemsetAsync(c->d_stats, 0, 3 * sizeof(unsigned long long), s));
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][0], s));
-	int rc = bt2x_launch_seed(c->ix, d_reads, d_in, n, do_extend, d_out, c->d_stats, s);
+	int rc = bt2x_launch_seed(c->ix, d_reads, d_in, n, do_extend, d_out, c->d_stats, c->ncu, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][1], s));
 	c->ev_valid[BT2X_K_SEED] = true;
 	c->n_seed_last = n;

@@ -30,7 +30,7 @@ struct DevScoring {
 // Launch helpers implemented in the kernel translation units.
 int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
                      uint32_t n, int do_extend, bt2x_seed_out* d_out,
-                     unsigned long long* d_ctr, void* stream);
+                     unsigned long long* d_ctr, int ncu, void* stream);
 
 struct DpLaunch {
 	const uint8_t* reads; const uint8_t* quals; const uint8_t* refs;

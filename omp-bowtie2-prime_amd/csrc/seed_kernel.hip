@@ -2,13 +2,25 @@
 //
 // Replaces MultiSeedAligner::searchAllSeedsDoAll(doExtend) (aligner_seed.cpp:674-725):
 // searchSeedBi<8> (:820-957, startSearchSeedBi :757-811) then MultiSeedAligner::extend
-// (:603-672) for every reported seed.  The reference interleaves 8 seeds per CPU thread
-// to overlap cache misses; here every lane owns one seed and thousands of waves keep
-// HBM busy, so the dependent LF chain of one seed is hidden by the others.
+// (:603-672) for every reported seed.
 //
-// Per LF step a lane reads the 128-byte side (one L2 line; 8 x dwordx4) that holds the
-// row, counts bit-pairs below the row with 64-bit popcounts and adds the side's occ[]
-// word and fchr[] (Ebwt::countBt2Side / countBt2SideEx, bt2_idx.h:1811-1972).
+// MI355X design: a persistent grid whose lanes are independent work loops.  Each lane
+// owns one seed at a time and advances it by ONE LF step per loop iteration, whether the
+// seed is in its exact search or its left extension; a lane whose seed finishes writes
+// the result and takes the next seed (grid-stride) at once.  So a wave's cost is the
+// mean per-seed LF chain of its 64 lanes' streams, not the maximum, and search and
+// extension share one instruction stream (no divergence between the two phases).
+//
+// Every LF step is the same computation for a range step (mapBiLFEx, bt2_idx.h:2474)
+// and a single-row step (mapLF1, :2511-2542): the occurrence counts of ONE character c
+// at the range's two ends.  For a one-row range [top, top+1) the second count comes from
+// the same side (the match bit at top), and a step that empties the range is exactly the
+// reference's `rowL != c || row == zOff` failure.  Only extension steps over a read N
+// (rdc = 4) need all four characters; they take a rare slow path.
+//
+// A side is 128 B (one L2 line; 96 B of 2-bit BWT + 4 x u64 occ).  The count of c in
+// [0, charOff) of a side (Ebwt::countBt2Side, bt2_idx.h:1811-1846) is computed over its
+// 24 dwords with bit-pair matches + v_bcnt, predicated by dword index, no scratch.
 // Algorithmic bytes per launch = 128*(2*n_mapBiLFEx + n_mapLF1) + 16*n_ftab.
 #include <hip/hip_runtime.h>
 #include "bt2x_device.h"
@@ -18,94 +30,53 @@
 namespace {
 
 struct Side {
-	uint64_t w[12];          // 12 words of packed BWT (384 chars); constant indices only
-	uint64_t o0, o1, o2, o3; // occ[A,C,G,T] at the side start (named: selected, not indexed)
-	uint64_t byte_off;       // side byte offset in ebwt
-	int charoff;             // row % 384
+	uint32_t w[24];          // 96 B of packed BWT, constant indices only
+	uint64_t occ[4];         // occ[A,C,G,T] at the side start
 };
 
-__device__ __forceinline__ void load_side(const DevIndex& ix, uint64_t row, Side& s) {
-	const uint64_t side = row / BT2X_SIDE_CHARS;
-	s.charoff = (int)(row - side * BT2X_SIDE_CHARS);
-	s.byte_off = side * BT2X_SIDE_BYTES;
-	const uint4* p = reinterpret_cast<const uint4*>(ix.ebwt + s.byte_off);
+__device__ __forceinline__ void load_side(const DevIndex& ix, uint64_t side, Side& s) {
+	const uint4* p = reinterpret_cast<const uint4*>(ix.ebwt + side * BT2X_SIDE_BYTES);
 #pragma unroll
 	for(int k = 0; k < 6; k++) {
-		uint4 v = p[k];
-		s.w[2 * k] = ((uint64_t)v.y << 32) | v.x;
-		s.w[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
+		const uint4 v = p[k];
+		s.w[4 * k] = v.x; s.w[4 * k + 1] = v.y; s.w[4 * k + 2] = v.z; s.w[4 * k + 3] = v.w;
 	}
 	const uint4 v6 = p[6], v7 = p[7];
-	s.o0 = ((uint64_t)v6.y << 32) | v6.x;
-	s.o1 = ((uint64_t)v6.w << 32) | v6.z;
-	s.o2 = ((uint64_t)v7.y << 32) | v7.x;
-	s.o3 = ((uint64_t)v7.w << 32) | v7.z;
+	s.occ[0] = ((uint64_t)v6.y << 32) | v6.x;
+	s.occ[1] = ((uint64_t)v6.w << 32) | v6.z;
+	s.occ[2] = ((uint64_t)v7.y << 32) | v7.x;
+	s.occ[3] = ((uint64_t)v7.w << 32) | v7.z;
 }
 
-// Bit-pair matches of character c in word w, on the low bit of each pair (countInU64,
-// bt2_idx.h:519-537).
-__device__ __forceinline__ uint64_t match_c(uint64_t w, int c) {
-	const uint64_t ct = c == 0 ? 0xffffffffffffffffULL : c == 1 ? 0xaaaaaaaaaaaaaaaaULL
-	                  : c == 2 ? 0x5555555555555555ULL : 0ULL;
-	const uint64_t x0 = w ^ ct;
-	return x0 & (x0 >> 1) & 0x5555555555555555ULL;
+// Bit-pair matches of character c in a dword, on the low bit of each pair
+// (countInU64, bt2_idx.h:519-537): pairs equal to c become 00 after xor with c*0x5555.
+__device__ __forceinline__ uint32_t match_c(uint32_t w, uint32_t pat) {
+	const uint32_t x = w ^ pat;
+	return ~(x | (x >> 1)) & 0x55555555u;
 }
 
-__device__ __forceinline__ uint64_t prefix_mask(int charoff, int k) {
-	int m = charoff - 32 * k;
-	m = m < 0 ? 0 : (m > 32 ? 32 : m);
-	return m >= 32 ? 0xffffffffffffffffULL : ((1ULL << (2 * m)) - 1ULL);
+__device__ __forceinline__ uint64_t sel4(const uint64_t v[4], int c) {
+	const uint64_t lo = (c & 1) ? v[1] : v[0];
+	const uint64_t hi = (c & 1) ? v[3] : v[2];
+	return (c & 2) ? hi : lo;
 }
 
-__device__ __forceinline__ bool dollar_before(const DevIndex& ix, const Side& s) {
-	const uint64_t here = s.byte_off + (uint64_t)(s.charoff >> 2);
-	if(s.byte_off <= ix.zbyte && here >= ix.zbyte)
-		return here > ix.zbyte || (here == ix.zbyte && (s.charoff & 3) > ix.zbp);
-	return false;
-}
-
-// Ebwt::countBt2Side (bt2_idx.h:1811-1846)
-__device__ __forceinline__ uint64_t count_one(const DevIndex& ix, const Side& s, int c) {
-	uint64_t cnt = 0;
+// Counts of c in [0, offa) and [0, offb) of one side (offb <= 384; offb = offa + 1 gives
+// the one-row step).  Per dword: prefix length s = clamp(2*off - 32*d, 0, 31) bits, and
+// v_bfe(m, 0, s) keeps the matches below the offset (match bits sit on even positions,
+// so 31 bits cover a full dword).  No lane-mask compares, hence no SGPR pressure.
+__device__ __forceinline__ void count_side(const Side& s, uint32_t c, int offa, int offb,
+                                           uint32_t& ca, uint32_t& cb) {
+	const uint32_t pat = c * 0x55555555u;
+	ca = 0; cb = 0;
 #pragma unroll
-	for(int k = 0; k < 12; k++) cnt += __popcll(match_c(s.w[k], c) & prefix_mask(s.charoff, k));
-	if(c == 0 && dollar_before(ix, s)) cnt--;
-	// mask-select (a ?: chain gets folded into an indexed, i.e. scratch, load)
-	const uint64_t m0 = 0ULL - (uint64_t)(c == 0), m1 = 0ULL - (uint64_t)(c == 1);
-	const uint64_t m2 = 0ULL - (uint64_t)(c == 2), m3 = 0ULL - (uint64_t)(c == 3);
-	const uint64_t occ = (s.o0 & m0) | (s.o1 & m1) | (s.o2 & m2) | (s.o3 & m3);
-	const uint64_t fc = (ix.fchr[0] & m0) | (ix.fchr[1] & m1) | (ix.fchr[2] & m2) | (ix.fchr[3] & m3);
-	return occ + cnt + fc;
-}
-
-// Ebwt::countBt2SideEx (bt2_idx.h:1940-1972)
-__device__ __forceinline__ void count_all(const DevIndex& ix, const Side& s, uint64_t o[4]) {
-	uint64_t a = 0, cc = 0, g = 0, t = 0;
-#pragma unroll
-	for(int k = 0; k < 12; k++) {
-		const uint64_t m = prefix_mask(s.charoff, k), w = s.w[k];
-		a += __popcll(match_c(w, 0) & m);
-		cc += __popcll(match_c(w, 1) & m);
-		g += __popcll(match_c(w, 2) & m);
-		t += __popcll(match_c(w, 3) & m);
+	for(int d = 0; d < 24; d++) {
+		const uint32_t m = match_c(s.w[d], pat);
+		const uint32_t wa = (uint32_t)min(max(2 * offa - 32 * d, 0), 31);
+		const uint32_t wb = (uint32_t)min(max(2 * offb - 32 * d, 0), 31);
+		ca += __popc(__builtin_amdgcn_ubfe(m, 0u, wa));
+		cb += __popc(__builtin_amdgcn_ubfe(m, 0u, wb));
 	}
-	if(dollar_before(ix, s)) a--;
-	o[0] = s.o0 + a + ix.fchr[0];
-	o[1] = s.o1 + cc + ix.fchr[1];
-	o[2] = s.o2 + g + ix.fchr[2];
-	o[3] = s.o3 + t + ix.fchr[3];
-}
-
-__device__ __forceinline__ int row_l(const Side& s) {
-	// select the word without a dynamic register index (that would spill Side to scratch)
-	const int k = s.charoff >> 5, sh = 2 * (s.charoff & 31);
-	int c = 0;
-#pragma unroll
-	for(int q = 0; q < 12; q++) {
-		const int cq = (int)((s.w[q] >> sh) & 3);   // computed per word, then selected
-		c = (q == k) ? cq : c;
-	}
-	return c;
 }
 
 __device__ __forceinline__ uint64_t ftab_hi(const DevIndex& ix, uint64_t i) {
@@ -117,105 +88,138 @@ __device__ __forceinline__ uint64_t ftab_lo(const DevIndex& ix, uint64_t i) {
 	return v <= ix.len ? v : ix.eftab[(v ^ OFF_MASK) * 2];
 }
 
-__global__ void __launch_bounds__(256)
+__device__ __forceinline__ uint64_t fchr_sel(const DevIndex& ix, int c) {
+	return c == 0 ? ix.fchr[0] : c == 1 ? ix.fchr[1] : c == 2 ? ix.fchr[2] : c == 3 ? ix.fchr[3] : ix.fchr[4];
+}
+
+enum { PH_START = 0, PH_SEARCH = 1, PH_EXTEND = 2, PH_EXIT = 3 };
+
+// One LF step of character c (0..3) over the range [ra, rb) (rb = ra + 1 for a single
+// row): the new range [na, nb).  '$' (row zOff, stored as A) is never counted.
+__device__ __forceinline__ void lf_step(const DevIndex& ix, uint64_t ra, uint64_t rb, uint32_t c,
+                                        bool one_row, uint64_t& na, uint64_t& nb) {
+	const uint64_t sa = ra / BT2X_SIDE_CHARS, sb = rb / BT2X_SIDE_CHARS;
+	const int offa = (int)(ra - sa * BT2X_SIDE_CHARS);
+	const bool same = one_row || sb == sa;
+	// a one-row range counts [0, offa+1) of the same side (offa+1 may be 384)
+	const int offb = same ? (int)(rb - sa * BT2X_SIDE_CHARS) : (int)(rb - sb * BT2X_SIDE_CHARS);
+	const uint64_t zs = ix.zoff / BT2X_SIDE_CHARS;
+	const int zo = (int)(ix.zoff - zs * BT2X_SIDE_CHARS);
+	const uint64_t fc = fchr_sel(ix, (int)c);
+	Side s;
+	load_side(ix, sa, s);
+	uint32_t ka, kb;
+	count_side(s, c, offa, same ? offb : offa, ka, kb);
+	// A-count adjustment for '$' (row zOff, stored as A) before the offset in this side
+	// (countBt2Side, bt2_idx.h:1824-1833)
+	const uint32_t dla = (c == 0 && sa == zs && zo < offa) ? 1u : 0u;
+	const uint64_t base = sel4(s.occ, (int)c) + fc;
+	na = base + (ka - dla);
+	if(same) {
+		const uint32_t dlb = (c == 0 && sa == zs && zo < offb) ? 1u : 0u;
+		nb = base + (kb - dlb);
+	} else {
+		Side t;
+		load_side(ix, sb, t);
+		uint32_t kt, kt2;
+		count_side(t, c, offb, offb, kt, kt2);
+		const uint32_t dlb = (c == 0 && sb == zs && zo < offb) ? 1u : 0u;
+		nb = sel4(t.occ, (int)c) + fc + (kt - dlb);
+	}
+}
+
+__global__ void __launch_bounds__(256, 4)
 seed_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* __restrict__ in,
             uint32_t n, int do_extend, bt2x_seed_out* __restrict__ out,
             unsigned long long* __restrict__ ctr) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t stride = gridDim.x * blockDim.x;
+	uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
 	uint32_t n_bilf = 0, n_lf1 = 0, n_ftab = 0;
-	if(i < n) {
-		const bt2x_seed_in p = in[i];
-		const uint8_t* rd = reads + p.read_off;
-		const uint8_t* seq = rd + p.seed_off;
-		const int nsteps = p.seed_len;
-		uint64_t top = 0, bot = 0;
-		int step = 0;
-		bool done = false, report = false;
-		const int off = nsteps - 1;
-		const int fc = ix.ftab_chars;
-		// startSearchSeedBi: ftab jump over the rightmost ftabChars characters
-		if(fc > 1 && fc <= nsteps) {
-			uint64_t fi = 0;
-			for(int k = 0; k < fc; k++) fi = (fi << 2) | (uint64_t)(seq[off - fc + 1 + k] & 3);
-			top = ftab_hi(ix, fi);
-			bot = ftab_lo(ix, fi + 1);
-			n_ftab++;
-			if(bot == top) done = true; else step += fc;
-		} else {
-			const int c = seq[off];
-			top = ix.fchr[c]; bot = ix.fchr[c + 1];
-			if(bot == top) done = true; else step++;
-		}
-		if(!done && step == nsteps) { done = true; report = true; }
-		Side st, sb;
-		while(!done) {
-			const int soff = nsteps - step - 1;
-			step++;
-			const int c = seq[soff];
-			uint64_t tc, bc;
-			if(bot - top > 1) {       // mapBiLFEx: both ends of the range
-				n_bilf++;
-				load_side(ix, top, st);
-				load_side(ix, bot, sb);
-				if(c == 4) break;
-				tc = count_one(ix, st, c);
-				bc = count_one(ix, sb, c);
-			} else {                  // mapLF1(row, l, c)
-				if(c == 4) break;
-				n_lf1++;
-				load_side(ix, top, st);
-				if(row_l(st) != c || top == ix.zoff) break;
-				tc = count_one(ix, st, c);
-				bc = tc + 1;
-			}
-			if(bc == tc) break;
-			top = tc; bot = bc;
-			if(step == nsteps) { report = true; break; }
-		}
-		int nlex = 0;
-		if(report && do_extend) {
-			// extend() works on copies; the seed's own range is reported unchanged
-			uint64_t etop = top, ebot = bot;
-			// MultiSeedAligner::extend: walk left over read[seed_off-1 .. 0]
-			const int lim = p.seed_off;
-			for(int ii = 0; ii < lim; ii++) {
-				const int rdc = seq[-1 - ii];
-				if(ebot - etop > 1) {
-					n_bilf++;
-					uint64_t t[4], b[4];
-					load_side(ix, etop, st);
-					load_side(ix, ebot, sb);
-					count_all(ix, st, t);
-					count_all(ix, sb, b);
-					int nonz = -1; bool abort_ = false;
-					const uint64_t orig = ebot - etop;
-#pragma unroll
-					for(int j = 0; j < 4; j++) {
-						if(!abort_ && b[j] > t[j]) {
-							if(nonz >= 0) abort_ = true;
-							else { nonz = j; etop = t[j]; ebot = b[j]; }
-						}
-					}
-					if(abort_ || (nonz != rdc && rdc <= 3) || ebot - etop < orig) break;
+	int phase = PH_START;
+	const uint8_t* seq = nullptr;
+	int nsteps = 0, step = 0, lim = 0, ii = 0, nlex = 0;
+	uint64_t top = 0, bot = 0, etop = 0, ebot = 0, ntop = 0, nbot = 0;
+	int kk = 0, nz = 0;
+	bool report = false;
+	const int fc = ix.ftab_chars;
+	while(true) {
+		bool fin = false;
+		if(phase == PH_START) {
+			if(idx >= n) {
+				phase = PH_EXIT;
+			} else {
+				const bt2x_seed_in p = in[idx];
+				seq = reads + p.read_off + p.seed_off;
+				nsteps = p.seed_len;
+				lim = do_extend ? p.seed_off : 0;
+				ii = 0; nlex = 0; report = false;
+				const int off = nsteps - 1;
+				// startSearchSeedBi: ftab jump over the rightmost ftabChars characters
+				if(fc > 1 && fc <= nsteps) {
+					uint64_t fi = 0;
+					for(int k = 0; k < fc; k++) fi = (fi << 2) | (uint64_t)(seq[off - fc + 1 + k] & 3);
+					top = ftab_hi(ix, fi);
+					bot = ftab_lo(ix, fi + 1);
+					n_ftab++;
+					step = fc;
 				} else {
-					n_lf1++;
-					int c = -1;
-					if(etop != ix.zoff) {
-						load_side(ix, etop, st);
-						c = row_l(st);
-						etop = count_one(ix, st, c);
-					}
-					if(c != rdc && rdc <= 3) break;
-					ebot = etop + 1;
+					const int c = seq[off];
+					top = fchr_sel(ix, c); bot = fchr_sel(ix, c + 1);
+					step = 1;
 				}
-				if(++nlex == 255) break;
+				if(bot == top) fin = true;
+				else if(step == nsteps) { report = true; fin = lim == 0; phase = PH_EXTEND; etop = top; ebot = bot; }
+				else phase = PH_SEARCH;
+			}
+		} else if(phase != PH_EXIT) {
+			const bool ext = phase == PH_EXTEND;
+			const uint64_t ra = ext ? etop : top, rb = ext ? ebot : bot;
+			const bool one = rb - ra == 1;
+			const int c = ext ? seq[-1 - ii] : seq[nsteps - step - 1];
+			if(kk == 0) { if(one) n_lf1 += (!ext && c == 4) ? 0u : 1u; else n_bilf++; }
+			if(!ext && c == 4) {
+				fin = true;                       // N in the seed: searchSeedBi drops it
+			} else {
+				// extension over a read N visits the four characters in four iterations
+				const bool nslow = c == 4;
+				uint64_t na, nb;
+				lf_step(ix, ra, rb, nslow ? (uint32_t)kk : (uint32_t)c, one, na, nb);
+				if(!ext) {
+					// searchSeedBi: an empty range ends the search unreported
+					if(nb == na) fin = true;
+					else {
+						top = na; bot = nb; step++;
+						if(step == nsteps) { report = true; etop = top; ebot = bot; phase = PH_EXTEND; fin = lim == 0; }
+					}
+				} else if(!nslow) {
+					// extend(): the step survives iff the range keeps its size under rdc
+					if(nb - na != rb - ra) fin = true;
+					else { etop = na; ebot = nb; ii++; nlex++; fin = (nlex == 255) || (ii == lim); }
+				} else {
+					// read N: the unique non-empty character continues, a one-row range
+					// follows rowL and zOff keeps its row (aligner_seed.cpp:636-660)
+					if(nb > na) { nz++; if(nz == 1) { ntop = na; nbot = nb; } }
+					if(++kk == 4) {
+						if(nz == 0) { ntop = ra; nbot = one ? ra + 1 : rb; }
+						else if(one) nbot = ntop + 1;
+						if(nz > 1 || (!one && nbot - ntop < rb - ra)) fin = true;
+						else { etop = ntop; ebot = nbot; ii++; nlex++; fin = (nlex == 255) || (ii == lim); }
+						kk = 0; nz = 0;
+					}
+				}
 			}
 		}
-		bt2x_seed_out o;
-		o.topf = top; o.botf = bot; o.nlex = (uint8_t)nlex; o.need_reporting = report ? 1 : 0;
+		if(fin) {
+			bt2x_seed_out o;
+			o.topf = top; o.botf = bot; o.nlex = (uint8_t)nlex;
+			o.need_reporting = report ? 1 : 0;
 #pragma unroll
-		for(int k = 0; k < 6; k++) o.pad[k] = 0;
-		out[i] = o;
+			for(int k = 0; k < 6; k++) o.pad[k] = 0;
+			out[idx] = o;
+			idx += stride;
+			phase = PH_START;
+		}
+		if(__all(phase == PH_EXIT)) break;
 	}
 	if(ctr) {
 		// wave-level reduction, one atomic per wave per counter
@@ -234,11 +238,24 @@ seed_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* 
 
 } // namespace
 
+// Resident 256-thread blocks per CU for the persistent seed grid.
+static int seed_blocks_per_cu() {
+	static int nb = 0;
+	if(nb == 0) {
+		int v = 0;
+		if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, seed_kernel, 256, 0) != hipSuccess || v < 1) v = 2;
+		nb = v;
+	}
+	return nb;
+}
+
 int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
                      uint32_t n, int do_extend, bt2x_seed_out* d_out,
-                     unsigned long long* d_ctr, void* stream) {
+                     unsigned long long* d_ctr, int ncu, void* stream) {
 	if(n == 0) return 0;
-	const uint32_t blocks = (n + 255) / 256;
+	uint32_t blocks = (uint32_t)(ncu > 0 ? ncu : 256) * (uint32_t)seed_blocks_per_cu();
+	const uint32_t need = (n + 255) / 256;
+	if(blocks > need) blocks = need;
 	hipLaunchKernelGGL(seed_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
 	                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
