@@ -111,6 +111,8 @@ void bt2x_scoring_init(bt2x_scoring* sc);
 
 typedef struct bt2x_ctx bt2x_ctx;
 
+/* sc = NULL: defaults.  Penalties above 15 (--mp MX > 15 or --np > 15) are rejected
+ * with BT2X_E_ARG: the u8 DP kernel packs a row's penalty into 4 bits. */
 int  bt2x_open(int hip_device, const bt2x_index_desc* idx, const bt2x_scoring* sc, bt2x_ctx** out);
 void bt2x_close(bt2x_ctx* ctx);
 /* Last kernel's duration in ms (HIP events on the launching stream), by kernel id. */

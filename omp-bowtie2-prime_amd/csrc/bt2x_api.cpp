@@ -156,6 +156,11 @@ DevScoring to_dev(const bt2x_scoring& s) {
 extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scoring* sc, bt2x_ctx** out) {
 	if(!idx || !out) return BT2X_E_ARG;
 	*out = nullptr;
+	if(sc) {
+		// the u8 DP kernel packs a row's mismatch/N penalty into 4 bits (defaults: <= 6 / 1)
+		for(int i = 0; i < 256; i++) if(sc->mmpens[i] < 0 || sc->mmpens[i] > 15) return BT2X_E_ARG;
+		if(sc->npens[0] < 0 || sc->npens[0] > 15) return BT2X_E_ARG;
+	}
 	int ndev = 0;
 	if(hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return BT2X_E_NODEVICE;
 	std::unique_ptr<bt2x_ctx> c(new bt2x_ctx());

@@ -7,19 +7,23 @@
 // backtraceNucleotidesEnd2EndSseU8 (u8.cpp:746-1352).
 //
 // Design (MI355X-first, not a Farrar port):
-//  * One problem per lane, 64 problems per wave; the lane sweeps its matrix column by
-//    column and computes the exact saturating-u8 recurrence (no striping, no lazy-F
-//    loop: every stored value equals the striped kernel's).
-//  * Per-row state (H and E of the previous column, the read code and its quality's
-//    mismatch penalty) lives in LDS, one dword per row per lane, lane-interleaved so a
-//    wave's access to a row is 64 consecutive dwords (conflict-free).
-//  * Instead of materialising E/F/H (3 B/cell in the reference) the fill writes ONE
-//    traceback byte per cell: the predecessor the reference's backtrace would pick for
-//    the H, E and F cell (its fixed priority diag > H-up > F-up > H-left > E-left,
-//    u8.cpp:968-990 and :843-916), plus bit 7 = reportedThrough.  The backtrace only ever
-//    consults a cell on its first visit (a second visit hits reportedThrough and fails),
-//    so this byte is all it needs.  Four rows are packed per dword; each wave store is
-//    256 contiguous bytes.
+//  * One problem per lane, 64 problems per wave; the lane computes the exact saturating
+//    u8 recurrence (no striping, no lazy-F loop: every value equals the striped kernel's,
+//    SURVEY F9).
+//  * The fill sweeps TWO columns at once, skewed by one row: step s computes cell
+//    (s, j) in the low 16-bit half and cell (s-1, j+1) in the high half of every packed
+//    operand, so each v_pk_{sub(clamp),max,min,mul}_u16 does two cells.  The high half's
+//    inputs are the low half's outputs of the previous step (no extra state), and its
+//    outputs replace row s-1 of the per-row state, which the low half has consumed.
+//  * Per-row state (H and E of the previous column, 4 rows per dword) and a row-info
+//    byte (read code, gap-barrier flag, quality mismatch penalty) live in VGPRs.
+//  * Instead of materialising E/F/H (3 B/cell in the reference) the fill writes one
+//    traceback byte per cell holding four "not equal" flags (d!=h, f!=h, hu_o!=f,
+//    hl_o!=e): exactly what backtraceNucleotidesEnd2EndSseU8's fixed priority
+//    (diag > H-up > F-up > H-left > E-left, E/F prefer the open; u8.cpp:843-990) needs
+//    at a cell of value >= 1, and a backtrace only visits such cells, each at most once
+//    (a revisit hits reportedThrough = bit 7 and fails).  Two steps' bytes of both
+//    columns form one dword; each wave store is 256 contiguous bytes.
 //  * Candidates (last-row cells with score >= minsc) are enumerated in DpBtCandidate
 //    order (score desc, col desc; aligner_sw_nuc.h:149) and backtraced in-kernel; only
 //    the final edit lists leave the GPU.
@@ -31,9 +35,11 @@
 namespace {
 
 constexpr int kRows = BT2X_MAX_ROWS;          // 160
-constexpr int kRowWords = kRows / 4;          // traceback dwords per column
+constexpr int kRowWords = kRows / 4;          // state dwords (4 rows each)
 constexpr int kCols = BT2X_MAX_COLS;          // 200
-constexpr uint32_t kDirBytesLane = kCols * kRowWords * 4;       // 32000
+constexpr int kSteps = kRows + 1;             // steps per column pair (rows 0..R-1, skew 1)
+constexpr int kPairWords = (kSteps + 1) / 2;  // traceback dwords per column pair (2 steps each)
+constexpr uint32_t kDirBytesLane = (kCols / 2) * kPairWords * 4;   // 32400
 constexpr uint32_t kLastRowBytesLane = 256;
 constexpr uint32_t kEditStage = 400;                               // >= R + C + 2
 constexpr uint32_t kRecStage = 200;                                // >= ncand
@@ -44,6 +50,32 @@ constexpr size_t kEditOff = kLastRowOff + (size_t)kLastRowBytesLane * 64;
 constexpr size_t kRecOff = kEditOff + (size_t)kEditStage * 4 * 64;
 constexpr size_t kSlotBytes = kRecOff + (size_t)kRecStage * sizeof(bt2x_aln_rec) * 64;
 static_assert(kSlotBytes <= (size_t)BT2X_DP_SCRATCH_PER_LANE * 64, "scratch slot too small");
+
+// Byte address (within a lane's interleaved traceback region) of cell (row, col):
+// column pair p = col/2; even columns sit at step row, odd columns at step row + 1.
+__device__ __forceinline__ size_t tb_addr(int row, int col, int lane) {
+	const int st = row + (col & 1);
+	return ((((size_t)(col >> 1) * kPairWords + (st >> 1)) * 64 + lane) << 2) + ((st & 1) << 1) + (col & 1);
+}
+
+// traceback flag bits (1 = the equality does NOT hold)
+enum { TB_DNE = 1, TB_FNE = 2, TB_FONE = 4, TB_EONE = 8, TB_MARK = 0x80 };
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as1(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t psubs(uint32_t a, uint32_t b) { return as1(__builtin_elementwise_sub_sat(as2(a), as2(b))); }
+__device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) { return as1(__builtin_elementwise_max(as2(a), as2(b))); }
+__device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) {
+	uint32_t r;   // v_pk_min_u16 (the generic min of a 0/1 bound is lowered to compares)
+	asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+	return r;
+}
+__device__ __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return as1(as2(a) * as2(b)); }
+__device__ __forceinline__ uint32_t pshr(uint32_t a, uint32_t sh) { return as1(as2(a) >> (u16x2){(unsigned short)sh, (unsigned short)sh}); }
+// per-half "not equal" flag, 0 or 1
+__device__ __forceinline__ uint32_t pne(uint32_t a, uint32_t b) { return pmin(a ^ b, 0x00010001u); }
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
 
 enum { H_NONE = 0, H_DIAG = 1, H_REF_OPEN = 2, H_RFGAP_EXT = 3, H_READ_OPEN = 4, H_RDGAP_EXT = 5 };
 enum { EDIT_READ_GAP = 1, EDIT_REF_GAP = 2, EDIT_MM = 3 };
@@ -77,8 +109,9 @@ __device__ __forceinline__ int wave_max(int v) {
 	return v;
 }
 
-// Per-row info byte kept in LDS during the fill: read code (3 bits), gap-barrier flag
-// (bit 3), mismatch penalty for the row's quality (bits 4-7; Scoring::mmpens <= 15).
+// Per-row info byte kept in VGPRs during the fill: read code (3 bits; a read N is 7,
+// which matches no reference code, with mm = the N penalty), gap-barrier flag (bit 3),
+// mismatch penalty for the row's quality (bits 4-7; penalties <= 15, checked at open).
 __device__ __forceinline__ uint32_t row_info(int rdc, bool gbar, int mm) {
 	return (uint32_t)rdc | (gbar ? 8u : 0u) | ((uint32_t)mm << 4);
 }
@@ -106,109 +139,148 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 		else { p.read_off = p.qual_off = p.ref_off = 0; p.refl = 0; p.rdlen = 0; p.ncol = 0;
 		       p.minsc = 0; p.nceil = 0; p.triml = p.corel = p.corer = 0; p.fw = 1; p.pad = 0; }
 		const int R = p.rdlen, C = p.ncol;
-		const int Rmax = wave_max(R), Cmax = wave_max(C);
+		// wave-uniform bounds in SGPRs: every per-step guard below is a scalar branch
+		const int Rmax = __builtin_amdgcn_readfirstlane(wave_max(R));
+		const int Cmax = __builtin_amdgcn_readfirstlane(wave_max(C));
 		const uint8_t* rd = a.reads + p.read_off;
 		const uint8_t* qu = a.quals + p.qual_off;
 		const uint8_t* rf = a.refs + p.ref_off;
 		const int thr = (int)p.minsc + 0xff;
-		// ------------- row info (rows >= R: N, barred, no penalty) ----------------
+		// ------------- row info (rows >= R: N, barred) ------------------------------
 		// 4 rows per dword, held in VGPRs for the whole fill (constant per problem)
+		const uint32_t kNone = row_info(7, true, npen);
 		uint32_t Info[kRowWords];
 #pragma unroll
 		for(int blk = 0; blk < kRowWords; blk++) {
-			uint32_t w = row_info(4, true, 0) * 0x01010101u;
+			uint32_t w = kNone * 0x01010101u;
 			if(blk * 4 < Rmax) {
 				w = 0;
 #pragma unroll
 				for(int r = 0; r < 4; r++) {
 					const int i = blk * 4 + r;
-					uint32_t b = row_info(4, true, 0);
+					uint32_t b = kNone;
 					if(i < R) {
 						int q = (int)qu[i] - 33;
 						q = q < 0 ? 0 : (q > 255 ? 255 : q);
 						const bool gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
-						b = row_info(rd[i], gbar, sc.mmpen[q]);
+						const int rc = rd[i];
+						b = rc > 3 ? row_info(7, gbar, npen) : row_info(rc, gbar, sc.mmpen[q]);
 					}
 					w |= b << (8 * r);
 				}
 			}
 			Info[blk] = w;
 		}
-		// ------------- fill: column-major, per-row state in VGPRs --------------
+		// ------------- fill: two columns per sweep, per-row state in VGPRs ------------
 		// H and E of the previous column, 4 rows per dword (40 dwords each for 160 rows).
 		uint32_t Hs[kRowWords], Es[kRowWords];
 #pragma unroll
 		for(int b = 0; b < kRowWords; b++) { Hs[b] = 0; Es[b] = 0; }
 		uint64_t dg0 = 0, dg1 = 0, dg2 = 0;
 		int lrmax = 0, ncand = 0;
-		const int lastblk = (R - 1) >> 2, lastsh = 8 * ((R - 1) & 3);
-		int refn = (C > 0) ? rf[0] : 4;
-		for(int j = 0; j < Cmax; j++) {
-			const int refc = refn;
-			if(j + 1 < C) refn = rf[j + 1];            // prefetch next column's base
-			const bool colok = j < C;
-			const bool refamb = refc > 3;
-			int hdiag = 0xff, hup = 0, fup = 0;        // H[-1][j-1] = 0xff: start anywhere
-			uint32_t lrw = 0;
+		const int Rmin = __builtin_amdgcn_readfirstlane(-wave_max(-R));
+		const uint32_t rdo2 = (uint32_t)rdo * 0x10001u, rde2 = (uint32_t)rde * 0x10001u;
+		const uint32_t rfo2 = (uint32_t)rfo * 0x10001u, rfe2 = (uint32_t)rfe * 0x10001u;
+		const uint32_t npen2 = (uint32_t)npen * 0x10001u;
+		const int npairs = (Cmax + 1) >> 1;
+		int refa = C > 0 ? rf[0] : 4, refb = C > 1 ? rf[1] : 4;
+		for(int pp = 0; pp < npairs; pp++) {
+			const int j0 = 2 * pp;
+			// opaque per pair: keeps the per-step guards and last-row compares from being
+			// hoisted out of the pair loop as 2 x 161 precomputed lane masks (SGPR spills)
+			int rmax = Rmax, rmin = Rmin, rl = R;
+			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl));
+			const int ca = refa, cb = refb;
+			refa = (j0 + 2 < C) ? rf[j0 + 2] : 4;      // prefetch the next pair's bases
+			refb = (j0 + 3 < C) ? rf[j0 + 3] : 4;
+			const uint32_t refc2 = (uint32_t)ca | ((uint32_t)cb << 16);
+			// N reference columns: every row pays the N penalty
+			const uint32_t coln = (ca > 3 ? 0x0000ffffu : 0u) | (cb > 3 ? 0xffff0000u : 0u);
+			uint32_t* dirp = dir + (size_t)pp * kPairWords * 64 + lane;
+			uint32_t hp = 0, fp = 0, ep = 0, hlp = 0;      // previous step's packed H, F, E, hl
+			uint32_t tbacc = 0;
+			int lra = 0, lrb = 0;                           // H[R-1][j0], H[R-1][j0+1]
 #pragma unroll
-			for(int blk = 0; blk < kRowWords; blk++) {
-				if(blk * 4 < Rmax) {                     // wave-uniform
-				uint32_t info = Info[blk];
-				asm volatile("" : "+v"(info));      // keep the per-row fields from being hoisted (VGPR blow-up)
-				const uint32_t hw = Hs[blk], ew = Es[blk];
-				uint32_t nh = 0, ne = 0, tbw = 0;
-#pragma unroll
-				for(int r = 0; r < 4; r++) {
-					const int i = blk * 4 + r;
-					const int hl = (int)((hw >> (8 * r)) & 0xffu);
-					const int el = (int)((ew >> (8 * r)) & 0xffu);
-					const uint32_t inf = (info >> (8 * r)) & 0xffu;
-					const int rdc = (int)(inf & 7u);
-					const bool gb = (inf & 8u) != 0;
-					const int mm = (int)(inf >> 4);
-					const int pen = (refamb || rdc > 3) ? npen : (rdc == refc ? 0 : mm);
-					// E[i][j] = max(E[i][j-1] - rde, H[i][j-1] - rdo (barred rows: none)), >= 0
-					const int hl_o = hl - rdo, el_e = el - rde;
-					const int e = imax(imax(el_e, gb ? 0 : hl_o), 0);
-					// F[i][j] = max(F[i-1][j] - rfe, H[i-1][j] - rfo), barred rows 0, row 0 = 0
-					const int hu_o = hup - rfo, fu_e = fup - rfe;
-					const int f = (i == 0 || gb) ? 0 : imax(imax(hu_o, fu_e), 0);
-					const int d = ((i == 0) ? 0xff : hdiag) - pen;
-					const int h = imax(imax(d, e), f);
-					uint32_t tb = 0;
-					if(i > 0) {
-						// Traceback choice of backtraceNucleotidesEnd2EndSseU8 for each cell type.
-						// Exact for every cell a backtrace can reach (value >= 1).
-						// branch-free: 0/1 flags combined arithmetically
-						const uint32_t f_open = hu_o == f, f_ext = (fu_e == f) & !f_open;
-						const uint32_t e_open = hl_o == e, e_ext = (el_e == e) & !e_open;
-						const uint32_t fd = f_open | (f_ext << 1), ed = e_open | (e_ext << 1);
-						const uint32_t isd = d == h;
-						const uint32_t isf = (f == h) & !isd;
-						const uint32_t ise = (e == h) & !isd & !isf;
-						const uint32_t hd = isd | (isf * (fd + 1)) | (ise * (ed + 3));
-						tb = hd | (ed << 3) | (fd << 5);
+			for(int st = 0; st < kSteps; st++) {
+				if(st <= rmax) {                             // wave-uniform
+				const int blk = st >> 2, r = st & 3;
+				// --- operands: low half = (row st, col j0), high half = (row st-1, col j0+1)
+				// opaque copies of the info words: the pair computed from them would otherwise
+				// be hoisted out of the pair loop for all 161 steps (VGPR blow-up)
+				uint32_t iw = Info[blk < kRowWords ? blk : kRowWords - 1];
+				uint32_t iv = Info[blk > 0 ? blk - 1 : 0];
+				asm volatile("" : "+v"(iw), "+v"(iv));
+				uint32_t info = (st == 0) ? perm(0, iw, 0x0c0c0c00u)
+				              : (st == kRows) ? (perm(iw, 0, 0x0c070c0cu) | (kNone & 0xffu))
+				              : (r == 0) ? perm(iv, iw, 0x0c070c00u)
+				                         : perm(0, iw, 0x0c000c00u | ((uint32_t)(r - 1) << 16) | (uint32_t)r);
+				const uint32_t hsw = st < kRows ? Hs[blk] : 0u, esw = st < kRows ? Es[blk] : 0u;
+				// hl: H[st][j0-1] | H[st-1][j0] (row -1 of any column is 0xff: start anywhere)
+				const uint32_t hl = (st == 0) ? perm(0, hsw, 0x0c0c0c00u) | 0x00ff0000u
+				                              : perm(hp, hsw, 0x0c040c00u | (uint32_t)r);
+				const uint32_t el = (st == 0) ? perm(0, esw, 0x0c0c0c00u)
+				                              : perm(ep, esw, 0x0c040c00u | (uint32_t)r);
+				const uint32_t hdiag = (st == 0) ? 0x000000ffu : hlp;
+				// penalty: 0 on a match, mm on a mismatch, npen if either base is N
+				// (x & 7) << 8 is >= 256 in a half whose codes differ: min(mm, that) = mm or 0
+				uint32_t pen = pmin(pshr(info, 4), ((info ^ refc2) & 0x00070007u) << 8);
+				pen = (pen & ~coln) | (npen2 & coln);
+				// gap barrier rows: open/extend penalties >= 256 saturate the term to 0;
+				// row 0 has no F (low half at st 0, high half at st 1)
+				const uint32_t gb = (info & 0x00080008u) << 5;
+				const uint32_t r0 = (st == 0) ? 0x00000100u : (st == 1) ? 0x01000000u : 0u;
+				const uint32_t rdoe = rdo2 + gb, rfoe = rfo2 + gb + r0, rfee = rfe2 + gb + r0;
+				const uint32_t d = psubs(hdiag, pen);
+				const uint32_t hl_o = psubs(hl, rdoe), el_e = psubs(el, rde2);
+				const uint32_t e = pmax(hl_o, el_e);
+				const uint32_t hu_o = psubs(hp, rfoe), fu_e = psubs(fp, rfee);
+				const uint32_t f = pmax(hu_o, fu_e);
+				const uint32_t h = pmax(pmax(d, e), f);
+				// traceback flags
+				const uint32_t tb = pne(d, h) | (pne(f, h) << 1) | (pne(hu_o, f) << 2) | (pne(hl_o, e) << 3);
+				if(kDebug && a.digests) {
+					if(st < R && j0 < C) {
+						dg0 += cell_digest(st, j0, 0, e & 0xffffu);
+						dg1 += cell_digest(st, j0, 1, f & 0xffffu);
+						dg2 += cell_digest(st, j0, 2, h & 0xffffu);
 					}
-					if(kDebug && a.digests && colok && i < R) {
-						dg0 += cell_digest(i, j, 0, e);
-						dg1 += cell_digest(i, j, 1, f);
-						dg2 += cell_digest(i, j, 2, h);
+					if(st >= 1 && st - 1 < R && j0 + 1 < C) {
+						dg0 += cell_digest(st - 1, j0 + 1, 0, e >> 16);
+						dg1 += cell_digest(st - 1, j0 + 1, 1, f >> 16);
+						dg2 += cell_digest(st - 1, j0 + 1, 2, h >> 16);
 					}
-					nh |= (uint32_t)h << (8 * r);
-					ne |= (uint32_t)e << (8 * r);
-					tbw |= tb << (8 * r);
-					hdiag = hl; hup = h; fup = f;
 				}
-				Hs[blk] = nh; Es[blk] = ne;
-				lrw = (blk == lastblk) ? nh : lrw;
-				if(colok) dir[((size_t)j * kRowWords + blk) * 64 + lane] = tbw;
+				// last row of each column (per-lane R; only in the wave's R range)
+				if(st + 1 >= rmin) {                         // wave-uniform
+					lra = (st == rl - 1) ? (int)(h & 0xffu) : lra;
+					lrb = (st == rl) ? (int)((h >> 16) & 0xffu) : lrb;
+				}
+				// the high half's outputs (row st-1 of column j0+1) replace row st-1 state
+				if(st >= 1) {
+					const int pb = (st - 1) >> 2, pr = (st - 1) & 3;
+					const uint32_t selh = (0x03020100u & ~(0xffu << (8 * pr))) | (6u << (8 * pr));
+					Hs[pb] = perm(h, Hs[pb], selh);
+					Es[pb] = perm(e, Es[pb], selh);
+				}
+				// two steps' flags of both columns per traceback dword
+				if(st & 1) {
+					dirp[(size_t)(st >> 1) * 64] = perm(tb, tbacc, 0x06040200u);
+				} else {
+					tbacc = tb;
+					if(st == rmax) dirp[(size_t)(st >> 1) * 64] = perm(0, tbacc, 0x0c0c0200u);
+				}
+				hlp = hl; hp = h; fp = f; ep = e;
 				}
 			}
-			if(colok) {
-				const int lr = (int)((lrw >> lastsh) & 0xffu);
-				lastrow[(size_t)j * 64 + lane] = (uint8_t)lr;
-				lrmax = imax(lrmax, lr);
-				ncand += (lr >= thr);
+			if(j0 < C) {
+				lastrow[(size_t)j0 * 64 + lane] = (uint8_t)lra;
+				lrmax = imax(lrmax, lra);
+				ncand += (lra >= thr);
+			}
+			if(j0 + 1 < C) {
+				lastrow[(size_t)(j0 + 1) * 64 + lane] = (uint8_t)lrb;
+				lrmax = imax(lrmax, lrb);
+				ncand += (lrb >= thr);
 			}
 		}
 		if(!active || a.ablate) continue;
@@ -269,10 +341,7 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 					a.cands[(size_t)pi * kCols + ndone] = BT2X_CAND_PACK(row0, col0, best >> 8);
 				ndone++;
 				// candidate start cell already traversed -> skipped, no RNG draw
-				{
-					const uint32_t w = dir[((size_t)col0 * kRowWords + (row0 >> 2)) * 64 + lane];
-					if((w >> (8 * (row0 & 3) + 7)) & 1) continue;
-				}
+				if(reinterpret_cast<const uint8_t*>(dir)[tb_addr(row0, col0, lane)] & TB_MARK) continue;
 				ntries++;
 				// ------------- backtraceNucleotidesEnd2EndSseU8 -------------
 				int row = row0, col = col0, ct = 2 /*H*/, bscore = 0, ns = 0, gaps = 0, ne = 0;
@@ -283,26 +352,24 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 				// byte and the staged edit), so the in-order vmcnt never waits on a store.
 				const uint8_t* dir8 = reinterpret_cast<const uint8_t*>(dir);
 				uint8_t* dirw8 = reinterpret_cast<uint8_t*>(dir);
-				size_t bi = (((size_t)col * kRowWords + (row >> 2)) * 64 + lane) * 4 + (row & 3);
+				size_t bi = tb_addr(row, col, lane);
 				uint32_t tb = dir8[bi];
 				int rdc = rd[row], refc = rf[col], qch = qu[row];
 				while(true) {
 					st_bt++;
-					if(tb & 0x80u) { ok = false; break; }          // reportedThrough
-					int move = H_NONE;
-					bool empty = false;
-					if(row > 0) {
-						if(ct == 2) move = (int)(tb & 7u);
-						else if(ct == 0) { const int ed = (int)((tb >> 3) & 3u); move = ed == 1 ? H_READ_OPEN : ed == 2 ? H_RDGAP_EXT : H_NONE; }
-						else { const int fd = (int)((tb >> 5) & 3u); move = fd == 1 ? H_REF_OPEN : fd == 2 ? H_RFGAP_EXT : H_NONE; }
-						empty = (move == H_NONE);
-					}
+					if(tb & TB_MARK) { ok = false; break; }         // reportedThrough
+					// the reference's fixed priority over the cell's flags (u8.cpp:843-990)
+					const int emove = (tb & TB_EONE) ? H_RDGAP_EXT : H_READ_OPEN;
+					const int fmove = (tb & TB_FONE) ? H_RFGAP_EXT : H_REF_OPEN;
+					const int move = ct == 0 ? emove : ct == 1 ? fmove
+					               : !(tb & TB_DNE) ? H_DIAG : !(tb & TB_FNE) ? fmove : emove;
+					const bool empty = false;
 					const int diag = col - row + (int)p.triml;
 					if(diag >= 0 && diag >= (int)p.corel && diag <= (int)p.corer) over_core = true;
 					const size_t cur_bi = bi;
 					const uint32_t cur_tb = tb;
 					if(empty || row == 0) {
-						dirw8[cur_bi] = (uint8_t)(cur_tb | 0x80u);  // setReportedThrough
+						dirw8[cur_bi] = (uint8_t)(cur_tb | TB_MARK);  // setReportedThrough
 						trimBeg = row;
 						break;
 					}
@@ -311,11 +378,11 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 					if(move == H_DIAG) { row--; col--; ct = 2; }
 					else if(move == H_REF_OPEN || move == H_RFGAP_EXT) { row--; ct = (move == H_REF_OPEN) ? 2 : 1; }
 					else { col--; ct = (move == H_READ_OPEN) ? 2 : 0; }
-					bi = (((size_t)col * kRowWords + (row >> 2)) * 64 + lane) * 4 + (row & 3);
+					bi = tb_addr(row, col, lane);
 					tb = dir8[bi];
 					rdc = rd[row]; refc = rf[col]; qch = qu[row];
 					// stores for the cell just left
-					dirw8[cur_bi] = (uint8_t)(cur_tb | 0x80u);      // setReportedThrough
+					dirw8[cur_bi] = (uint8_t)(cur_tb | TB_MARK);    // setReportedThrough
 					if(move == H_DIAG) {
 						const bool amb = crdc > 3 || crefc > 3;
 						if(amb || crdc != crefc) {
