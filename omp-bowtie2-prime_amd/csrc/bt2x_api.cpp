@@ -13,8 +13,6 @@
 
 #include "bt2x_device.h"
 
-size_t bt2x_dp_slot_bytes();
-int bt2x_dp_blocks_per_cu();
 
 #define HIPCHK(x) do { if((x) != hipSuccess) return BT2X_E_NODEVICE; } while(0)
 
@@ -135,8 +133,9 @@ struct bt2x_ctx {
 	void* d_ebwt = nullptr; void* d_ftab = nullptr; void* d_eftab = nullptr;
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
 	DevBuf scratch;
-	uint32_t nslots = 0;
 	int ncu = 0;
+	uint32_t chunk_groups = 16384;             // DP chunk: 1 Mi problems, ~34 GB of traceback bytes
+	uint32_t* d_queue = nullptr;
 	unsigned long long* d_stats = nullptr;     // [0..2] seed, [4..6] dp
 	uint32_t* d_counters = nullptr;
 	uint64_t n_seed_last = 0, n_dp_last = 0;
@@ -197,7 +196,8 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	HIPCHK(hipGetDeviceProperties(&prop, device));
 	// one 64-lane wave per workgroup; as many as are co-resident (register-bound)
 	c->ncu = prop.multiProcessorCount;
-	c->nslots = (uint32_t)prop.multiProcessorCount * (uint32_t)bt2x_dp_blocks_per_cu();
+	HIPCHK(hipMalloc((void**)&c->d_queue, 4 * sizeof(uint32_t)));
+	if(const char* cg = getenv("BT2X_DP_CHUNK_GROUPS")) { const long v = atol(cg); if(v >= 1 && v <= 65536) c->chunk_groups = (uint32_t)v; }
 	*out = c.release();
 	return BT2X_OK;
 }
@@ -209,7 +209,7 @@ extern "C" void bt2x_close(bt2x_ctx* c) {
 	for(DevBuf* b : {&c->b_reads, &c->b_quals, &c->b_refs, &c->b_in, &c->b_out, &c->b_recs,
 	                 &c->b_edits, &c->b_dbg_dig, &c->b_dbg_cand, &c->scratch}) b->release();
 	(void)hipFree(c->d_ebwt); (void)hipFree(c->d_ftab); (void)hipFree(c->d_eftab);
-	(void)hipFree(c->d_stats); (void)hipFree(c->d_counters);
+	(void)hipFree(c->d_stats); (void)hipFree(c->d_counters); (void)hipFree(c->d_queue);
 	for(int k = 0; k < BT2X_K_COUNT; k++) { (void)hipEventDestroy(c->ev[k][0]); (void)hipEventDestroy(c->ev[k][1]); }
 	(void)hipStreamDestroy(c->stream);
 	delete c;
@@ -280,8 +280,16 @@ extern "C" int bt2x_seed_search(bt2x_ctx* c, const uint8_t* reads, uint64_t read
 }
 
 // ---------------------------------------------------------------------- DP
-static int ensure_scratch(bt2x_ctx* c) {
-	return c->scratch.ensure(bt2x_dp_slot_bytes() * c->nslots);
+// Scratch sized for min(batch, chunk) groups; grows with the largest batch seen.
+static int ensure_scratch(bt2x_ctx* c, uint32_t n, uint32_t* groups) {
+	uint32_t g = (n + 63) / 64;
+	if(g > c->chunk_groups) g = c->chunk_groups;
+	if(g < 1) g = 1;
+	const size_t need = bt2x_dp_scratch_bytes(c->ncu, g);
+	int rc = c->scratch.ensure(need);
+	// use every group the buffer holds (a larger earlier batch may have grown it)
+	*groups = g;
+	return rc;
 }
 
 extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint8_t* d_quals,
@@ -292,7 +300,8 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	if(!c || !d_counters) return BT2X_E_ARG;
 	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
 	HIPCHK(hipSetDevice(c->device));
-	int rc = ensure_scratch(c);
+	uint32_t groups = 0;
+	int rc = ensure_scratch(c, n, &groups);
 	if(rc) return rc;
 	HIPCHK(hipMemsetAsync(d_counters, 0, 2 * sizeof(uint32_t), s));
 	HIPCHK(hipMemsetAsync(c->d_stats + 4, 0, 3 * sizeof(unsigned long long), s));
@@ -302,8 +311,8 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	a.counters = d_counters; a.stats = c->d_stats + 4;
 	a.digests = d_debug ? d_debug->digests : nullptr;
 	a.cands = d_debug ? d_debug->cands : nullptr;
-	a.scratch = (uint8_t*)c->scratch.p; a.nslots = c->nslots;
-	{ const char* ab = getenv("BT2X_DP_ABLATE"); a.ablate = (ab && *ab == '1') ? 1u : 0u; }
+	a.scratch = (uint8_t*)c->scratch.p; a.chunk_groups = groups; a.ncu = c->ncu; a.queue = c->d_queue;
+	{ const char* ab = getenv("BT2X_DP_ABLATE"); a.ablate = (ab && *ab >= '1' && *ab <= '2') ? (uint32_t)(*ab - '0') : 0u; }
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));

@@ -42,9 +42,12 @@ struct DpLaunch {
 	unsigned long long* stats;     // dp_cells, dp_cols, bt_cells
 	uint64_t* digests;             // optional, 3 per problem
 	uint32_t* cands;               // optional, BT2X_MAX_COLS per problem
-	uint8_t* scratch;              // per resident wave: BT2X_DP_SCRATCH_PER_LANE * 64
-	uint32_t nslots;               // resident wave slots backed by scratch
-	uint32_t ablate;               // profiling only: 1 = stop after the fill (outputs invalid)
+	uint8_t* scratch;              // chunk_groups fill regions, then the walk staging slots
+	uint8_t* walk_scratch;         // set by bt2x_launch_dp
+	uint32_t chunk_groups;         // 64-problem groups per fill/walk chunk
+	int ncu;                       // compute units (persistent grid sizing)
+	uint32_t* queue;               // walk-kernel problem queue counter (device)
+	uint32_t ablate;               // profiling only: 1 = stop after the fill, 2 = no backtrace walks (outputs invalid)
 };
-#define BT2X_DP_SCRATCH_PER_LANE (32768u + 8192u)
+size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups);
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream);

@@ -41,25 +41,33 @@ constexpr int kSteps = kRows + 1;             // steps per column pair (rows 0..
 constexpr int kPairWords = (kSteps + 1) / 2;  // traceback dwords per column pair (2 steps each)
 constexpr uint32_t kDirBytesLane = (kCols / 2) * kPairWords * 4;   // 32400
 constexpr uint32_t kLastRowBytesLane = 256;
+constexpr uint32_t kCandBytesLane = kCols;                         // sorted candidate columns
 constexpr uint32_t kEditStage = 400;                               // >= R + C + 2
-constexpr uint32_t kRecStage = 200;                                // >= ncand
-// scratch layout of one wave slot (all regions lane-interleaved)
+constexpr uint32_t kRecStage = kCols + 8;                          // >= ncand + 1
+// Group region: the fill's output for 64 problems (all regions lane-interleaved).
 constexpr size_t kDirOff = 0;
 constexpr size_t kLastRowOff = kDirOff + (size_t)kDirBytesLane * 64;
-constexpr size_t kEditOff = kLastRowOff + (size_t)kLastRowBytesLane * 64;
+constexpr size_t kCandOff = kLastRowOff + (size_t)kLastRowBytesLane * 64;
+constexpr size_t kGroupBytes = kCandOff + (size_t)kCandBytesLane * 64;
+// Walk slot: staging of one resident walk wave (lane-interleaved).
+constexpr size_t kEditOff = 0;
 constexpr size_t kRecOff = kEditOff + (size_t)kEditStage * 4 * 64;
-constexpr size_t kSlotBytes = kRecOff + (size_t)kRecStage * sizeof(bt2x_aln_rec) * 64;
-static_assert(kSlotBytes <= (size_t)BT2X_DP_SCRATCH_PER_LANE * 64, "scratch slot too small");
+constexpr size_t kWalkSlotBytes = kRecOff + (size_t)kRecStage * sizeof(bt2x_aln_rec) * 64;
 
-// Byte address (within a lane's interleaved traceback region) of cell (row, col):
-// column pair p = col/2; even columns sit at step row, odd columns at step row + 1.
+// Byte address (within a group's lane-interleaved traceback region) of cell (row, col)
+// of lane `lane`: column pair p = col/2; even columns sit at step row, odd columns at
+// step row + 1; one dword holds two steps of both columns of a pair.  Lane-interleaved
+// dwords keep the fill's stores coalesced (256 B per wave store) and let the 64 lanes'
+// walks, which follow nearly the same diagonal (every rectangle is framed around its
+// seed diagonal), share cache lines.
 __device__ __forceinline__ size_t tb_addr(int row, int col, int lane) {
 	const int st = row + (col & 1);
 	return ((((size_t)(col >> 1) * kPairWords + (st >> 1)) * 64 + lane) << 2) + ((st & 1) << 1) + (col & 1);
 }
 
-// traceback flag bits (1 = the equality does NOT hold)
-enum { TB_DNE = 1, TB_FNE = 2, TB_FONE = 4, TB_EONE = 8, TB_MARK = 0x80 };
+// traceback flag bits (1 = the equality does NOT hold); TB_MM: read and reference
+// bases differ or either is N (the diagonal move records an edit)
+enum { TB_DNE = 1, TB_FNE = 2, TB_FONE = 4, TB_EONE = 8, TB_MM = 0x10, TB_MARK = 0x80 };
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
@@ -76,6 +84,13 @@ __device__ __forceinline__ uint32_t pshr(uint32_t a, uint32_t sh) { return as1(a
 // per-half "not equal" flag, 0 or 1
 __device__ __forceinline__ uint32_t pne(uint32_t a, uint32_t b) { return pmin(a ^ b, 0x00010001u); }
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+// (a << 1) | b and (a << 5) + b as single VOP3 ops (the generic forms get re-associated)
+__device__ __forceinline__ uint32_t shl1_or(uint32_t a, uint32_t b) {
+	uint32_t r; asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ __forceinline__ uint32_t shl5_add(uint32_t a, uint32_t b) {
+	uint32_t r; asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
 
 enum { H_NONE = 0, H_DIAG = 1, H_REF_OPEN = 2, H_RFGAP_EXT = 3, H_READ_OPEN = 4, H_RDGAP_EXT = 5 };
 enum { EDIT_READ_GAP = 1, EDIT_REF_GAP = 2, EDIT_MM = 3 };
@@ -100,10 +115,6 @@ __device__ __forceinline__ uint64_t cell_digest(uint32_t row, uint32_t col, uint
 	return z ^ (z >> 31);
 }
 
-struct BtResult {
-	int score, ns, gaps, nedit, bases, refns, off;
-};
-
 __device__ __forceinline__ int wave_max(int v) {
 	for(int d = 32; d > 0; d >>= 1) { const int o = __shfl_xor(v, d); v = v > o ? v : o; }
 	return v;
@@ -116,24 +127,167 @@ __device__ __forceinline__ uint32_t row_info(int rdc, bool gbar, int mm) {
 	return (uint32_t)rdc | (gbar ? 8u : 0u) | ((uint32_t)mm << 4);
 }
 
-template<bool kDebug>
+// SwAligner::nextAlignment until done() for problem pi (lane gl of the group whose fill
+// output starts at gslot): its candidates in order, each not already reportedThrough
+// backtraced over the fill's traceback bytes; records and edits staged per lane.
+__device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunch& a, uint32_t pi,
+                                             int lane, uint8_t* gslot, uint32_t* stage_ed,
+                                             bt2x_aln_rec* stage_rec, unsigned long long& st_bt) {
+	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
+	const uint32_t gl = (uint32_t)lane;
+	const uint8_t* dir8 = gslot + kDirOff;
+	uint8_t* dirw8 = gslot + kDirOff;
+	const uint8_t* cands = gslot + kCandOff;
+	bt2x_dp_out o = a.out[pi];
+	if(o.status != 0 && o.ncand > 0 && a.ablate != 1) {
+		const bt2x_dp_in p = a.in[pi];
+		const int R = p.rdlen;
+		const uint8_t* rd = a.reads + p.read_off;
+		const uint8_t* qu = a.quals + p.qual_off;
+		const uint8_t* rf = a.refs + p.ref_off;
+		const int ncand = o.ncand;
+		const int row0 = R - 1;
+		int ndone = 0, nrec = 0;
+		while(ndone < ncand) {
+			int ntries = 0;
+			bool found = false;
+			while(ndone < ncand) {
+				const int col0 = cands[(size_t)ndone * 64 + gl];
+				ndone++;
+				// candidate start cell already traversed -> skipped, no RNG draw
+				if(dir8[tb_addr(row0, col0, gl)] & TB_MARK) continue;
+				ntries++;
+				if(a.ablate == 2) continue;          // profiling: no backtrace walks
+				// ------------- backtraceNucleotidesEnd2EndSseU8 -------------
+				int row = row0, col = col0, ct = 2 /*H*/, bscore = 0, ns = 0, gaps = 0, ne = 0;
+				bool over_core = false, ok = true;
+				uint32_t tb_end = 0;
+				// One dependent load per step: the next cell's byte is issued before
+				// this cell's mark store, so the in-order vmcnt never waits on a store.
+				// Read/reference/quality bytes only where TB_MM says an edit is recorded.
+				size_t bi = tb_addr(row, col, gl);
+				uint32_t tb = dir8[bi];
+				while(true) {
+					st_bt++;
+					if(tb & TB_MARK) { ok = false; break; }         // reportedThrough
+					const int diag = col - row + (int)p.triml;
+					if(diag >= 0 && diag >= (int)p.corel && diag <= (int)p.corer) over_core = true;
+					if(row == 0) {
+						dirw8[bi] = (uint8_t)TB_MARK;              // setReportedThrough
+						tb_end = tb;
+						break;
+					}
+					// the reference's fixed priority over the cell's flags (u8.cpp:843-990)
+					const int emove = (tb & TB_EONE) ? H_RDGAP_EXT : H_READ_OPEN;
+					const int fmove = (tb & TB_FONE) ? H_RFGAP_EXT : H_REF_OPEN;
+					const int move = ct == 0 ? emove : ct == 1 ? fmove
+					               : !(tb & TB_DNE) ? H_DIAG : !(tb & TB_FNE) ? fmove : emove;
+					const int crow = row, ccol = col;
+					const uint32_t ctb = tb;
+					const size_t cur_bi = bi;
+					if(move == H_DIAG) { row--; col--; ct = 2; }
+					else if(move == H_REF_OPEN || move == H_RFGAP_EXT) { row--; ct = (move == H_REF_OPEN) ? 2 : 1; }
+					else { col--; ct = (move == H_READ_OPEN) ? 2 : 0; }
+					bi = tb_addr(row, col, gl);
+					tb = dir8[bi];
+					dirw8[cur_bi] = (uint8_t)TB_MARK;              // setReportedThrough
+					if(move == H_DIAG) {
+						if(ctb & TB_MM) {
+							const int rdc = rd[crow], refc = rf[ccol];
+							const bool amb = rdc > 3 || refc > 3;
+							const int q0 = (int)qu[crow] - 33;
+							const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
+							stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(refc), acgtn(rdc));
+							ne++;
+							bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
+							if(amb) ns++;
+						}
+					} else if(move == H_REF_OPEN || move == H_RFGAP_EXT) {
+						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rd[crow]));
+						ne++;
+						bscore -= (move == H_REF_OPEN) ? rfo : rfe;
+						gaps++;
+					} else {
+						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(rf[ccol]), '-');
+						ne++;
+						bscore -= (move == H_READ_OPEN) ? rdo : rde;
+						gaps++;
+					}
+				}
+				if(!ok || !over_core) continue;
+				if(tb_end & TB_MM) {                     // the final (row 0) cell
+					const int rdc = rd[row], refc = rf[col];
+					const bool amb = rdc > 3 || refc > 3;
+					const int q0 = (int)qu[row] - 33;
+					const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
+					stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
+					ne++;
+					bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
+					if(amb) ns++;
+				}
+				if(ns > p.nceil) continue;
+				int refns = 0;
+				for(int k = col; k <= col0; k++) refns += (rf[k] > 3);
+				const int trimBeg = 0;
+				const int extent = R - trimBeg - (R - row0 - 1);
+				// publish the edit list in ned() order: reverse(), pos -= trimBeg, and
+				// for the reverse-complement strand invertEdits() (edit.cpp:50-78)
+				const uint32_t eo = atomicAdd(&a.counters[1], (uint32_t)ne);
+				if(eo + (uint32_t)ne <= a.edit_cap) {
+					for(int k = 0; k < ne; k++) {
+						const uint32_t e = stage_ed[(size_t)(p.fw ? ne - 1 - k : k) * 64 + lane];
+						uint32_t pos = (e & 0x3ffu) - (uint32_t)trimBeg;
+						if(!p.fw) pos = (uint32_t)extent - pos - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
+						a.edits[eo + k] = (e & ~0x3ffu) | (pos & 0x3ffu);
+					}
+				}
+				found = true;
+				bt2x_aln_rec r;
+				r.ntries = (uint16_t)ntries; r.ok = 1; r.pad0 = 0;
+				r.score = (int16_t)bscore; r.ns = (uint16_t)ns; r.gaps = (uint16_t)gaps;
+				r.nedit = (uint16_t)ne; r.bases_aligned = (uint16_t)(extent - ne);
+				r.refns = (uint16_t)refns; r.refoff = (int64_t)col + p.refl;
+				r.edit_off = eo; r.pad1 = 0;
+				stage_rec[(size_t)nrec * 64 + lane] = r;
+				break;
+			}
+			if(!found) {
+				bt2x_aln_rec r;
+				r.ntries = (uint16_t)ntries; r.ok = 0; r.pad0 = 0; r.score = 0; r.ns = 0; r.gaps = 0;
+				r.nedit = 0; r.bases_aligned = 0; r.refns = 0; r.refoff = 0; r.edit_off = 0; r.pad1 = 0;
+				stage_rec[(size_t)nrec * 64 + lane] = r;
+				nrec++;
+				break;
+			}
+			nrec++;
+		}
+		const uint32_t ro = atomicAdd(&a.counters[0], (uint32_t)nrec);
+		if(ro + (uint32_t)nrec <= a.rec_cap)
+			for(int k = 0; k < nrec; k++) a.recs[ro + k] = stage_rec[(size_t)k * 64 + lane];
+		o.nrec = (uint16_t)nrec; o.rec_off = ro;
+		a.out[pi] = o;
+	}
+}
+
+// kFused: the same wave walks its 64 problems right after their fill, while the
+// traceback bytes are still in the Infinity Cache; slots are per resident wave.
+template<bool kDebug, bool kFused>
 __global__ void __launch_bounds__(64)
-dp_kernel(DevScoring sc, DpLaunch a) {
-	// LDS, reused: during the fill the row-info bytes (4 rows per dword), afterwards the
-	// last DP row (4 columns per dword) for candidate enumeration.  12.8 KiB per wave.
+dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
+	// LDS: the last DP row (4 columns per dword) for candidate ordering.  12.8 KiB per wave.
 	__shared__ uint32_t lds[(kCols / 4) * 64];
 	const int lane = threadIdx.x;
-	uint8_t* slot = a.scratch + (size_t)blockIdx.x * kSlotBytes;
-	uint32_t* dir = reinterpret_cast<uint32_t*>(slot + kDirOff);
-	uint8_t* lastrow = slot + kLastRowOff;
-	uint32_t* stage_ed = reinterpret_cast<uint32_t*>(slot + kEditOff);
-	bt2x_aln_rec* stage_rec = reinterpret_cast<bt2x_aln_rec*>(slot + kRecOff);
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0;
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 
-	for(uint32_t chunk = blockIdx.x; (uint64_t)chunk * 64 < a.n; chunk += gridDim.x) {
-		const uint32_t pi = chunk * 64 + lane;
-		const bool active = pi < a.n;
+	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
+		uint8_t* gslot = kFused ? a.scratch + (size_t)blockIdx.x * (kGroupBytes + kWalkSlotBytes)
+		                        : a.scratch + (size_t)grp * kGroupBytes;
+		uint32_t* dir = reinterpret_cast<uint32_t*>(gslot + kDirOff);
+		uint8_t* lastrow = gslot + kLastRowOff;
+		uint8_t* cands = gslot + kCandOff;
+		const uint32_t pi = base + grp * 64 + lane;
+		const bool active = grp * 64 + lane < nprob;
 		bt2x_dp_in p;
 		if(active) p = a.in[pi];
 		else { p.read_off = p.qual_off = p.ref_off = 0; p.refl = 0; p.rdlen = 0; p.ncol = 0;
@@ -183,6 +337,8 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 		const uint32_t rfo2 = (uint32_t)rfo * 0x10001u, rfe2 = (uint32_t)rfe * 0x10001u;
 		const uint32_t npen2 = (uint32_t)npen * 0x10001u;
 		const int npairs = (Cmax + 1) >> 1;
+		const __amdgpu_buffer_rsrc_t dirsrc =
+			__builtin_amdgcn_make_buffer_rsrc(dir, 0, (int)(kDirBytesLane * 64u), 0x00020000);
 		int refa = C > 0 ? rf[0] : 4, refb = C > 1 ? rf[1] : 4;
 		for(int pp = 0; pp < npairs; pp++) {
 			const int j0 = 2 * pp;
@@ -190,13 +346,19 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 			// hoisted out of the pair loop as 2 x 161 precomputed lane masks (SGPR spills)
 			int rmax = Rmax, rmin = Rmin, rl = R;
 			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl));
+			// opaque row info per pair: the per-step info pairs built from it would
+			// otherwise be hoisted out of the pair loop for all 161 steps (VGPR blow-up)
+#pragma unroll
+			for(int k = 0; k < kRowWords; k++) asm volatile("" : "+v"(Info[k]));
 			const int ca = refa, cb = refb;
 			refa = (j0 + 2 < C) ? rf[j0 + 2] : 4;      // prefetch the next pair's bases
 			refb = (j0 + 3 < C) ? rf[j0 + 3] : 4;
 			const uint32_t refc2 = (uint32_t)ca | ((uint32_t)cb << 16);
 			// N reference columns: every row pays the N penalty
 			const uint32_t coln = (ca > 3 ? 0x0000ffffu : 0u) | (cb > 3 ? 0xffff0000u : 0u);
-			uint32_t* dirp = dir + (size_t)pp * kPairWords * 64 + lane;
+			// traceback stores through a buffer resource: lane offset in a VGPR, the step
+			// offset in an SGPR (no per-store 64-bit address arithmetic)
+			const uint32_t pbase = (uint32_t)pp * kPairWords * 256u;
 			uint32_t hp = 0, fp = 0, ep = 0, hlp = 0;      // previous step's packed H, F, E, hl
 			uint32_t tbacc = 0;
 			int lra = 0, lrb = 0;                           // H[R-1][j0], H[R-1][j0+1]
@@ -205,11 +367,8 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 				if(st <= rmax) {                             // wave-uniform
 				const int blk = st >> 2, r = st & 3;
 				// --- operands: low half = (row st, col j0), high half = (row st-1, col j0+1)
-				// opaque copies of the info words: the pair computed from them would otherwise
-				// be hoisted out of the pair loop for all 161 steps (VGPR blow-up)
-				uint32_t iw = Info[blk < kRowWords ? blk : kRowWords - 1];
-				uint32_t iv = Info[blk > 0 ? blk - 1 : 0];
-				asm volatile("" : "+v"(iw), "+v"(iv));
+				const uint32_t iw = Info[blk < kRowWords ? blk : kRowWords - 1];
+				const uint32_t iv = Info[blk > 0 ? blk - 1 : 0];
 				uint32_t info = (st == 0) ? perm(0, iw, 0x0c0c0c00u)
 				              : (st == kRows) ? (perm(iw, 0, 0x0c070c0cu) | (kNone & 0xffu))
 				              : (r == 0) ? perm(iv, iw, 0x0c070c00u)
@@ -223,13 +382,15 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 				const uint32_t hdiag = (st == 0) ? 0x000000ffu : hlp;
 				// penalty: 0 on a match, mm on a mismatch, npen if either base is N
 				// (x & 7) << 8 is >= 256 in a half whose codes differ: min(mm, that) = mm or 0
-				uint32_t pen = pmin(pshr(info, 4), ((info ^ refc2) & 0x00070007u) << 8);
+				// (x != 0 also for N bases: a read N is 7 and a reference N is 4)
+				const uint32_t xrc = (info ^ refc2) & 0x00070007u;
+				uint32_t pen = pmin(pshr(info, 4), xrc << 8);
 				pen = (pen & ~coln) | (npen2 & coln);
 				// gap barrier rows: open/extend penalties >= 256 saturate the term to 0;
 				// row 0 has no F (low half at st 0, high half at st 1)
-				const uint32_t gb = (info & 0x00080008u) << 5;
+				const uint32_t gbm = info & 0x00080008u;
 				const uint32_t r0 = (st == 0) ? 0x00000100u : (st == 1) ? 0x01000000u : 0u;
-				const uint32_t rdoe = rdo2 + gb, rfoe = rfo2 + gb + r0, rfee = rfe2 + gb + r0;
+				const uint32_t rdoe = shl5_add(gbm, rdo2), rfoe = shl5_add(gbm, rfo2 + r0), rfee = shl5_add(gbm, rfe2 + r0);
 				const uint32_t d = psubs(hdiag, pen);
 				const uint32_t hl_o = psubs(hl, rdoe), el_e = psubs(el, rde2);
 				const uint32_t e = pmax(hl_o, el_e);
@@ -237,7 +398,11 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 				const uint32_t f = pmax(hu_o, fu_e);
 				const uint32_t h = pmax(pmax(d, e), f);
 				// traceback flags
-				const uint32_t tb = pne(d, h) | (pne(f, h) << 1) | (pne(hu_o, f) << 2) | (pne(hl_o, e) << 3);
+				uint32_t tb = pmin(xrc, 0x00010001u);                 // TB_MM
+				tb = shl1_or(tb, pne(hl_o, e));                        // TB_EONE
+				tb = shl1_or(tb, pne(hu_o, f));                        // TB_FONE
+				tb = shl1_or(tb, pne(f, h));                           // TB_FNE
+				tb = shl1_or(tb, pne(d, h));                           // TB_DNE
 				if(kDebug && a.digests) {
 					if(st < R && j0 < C) {
 						dg0 += cell_digest(st, j0, 0, e & 0xffffu);
@@ -264,10 +429,13 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 				}
 				// two steps' flags of both columns per traceback dword
 				if(st & 1) {
-					dirp[(size_t)(st >> 1) * 64] = perm(tb, tbacc, 0x06040200u);
+					__builtin_amdgcn_raw_buffer_store_b32(perm(tb, tbacc, 0x06040200u), dirsrc, lane * 4,
+					                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
 				} else {
 					tbacc = tb;
-					if(st == rmax) dirp[(size_t)(st >> 1) * 64] = perm(0, tbacc, 0x0c0c0200u);
+					if(st == rmax)
+						__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, lane * 4,
+						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
 				}
 				hlp = hl; hp = h; fp = f; ep = e;
 				}
@@ -283,7 +451,7 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 				ncand += (lrb >= thr);
 			}
 		}
-		if(!active || a.ablate) continue;
+		if(!active) continue;
 		st_cells += (unsigned long long)R * C;
 		st_cols += C;
 		if(kDebug && a.digests) {
@@ -302,8 +470,9 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 			continue;
 		}
 		o.status = ncand > 0 ? 1 : 0; o.best = score; o.ncand = (uint16_t)ncand;
-		// ------------- nextAlignment() sequence until done() -----------------
-		// move the last row into LDS (the row state is no longer needed)
+		// ------------- candidate order (DpBtCandidate: score desc, col desc) --------
+		// the last row moves into LDS; repeated max-below-key scans emit the sorted
+		// candidate columns for the walk kernel
 		for(int q = 0; q < (C + 3) >> 2; q++) {
 			uint32_t w4 = 0;
 			for(int r = 0; r < 4; r++) {
@@ -312,158 +481,34 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 			}
 			lds[q * 64 + lane] = w4;
 		}
-		int cur_key = 0x7fffffff, ndone = 0, nrec = 0;
-		const int row0 = R - 1;
-		while(ndone < ncand) {
-			int ntries = 0;
-			bool found = false;
-			BtResult res;
-			res.nedit = 0;
-			while(ndone < ncand) {
-				// next candidate in DpBtCandidate order: largest key = score*256+col below cur_key
-				// (4 columns per LDS dword; columns >= C hold 0 and never qualify)
-				int best = -1;
-				const int nw = (C + 3) >> 2;
-#pragma unroll 2
-				for(int q = 0; q < nw; q++) {
-					const uint32_t w4 = lds[q * 64 + lane];
-#pragma unroll
-					for(int r = 0; r < 4; r++) {
-						const int s = (int)((w4 >> (8 * r)) & 0xffu);
-						const int key = s * 256 + q * 4 + r;
-						best = (s >= thr && key < cur_key && key > best) ? key : best;
-					}
-				}
-				if(best < 0) { ndone = ncand; break; }   // unreachable: ncand counted above
-				cur_key = best;
-				const int col0 = best & 0xff;
-				if(kDebug && a.cands)
-					a.cands[(size_t)pi * kCols + ndone] = BT2X_CAND_PACK(row0, col0, best >> 8);
-				ndone++;
-				// candidate start cell already traversed -> skipped, no RNG draw
-				if(reinterpret_cast<const uint8_t*>(dir)[tb_addr(row0, col0, lane)] & TB_MARK) continue;
-				ntries++;
-				// ------------- backtraceNucleotidesEnd2EndSseU8 -------------
-				int row = row0, col = col0, ct = 2 /*H*/, bscore = 0, ns = 0, gaps = 0, ne = 0;
-				bool over_core = false, ok = true;
-				int trimBeg = 0;
-				// One dependent load round trip per step: the next cell's traceback byte and
-				// its read/ref/quality bytes are issued before this cell's stores (the mark
-				// byte and the staged edit), so the in-order vmcnt never waits on a store.
-				const uint8_t* dir8 = reinterpret_cast<const uint8_t*>(dir);
-				uint8_t* dirw8 = reinterpret_cast<uint8_t*>(dir);
-				size_t bi = tb_addr(row, col, lane);
-				uint32_t tb = dir8[bi];
-				int rdc = rd[row], refc = rf[col], qch = qu[row];
-				while(true) {
-					st_bt++;
-					if(tb & TB_MARK) { ok = false; break; }         // reportedThrough
-					// the reference's fixed priority over the cell's flags (u8.cpp:843-990)
-					const int emove = (tb & TB_EONE) ? H_RDGAP_EXT : H_READ_OPEN;
-					const int fmove = (tb & TB_FONE) ? H_RFGAP_EXT : H_REF_OPEN;
-					const int move = ct == 0 ? emove : ct == 1 ? fmove
-					               : !(tb & TB_DNE) ? H_DIAG : !(tb & TB_FNE) ? fmove : emove;
-					const bool empty = false;
-					const int diag = col - row + (int)p.triml;
-					if(diag >= 0 && diag >= (int)p.corel && diag <= (int)p.corer) over_core = true;
-					const size_t cur_bi = bi;
-					const uint32_t cur_tb = tb;
-					if(empty || row == 0) {
-						dirw8[cur_bi] = (uint8_t)(cur_tb | TB_MARK);  // setReportedThrough
-						trimBeg = row;
-						break;
-					}
-					const int crow = row, ccol = col, crdc = rdc, crefc = refc, cq = qch;
-					// next cell
-					if(move == H_DIAG) { row--; col--; ct = 2; }
-					else if(move == H_REF_OPEN || move == H_RFGAP_EXT) { row--; ct = (move == H_REF_OPEN) ? 2 : 1; }
-					else { col--; ct = (move == H_READ_OPEN) ? 2 : 0; }
-					bi = tb_addr(row, col, lane);
-					tb = dir8[bi];
-					rdc = rd[row]; refc = rf[col]; qch = qu[row];
-					// stores for the cell just left
-					dirw8[cur_bi] = (uint8_t)(cur_tb | TB_MARK);    // setReportedThrough
-					if(move == H_DIAG) {
-						const bool amb = crdc > 3 || crefc > 3;
-						if(amb || crdc != crefc) {
-							const int q0 = cq - 33;
-							const int q = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
-							stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(crefc), acgtn(crdc));
-							ne++;
-							bscore -= amb ? sc.npen : (int)sc.mmpen[q];
-						}
-						if(amb) ns++;
-					} else if(move == H_REF_OPEN || move == H_RFGAP_EXT) {
-						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(crdc));
-						ne++;
-						bscore -= (move == H_REF_OPEN) ? rfo : rfe;
-						gaps++;
-					} else {
-						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(crefc), '-');
-						ne++;
-						bscore -= (move == H_READ_OPEN) ? rdo : rde;
-						gaps++;
-					}
-					(void)ccol;
-				}
-				if(!ok || !over_core) continue;
-				{
-					const bool amb = rdc > 3 || refc > 3;
-					if(amb || rdc != refc) {
-						const int q0 = qch - 33;
-						const int q = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
-						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
-						ne++;
-						bscore -= amb ? sc.npen : (int)sc.mmpen[q];
-					}
-					if(amb) ns++;
-				}
-				if(ns > p.nceil) continue;
-				int refns = 0;
-				for(int k = col; k <= col0; k++) refns += (rf[k] > 3);
-				const int extent = R - trimBeg - (R - row0 - 1);
-				res.score = bscore; res.ns = ns; res.gaps = gaps; res.nedit = ne;
-				res.bases = extent - ne; res.refns = refns; res.off = col;
-				// publish the edit list in ned() order: reverse(), pos -= trimBeg, and for
-				// the reverse-complement strand invertEdits() (edit.cpp:50-78)
-				const uint32_t eo = atomicAdd(&a.counters[1], (uint32_t)ne);
-				if(eo + (uint32_t)ne <= a.edit_cap) {
-					for(int k = 0; k < ne; k++) {
-						const uint32_t e = stage_ed[(size_t)(p.fw ? ne - 1 - k : k) * 64 + lane];
-						uint32_t pos = (e & 0x3ffu) - (uint32_t)trimBeg;
-						if(!p.fw) pos = (uint32_t)extent - pos - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
-						a.edits[eo + k] = (e & ~0x3ffu) | (pos & 0x3ffu);
-					}
-				}
-				found = true;
-				{
-					bt2x_aln_rec r;
-					r.ntries = (uint16_t)ntries; r.ok = 1; r.pad0 = 0;
-					r.score = (int16_t)res.score; r.ns = (uint16_t)res.ns; r.gaps = (uint16_t)res.gaps;
-					r.nedit = (uint16_t)res.nedit; r.bases_aligned = (uint16_t)res.bases;
-					r.refns = (uint16_t)res.refns; r.refoff = (int64_t)res.off + p.refl;
-					r.edit_off = eo; r.pad1 = 0;
-					stage_rec[(size_t)nrec * 64 + lane] = r;
-				}
-				break;
-			}
-			if(!found) {
-				bt2x_aln_rec r;
-				r.ntries = (uint16_t)ntries; r.ok = 0; r.pad0 = 0; r.score = 0; r.ns = 0; r.gaps = 0;
-				r.nedit = 0; r.bases_aligned = 0; r.refns = 0; r.refoff = 0; r.edit_off = 0; r.pad1 = 0;
-				stage_rec[(size_t)nrec * 64 + lane] = r;
-				nrec++;
-				break;
-			}
-			nrec++;
-		}
-		const uint32_t ro = atomicAdd(&a.counters[0], (uint32_t)nrec);
-		if(ro + (uint32_t)nrec <= a.rec_cap)
-			for(int k = 0; k < nrec; k++) a.recs[ro + k] = stage_rec[(size_t)k * 64 + lane];
-		o.nrec = (uint16_t)nrec; o.rec_off = ro;
 		a.out[pi] = o;
+		int cur_key = 0x7fffffff;
+		const int row0 = R - 1;
+		for(int k = 0; k < ncand; k++) {
+			int best = -1;
+			const int nw = (C + 3) >> 2;
+#pragma unroll 2
+			for(int q = 0; q < nw; q++) {
+				const uint32_t w4 = lds[q * 64 + lane];
+#pragma unroll
+				for(int r = 0; r < 4; r++) {
+					const int s = (int)((w4 >> (8 * r)) & 0xffu);
+					const int key = s * 256 + q * 4 + r;
+					best = (s >= thr && key < cur_key && key > best) ? key : best;
+				}
+			}
+			cur_key = best;
+			cands[(size_t)k * 64 + lane] = (uint8_t)(best & 0xff);
+			if(kDebug && a.cands)
+				a.cands[(size_t)pi * kCols + k] = BT2X_CAND_PACK(row0, best & 0xff, best >> 8);
+		}
 		if(kDebug && a.cands)
 			for(int k = ncand; k < kCols; k++) a.cands[(size_t)pi * kCols + k] = 0xffffffffu;
+		if(kFused) {
+			uint8_t* wslot = gslot + kGroupBytes;
+			walk_problem(sc, a, pi, lane, gslot, reinterpret_cast<uint32_t*>(wslot + kEditOff),
+			             reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt);
+		}
 	}
 	if(a.stats) {
 		for(int d = 32; d > 0; d >>= 1) {
@@ -474,30 +519,101 @@ dp_kernel(DevScoring sc, DpLaunch a) {
 		if(lane == 0) {
 			atomicAdd(&a.stats[0], st_cells);
 			atomicAdd(&a.stats[1], st_cols);
-			atomicAdd(&a.stats[2], st_bt);
+			if(kFused) atomicAdd(&a.stats[2], st_bt);
 		}
+	}
+}
+
+// ------------------------------------------------------------------ walk kernel
+// SwAligner::nextAlignment until done(): per problem, its candidates in order, each
+// not already reportedThrough backtraced over the fill's traceback bytes.  Low VGPR use
+// keeps many waves resident to hide the walk's dependent load chain.
+__global__ void __launch_bounds__(64)
+dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
+	const int lane = threadIdx.x;
+	uint8_t* wslot = a.walk_scratch + (size_t)blockIdx.x * kWalkSlotBytes;
+	uint32_t* stage_ed = reinterpret_cast<uint32_t*>(wslot + kEditOff);
+	bt2x_aln_rec* stage_rec = reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff);
+	unsigned long long st_bt = 0;
+	// one wave per 64-problem group, lane = problem: the lanes' main walks follow nearly
+	// the same diagonal, so their loads of the lane-interleaved bytes share lines
+	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
+		const uint32_t q = grp * 64 + lane;
+		if(q < nprob) {
+			const uint32_t pi = base + q;
+			walk_problem(sc, a, pi, lane, a.scratch + (size_t)grp * kGroupBytes, stage_ed, stage_rec, st_bt);
+		}
+	}
+	if(a.stats) {
+		for(int d = 32; d > 0; d >>= 1) st_bt += __shfl_xor(st_bt, d);
+		if(lane == 0) atomicAdd(&a.stats[2], st_bt);
 	}
 }
 
 } // namespace
 
-size_t bt2x_dp_slot_bytes() { return kSlotBytes; }
-
-// Resident 64-lane workgroups per CU for the DP kernel (VGPR/LDS-limited), so the
-// persistent grid fills the chip exactly once.
-int bt2x_dp_blocks_per_cu() {
+static int blocks_per_cu(const void* fn) {
 	int nb = 0;
-	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dp_kernel<false>, 64, 0) != hipSuccess || nb < 1) nb = 4;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64, 0) != hipSuccess || nb < 1) nb = 2;
 	return nb;
 }
 
-int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream) {
-	if(a.n == 0) return 0;
-	uint32_t waves = (a.n + 63) / 64;
-	if(waves > a.nslots) waves = a.nslots;
-	if(a.digests || a.cands)
-		hipLaunchKernelGGL(dp_kernel<true>, dim3(waves), dim3(64), 0, (hipStream_t)stream, sc, a);
-	else
-		hipLaunchKernelGGL(dp_kernel<false>, dim3(waves), dim3(64), 0, (hipStream_t)stream, sc, a);
+// DP modes: fused (default): one persistent kernel fills and walks each group (the walk
+// reads bytes written moments ago); split: fill kernel over a chunk, then a walk kernel.
+static bool dp_split_mode() {
+	static int m = -1;
+	if(m < 0) { const char* e = getenv("BT2X_DP_MODE"); m = (e && e[0] == 's') ? 1 : 0; }
+	return m == 1;
+}
+
+// Scratch: split = `chunk_groups` fill group regions + one staging slot per resident walk
+// wave; fused = one group region + staging slot per resident fill wave.
+size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups) {
+	if(!dp_split_mode()) {
+		const int nb = max(blocks_per_cu((const void*)dp_fill_kernel<false, true>),
+		                   blocks_per_cu((const void*)dp_fill_kernel<true, true>));
+		return (size_t)ncu * nb * (kGroupBytes + kWalkSlotBytes);
+	}
+	const size_t walk_slots = (size_t)ncu * blocks_per_cu((const void*)dp_walk_kernel);
+	return (size_t)chunk_groups * kGroupBytes + walk_slots * kWalkSlotBytes;
+}
+
+// Split mode runs the batch in chunks of chunk_groups x 64 problems: fill (persistent grid
+// sized by occupancy, VGPR-bound) then walk per chunk, on one stream.
+int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
+	if(a0.n == 0) return 0;
+	hipStream_t s = (hipStream_t)stream;
+	static int fill_bpc_dbg = 0, fill_bpc = 0, fused_bpc_dbg = 0, fused_bpc = 0, walk_bpc = 0;
+	if(!fill_bpc) {
+		fill_bpc = blocks_per_cu((const void*)dp_fill_kernel<false, false>);
+		fill_bpc_dbg = blocks_per_cu((const void*)dp_fill_kernel<true, false>);
+		fused_bpc = blocks_per_cu((const void*)dp_fill_kernel<false, true>);
+		fused_bpc_dbg = blocks_per_cu((const void*)dp_fill_kernel<true, true>);
+		walk_bpc = blocks_per_cu((const void*)dp_walk_kernel);
+	}
+	const bool dbg = a0.digests || a0.cands;
+	DpLaunch a = a0;
+	const uint32_t groups_all = (a0.n + 63) / 64;
+	if(!dp_split_mode()) {
+		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)(dbg ? fused_bpc_dbg : fused_bpc);
+		if(fb > groups_all) fb = groups_all;
+		if(dbg) hipLaunchKernelGGL((dp_fill_kernel<true, true>), dim3(fb), dim3(64), 0, s, sc, a, 0u, a0.n);
+		else hipLaunchKernelGGL((dp_fill_kernel<false, true>), dim3(fb), dim3(64), 0, s, sc, a, 0u, a0.n);
+		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+	}
+	a.walk_scratch = a0.scratch + (size_t)a0.chunk_groups * kGroupBytes;
+	const uint32_t chunk = a0.chunk_groups * 64;
+	for(uint32_t base = 0; base < a0.n; base += chunk) {
+		const uint32_t np = (a0.n - base < chunk) ? a0.n - base : chunk;
+		const uint32_t groups = (np + 63) / 64;
+		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)(dbg ? fill_bpc_dbg : fill_bpc);
+		if(fb > groups) fb = groups;
+		if(dbg) hipLaunchKernelGGL((dp_fill_kernel<true, false>), dim3(fb), dim3(64), 0, s, sc, a, base, np);
+		else hipLaunchKernelGGL((dp_fill_kernel<false, false>), dim3(fb), dim3(64), 0, s, sc, a, base, np);
+		if(a0.ablate == 1) continue;
+		uint32_t wb = (uint32_t)a0.ncu * (uint32_t)walk_bpc;
+		if(wb > groups) wb = groups;
+		hipLaunchKernelGGL(dp_walk_kernel, dim3(wb), dim3(64), 0, s, sc, a, base, np);
+	}
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }

@@ -8,7 +8,7 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_sq/run_counter_col
 d = collections.defaultdict(lambda: collections.defaultdict(float))
 for r in csv.DictReader(open(path)):
     k = r["Kernel_Name"]
-    for tag in ("seed_kernel", "dp_kernel"):
+    for tag in ("seed_kernel", "dp_fill", "dp_walk", "dp_kernel"):
         if tag in k:
             d[tag][r["Counter_Name"]] += float(r["Counter_Value"])
             d[tag]["_vgpr"] = float(r["VGPR_Count"])
