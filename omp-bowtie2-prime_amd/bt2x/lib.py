@@ -54,7 +54,11 @@ FUNCS = {
 
 
 class Bt2xError(RuntimeError):
-    pass
+    """A bt2x_* call returned a negative BT2X_E_* code (kept in .code)."""
+
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code
 
 
 def load():
@@ -75,7 +79,7 @@ def load():
 
 def check(rc: int, what: str) -> None:
     if rc != 0:
-        raise Bt2xError(f"{what} failed with bt2x error {rc}")
+        raise Bt2xError(f"{what} failed with bt2x error {rc}", rc)
 
 
 def default_scoring(**overrides) -> abi.Scoring:

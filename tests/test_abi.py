@@ -93,3 +93,14 @@ def test_cpp_shim_binary_links_and_runs_without_gpu_work():
         subprocess.run(["make", "-C", os.path.dirname(exe)], check=True, capture_output=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_open_rejects_penalties_the_u8_kernel_cannot_pack(golden_dir):
+    """--mp MX > 15 / --np > 15 are refused up front (BT2X_E_ARG), before any device
+    work; the u8 DP kernel packs a row's penalty into 4 bits."""
+    base = g.materialize_index("lambda_virus", str(golden_dir))
+    idx = lib.Index(base)
+    for kw in ({"mm_max": 16, "mm_min": 2}, {"n_pen": 16}):
+        with pytest.raises(lib.Bt2xError) as e:
+            lib.Context(idx, scoring=lib.default_scoring(**kw))
+        assert e.value.code == abi.E_ARG
