@@ -130,7 +130,7 @@ struct bt2x_ctx {
 	bool ev_valid[BT2X_K_COUNT] = {false, false};
 	DevIndex ix{};
 	DevScoring sc{};
-	void* d_ebwt = nullptr; void* d_ftab = nullptr; void* d_eftab = nullptr;
+	void* d_ebwt = nullptr; void* d_ftab = nullptr; void* d_eftab = nullptr; void* d_blk = nullptr;
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
 	DevBuf scratch;
 	int ncu = 0;
@@ -186,6 +186,22 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	c->ix.zbp = (int32_t)(zc & 3);
 	for(int k = 0; k < 5; k++) c->ix.fchr[k] = idx->fchr[k];
 	c->ix.ftab_chars = idx->ftab_chars;
+	c->ix.blk = nullptr;
+	// device re-layout of the BWT into 64-byte blocks (u32 counts: rows < 2^32); the
+	// seed kernel then reads one 64 B block per LF step.  BT2X_FM_SIDES=1 keeps the sides.
+	{
+		const char* e = getenv("BT2X_FM_SIDES");
+		const uint64_t nsides = idx->ebwt_bytes / BT2X_SIDE_BYTES;
+		if(!(e && e[0] == '1') && idx->len + 1 < 0xffffffffULL && nsides > 0) {
+			HIPCHK(hipMalloc(&c->d_blk, 2 * nsides * BT2X_BLK_BYTES + 256));
+			if(bt2x_build_blocks(c->ix, nsides, (uint8_t*)c->d_blk, c->stream)) return BT2X_E_NODEVICE;
+			HIPCHK(hipStreamSynchronize(c->stream));
+			c->ix.blk = (const uint8_t*)c->d_blk;
+			HIPCHK(hipFree(c->d_ebwt));
+			c->d_ebwt = nullptr;
+			c->ix.ebwt = nullptr;
+		}
+	}
 	bt2x_scoring s;
 	if(sc) s = *sc; else bt2x_scoring_default(&s);
 	c->sc = to_dev(s);
@@ -208,7 +224,7 @@ extern "C" void bt2x_close(bt2x_ctx* c) {
 	(void)hipStreamSynchronize(c->stream);
 	for(DevBuf* b : {&c->b_reads, &c->b_quals, &c->b_refs, &c->b_in, &c->b_out, &c->b_recs,
 	                 &c->b_edits, &c->b_dbg_dig, &c->b_dbg_cand, &c->scratch}) b->release();
-	(void)hipFree(c->d_ebwt); (void)hipFree(c->d_ftab); (void)hipFree(c->d_eftab);
+	(void)hipFree(c->d_ebwt); (void)hipFree(c->d_ftab); (void)hipFree(c->d_eftab); (void)hipFree(c->d_blk);
 	(void)hipFree(c->d_stats); (void)hipFree(c->d_counters); (void)hipFree(c->d_queue);
 	for(int k = 0; k < BT2X_K_COUNT; k++) { (void)hipEventDestroy(c->ev[k][0]); (void)hipEventDestroy(c->ev[k][1]); }
 	(void)hipStreamDestroy(c->stream);

@@ -9,7 +9,10 @@
 #include "../../include/bt2x.h"
 
 struct DevIndex {
-	const uint8_t* ebwt;      // numSides * 128 bytes
+	const uint8_t* ebwt;      // numSides * 128 bytes (.bt2l sides, as uploaded)
+	const uint8_t* blk;       // device re-layout (bt2x_build_blocks): 64-byte blocks of 192
+	                          // rows = 4 x u32 occ at the block start + 48 B of BWT; NULL if
+	                          // the text is too long for u32 counts (then sides are used)
 	const uint64_t* ftab;     // 4^ftabChars + 1
 	const uint64_t* eftab;    // 2 * ftabChars
 	uint64_t len;             // joined text length
@@ -28,6 +31,9 @@ struct DevScoring {
 };
 
 // Launch helpers implemented in the kernel translation units.
+#define BT2X_BLK_ROWS 192
+#define BT2X_BLK_BYTES 64
+int bt2x_build_blocks(const DevIndex& ix, uint64_t nsides, uint8_t* d_blk, void* stream);
 int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
                      uint32_t n, int do_extend, bt2x_seed_out* d_out,
                      unsigned long long* d_ctr, int ncu, void* stream);

@@ -79,6 +79,44 @@ __device__ __forceinline__ void count_side(const Side& s, uint32_t c, int offa, 
 	}
 }
 
+// ---- device block layout: 64 B per 192 rows, one HBM burst per LF step ---------------
+// A block is half a .bt2l side with the side's occ[] advanced to its own start, stored
+// as u32 (texts < 2^32 rows), so an LF step counts at most 11 dwords instead of 23 and
+// reads 64 bytes instead of 128.  Counts are identical to countBt2Side's.
+struct Blk {
+	uint32_t occ[4];
+	uint32_t w[12];
+};
+
+__device__ __forceinline__ void load_blk(const DevIndex& ix, uint64_t b, Blk& k) {
+	const uint4* p = reinterpret_cast<const uint4*>(ix.blk + b * BT2X_BLK_BYTES);
+	const uint4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
+	k.occ[0] = v0.x; k.occ[1] = v0.y; k.occ[2] = v0.z; k.occ[3] = v0.w;
+	k.w[0] = v1.x; k.w[1] = v1.y; k.w[2] = v1.z; k.w[3] = v1.w;
+	k.w[4] = v2.x; k.w[5] = v2.y; k.w[6] = v2.z; k.w[7] = v2.w;
+	k.w[8] = v3.x; k.w[9] = v3.y; k.w[10] = v3.z; k.w[11] = v3.w;
+}
+
+__device__ __forceinline__ void count_blk(const Blk& k, uint32_t c, int offa, int offb,
+                                          uint32_t& ca, uint32_t& cb) {
+	const uint32_t pat = c * 0x55555555u;
+	ca = 0; cb = 0;
+#pragma unroll
+	for(int d = 0; d < 12; d++) {
+		const uint32_t m = match_c(k.w[d], pat);
+		const uint32_t wa = (uint32_t)min(max(2 * offa - 32 * d, 0), 31);
+		const uint32_t wb = (uint32_t)min(max(2 * offb - 32 * d, 0), 31);
+		ca += __popc(__builtin_amdgcn_ubfe(m, 0u, wa));
+		cb += __popc(__builtin_amdgcn_ubfe(m, 0u, wb));
+	}
+}
+
+__device__ __forceinline__ uint32_t sel4u(const uint32_t v[4], int c) {
+	const uint32_t lo = (c & 1) ? v[1] : v[0];
+	const uint32_t hi = (c & 1) ? v[3] : v[2];
+	return (c & 2) ? hi : lo;
+}
+
 __device__ __forceinline__ uint64_t ftab_hi(const DevIndex& ix, uint64_t i) {
 	const uint64_t v = ix.ftab[i];
 	return v <= ix.len ? v : ix.eftab[(v ^ OFF_MASK) * 2 + 1];
@@ -128,6 +166,37 @@ __device__ __forceinline__ void lf_step(const DevIndex& ix, uint64_t ra, uint64_
 	}
 }
 
+// LF step over the block layout (same contract as lf_step).
+__device__ __forceinline__ void lf_step_blk(const DevIndex& ix, uint64_t ra, uint64_t rb, uint32_t c,
+                                            bool one_row, uint64_t& na, uint64_t& nb) {
+	const uint64_t ba = ra / BT2X_BLK_ROWS, bb = rb / BT2X_BLK_ROWS;
+	const int offa = (int)(ra - ba * BT2X_BLK_ROWS);
+	const bool same = one_row || bb == ba;
+	const int offb = same ? (int)(rb - ba * BT2X_BLK_ROWS) : (int)(rb - bb * BT2X_BLK_ROWS);
+	const uint64_t zb = ix.zoff / BT2X_BLK_ROWS;
+	const int zo = (int)(ix.zoff - zb * BT2X_BLK_ROWS);
+	const uint64_t fc = fchr_sel(ix, (int)c);
+	Blk k;
+	load_blk(ix, ba, k);
+	uint32_t ka, kb;
+	count_blk(k, c, offa, same ? offb : offa, ka, kb);
+	const uint32_t dla = (c == 0 && ba == zb && zo < offa) ? 1u : 0u;
+	const uint64_t base = (uint64_t)sel4u(k.occ, (int)c) + fc;
+	na = base + (ka - dla);
+	if(same) {
+		const uint32_t dlb = (c == 0 && ba == zb && zo < offb) ? 1u : 0u;
+		nb = base + (kb - dlb);
+	} else {
+		Blk t;
+		load_blk(ix, bb, t);
+		uint32_t kt, kt2;
+		count_blk(t, c, offb, offb, kt, kt2);
+		const uint32_t dlb = (c == 0 && bb == zb && zo < offb) ? 1u : 0u;
+		nb = (uint64_t)sel4u(t.occ, (int)c) + fc + (kt - dlb);
+	}
+}
+
+template<bool kBlk>
 __global__ void __launch_bounds__(256, 4)
 seed_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* __restrict__ in,
             uint32_t n, int do_extend, bt2x_seed_out* __restrict__ out,
@@ -183,7 +252,8 @@ seed_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* 
 				// extension over a read N visits the four characters in four iterations
 				const bool nslow = c == 4;
 				uint64_t na, nb;
-				lf_step(ix, ra, rb, nslow ? (uint32_t)kk : (uint32_t)c, one, na, nb);
+				if(kBlk) lf_step_blk(ix, ra, rb, nslow ? (uint32_t)kk : (uint32_t)c, one, na, nb);
+				else lf_step(ix, ra, rb, nslow ? (uint32_t)kk : (uint32_t)c, one, na, nb);
 				if(!ext) {
 					// searchSeedBi: an empty range ends the search unreported
 					if(nb == na) fin = true;
@@ -236,27 +306,74 @@ seed_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* 
 	}
 }
 
+// Block b = half h of side s = b/2: its 48 BWT bytes, and occ[] at its start = the side's
+// occ[] plus (for h = 1) the counts over the side's first 192 rows, '$' excluded.
+__global__ void __launch_bounds__(256)
+build_blocks_kernel(DevIndex ix, uint64_t nsides, uint8_t* __restrict__ blk) {
+	const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if(b >= 2 * nsides) return;
+	const uint64_t side = b >> 1;
+	const int h = (int)(b & 1);
+	Side s;
+	load_side(ix, side, s);
+	uint32_t occ[4];
+#pragma unroll
+	for(int c = 0; c < 4; c++) {
+		uint32_t n = 0;
+		if(h) {
+#pragma unroll
+			for(int d = 0; d < 12; d++) n += __popc(match_c(s.w[d], (uint32_t)c * 0x55555555u));
+		}
+		occ[c] = (uint32_t)s.occ[c] + n;
+	}
+	const uint64_t zs = ix.zoff / BT2X_SIDE_CHARS;
+	const uint64_t zc = ix.zoff - zs * BT2X_SIDE_CHARS;
+	if(h && zs == side && zc < BT2X_BLK_ROWS) occ[0]--;      // '$' is stored as A
+	uint4* o = reinterpret_cast<uint4*>(blk + b * BT2X_BLK_BYTES);
+	o[0] = make_uint4(occ[0], occ[1], occ[2], occ[3]);
+	uint32_t w[12];
+#pragma unroll
+	for(int d = 0; d < 12; d++) w[d] = h ? s.w[12 + d] : s.w[d];
+	o[1] = make_uint4(w[0], w[1], w[2], w[3]);
+	o[2] = make_uint4(w[4], w[5], w[6], w[7]);
+	o[3] = make_uint4(w[8], w[9], w[10], w[11]);
+}
+
 } // namespace
 
+int bt2x_build_blocks(const DevIndex& ix, uint64_t nsides, uint8_t* d_blk, void* stream) {
+	const uint64_t nb = 2 * nsides;
+	if(nb == 0) return 0;
+	hipLaunchKernelGGL(build_blocks_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
+	                   (hipStream_t)stream, ix, nsides, d_blk);
+	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+}
+
 // Resident 256-thread blocks per CU for the persistent seed grid.
-static int seed_blocks_per_cu() {
-	static int nb = 0;
-	if(nb == 0) {
+static int seed_blocks_per_cu(bool blk) {
+	static int nb[2] = {0, 0};
+	if(nb[blk] == 0) {
 		int v = 0;
-		if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, seed_kernel, 256, 0) != hipSuccess || v < 1) v = 2;
-		nb = v;
+		const void* fn = blk ? (const void*)seed_kernel<true> : (const void*)seed_kernel<false>;
+		if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, 256, 0) != hipSuccess || v < 1) v = 2;
+		nb[blk] = v;
 	}
-	return nb;
+	return nb[blk];
 }
 
 int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
                      uint32_t n, int do_extend, bt2x_seed_out* d_out,
                      unsigned long long* d_ctr, int ncu, void* stream) {
 	if(n == 0) return 0;
-	uint32_t blocks = (uint32_t)(ncu > 0 ? ncu : 256) * (uint32_t)seed_blocks_per_cu();
+	const bool blk = ix.blk != nullptr;
+	uint32_t blocks = (uint32_t)(ncu > 0 ? ncu : 256) * (uint32_t)seed_blocks_per_cu(blk);
 	const uint32_t need = (n + 255) / 256;
 	if(blocks > need) blocks = need;
-	hipLaunchKernelGGL(seed_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-	                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+	if(blk)
+		hipLaunchKernelGGL(seed_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+		                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+	else
+		hipLaunchKernelGGL(seed_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+		                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }
