@@ -166,6 +166,37 @@ __device__ __forceinline__ void lf_step(const DevIndex& ix, uint64_t ra, uint64_
 	}
 }
 
+// LF step over the block layout, 32-bit rows (texts < 2^32 rows; same contract as lf_step).
+__device__ __forceinline__ void lf_step_blk32(const DevIndex& ix, uint32_t ra, uint32_t rb, uint32_t c,
+                                              bool one_row, uint32_t& na, uint32_t& nb) {
+	const uint32_t ba = ra / BT2X_BLK_ROWS, bb = rb / BT2X_BLK_ROWS;
+	const int offa = (int)(ra - ba * BT2X_BLK_ROWS);
+	const bool same = one_row || bb == ba;
+	const int offb = same ? (int)(rb - ba * BT2X_BLK_ROWS) : (int)(rb - bb * BT2X_BLK_ROWS);
+	const uint32_t zoff = (uint32_t)ix.zoff;
+	const uint32_t zb = zoff / BT2X_BLK_ROWS;
+	const int zo = (int)(zoff - zb * BT2X_BLK_ROWS);
+	const uint32_t fc = (uint32_t)fchr_sel(ix, (int)c);
+	Blk k;
+	load_blk(ix, ba, k);
+	uint32_t ka, kb;
+	count_blk(k, c, offa, same ? offb : offa, ka, kb);
+	const uint32_t dla = (c == 0 && ba == zb && zo < offa) ? 1u : 0u;
+	const uint32_t base = sel4u(k.occ, (int)c) + fc;
+	na = base + ka - dla;
+	if(same) {
+		const uint32_t dlb = (c == 0 && ba == zb && zo < offb) ? 1u : 0u;
+		nb = base + kb - dlb;
+	} else {
+		Blk t;
+		load_blk(ix, bb, t);
+		uint32_t kt, kt2;
+		count_blk(t, c, offb, offb, kt, kt2);
+		const uint32_t dlb = (c == 0 && bb == zb && zo < offb) ? 1u : 0u;
+		nb = sel4u(t.occ, (int)c) + fc + kt - dlb;
+	}
+}
+
 // LF step over the block layout (same contract as lf_step).
 __device__ __forceinline__ void lf_step_blk(const DevIndex& ix, uint64_t ra, uint64_t rb, uint32_t c,
                                             bool one_row, uint64_t& na, uint64_t& nb) {
@@ -306,6 +337,136 @@ seed_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* 
 	}
 }
 
+// startSearchSeedBi for every seed (aligner_seed.cpp:757-811): the ftab jump over the
+// rightmost ftabChars characters (or the fchr range of one character), in a pre-pass so
+// its dependent read -> ftab -> eftab loads overlap across all seeds instead of stalling
+// the LF loop.  State per seed in out[]: topf/botf = range, nlex = steps consumed,
+// pad[0] = 0 continue, 1 empty (done, unreported), 2 matched (report, then extend).
+__global__ void __launch_bounds__(256)
+seed_init_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* __restrict__ in,
+                 uint32_t n, bt2x_seed_out* __restrict__ out, unsigned long long* __restrict__ ctr) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	uint32_t n_ftab = 0;
+	if(i < n) {
+		const bt2x_seed_in p = in[i];
+		const uint8_t* seq = reads + p.read_off + p.seed_off;
+		const int nsteps = p.seed_len, off = nsteps - 1, fc = ix.ftab_chars;
+		uint64_t top, bot;
+		int step;
+		if(fc > 1 && fc <= nsteps) {
+			uint64_t fi = 0;
+			for(int k = 0; k < fc; k++) fi = (fi << 2) | (uint64_t)(seq[off - fc + 1 + k] & 3);
+			top = ftab_hi(ix, fi);
+			bot = ftab_lo(ix, fi + 1);
+			n_ftab = 1;
+			step = fc;
+		} else {
+			const int c = seq[off];
+			top = fchr_sel(ix, c); bot = fchr_sel(ix, c + 1);
+			step = 1;
+		}
+		bt2x_seed_out o;
+		o.topf = top; o.botf = bot; o.nlex = (uint8_t)step; o.need_reporting = 0;
+#pragma unroll
+		for(int k = 0; k < 6; k++) o.pad[k] = 0;
+		o.pad[0] = bot == top ? 1 : (step == nsteps ? 2 : 0);
+		out[i] = o;
+	}
+	if(ctr) {
+		for(int d = 32; d > 0; d >>= 1) n_ftab += __shfl_xor(n_ftab, d);
+		if((threadIdx.x & 63) == 0) atomicAdd(&ctr[2], (unsigned long long)n_ftab);
+	}
+}
+
+// The LF loop over the block layout with 32-bit rows; starts from seed_init_kernel's state.
+__global__ void __launch_bounds__(256, 4)
+seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* __restrict__ in,
+                uint32_t n, int do_extend, bt2x_seed_out* __restrict__ out,
+                unsigned long long* __restrict__ ctr) {
+	const uint32_t stride = gridDim.x * blockDim.x;
+	uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+	uint32_t n_bilf = 0, n_lf1 = 0;
+	int phase = PH_START;
+	const uint8_t* seq = nullptr;
+	int nsteps = 0, step = 0, lim = 0, ii = 0, nlex = 0;
+	uint32_t top = 0, bot = 0, etop = 0, ebot = 0, ntop = 0, nbot = 0;
+	int kk = 0, nz = 0;
+	bool report = false;
+	while(true) {
+		bool fin = false;
+		if(phase == PH_START) {
+			if(idx >= n) {
+				phase = PH_EXIT;
+			} else {
+				const bt2x_seed_in p = in[idx];
+				const bt2x_seed_out s0 = out[idx];
+				seq = reads + p.read_off + p.seed_off;
+				nsteps = p.seed_len;
+				lim = do_extend ? p.seed_off : 0;
+				ii = 0; nlex = 0;
+				top = (uint32_t)s0.topf; bot = (uint32_t)s0.botf; step = s0.nlex;
+				report = s0.pad[0] == 2;
+				if(s0.pad[0] == 1) fin = true;
+				else if(report) { etop = top; ebot = bot; phase = PH_EXTEND; fin = lim == 0; }
+				else phase = PH_SEARCH;
+			}
+		} else if(phase != PH_EXIT) {
+			const bool ext = phase == PH_EXTEND;
+			const uint32_t ra = ext ? etop : top, rb = ext ? ebot : bot;
+			const bool one = rb - ra == 1;
+			const int c = ext ? seq[-1 - ii] : seq[nsteps - step - 1];
+			if(kk == 0) { if(one) n_lf1 += (!ext && c == 4) ? 0u : 1u; else n_bilf++; }
+			if(!ext && c == 4) {
+				fin = true;                       // N in the seed: searchSeedBi drops it
+			} else {
+				const bool nslow = c == 4;
+				uint32_t na, nb;
+				lf_step_blk32(ix, ra, rb, nslow ? (uint32_t)kk : (uint32_t)c, one, na, nb);
+				if(!ext) {
+					if(nb == na) fin = true;
+					else {
+						top = na; bot = nb; step++;
+						if(step == nsteps) { report = true; etop = top; ebot = bot; phase = PH_EXTEND; fin = lim == 0; }
+					}
+				} else if(!nslow) {
+					if(nb - na != rb - ra) fin = true;
+					else { etop = na; ebot = nb; ii++; nlex++; fin = (nlex == 255) || (ii == lim); }
+				} else {
+					if(nb > na) { nz++; if(nz == 1) { ntop = na; nbot = nb; } }
+					if(++kk == 4) {
+						if(nz == 0) { ntop = ra; nbot = one ? ra + 1 : rb; }
+						else if(one) nbot = ntop + 1;
+						if(nz > 1 || (!one && nbot - ntop < rb - ra)) fin = true;
+						else { etop = ntop; ebot = nbot; ii++; nlex++; fin = (nlex == 255) || (ii == lim); }
+						kk = 0; nz = 0;
+					}
+				}
+			}
+		}
+		if(fin) {
+			bt2x_seed_out o;
+			o.topf = top; o.botf = bot; o.nlex = (uint8_t)nlex;
+			o.need_reporting = report ? 1 : 0;
+#pragma unroll
+			for(int k = 0; k < 6; k++) o.pad[k] = 0;
+			out[idx] = o;
+			idx += stride;
+			phase = PH_START;
+		}
+		if(__all(phase == PH_EXIT)) break;
+	}
+	if(ctr) {
+		for(int d = 32; d > 0; d >>= 1) {
+			n_bilf += __shfl_xor(n_bilf, d);
+			n_lf1 += __shfl_xor(n_lf1, d);
+		}
+		if((threadIdx.x & 63) == 0) {
+			atomicAdd(&ctr[0], (unsigned long long)n_bilf);
+			atomicAdd(&ctr[1], (unsigned long long)n_lf1);
+		}
+	}
+}
+
 // Block b = half h of side s = b/2: its 48 BWT bytes, and occ[] at its start = the side's
 // occ[] plus (for h = 1) the counts over the side's first 192 rows, '$' excluded.
 __global__ void __launch_bounds__(256)
@@ -354,7 +515,7 @@ static int seed_blocks_per_cu(bool blk) {
 	static int nb[2] = {0, 0};
 	if(nb[blk] == 0) {
 		int v = 0;
-		const void* fn = blk ? (const void*)seed_kernel<true> : (const void*)seed_kernel<false>;
+		const void* fn = blk ? (const void*)seed_kernel_blk : (const void*)seed_kernel<false>;
 		if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, 256, 0) != hipSuccess || v < 1) v = 2;
 		nb[blk] = v;
 	}
@@ -369,9 +530,12 @@ int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed
 	uint32_t blocks = (uint32_t)(ncu > 0 ? ncu : 256) * (uint32_t)seed_blocks_per_cu(blk);
 	const uint32_t need = (n + 255) / 256;
 	if(blocks > need) blocks = need;
-	if(blk)
-		hipLaunchKernelGGL(seed_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+	if(blk) {
+		hipLaunchKernelGGL(seed_init_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+		                   ix, d_reads, d_in, n, d_out, d_ctr);
+		hipLaunchKernelGGL(seed_kernel_blk, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
 		                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+	}
 	else
 		hipLaunchKernelGGL(seed_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
 		                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
