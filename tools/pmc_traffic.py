@@ -19,14 +19,22 @@ import os
 import shutil
 from collections import defaultdict
 
-KERNELS = {"seed": "seed_kernel", "dp": "dp_kernel"}
+# logical op -> the kernels one call launches (per-launch figures are summed over them)
+KERNELS = {"seed": ("seed_init_kernel", "seed_kernel"), "dp": ("dp_fill_kernel", "dp_walk_kernel", "dp_kernel")}
 
 
 def short(name: str) -> str | None:
-    for k, pat in KERNELS.items():
-        if pat in name:
-            return k
+    for k, pats in KERNELS.items():
+        for pat in pats:
+            if pat in name:
+                return k
     return None
+
+
+def kname(name: str) -> str:
+    """Kernel identity within a logical op (template arguments and namespaces dropped)."""
+    base = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return base.split("(")[0].split("<")[0].strip()
 
 
 def main() -> None:
@@ -41,7 +49,7 @@ def main() -> None:
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(a.src, "prof_kt", "run_kernel_stats.csv"),
                 os.path.join(out, f"{a.tag}_kernel_stats.csv"))
-    dur = defaultdict(list)
+    dur = defaultdict(lambda: defaultdict(list))
     with open(os.path.join(a.src, "prof_kt", "run_kernel_trace.csv")) as f, \
             open(os.path.join(out, f"{a.tag}_bt2x_trace.csv"), "w", newline="") as g:
         rd = csv.DictReader(f)
@@ -51,8 +59,8 @@ def main() -> None:
             k = short(r["Kernel_Name"])
             if k:
                 wr.writerow(r)
-                dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    ctr = defaultdict(lambda: defaultdict(list))
+                dur[k][kname(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    ctr = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
     rows = []
     for sub in ("prof_fetch", "prof_write"):
         p = os.path.join(a.src, sub, "run_counter_collection.csv")
@@ -62,7 +70,7 @@ def main() -> None:
                 k = short(r["Kernel_Name"])
                 if k:
                     rows.append(r)
-                    ctr[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                    ctr[k][r["Counter_Name"]][kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     if rows:
         with open(os.path.join(out, f"{a.tag}_pmc.csv"), "w", newline="") as g:
             wr = csv.DictWriter(g, fieldnames=list(rows[0].keys()))
@@ -71,20 +79,24 @@ def main() -> None:
     res = {"workload": a.workload, "command": a.cmd,
            "correction": "traffic = 2 x FETCH_SIZE(KiB) x 1024 + WRITE_SIZE(KiB) x 1024 per launch "
                          "(gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM section); Infinity-Cache "
-                         "hits are included by the counters",
+                         "hits are included by the counters; per-call figures sum the op's kernels",
            "kernels": {}}
+
+    def per_call(d):            # mean per launch of each kernel, summed over the op's kernels
+        return sum(sum(v) / len(v) for v in d.values() if v)
+
     for k in KERNELS:
-        f = ctr[k].get("FETCH_SIZE", [])
-        w = ctr[k].get("WRITE_SIZE", [])
-        d = dur.get(k, [])
+        f = ctr[k].get("FETCH_SIZE", {})
+        w = ctr[k].get("WRITE_SIZE", {})
         if not f or not w:
             continue
-        fetch = sum(f) / len(f) * 1024 * 2
-        write = sum(w) / len(w) * 1024
+        fetch = per_call(f) * 1024 * 2
+        write = per_call(w) * 1024
         res["kernels"][k] = {"fetch_bytes": round(fetch), "write_bytes": round(write),
-                             "traffic_bytes": round(fetch + write), "launches_fetch": len(f),
-                             "launches_write": len(w),
-                             "avg_duration_ms": round(sum(d) / len(d) / 1e6, 4) if d else None}
+                             "traffic_bytes": round(fetch + write),
+                             "kernels": sorted(set(f) | set(w)),
+                             "avg_duration_ms": round(per_call(dur[k]) / 1e6, 4) if dur.get(k) else None,
+                             "per_kernel_ms": {n: round(sum(v) / len(v) / 1e6, 4) for n, v in dur[k].items()}}
     with open(os.path.join(out, f"{a.tag}_traffic.json"), "w") as g:
         json.dump(res, g, indent=1)
     print(json.dumps(res, indent=1))
