@@ -149,7 +149,7 @@ def main():
                                                              reads, quals, maxhalf=args.dpad)
     nseed, ndp = len(sin), len(dpin)
 
-    idx = lib.Index(base)
+    idx = lib.Index(base, load_offs=True)     # SA sample + text: full SA rebuilt in HBM
     ctx = lib.Context(idx, device=local)
     dev = torch.device("cuda", local)
 

@@ -69,10 +69,15 @@ typedef struct {
 	const uint64_t* offs;    uint64_t offs_len;    /* _offs (SA sample, .2.bt2l)  */
 	const uint64_t* plen;    uint64_t npat;        /* _plen: reference lengths    */
 	const uint64_t* rstarts; uint64_t nfrag;       /* _rstarts: 3 words/fragment  */
+	const uint8_t*  text2;   uint64_t text2_bytes; /* joined text, 2 bits/base LSB-first
+	                                                  (.4.bt2l, BitPairReference)      */
 	void* owner;             /* loader-owned storage (bt2x_index_free) */
 } bt2x_index_desc;
 
-/* Parse <base>.1.bt2l (+ <base>.2.bt2l when load_offs) like Ebwt::readIntoMemory. */
+/* Parse <base>.1.bt2l like Ebwt::readIntoMemory; with load_offs also <base>.2.bt2l (SA
+ * sample) and <base>.4.bt2l (packed joined text).  Given both, bt2x_open rebuilds the
+ * full suffix array in HBM (an MI355X-first choice: 4 B/row resident, so SA lookups
+ * and unique-range seed extension need no LF walks). */
 int  bt2x_index_load(const char* basename, int load_offs, bt2x_index_desc* out);
 void bt2x_index_free(bt2x_index_desc* idx);
 
@@ -248,6 +253,10 @@ static inline uint64_t bt2x_cell_digest(uint32_t row, uint32_t col, uint32_t mat
 	z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
 	return z ^ (z >> 31);
 }
+
+/* Rows [first, first+n) of the device-resident full suffix array (BT2X_E_ARG if the
+ * context has none: no SA sample/text loaded, or a text of 2^32 rows or more). */
+int bt2x_suffix_array(bt2x_ctx* ctx, uint64_t first, uint64_t n, uint32_t* out);
 
 const char* bt2x_version(void);
 /* sizeof of the ABI structs (seed_in, seed_out, dp_in, dp_out, aln_rec, scoring,

@@ -53,6 +53,7 @@ class IndexDesc(ctypes.Structure):
                 ("offs", ctypes.c_void_p), ("offs_len", ctypes.c_uint64),
                 ("plen", ctypes.c_void_p), ("npat", ctypes.c_uint64),
                 ("rstarts", ctypes.c_void_p), ("nfrag", ctypes.c_uint64),
+                ("text2", ctypes.c_void_p), ("text2_bytes", ctypes.c_uint64),
                 ("owner", ctypes.c_void_p)]
 
     def array(self, name: str, dtype, count_field: str) -> np.ndarray:

@@ -45,6 +45,7 @@ FUNCS = {
                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                          ctypes.POINTER(abi.DpDebug), ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
+    "bt2x_suffix_array": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
     "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
     "bt2x_build_index_sa": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -190,6 +191,14 @@ class Context:
     # ------------------------------------------------------------ metrics
     def last_kernel_ms(self, kernel: int) -> float:
         return float(load().bt2x_last_kernel_ms(self.h, kernel))
+
+    def suffix_array(self, first: int = 0, n: int | None = None) -> np.ndarray:
+        """Rows [first, first+n) of the device-resident full suffix array (uint32)."""
+        if n is None:
+            n = int(self.index.desc.len) + 1 - first
+        out = np.zeros(n, dtype=np.uint32)
+        check(load().bt2x_suffix_array(self.h, first, n, abi.ptr(out)), "bt2x_suffix_array")
+        return out
 
     def last_counters(self, kernel: int) -> dict:
         c = abi.Counters()

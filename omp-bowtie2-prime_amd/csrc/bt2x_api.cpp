@@ -75,6 +75,17 @@ extern "C" int bt2x_index_load(const char* base, int load_offs, bt2x_index_desc*
 		fclose(f);
 		if(!ok) return BT2X_E_IO;
 		o->offs = offs; o->offs_len = offsLen;
+		// packed joined text (BitPairReference .4: the non-N bases, 4 per byte)
+		std::string p4 = std::string(base) + ".4.bt2l";
+		f = fopen(p4.c_str(), "rb");
+		if(f) {
+			const uint64_t tb = (len + 3) / 4;
+			uint8_t* t = take<uint8_t>(own.get(), tb + 16);
+			ok = read_exact(f, t, tb);
+			fclose(f);
+			if(!ok) return BT2X_E_IO;
+			o->text2 = t; o->text2_bytes = tb;
+		}
 	}
 	o->owner = own.release();
 	return BT2X_OK;
@@ -131,6 +142,7 @@ struct bt2x_ctx {
 	DevIndex ix{};
 	DevScoring sc{};
 	void* d_ebwt = nullptr; void* d_ftab = nullptr; void* d_eftab = nullptr; void* d_blk = nullptr;
+	void* d_sa = nullptr; void* d_text = nullptr;
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
 	DevBuf scratch;
 	int ncu = 0;
@@ -202,6 +214,29 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 			c->ix.ebwt = nullptr;
 		}
 	}
+	// full suffix array + packed text in HBM (needs the SA sample and .4 text; load_offs)
+	c->ix.off_rate = idx->off_rate;
+	c->ix.sa = nullptr; c->ix.text = nullptr;
+	{
+		const char* e = getenv("BT2X_FULL_SA");
+		if(!(e && e[0] == '0') && c->ix.blk && idx->offs && idx->offs_len && idx->text2 &&
+		   idx->off_rate >= 0 && idx->off_rate < 16) {
+			const size_t tbytes = ((idx->text2_bytes + 3) & ~(size_t)3) + 64;
+			HIPCHK(hipMalloc(&c->d_text, tbytes));
+			HIPCHK(hipMemset(c->d_text, 0, tbytes));
+			HIPCHK(hipMemcpy(c->d_text, idx->text2, idx->text2_bytes, hipMemcpyHostToDevice));
+			HIPCHK(hipMalloc(&c->d_sa, (idx->len + 1) * sizeof(uint32_t) + 64));
+			void* d_offs = nullptr;
+			HIPCHK(hipMalloc(&d_offs, idx->offs_len * sizeof(uint64_t)));
+			HIPCHK(hipMemcpy(d_offs, idx->offs, idx->offs_len * sizeof(uint64_t), hipMemcpyHostToDevice));
+			const int rc = bt2x_build_sa(c->ix, (const uint64_t*)d_offs, idx->offs_len, (uint32_t*)c->d_sa, c->stream);
+			HIPCHK(hipStreamSynchronize(c->stream));
+			(void)hipFree(d_offs);
+			if(rc) return rc;
+			c->ix.sa = (const uint32_t*)c->d_sa;
+			c->ix.text = (const uint32_t*)c->d_text;
+		}
+	}
 	bt2x_scoring s;
 	if(sc) s = *sc; else bt2x_scoring_default(&s);
 	c->sc = to_dev(s);
@@ -225,6 +260,7 @@ extern "C" void bt2x_close(bt2x_ctx* c) {
 	for(DevBuf* b : {&c->b_reads, &c->b_quals, &c->b_refs, &c->b_in, &c->b_out, &c->b_recs,
 	                 &c->b_edits, &c->b_dbg_dig, &c->b_dbg_cand, &c->scratch}) b->release();
 	(void)hipFree(c->d_ebwt); (void)hipFree(c->d_ftab); (void)hipFree(c->d_eftab); (void)hipFree(c->d_blk);
+	(void)hipFree(c->d_sa); (void)hipFree(c->d_text);
 	(void)hipFree(c->d_stats); (void)hipFree(c->d_counters); (void)hipFree(c->d_queue);
 	for(int k = 0; k < BT2X_K_COUNT; k++) { (void)hipEventDestroy(c->ev[k][0]); (void)hipEventDestroy(c->ev[k][1]); }
 	(void)hipStreamDestroy(c->stream);
@@ -407,4 +443,13 @@ extern "C" int bt2x_abi_sizes(uint32_t* out, int n) {
 	const int m = (int)(sizeof s / sizeof s[0]);
 	for(int i = 0; i < n && i < m; i++) out[i] = s[i];
 	return m;
+}
+
+extern "C" int bt2x_suffix_array(bt2x_ctx* c, uint64_t first, uint64_t n, uint32_t* out) {
+	if(!c || !out) return BT2X_E_ARG;
+	if(!c->ix.sa) return BT2X_E_ARG;
+	if(first + n > c->ix.len + 1) return BT2X_E_ARG;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipMemcpy(out, c->ix.sa + first, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+	return BT2X_OK;
 }

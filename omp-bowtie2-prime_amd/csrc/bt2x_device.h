@@ -21,6 +21,9 @@ struct DevIndex {
 	uint64_t fchr[5];
 	int32_t zbp;              // bit-pair of '$' within zbyte
 	int32_t ftab_chars;
+	int32_t off_rate;
+	const uint32_t* sa;       // full suffix array (rows 0..len), rebuilt in HBM at open; or NULL
+	const uint32_t* text;     // joined text, 16 bases per u32 (LSB-first); with sa
 };
 
 struct DevScoring {
@@ -34,6 +37,7 @@ struct DevScoring {
 #define BT2X_BLK_ROWS 192
 #define BT2X_BLK_BYTES 64
 int bt2x_build_blocks(const DevIndex& ix, uint64_t nsides, uint8_t* d_blk, void* stream);
+int bt2x_build_sa(const DevIndex& ix, const uint64_t* d_offs, uint64_t noffs, uint32_t* d_sa, void* stream);
 int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
                      uint32_t n, int do_extend, bt2x_seed_out* d_out,
                      unsigned long long* d_ctr, int ncu, void* stream);

@@ -389,9 +389,9 @@ seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_
 	int phase = PH_START;
 	const uint8_t* seq = nullptr;
 	int nsteps = 0, step = 0, lim = 0, ii = 0, nlex = 0;
-	uint32_t top = 0, bot = 0, etop = 0, ebot = 0, ntop = 0, nbot = 0;
+	uint32_t top = 0, bot = 0, etop = 0, ebot = 0, ntop = 0, nbot = 0, tp = 0;
 	int kk = 0, nz = 0;
-	bool report = false;
+	bool report = false, tmode = false;
 	while(true) {
 		bool fin = false;
 		if(phase == PH_START) {
@@ -406,10 +406,37 @@ seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_
 				ii = 0; nlex = 0;
 				top = (uint32_t)s0.topf; bot = (uint32_t)s0.botf; step = s0.nlex;
 				report = s0.pad[0] == 2;
+				tmode = false;
 				if(s0.pad[0] == 1) fin = true;
 				else if(report) { etop = top; ebot = bot; phase = PH_EXTEND; fin = lim == 0; }
 				else phase = PH_SEARCH;
+				if(phase == PH_EXTEND && !fin && ix.sa && ebot - etop == 1) { tmode = true; tp = ix.sa[etop]; }
 			}
+		} else if(phase == PH_EXTEND && tmode) {
+			// extend() over a one-row range in text terms: row etop is the suffix at text
+			// position tp, its LF step reads text[tp-1]; up to 16 steps per iteration.
+			// Same outcomes as the LF1 walk: a read N matches anything, text position 0
+			// (row zOff) keeps its row and only read Ns pass it (aligner_seed.cpp:655-664).
+			const int cap = min(lim, 255);
+			const uint32_t hi = tp > 0 ? (tp - 1) >> 4 : 0;
+			const uint32_t whi = tp > 0 ? ix.text[hi] : 0u, wlo = hi > 0 ? ix.text[hi - 1] : 0u;
+			bool stop = false;
+#pragma unroll
+			for(int j = 0; j < 16; j++) {
+				if(!stop && ii < cap) {
+					const int rdc = seq[-1 - ii];
+					n_lf1++;
+					if(tp == 0) {
+						if(rdc <= 3) stop = true; else { ii++; nlex++; }
+					} else {
+						const uint32_t pos = tp - 1;
+						const uint32_t w = (pos >> 4) == hi ? whi : wlo;
+						const int t = (int)((w >> (2 * (pos & 15))) & 3u);
+						if(rdc <= 3 && t != rdc) stop = true; else { tp--; ii++; nlex++; }
+					}
+				}
+			}
+			fin = stop || ii == lim || nlex == 255;
 		} else if(phase != PH_EXIT) {
 			const bool ext = phase == PH_EXTEND;
 			const uint32_t ra = ext ? etop : top, rb = ext ? ebot : bot;
@@ -426,7 +453,10 @@ seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_
 					if(nb == na) fin = true;
 					else {
 						top = na; bot = nb; step++;
-						if(step == nsteps) { report = true; etop = top; ebot = bot; phase = PH_EXTEND; fin = lim == 0; }
+						if(step == nsteps) {
+							report = true; etop = top; ebot = bot; phase = PH_EXTEND; fin = lim == 0;
+							if(!fin && ix.sa && ebot - etop == 1) { tmode = true; tp = ix.sa[etop]; }
+						}
 					}
 				} else if(!nslow) {
 					if(nb - na != rb - ra) fin = true;
@@ -467,6 +497,46 @@ seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_
 	}
 }
 
+// BWT character of row r (the block's 2-bit code; row zOff holds '$' stored as A).
+__device__ __forceinline__ uint32_t row_l_blk32(const DevIndex& ix, uint32_t r) {
+	const uint32_t b = r / BT2X_BLK_ROWS, off = r - b * BT2X_BLK_ROWS;
+	Blk k;
+	load_blk(ix, b, k);
+	const uint32_t q = off >> 4;
+	uint32_t w = 0;
+#pragma unroll
+	for(int d = 0; d < 12; d++) w = ((uint32_t)d == q) ? k.w[d] : w;
+	return (w >> (2 * (off & 15))) & 3u;
+}
+
+// Full suffix array from the SA sample (Ebwt::_offs, rows r with r % 2^offRate == 0):
+// from each sampled row walk LF (text position - 1 per step) until the next sampled row;
+// the LF cycle visits every row once, so every row is written exactly once.  LF of zOff
+// (text position 0) wraps to the '$' row len (position len).
+__global__ void __launch_bounds__(256)
+sa_fill_kernel(DevIndex ix, const uint64_t* __restrict__ offs, uint64_t noffs, uint32_t* __restrict__ sa) {
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if(i >= noffs) return;
+	const uint32_t len = (uint32_t)ix.len, zoff = (uint32_t)ix.zoff;
+	const uint32_t mask = (1u << ix.off_rate) - 1u;
+	uint32_t r = (uint32_t)(i << ix.off_rate);
+	if(r > len) return;
+	uint32_t p = (uint32_t)offs[i];
+	for(uint32_t guard = 0; guard <= len; guard++) {
+		sa[r] = p;
+		uint32_t rn;
+		if(r == zoff) { rn = len; p = len; }
+		else {
+			const uint32_t c = row_l_blk32(ix, r);
+			uint32_t na, nb;
+			lf_step_blk32(ix, r, r + 1, c, true, na, nb);
+			rn = na; p = p - 1;
+		}
+		if((rn & mask) == 0) break;                // sampled: written by its own thread
+		r = rn;
+	}
+}
+
 // Block b = half h of side s = b/2: its 48 BWT bytes, and occ[] at its start = the side's
 // occ[] plus (for h = 1) the counts over the side's first 192 rows, '$' excluded.
 __global__ void __launch_bounds__(256)
@@ -501,6 +571,13 @@ build_blocks_kernel(DevIndex ix, uint64_t nsides, uint8_t* __restrict__ blk) {
 }
 
 } // namespace
+
+int bt2x_build_sa(const DevIndex& ix, const uint64_t* d_offs, uint64_t noffs, uint32_t* d_sa, void* stream) {
+	if(noffs == 0 || !ix.blk) return BT2X_E_ARG;
+	hipLaunchKernelGGL(sa_fill_kernel, dim3((unsigned)((noffs + 255) / 256)), dim3(256), 0,
+	                   (hipStream_t)stream, ix, d_offs, noffs, d_sa);
+	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+}
 
 int bt2x_build_blocks(const DevIndex& ix, uint64_t nsides, uint8_t* d_blk, void* stream) {
 	const uint64_t nb = 2 * nsides;

@@ -21,7 +21,7 @@ def ctxs(golden_dir):
     out = {}
     for name in ("lambda_virus", "rep"):
         base = g.materialize_index(name, str(golden_dir))
-        idx = lib.Index(base)
+        idx = lib.Index(base, load_offs=True)            # SA sample + text: full SA in HBM
         out[name] = (lib.Context(idx), ol.OracleIndex(base))
     return out
 
@@ -193,3 +193,39 @@ def test_cpp_host_shims_match_golden(golden_dir, tmp_path, gold, mode, limit):
         assert gn == ns, (i, gn, ns)
         ncalls += len(ns)
     assert ncalls > 0
+
+
+@pytest.mark.parametrize("name,fasta", [("lambda_virus", "lambda_virus.fa"), ("rep", "rep.fa.xz")])
+def test_device_full_suffix_array(ctxs, tmp_path, name, fasta):
+    """The suffix array rebuilt in HBM from the SA sample (LF walks from sampled rows)
+    equals the suffix array of the joined text (tools/gpu_sa.py on the CPU)."""
+    import lzma
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(g.HERE), "tools"))
+    import gpu_sa
+    import simdata as sd
+    src = os.path.join(g.GOLDEN, fasta)
+    fa = str(tmp_path / "in.fa")
+    with (lzma.open(src, "rb") if src.endswith(".xz") else open(src, "rb")) as fi, open(fa, "wb") as fo:
+        fo.write(fi.read())
+    codes, _ = sd.concat_genome(sd.read_fasta(fa))
+    sa, _, _ = gpu_sa.suffix_array(codes[codes < 4], device="cpu")
+    ctx = ctxs[name][0]
+    got = ctx.suffix_array()
+    np.testing.assert_array_equal(got, sa.astype(np.uint32))
+
+
+def test_seed_kernel_lf_extension_path(golden_dir, monkeypatch):
+    """Without the full SA (BT2X_FULL_SA=0) unique-range extension runs as LF walks;
+    same results against the reference golden."""
+    monkeypatch.setenv("BT2X_FULL_SA", "0")
+    base = g.materialize_index("rep", str(golden_dir))
+    ctx = lib.Context(lib.Index(base, load_offs=True))
+    case = g.SeedCase(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), os.path.join(g.GOLDEN, "seeds_rep.txt.xz"))
+    out = ctx.seed_search(case.reads, case.inp, do_extend=True)
+    np.testing.assert_array_equal(out["topf"], case.exp_topf)
+    np.testing.assert_array_equal(out["botf"], case.exp_botf)
+    np.testing.assert_array_equal(out["nlex"], case.exp_nlex)
+    np.testing.assert_array_equal(out["need_reporting"], case.exp_rep)
+    with pytest.raises(lib.Bt2xError):
+        ctx.suffix_array(0, 1)
