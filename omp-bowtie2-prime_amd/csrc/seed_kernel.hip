@@ -378,14 +378,16 @@ seed_init_kernel(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed
 	}
 }
 
-// The LF loop over the block layout with 32-bit rows; starts from seed_init_kernel's state.
+// The LF loop over the block layout with 32-bit rows.  kInit: the ftab start was done
+// by seed_init_kernel (state in out[]); otherwise the START phase does it inline.
+template<bool kInit>
 __global__ void __launch_bounds__(256, 4)
 seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_in* __restrict__ in,
                 uint32_t n, int do_extend, bt2x_seed_out* __restrict__ out,
                 unsigned long long* __restrict__ ctr) {
 	const uint32_t stride = gridDim.x * blockDim.x;
 	uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-	uint32_t n_bilf = 0, n_lf1 = 0;
+	uint32_t n_bilf = 0, n_lf1 = 0, n_ftab = 0;
 	int phase = PH_START;
 	const uint8_t* seq = nullptr;
 	int nsteps = 0, step = 0, lim = 0, ii = 0, nlex = 0;
@@ -399,15 +401,34 @@ seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_
 				phase = PH_EXIT;
 			} else {
 				const bt2x_seed_in p = in[idx];
-				const bt2x_seed_out s0 = out[idx];
 				seq = reads + p.read_off + p.seed_off;
 				nsteps = p.seed_len;
 				lim = do_extend ? p.seed_off : 0;
 				ii = 0; nlex = 0;
-				top = (uint32_t)s0.topf; bot = (uint32_t)s0.botf; step = s0.nlex;
-				report = s0.pad[0] == 2;
+				int st0;
+				if(kInit) {
+					const bt2x_seed_out s0 = out[idx];
+					top = (uint32_t)s0.topf; bot = (uint32_t)s0.botf; step = s0.nlex; st0 = s0.pad[0];
+				} else {
+					// startSearchSeedBi: ftab jump over the rightmost ftabChars characters
+					const int off = nsteps - 1, fc = ix.ftab_chars;
+					if(fc > 1 && fc <= nsteps) {
+						uint64_t fi = 0;
+						for(int k = 0; k < fc; k++) fi = (fi << 2) | (uint64_t)(seq[off - fc + 1 + k] & 3);
+						top = (uint32_t)ftab_hi(ix, fi);
+						bot = (uint32_t)ftab_lo(ix, fi + 1);
+						n_ftab++;
+						step = fc;
+					} else {
+						const int c = seq[off];
+						top = (uint32_t)fchr_sel(ix, c); bot = (uint32_t)fchr_sel(ix, c + 1);
+						step = 1;
+					}
+					st0 = bot == top ? 1 : (step == nsteps ? 2 : 0);
+				}
+				report = st0 == 2;
 				tmode = false;
-				if(s0.pad[0] == 1) fin = true;
+				if(st0 == 1) fin = true;
 				else if(report) { etop = top; ebot = bot; phase = PH_EXTEND; fin = lim == 0; }
 				else phase = PH_SEARCH;
 				if(phase == PH_EXTEND && !fin && ix.sa && ebot - etop == 1) { tmode = true; tp = ix.sa[etop]; }
@@ -489,10 +510,12 @@ seed_kernel_blk(DevIndex ix, const uint8_t* __restrict__ reads, const bt2x_seed_
 		for(int d = 32; d > 0; d >>= 1) {
 			n_bilf += __shfl_xor(n_bilf, d);
 			n_lf1 += __shfl_xor(n_lf1, d);
+			n_ftab += __shfl_xor(n_ftab, d);
 		}
 		if((threadIdx.x & 63) == 0) {
 			atomicAdd(&ctr[0], (unsigned long long)n_bilf);
 			atomicAdd(&ctr[1], (unsigned long long)n_lf1);
+			if(!kInit) atomicAdd(&ctr[2], (unsigned long long)n_ftab);
 		}
 	}
 }
@@ -592,7 +615,7 @@ static int seed_blocks_per_cu(bool blk) {
 	static int nb[2] = {0, 0};
 	if(nb[blk] == 0) {
 		int v = 0;
-		const void* fn = blk ? (const void*)seed_kernel_blk : (const void*)seed_kernel<false>;
+		const void* fn = blk ? (const void*)seed_kernel_blk<false> : (const void*)seed_kernel<false>;
 		if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, fn, 256, 0) != hipSuccess || v < 1) v = 2;
 		nb[blk] = v;
 	}
@@ -608,10 +631,17 @@ int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed
 	const uint32_t need = (n + 255) / 256;
 	if(blocks > need) blocks = need;
 	if(blk) {
-		hipLaunchKernelGGL(seed_init_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-		                   ix, d_reads, d_in, n, d_out, d_ctr);
-		hipLaunchKernelGGL(seed_kernel_blk, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-		                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+		static int init_pass = -1;
+		if(init_pass < 0) { const char* e = getenv("BT2X_SEED_INIT_PASS"); init_pass = (e && e[0] == '1') ? 1 : 0; }
+		if(init_pass) {
+			hipLaunchKernelGGL(seed_init_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+			                   ix, d_reads, d_in, n, d_out, d_ctr);
+			hipLaunchKernelGGL(seed_kernel_blk<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+			                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+		} else {
+			hipLaunchKernelGGL(seed_kernel_blk<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+			                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+		}
 	}
 	else
 		hipLaunchKernelGGL(seed_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
