@@ -103,7 +103,8 @@ __device__ __forceinline__ uint32_t pack_edit(uint32_t pos, int type, int chr, i
 	       ((uint32_t)(uint8_t)qchr << 24);
 }
 
-__device__ __forceinline__ char acgtn(int c) { return c == 0 ? 'A' : c == 1 ? 'C' : c == 2 ? 'G' : c == 3 ? 'T' : 'N'; }
+// "ACGTN"[c] without a branch tree (c in 0..4)
+__device__ __forceinline__ char acgtn(int c) { return (char)((0x4e54474341ULL >> (8 * c)) & 0xffu); }
 // mask2dna of a single-base mask 1<<c (c = 4 -> mask 16 -> 'N'), alphabet.cpp:71
 __device__ __forceinline__ char mask_chr(int c) { return acgtn(c); }
 
@@ -136,7 +137,8 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 	const uint32_t gl = (uint32_t)lane;
 	const uint8_t* dir8 = gslot + kDirOff;
-	uint8_t* dirw8 = gslot + kDirOff;
+	const __amdgpu_buffer_rsrc_t dirsrc =
+		__builtin_amdgcn_make_buffer_rsrc(gslot + kDirOff, 0, (int)(kDirBytesLane * 64u), 0x00020000);
 	const uint8_t* cands = gslot + kCandOff;
 	bt2x_dp_out o = a.out[pi];
 	if(o.status != 0 && o.ncand > 0 && a.ablate != 1) {
@@ -162,36 +164,45 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				int row = row0, col = col0, ct = 2 /*H*/, bscore = 0, ns = 0, gaps = 0, ne = 0;
 				bool over_core = false, ok = true;
 				uint32_t tb_end = 0;
-				// One dependent load per step: the next cell's byte is issued before
-				// this cell's mark store, so the in-order vmcnt never waits on a store.
-				// Read/reference/quality bytes only where TB_MM says an edit is recorded.
-				size_t bi = tb_addr(row, col, gl);
-				uint32_t tb = dir8[bi];
+				// One dependent load per step: the next cell's byte is issued before this
+				// cell's mark store, so the in-order vmcnt never waits on a store.  Moves are
+				// decided branch-free and the byte offset is updated incrementally (32-bit,
+				// buffer addressing); read/reference/quality bytes only where TB_MM says an
+				// edit is recorded.
+				uint32_t bo = (uint32_t)tb_addr(row, col, gl);
+				uint32_t tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)bo, 0, 0);
 				while(true) {
 					st_bt++;
 					if(tb & TB_MARK) { ok = false; break; }         // reportedThrough
 					const int diag = col - row + (int)p.triml;
-					if(diag >= 0 && diag >= (int)p.corel && diag <= (int)p.corer) over_core = true;
+					over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);
 					if(row == 0) {
-						dirw8[bi] = (uint8_t)TB_MARK;              // setReportedThrough
+						__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)bo, 0, 0);
 						tb_end = tb;
 						break;
 					}
-					// the reference's fixed priority over the cell's flags (u8.cpp:843-990)
-					const int emove = (tb & TB_EONE) ? H_RDGAP_EXT : H_READ_OPEN;
-					const int fmove = (tb & TB_FONE) ? H_RFGAP_EXT : H_REF_OPEN;
-					const int move = ct == 0 ? emove : ct == 1 ? fmove
-					               : !(tb & TB_DNE) ? H_DIAG : !(tb & TB_FNE) ? fmove : emove;
+					// the reference's fixed priority over the cell's flags (u8.cpp:843-990):
+					// H: diag > F (H-up / F-up) > E (H-left / E-left); E/F prefer the open
+					const uint32_t dne = tb & TB_DNE, fne = (tb >> 1) & 1u;
+					const uint32_t fext = (tb >> 2) & 1u, eext = (tb >> 3) & 1u;
+					const bool inH = ct == 2;
+					const bool isD = inH && !dne;
+					const bool isF = (ct == 1) || (inH && dne && !fne);
+					const int drow = (isD || isF) ? 1 : 0, dcol = isF ? 0 : 1;
+					const int nct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);
+					// byte-offset delta of the move (tb_addr's pair/step layout)
+					const int st = row + (col & 1);
+					const int dD = (col & 1) ? -257 : -(kPairWords * 256) + 1;
+					const int dU = (st & 1) ? -2 : -254;
+					const int dL = (col & 1) ? ((row & 1) ? -255 : -3) : ((row & 1) ? -(kPairWords * 256) + 255 : -(kPairWords * 256) + 3);
+					const uint32_t cbo = bo;
+					bo = (uint32_t)((int)bo + (isD ? dD : isF ? dU : dL));
 					const int crow = row, ccol = col;
+					row -= drow; col -= dcol; ct = nct;
 					const uint32_t ctb = tb;
-					const size_t cur_bi = bi;
-					if(move == H_DIAG) { row--; col--; ct = 2; }
-					else if(move == H_REF_OPEN || move == H_RFGAP_EXT) { row--; ct = (move == H_REF_OPEN) ? 2 : 1; }
-					else { col--; ct = (move == H_READ_OPEN) ? 2 : 0; }
-					bi = tb_addr(row, col, gl);
-					tb = dir8[bi];
-					dirw8[cur_bi] = (uint8_t)TB_MARK;              // setReportedThrough
-					if(move == H_DIAG) {
+					tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)bo, 0, 0);
+					__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)cbo, 0, 0);   // setReportedThrough
+					if(isD) {
 						if(ctb & TB_MM) {
 							const int rdc = rd[crow], refc = rf[ccol];
 							const bool amb = rdc > 3 || refc > 3;
@@ -202,15 +213,13 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 							bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
 							if(amb) ns++;
 						}
-					} else if(move == H_REF_OPEN || move == H_RFGAP_EXT) {
-						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rd[crow]));
-						ne++;
-						bscore -= (move == H_REF_OPEN) ? rfo : rfe;
-						gaps++;
 					} else {
-						stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(rf[ccol]), '-');
+						const bool open = nct == 2;
+						const uint32_t e = isF ? pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rd[crow]))
+						                       : pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(rf[ccol]), '-');
+						stage_ed[(size_t)ne * 64 + lane] = e;
 						ne++;
-						bscore -= (move == H_READ_OPEN) ? rdo : rde;
+						bscore -= isF ? (open ? rfo : rfe) : (open ? rdo : rde);
 						gaps++;
 					}
 				}
