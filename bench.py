@@ -50,6 +50,7 @@ def parse():
                     help="OpenMP threads for the reference CPU baseline (the box's CPU share)")
     ap.add_argument("--port-sample", type=int, default=20000, help="reads timed on the 1-thread C port")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--overlap", type=int, default=0, help="1: seed and DP stages on two streams")
     return ap.parse_args()
 
 
@@ -166,12 +167,22 @@ def main():
     d_cnt = torch.zeros(16, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    # --overlap: the seed stage and the DP stage on two HIP streams, the way a streaming
+    # aligner pipelines seed(batch k+1) with DP(batch k); the seed kernel is latency-bound
+    # and the DP fill VALU-bound, so they share the CUs well.  Every step still runs both
+    # stages over the whole batch; the timed region waits for both streams.
+    s2 = torch.cuda.Stream(dev) if args.overlap else stream
+    sh2 = s2.cuda_stream
 
     def step():
-        ctx.seed_search_dev(d_sbuf.data_ptr(), d_sin.data_ptr(), nseed, d_sout.data_ptr(), True, sh)
+        if args.overlap:
+            s2.wait_stream(stream)
+        ctx.seed_search_dev(d_sbuf.data_ptr(), d_sin.data_ptr(), nseed, d_sout.data_ptr(), True, sh2)
         ctx.dp_align_dev(d_rd.data_ptr(), d_qu.data_ptr(), d_rf.data_ptr(), d_dpin.data_ptr(), ndp,
                          d_dpout.data_ptr(), d_recs.data_ptr(), rec_cap, d_edits.data_ptr(),
                          edit_cap, d_cnt.data_ptr(), sh)
+        if args.overlap:
+            stream.wait_stream(s2)
 
     for _ in range(args.warmup):
         step()
@@ -218,7 +229,8 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded genome + simulated 150 bp reads, BASELINE.md error model)",
         "config": {"workload": f"C3 stand-in: {R} bp SE, --dpad {args.dpad}, genome {gdesc}; "
-                               f"step = seed search+extend ({nseed} seeds) + DP ({ndp} problems)",
+                               f"step = seed search+extend ({nseed} seeds) + DP ({ndp} problems)"
+                               + (", the two stages on two streams" if args.overlap else ""),
                    "reads_per_gpu_step": n, "read_len": R, "parallelism": f"dp{world} (read shards)",
                    "key": workload_key(args)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,

@@ -229,3 +229,87 @@ def test_seed_kernel_lf_extension_path(golden_dir, monkeypatch):
     np.testing.assert_array_equal(out["need_reporting"], case.exp_rep)
     with pytest.raises(lib.Bt2xError):
         ctx.suffix_array(0, 1)
+
+
+def _random_dp_problems(n, seed):
+    """Unframed DP problems over the ABI's whole shape range: R 1..160, ncol 1..199
+    (ncol + 1 <= 200), minsc -254..0, random core diagonals / trims, both strands, N-rich
+    reads and windows, every quality; lengths mixed within waves."""
+    rng = np.random.default_rng(seed)
+    R = rng.integers(1, 161, size=n)
+    R[rng.random(n) < 0.1] = 160
+    C = rng.integers(1, 200, size=n)
+    C[rng.random(n) < 0.1] = 199
+    rd, qu, rf = [], [], []
+    inp = np.zeros(n, dtype=abi.DP_IN)
+    pr = pf = 0
+    for i in range(n):
+        r, c = int(R[i]), int(C[i])
+        ref = rng.integers(0, 4, size=c).astype(np.uint8)
+        ref[rng.random(c) < rng.choice([0.0, 0.02, 0.3])] = 4
+        # reads: a mutated copy of a window slice (so alignments exist) or random
+        st = int(rng.integers(0, max(1, c - r + 1)))
+        read = np.resize(ref[st:st + r], r).copy() if rng.random() < 0.7 else rng.integers(0, 4, r).astype(np.uint8)
+        read[read > 3] = rng.integers(0, 4)
+        mut = rng.random(r) < rng.choice([0.0, 0.02, 0.1])
+        read[mut] = rng.integers(0, 5, size=int(mut.sum()))
+        q = rng.integers(33, 33 + 42, size=r).astype(np.uint8)
+        rd.append(read); qu.append(q); rf.append(ref)
+        x = inp[i]
+        x["read_off"], x["qual_off"], x["ref_off"] = pr, pr, pf
+        x["refl"] = int(rng.integers(-50, 10**6))
+        x["rdlen"], x["ncol"] = r, c
+        x["minsc"] = int(rng.choice([0, -1, -30, -90, -150, -254, int(rng.integers(-254, 1))]))
+        x["nceil"] = int(rng.integers(0, r + 1))
+        x["triml"] = int(rng.integers(0, 20))
+        lo = int(rng.integers(0, c + 20))
+        x["corel"], x["corer"] = lo, lo + int(rng.integers(0, 40))
+        x["fw"] = int(rng.random() < 0.5)
+        pr += r; pf += c
+    return np.concatenate(rd), np.concatenate(qu), np.concatenate(rf), inp
+
+
+def _compare_dp(out, recs, edits, eo, erecs, eedits):
+    np.testing.assert_array_equal(out[["status", "best", "ncand", "nrec"]], eo[["status", "best", "ncand", "nrec"]])
+    fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff"]
+    for i in np.nonzero(out["nrec"])[0]:
+        a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
+        b = erecs[eo["rec_off"][i]: eo["rec_off"][i] + eo["nrec"][i]]
+        assert (a[fields] == b[fields]).all(), i
+        for ra, rb in zip(a, b):
+            np.testing.assert_array_equal(edits[ra["edit_off"]: ra["edit_off"] + ra["nedit"]],
+                                          eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
+
+
+@pytest.mark.parametrize("debug", [False, True])
+def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug):
+    """Production (debug=False) and debug kernels on random shapes/penalty thresholds at the
+    ABI limits vs the oracle: statuses, candidates, every nextAlignment record and edit."""
+    rd, qu, rf, inp = _random_dp_problems(6000, seed=77 + int(debug))
+    ctx = ctxs["rep"][0]
+    res = ctx.dp_align(rd, qu, rf, inp, debug=debug)
+    eo, erecs, eedits, edig, ecands, _ = ol.dp_align(ol.default_scoring(), rd, qu, rf, inp)
+    out, recs, edits = res[0], res[1], res[2]
+    _compare_dp(out, recs, edits, eo, erecs, eedits)
+    if debug:
+        np.testing.assert_array_equal(res[3], edig)
+        np.testing.assert_array_equal(res[4], ecands)
+    assert (out["status"] == 1).sum() > 1000 and (out["status"] == 0).sum() > 100
+
+
+def test_dp_production_kernel_on_golden(ctxs):
+    """The production (non-debug) kernel reproduces the reference records of the golden set."""
+    case = g.DpCase(os.path.join(g.GOLDEN, "dp_rep_dpad12.txt.xz"))
+    ctx = ctxs["rep"][0]
+    out, recs, edits = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
+    eo, erecs, eedits, _, _, _ = ol.dp_align(ol.default_scoring(), case.reads, case.quals, case.refs, case.inp)
+    _compare_dp(out, recs, edits, eo, erecs, eedits)
+
+
+def test_empty_batches(ctxs):
+    ctx = ctxs["rep"][0]
+    out = ctx.seed_search(np.zeros(16, np.uint8), np.zeros(0, dtype=abi.SEED_IN), do_extend=True)
+    assert len(out) == 0
+    res = ctx.dp_align(np.zeros(1, np.uint8), np.zeros(1, np.uint8), np.zeros(1, np.uint8),
+                       np.zeros(0, dtype=abi.DP_IN), debug=False)
+    assert len(res[0]) == 0
