@@ -80,6 +80,9 @@ __device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) {
 	return r;
 }
 __device__ __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return as1(as2(a) * as2(b)); }
+__device__ __forceinline__ uint32_t pmul_lo(uint32_t a, uint32_t b) {
+	uint32_t r; asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
 __device__ __forceinline__ uint32_t pshr(uint32_t a, uint32_t sh) { return as1(as2(a) >> (u16x2){(unsigned short)sh, (unsigned short)sh}); }
 // per-half "not equal" flag, 0 or 1
 __device__ __forceinline__ uint32_t pne(uint32_t a, uint32_t b) { return pmin(a ^ b, 0x00010001u); }
@@ -482,7 +485,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		// ------------- candidate order (DpBtCandidate: score desc, col desc) --------
 		// the last row moves into LDS; repeated max-below-key scans emit the sorted
 		// candidate columns for the walk kernel
-		for(int q = 0; q < (C + 3) >> 2; q++) {
+		// (up to the wave's widest problem: columns >= C read as score 0)
+		const int nw = (Cmax + 3) >> 2;                  // wave-uniform (Cmax: all lanes)
+		for(int q = 0; q < nw; q++) {
 			uint32_t w4 = 0;
 			for(int r = 0; r < 4; r++) {
 				const int j = q * 4 + r;
@@ -491,21 +496,24 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			lds[q * 64 + lane] = w4;
 		}
 		a.out[pi] = o;
-		int cur_key = 0x7fffffff;
+		int cur_key = 0xffff;
 		const int row0 = R - 1;
+		// Two columns per packed op: key = score << 8 | col in each 16-bit half; the max
+		// key below the previous one is the next candidate (keys of scores below the
+		// threshold are smaller than every qualifying key and are never reached).
 		for(int k = 0; k < ncand; k++) {
-			int best = -1;
-			const int nw = (C + 3) >> 2;
+			const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
+			uint32_t best2 = 0;
 #pragma unroll 2
 			for(int q = 0; q < nw; q++) {
 				const uint32_t w4 = lds[q * 64 + lane];
-#pragma unroll
-				for(int r = 0; r < 4; r++) {
-					const int s = (int)((w4 >> (8 * r)) & 0xffu);
-					const int key = s * 256 + q * 4 + r;
-					best = (s >= thr && key < cur_key && key > best) ? key : best;
-				}
+				const uint32_t cq = (uint32_t)q * 0x40004u + 0x10000u;     // cols 4q, 4q+1
+				const uint32_t ka = perm(cq, w4, 0x01060004u);             // [4q, s0, 4q+1, s1]
+				const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);  // [4q+2, s2, 4q+3, s3]
+				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), 0x00010001u), ka));
+				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), 0x00010001u), kb));
 			}
+			const int best = (int)max(best2 & 0xffffu, best2 >> 16);
 			cur_key = best;
 			cands[(size_t)k * 64 + lane] = (uint8_t)(best & 0xff);
 			if(kDebug && a.cands)
