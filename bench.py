@@ -126,11 +126,18 @@ def main():
     import torch
     from bt2x import dist as bdist
     rank, world, local = bdist.world()
-    torch.cuda.set_device(local)
+    # rehearsal knobs (not used by the driver): BT2X_BENCH_DEVICE pins every rank to one
+    # GPU, BT2X_BENCH_DIST_BACKEND=gloo runs the rank reductions on the host
+    gpu = int(os.environ.get("BT2X_BENCH_DEVICE", local))
+    backend = os.environ.get("BT2X_BENCH_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
 
     from bt2x import abi, framing, lib, seeds
     import simdata as sd
@@ -151,8 +158,8 @@ def main():
     nseed, ndp = len(sin), len(dpin)
 
     idx = lib.Index(base, load_offs=True)     # SA sample + text: full SA rebuilt in HBM
-    ctx = lib.Context(idx, device=local)
-    dev = torch.device("cuda", local)
+    ctx = lib.Context(idx, device=gpu)
+    dev = torch.device("cuda", gpu)
 
     def to_dev(a):
         return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
@@ -201,7 +208,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        elapsed = bdist.max_over_ranks(elapsed, dist, dev)
+        elapsed = bdist.max_over_ranks(elapsed, dist, dev if backend == "nccl" else None)
     used = d_cnt[:2].cpu().numpy()
     if used[0] > rec_cap or used[1] > edit_cap:
         raise SystemExit(f"result arena overflow {used} vs {(rec_cap, edit_cap)}")
