@@ -121,7 +121,7 @@ typedef struct bt2x_ctx bt2x_ctx;
 int  bt2x_open(int hip_device, const bt2x_index_desc* idx, const bt2x_scoring* sc, bt2x_ctx** out);
 void bt2x_close(bt2x_ctx* ctx);
 /* Last kernel's duration in ms (HIP events on the launching stream), by kernel id. */
-enum { BT2X_K_SEED = 0, BT2X_K_DP = 1, BT2X_K_COUNT = 2 };
+enum { BT2X_K_SEED = 0, BT2X_K_DP = 1, BT2X_K_RESOLVE = 2, BT2X_K_COUNT = 3 };
 double bt2x_last_kernel_ms(const bt2x_ctx* ctx, int kernel);
 /* Algorithmic bytes / counters of the last call, by kernel id. */
 typedef struct {
@@ -257,6 +257,42 @@ static inline uint64_t bt2x_cell_digest(uint32_t row, uint32_t col, uint32_t mat
 /* Rows [first, first+n) of the device-resident full suffix array (BT2X_E_ARG if the
  * context has none: no SA sample/text loaded, or a text of 2^32 rows or more). */
 int bt2x_suffix_array(bt2x_ctx* ctx, uint64_t first, uint64_t n, uint32_t* out);
+
+/* --------------------------------------------------------- SA resolution */
+
+/* One BW element of a seed hit to place on the reference.  Replaces, per element,
+ * GroupWalk2S::advanceElement (group_walk.h:969; GWState::init/advance :402/:687,
+ * Ebwt::tryOffset bt2_idx.h:1621), whose WalkResult::toff is the joined-text offset
+ * of the row (== Ebwt::getOffset(row), bt2_idx.cpp:150, asserted at group_walk.h:430),
+ * followed by Ebwt::joinedToTextOff(qlen, toff, ...) (bt2_idx.cpp:54) as
+ * SwDriver::extendSeeds calls it (aligner_sw_driver.cpp:388-402; qlen = wr.elt.len,
+ * the seed key length). */
+typedef struct {
+	uint64_t row;            /* BWT row, <= len                                         */
+	uint32_t qlen;           /* hit length                                              */
+	uint32_t pad;
+} bt2x_resolve_in;
+
+typedef struct {
+	uint64_t joff;           /* offset into the joined text (WalkResult::toff)           */
+	uint64_t toff;           /* textoff: offset into reference tidx                      */
+	uint64_t tlen;           /* plen[tidx]                                               */
+	uint32_t tidx;           /* reference index; BT2X_NO_TIDX when reject_straddle
+	                            rejected the hit (toff = tlen = 0 then, the caller's
+	                            zero-initialised values at aligner_sw_driver.cpp:392) or
+	                            joff lies in no fragment (only row len, the '$' suffix) */
+	uint32_t straddled;      /* 1 if joff + qlen runs past the fragment's end            */
+} bt2x_resolve_out;
+#define BT2X_NO_TIDX 0xffffffffu
+
+/* With the resident full suffix array this is one 4-byte lookup per element; without
+ * it (texts of 2^32 rows or more, BT2X_FULL_SA=0) the kernel walks LF to the SA sample
+ * exactly like GWState (<= 2^offRate - 1 steps).  Needs an index loaded with
+ * load_offs (BT2X_E_ARG otherwise).  Rows > len give BT2X_E_ARG (host variant). */
+int bt2x_resolve(bt2x_ctx* ctx, const bt2x_resolve_in* in, uint32_t n, int reject_straddle,
+                 bt2x_resolve_out* out);
+int bt2x_resolve_dev(bt2x_ctx* ctx, const bt2x_resolve_in* d_in, uint32_t n, int reject_straddle,
+                     bt2x_resolve_out* d_out, void* stream);
 
 const char* bt2x_version(void);
 /* sizeof of the ABI structs (seed_in, seed_out, dp_in, dp_out, aln_rec, scoring,

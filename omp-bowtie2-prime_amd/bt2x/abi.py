@@ -22,11 +22,15 @@ ALN_REC = np.dtype([("ntries", "<u2"), ("ok", "u1"), ("pad0", "u1"), ("score", "
                     ("ns", "<u2"), ("gaps", "<u2"), ("nedit", "<u2"),
                     ("bases_aligned", "<u2"), ("refns", "<u2"), ("refoff", "<i8"),
                     ("edit_off", "<u4"), ("pad1", "<u4")], align=True)
+RESOLVE_IN = np.dtype([("row", "<u8"), ("qlen", "<u4"), ("pad", "<u4")], align=True)
+RESOLVE_OUT = np.dtype([("joff", "<u8"), ("toff", "<u8"), ("tlen", "<u8"), ("tidx", "<u4"),
+                        ("straddled", "<u4")], align=True)
+NO_TIDX = 0xFFFFFFFF
 
 MAX_ROWS = 160
 MAX_COLS = 200
 E_OK, E_ARG, E_IO, E_NODEVICE, E_OVERFLOW, E_NOMEM = 0, -1, -2, -3, -4, -5
-K_SEED, K_DP = 0, 1
+K_SEED, K_DP, K_RESOLVE = 0, 1, 2
 
 EDIT_READ_GAP, EDIT_REF_GAP, EDIT_MM = 1, 2, 3
 

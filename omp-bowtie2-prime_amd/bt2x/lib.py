@@ -44,6 +44,10 @@ FUNCS = {
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                          ctypes.POINTER(abi.DpDebug), ctypes.c_void_p]),
+    "bt2x_resolve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                    ctypes.c_void_p]),
+    "bt2x_resolve_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
     "bt2x_suffix_array": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
     "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
@@ -180,6 +184,23 @@ class Context:
         check(load().bt2x_dp_align_dev(self.h, d_reads, d_quals, d_refs, d_in, n, d_out, d_recs,
                                        rec_cap, d_edits, edit_cap, d_counters, None, stream),
               "bt2x_dp_align_dev")
+
+    # ------------------------------------------------------- SA resolution
+    def resolve(self, rows, qlen, reject_straddle: bool = False) -> np.ndarray:
+        """BW rows (+ hit lengths) -> RESOLVE_OUT records: joined offset, reference
+        index/offset/length, straddle flag (GroupWalk2S::advanceElement + joinedToTextOff)."""
+        rows = np.asarray(rows, dtype=np.uint64)
+        inp = np.zeros(len(rows), dtype=abi.RESOLVE_IN)
+        inp["row"] = rows
+        inp["qlen"] = qlen
+        out = np.zeros(len(rows), dtype=abi.RESOLVE_OUT)
+        check(load().bt2x_resolve(self.h, abi.ptr(inp), len(inp), int(reject_straddle), abi.ptr(out)),
+              "bt2x_resolve")
+        return out
+
+    def resolve_dev(self, d_in: int, n: int, d_out: int, reject_straddle=False, stream=0):
+        check(load().bt2x_resolve_dev(self.h, d_in, n, int(reject_straddle), d_out, stream),
+              "bt2x_resolve_dev")
 
     def device_name(self) -> str:
         try:

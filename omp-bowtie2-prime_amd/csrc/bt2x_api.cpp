@@ -138,19 +138,20 @@ struct bt2x_ctx {
 	int device = 0;
 	hipStream_t stream = nullptr;
 	hipEvent_t ev[BT2X_K_COUNT][2];
-	bool ev_valid[BT2X_K_COUNT] = {false, false};
+	bool ev_valid[BT2X_K_COUNT] = {};
 	DevIndex ix{};
 	DevScoring sc{};
 	void* d_ebwt = nullptr; void* d_ftab = nullptr; void* d_eftab = nullptr; void* d_blk = nullptr;
 	void* d_sa = nullptr; void* d_text = nullptr;
+	void* d_offs = nullptr; void* d_rstarts = nullptr; void* d_plen = nullptr;
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
 	DevBuf scratch;
 	int ncu = 0;
 	uint32_t chunk_groups = 16384;             // DP chunk: 1 Mi problems, ~34 GB of traceback bytes
 	uint32_t* d_queue = nullptr;
-	unsigned long long* d_stats = nullptr;     // [0..2] seed, [4..6] dp
+	unsigned long long* d_stats = nullptr;     // [0..2] seed, [4..6] dp, [8..10] resolve
 	uint32_t* d_counters = nullptr;
-	uint64_t n_seed_last = 0, n_dp_last = 0;
+	uint64_t n_seed_last = 0, n_dp_last = 0, n_resolve_last = 0;
 };
 
 namespace {
@@ -237,6 +238,24 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 			c->ix.text = (const uint32_t*)c->d_text;
 		}
 	}
+	// SA resolution (bt2x_resolve): fragment table always; the SA sample only when no
+	// full SA was built (the resolve kernel then walks LF to it, as GroupWalk does)
+	c->ix.offs = nullptr; c->ix.rstarts = nullptr; c->ix.plen = nullptr; c->ix.nfrag = idx->nfrag;
+	if(idx->nfrag && idx->rstarts && idx->plen && idx->npat) {
+		HIPCHK(hipMalloc(&c->d_rstarts, 24 * idx->nfrag));
+		HIPCHK(hipMemcpy(c->d_rstarts, idx->rstarts, 24 * idx->nfrag, hipMemcpyHostToDevice));
+		HIPCHK(hipMalloc(&c->d_plen, 8 * idx->npat));
+		HIPCHK(hipMemcpy(c->d_plen, idx->plen, 8 * idx->npat, hipMemcpyHostToDevice));
+		c->ix.rstarts = (const uint64_t*)c->d_rstarts;
+		c->ix.plen = (const uint64_t*)c->d_plen;
+	} else {
+		c->ix.nfrag = 0;
+	}
+	if(!c->ix.sa && idx->offs && idx->offs_len && idx->off_rate >= 0 && idx->off_rate < 32) {
+		HIPCHK(hipMalloc(&c->d_offs, 8 * idx->offs_len));
+		HIPCHK(hipMemcpy(c->d_offs, idx->offs, 8 * idx->offs_len, hipMemcpyHostToDevice));
+		c->ix.offs = (const uint64_t*)c->d_offs;
+	}
 	bt2x_scoring s;
 	if(sc) s = *sc; else bt2x_scoring_default(&s);
 	c->sc = to_dev(s);
@@ -261,6 +280,7 @@ extern "C" void bt2x_close(bt2x_ctx* c) {
 	                 &c->b_edits, &c->b_dbg_dig, &c->b_dbg_cand, &c->scratch}) b->release();
 	(void)hipFree(c->d_ebwt); (void)hipFree(c->d_ftab); (void)hipFree(c->d_eftab); (void)hipFree(c->d_blk);
 	(void)hipFree(c->d_sa); (void)hipFree(c->d_text);
+	(void)hipFree(c->d_offs); (void)hipFree(c->d_rstarts); (void)hipFree(c->d_plen);
 	(void)hipFree(c->d_stats); (void)hipFree(c->d_counters); (void)hipFree(c->d_queue);
 	for(int k = 0; k < BT2X_K_COUNT; k++) { (void)hipEventDestroy(c->ev[k][0]); (void)hipEventDestroy(c->ev[k][1]); }
 	(void)hipStreamDestroy(c->stream);
@@ -286,6 +306,14 @@ extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) 
 		out->n_bilf = st[0]; out->n_lf1 = st[1]; out->n_ftab = st[2];
 		out->n_problems = c->n_seed_last;
 		out->alg_bytes = 128 * (2 * out->n_bilf + out->n_lf1) + 16 * out->n_ftab;
+	} else if(k == BT2X_K_RESOLVE) {
+		out->n_lf1 = st[9];
+		out->n_problems = c->n_resolve_last;
+		// per element: 16 B in + 32 B out + one 4 B SA entry, or per LF step one 64 B
+		// block (128 B side) and one 8 B sample word at the end of the walk
+		const uint64_t step_b = c->ix.blk ? BT2X_BLK_BYTES : BT2X_SIDE_BYTES;
+		out->alg_bytes = out->n_problems * (16 + 32) +
+		                 (c->ix.sa ? 4 * out->n_problems : step_b * out->n_lf1 + 8 * out->n_problems);
 	} else {
 		out->dp_cells = st[4]; out->dp_cols = st[5]; out->bt_cells = st[6];
 		out->n_problems = c->n_dp_last;
@@ -439,7 +467,8 @@ extern "C" int bt2x_abi_sizes(uint32_t* out, int n) {
 	const uint32_t s[] = {(uint32_t)sizeof(bt2x_seed_in), (uint32_t)sizeof(bt2x_seed_out),
 	                      (uint32_t)sizeof(bt2x_dp_in), (uint32_t)sizeof(bt2x_dp_out),
 	                      (uint32_t)sizeof(bt2x_aln_rec), (uint32_t)sizeof(bt2x_scoring),
-	                      (uint32_t)sizeof(bt2x_index_desc), (uint32_t)sizeof(bt2x_counters)};
+	                      (uint32_t)sizeof(bt2x_index_desc), (uint32_t)sizeof(bt2x_counters),
+	                      (uint32_t)sizeof(bt2x_resolve_in), (uint32_t)sizeof(bt2x_resolve_out)};
 	const int m = (int)(sizeof s / sizeof s[0]);
 	for(int i = 0; i < n && i < m; i++) out[i] = s[i];
 	return m;
@@ -451,5 +480,40 @@ extern "C" int bt2x_suffix_array(bt2x_ctx* c, uint64_t first, uint64_t n, uint32
 	if(first + n > c->ix.len + 1) return BT2X_E_ARG;
 	HIPCHK(hipSetDevice(c->device));
 	HIPCHK(hipMemcpy(out, c->ix.sa + first, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+	return BT2X_OK;
+}
+
+// ---------------------------------------------------------------- SA resolve
+extern "C" int bt2x_resolve_dev(bt2x_ctx* c, const bt2x_resolve_in* d_in, uint32_t n, int reject_straddle,
+                                bt2x_resolve_out* d_out, void* stream) {
+	if(!c) return BT2X_E_ARG;
+	if(!c->ix.sa && !c->ix.offs) return BT2X_E_ARG;       // index loaded without load_offs
+	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipMemsetAsync(c->d_stats + 8, 0, 3 * sizeof(unsigned long long), s));
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][0], s));
+	const int rc = bt2x_launch_resolve(c->ix, d_in, n, reject_straddle ? 1 : 0, d_out, c->d_stats + 8, s);
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][1], s));
+	c->ev_valid[BT2X_K_RESOLVE] = true;
+	c->n_resolve_last = n;
+	return rc;
+}
+
+extern "C" int bt2x_resolve(bt2x_ctx* c, const bt2x_resolve_in* in, uint32_t n, int reject_straddle,
+                            bt2x_resolve_out* out) {
+	if(!c || (n && (!in || !out))) return BT2X_E_ARG;
+	if(!c->ix.sa && !c->ix.offs) return BT2X_E_ARG;
+	if(n == 0) return BT2X_OK;
+	for(uint32_t i = 0; i < n; i++) if(in[i].row > c->ix.len) return BT2X_E_ARG;
+	HIPCHK(hipSetDevice(c->device));
+	int rc;
+	if((rc = c->b_in.ensure(sizeof(bt2x_resolve_in) * n)) || (rc = c->b_out.ensure(sizeof(bt2x_resolve_out) * n)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(c->b_in.p, in, sizeof(bt2x_resolve_in) * n, hipMemcpyHostToDevice, c->stream));
+	rc = bt2x_resolve_dev(c, (const bt2x_resolve_in*)c->b_in.p, n, reject_straddle,
+	                      (bt2x_resolve_out*)c->b_out.p, c->stream);
+	if(rc) return rc;
+	HIPCHK(hipMemcpyAsync(out, c->b_out.p, sizeof(bt2x_resolve_out) * n, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
 	return BT2X_OK;
 }

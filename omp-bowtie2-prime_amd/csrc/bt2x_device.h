@@ -24,6 +24,10 @@ struct DevIndex {
 	int32_t off_rate;
 	const uint32_t* sa;       // full suffix array (rows 0..len), rebuilt in HBM at open; or NULL
 	const uint32_t* text;     // joined text, 16 bases per u32 (LSB-first); with sa
+	const uint64_t* offs;     // SA sample (.2.bt2l), kept only when there is no full sa
+	const uint64_t* rstarts;  // 3 words per fragment (joined off, tidx, text off)
+	const uint64_t* plen;     // reference lengths
+	uint64_t nfrag;
 };
 
 struct DevScoring {
@@ -41,6 +45,9 @@ int bt2x_build_sa(const DevIndex& ix, const uint64_t* d_offs, uint64_t noffs, ui
 int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
                      uint32_t n, int do_extend, bt2x_seed_out* d_out,
                      unsigned long long* d_ctr, int ncu, void* stream);
+
+int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_t n, int reject,
+                        bt2x_resolve_out* d_out, unsigned long long* d_ctr, void* stream);
 
 struct DpLaunch {
 	const uint8_t* reads; const uint8_t* quals; const uint8_t* refs;

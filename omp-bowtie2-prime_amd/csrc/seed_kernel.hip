@@ -593,6 +593,83 @@ build_blocks_kernel(DevIndex ix, uint64_t nsides, uint8_t* __restrict__ blk) {
 	o[3] = make_uint4(w[8], w[9], w[10], w[11]);
 }
 
+// ---- SA resolution (GroupWalk2S::advanceElement + Ebwt::joinedToTextOff) ----------
+
+// BWT character of row r over the 64-bit block / side layouts.
+__device__ __forceinline__ uint32_t row_l_any(const DevIndex& ix, uint64_t r) {
+	if(ix.blk) {
+		const uint64_t b = r / BT2X_BLK_ROWS, off = r - b * BT2X_BLK_ROWS;
+		const uint8_t by = ix.blk[b * BT2X_BLK_BYTES + 16 + (off >> 2)];
+		return (by >> (2 * (off & 3))) & 3u;
+	}
+	const uint64_t s = r / BT2X_SIDE_CHARS, off = r - s * BT2X_SIDE_CHARS;
+	const uint8_t by = ix.ebwt[s * BT2X_SIDE_BYTES + (off >> 2)];
+	return (by >> (2 * (off & 3))) & 3u;
+}
+
+// Ebwt::getOffset (bt2_idx.cpp:150-174), the value GWState's walk produces
+// (group_walk.h:425-432): the resident SA when there is one, else LF to the sample.
+__device__ __forceinline__ uint64_t sa_offset(const DevIndex& ix, uint64_t row, uint32_t& steps) {
+	steps = 0;
+	if(ix.sa) return ix.sa[row];
+	const uint64_t mask = (1ULL << ix.off_rate) - 1ULL;
+	uint64_t jumps = 0;
+	for(int guard = 0; guard < (1 << 16); guard++) {
+		if(row == ix.zoff) return jumps;
+		if((row & mask) == 0) return jumps + ix.offs[row >> ix.off_rate];
+		const uint32_t c = row_l_any(ix, row);
+		uint64_t na, nb;
+		if(ix.blk) lf_step_blk(ix, row, row + 1, c, true, na, nb);
+		else lf_step(ix, row, row + 1, c, true, na, nb);
+		row = na; jumps++; steps++;
+	}
+	return OFF_MASK;
+}
+
+__global__ void __launch_bounds__(256)
+sa_resolve_kernel(DevIndex ix, const bt2x_resolve_in* __restrict__ in, uint32_t n, int reject,
+                  bt2x_resolve_out* __restrict__ out, unsigned long long* __restrict__ ctr) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	uint32_t steps = 0;
+	if(i < n) {
+		const bt2x_resolve_in e = in[i];
+		bt2x_resolve_out o;
+		o.joff = e.row <= ix.len ? sa_offset(ix, e.row, steps) : OFF_MASK;
+		o.toff = 0; o.tlen = 0; o.tidx = BT2X_NO_TIDX; o.straddled = 0;
+		// joinedToTextOff's binary search over rstarts (bt2_idx.cpp:62-121), same probe
+		// order; bounded so an offset in no fragment ('$' suffix) ends with BT2X_NO_TIDX
+		const uint64_t off = o.joff;
+		uint64_t top = 0, bot = ix.nfrag;
+		for(int it = 0; it < 70 && off < ix.len && ix.nfrag > 0; it++) {
+			const uint64_t elt = top + ((bot - top) >> 1);
+			const uint64_t lower = ix.rstarts[elt * 3];
+			const uint64_t upper = elt == ix.nfrag - 1 ? ix.len : ix.rstarts[(elt + 1) * 3];
+			if(lower <= off) {
+				if(upper > off) {
+					const bool st = off + e.qlen > upper;
+					o.straddled = st ? 1u : 0u;
+					if(!(st && reject)) {
+						o.tidx = (uint32_t)ix.rstarts[elt * 3 + 1];
+						o.toff = off - lower + ix.rstarts[elt * 3 + 2];   // fw index: no flip
+						o.tlen = ix.plen[o.tidx];
+					}
+					break;
+				}
+				top = elt;
+			} else {
+				bot = elt;
+			}
+		}
+		out[i] = o;
+	}
+	if(ctr) {
+		// LF steps of this wave, one atomic per wave
+		uint64_t s = steps;
+		for(int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k);
+		if((threadIdx.x & 63) == 0 && s) atomicAdd(&ctr[1], (unsigned long long)s);
+	}
+}
+
 } // namespace
 
 int bt2x_build_sa(const DevIndex& ix, const uint64_t* d_offs, uint64_t noffs, uint32_t* d_sa, void* stream) {
@@ -646,5 +723,14 @@ int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed
 	else
 		hipLaunchKernelGGL(seed_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
 		                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+}
+
+int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_t n, int reject,
+                        bt2x_resolve_out* d_out, unsigned long long* d_ctr, void* stream) {
+	if(n == 0) return 0;
+	if(!ix.sa && !ix.offs) return BT2X_E_ARG;
+	hipLaunchKernelGGL(sa_resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+	                   ix, d_in, n, reject, d_out, d_ctr);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }

@@ -19,6 +19,9 @@
  *   backtrace       backtraceNucleotidesEnd2EndSseU8  u8.cpp:746-1352
  *   call sequence   SwAligner::nextAlignment          aligner_sw.cpp:252-375
  *   scoring         Scoring::initPens/score/mm        scoring.h:94-132, 232-288
+ *   SA resolution   Ebwt::getOffset                   bt2_idx.cpp:150-174 (the value
+ *                   GroupWalk2S::advanceElement yields, group_walk.h:425-432, 969-1005)
+ *                   Ebwt::joinedToTextOff             bt2_idx.cpp:54-121
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
  */
@@ -616,6 +619,71 @@ int bt2o_dp_align(const bt2x_scoring* sc,
 	if(nrec_used) *nrec_used = nrec;
 	if(nedit_used) *nedit_used = nedit;
 	return overflow ? BT2X_E_OVERFLOW : BT2X_OK;
+}
+
+/* ---------------------------------------------------------- SA resolution */
+
+/* Ebwt::getOffset(row) (bt2_idx.cpp:150-174): LF-walk left until row zOff (offset =
+ * jumps) or a sampled row (offs[row >> offRate] + jumps). */
+static uint64_t get_offset(const bt2x_index_desc* idx, uint64_t row, uint64_t* steps) {
+	const uint64_t mask = ((uint64_t)1 << idx->off_rate) - 1;
+	uint64_t jumps = 0;
+	for(;;) {
+		if(row == idx->zoff) return jumps;
+		if((row & mask) == 0) return jumps + idx->offs[row >> idx->off_rate];
+		map_lf1(idx, &row);
+		jumps++;
+		if(steps) (*steps)++;
+	}
+}
+
+/* Ebwt::joinedToTextOff (bt2_idx.cpp:54-121) for the forward index (fw_ = true), with
+ * the outputs a zero-initialised caller sees (aligner_sw_driver.cpp:392-402).  The
+ * reference's search never ends for an offset in no fragment; here that gives
+ * BT2X_NO_TIDX (only the '$' suffix row reaches it). */
+static void joined_to_text_off(const bt2x_index_desc* idx, uint64_t qlen, uint64_t off, int reject,
+                               bt2x_resolve_out* o) {
+	uint64_t top = 0, bot = idx->nfrag;
+	o->tidx = BT2X_NO_TIDX; o->toff = 0; o->tlen = 0; o->straddled = 0;
+	if(off >= idx->len || idx->nfrag == 0) return;
+	for(;;) {
+		const uint64_t elt = top + ((bot - top) >> 1);
+		const uint64_t lower = idx->rstarts[elt * 3];
+		const uint64_t upper = elt == idx->nfrag - 1 ? idx->len : idx->rstarts[(elt + 1) * 3];
+		if(lower <= off) {
+			if(upper > off) {
+				if(off + qlen > upper) {
+					o->straddled = 1;
+					if(reject) return;
+				}
+				o->tidx = (uint32_t)idx->rstarts[elt * 3 + 1];
+				o->toff = off - lower + idx->rstarts[elt * 3 + 2];
+				o->tlen = idx->plen[o->tidx];
+				return;
+			}
+			top = elt;
+		} else {
+			bot = elt;
+		}
+	}
+}
+
+int bt2o_resolve(const bt2x_index_desc* idx, const bt2x_resolve_in* in, uint32_t n, int reject_straddle,
+                 bt2x_resolve_out* out, bt2x_counters* ctr) {
+	uint64_t steps = 0;
+	if(!idx->offs) return BT2X_E_ARG;
+	for(uint32_t i = 0; i < n; i++) {
+		if(in[i].row > idx->len) return BT2X_E_ARG;
+		const uint64_t off = get_offset(idx, in[i].row, &steps);
+		joined_to_text_off(idx, in[i].qlen, off, reject_straddle, &out[i]);
+		out[i].joff = off;
+	}
+	if(ctr) {
+		memset(ctr, 0, sizeof(*ctr));
+		ctr->n_lf1 = steps;
+		ctr->n_problems = n;
+	}
+	return BT2X_OK;
 }
 
 /* ------------------------------------------------------------------- RNG */

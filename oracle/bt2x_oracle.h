@@ -31,6 +31,10 @@ int bt2o_dp_align(const bt2x_scoring* sc,
                   uint32_t* edits, uint32_t edit_cap, uint32_t* nedit_used,
                   bt2x_dp_debug* debug, bt2x_counters* ctr);
 
+/* SA resolution of BW elements: getOffset + joinedToTextOff (needs load_offs). */
+int bt2o_resolve(const bt2x_index_desc* idx, const bt2x_resolve_in* in, uint32_t n, int reject_straddle,
+                 bt2x_resolve_out* out, bt2x_counters* ctr);
+
 /* Helpers exposed for unit tests of the primitives. */
 uint64_t bt2o_count_side(const bt2x_index_desc* idx, uint64_t row, int c);
 void     bt2o_count_side_ex(const bt2x_index_desc* idx, uint64_t row, uint64_t out[4]);

@@ -11,6 +11,10 @@
 //           SwAligner::initRead/initRef/align/nextAlignment (aligner_sw.cpp:35-375)
 //           -> rectangle, reference window, E/F/H digests, sorted candidates and
 //           the full sequence of nextAlignment() results with RNG state.
+//   resolve : the seeds' reported BW ranges through GroupWalk2S::init/advanceElement
+//           (group_walk.h:917-1005) and Ebwt::joinedToTextOff (bt2_idx.cpp:54) as
+//           SwDriver::extendSeeds calls them (aligner_sw_driver.cpp:383-402), plus
+//           joinedToTextOff at every fragment boundary (straddle / reject cases).
 //
 // Options (scoring, seed length, --dpad, ...) are parsed by the reference's own
 // parseOptions() (bt2_search.cpp:1578) so every default is the reference's.
@@ -311,6 +315,128 @@ static int cmdDp(int argc, char** argv) {
 }
 
 
+// ------------------------------------------------------------------ resolve
+static void printJ(FILE* fo, const Ebwt* ebwt, TIndexOffU qlen, TIndexOffU off) {
+	for(int rej = 0; rej < 2; rej++) {
+		TIndexOffU tidx = 0, toff = 0, tlen = 0;      // zero-initialised like the caller
+		bool straddled = false;
+		ebwt->joinedToTextOff(qlen, off, tidx, toff, tlen, rej != 0, straddled);
+		fprintf(fo, " %lld %llu %llu %d", tidx == OFF_MASK ? -1LL : (long long)tidx,
+		        (unsigned long long)toff, (unsigned long long)tlen, (int)straddled);
+	}
+}
+
+static int cmdResolve(int argc, char** argv) {
+	if(argc < 4) { fprintf(stderr, "resolve <idx> <reads.fq> <out> [bt2 opts]\n"); return 2; }
+	std::string idx = argv[1], fq = argv[2], out = argv[3];
+	parseRefOptions(idx, fq, argc - 4, argv + 4);
+	Ebwt* ebwt = loadEbwt(idx);
+	BitPairReference ref(idx, false, false, NULL, NULL, false, false, false, false, false, false);
+	if(!ref.loaded()) { fprintf(stderr, "reference not loaded\n"); return 1; }
+	FILE* fo = fopen(out.c_str(), "w");
+	if(getenv("HARNESS_UNBUF")) setvbuf(fo, NULL, _IONBF, 0);
+	fprintf(fo, "# resolve idx=%s reads=%s len=%llu nfrag=%llu offrate=%d\n", idx.c_str(), fq.c_str(),
+	        (unsigned long long)ebwt->_eh._len, (unsigned long long)ebwt->_nFrag, (int)ebwt->_eh._offRate);
+	// fragment boundaries: J off qlen  {tidx toff tlen straddled} x {keep, reject}
+	const TIndexOffU nf = ebwt->_nFrag, len = ebwt->_eh._len;
+	size_t nj = 0;
+	for(TIndexOffU f = 0; f < nf && f < 400; f++) {
+		const TIndexOffU lower = ebwt->rstarts()[f * 3];
+		const TIndexOffU upper = f + 1 == nf ? len : ebwt->rstarts()[(f + 1) * 3];
+		const TIndexOffU qls[3] = {1, (TIndexOffU)multiseedLen, 100};
+		for(int q = 0; q < 3; q++) {
+			const TIndexOffU ql = qls[q];
+			std::set<TIndexOffU> offs;
+			offs.insert(lower); offs.insert(lower + 1); offs.insert(upper - 1);
+			if(upper >= ql) { offs.insert(upper - ql); offs.insert(upper - ql + 1); }
+			if(upper >= ql + 1) offs.insert(upper - ql - 1);
+			for(TIndexOffU o : offs) {
+				if(o < lower || o >= upper) continue;
+				fprintf(fo, "J %llu %llu", (unsigned long long)o, (unsigned long long)ql);
+				printJ(fo, ebwt, ql, o);
+				fprintf(fo, "\n");
+				nj++;
+			}
+		}
+	}
+	// seed ranges through GroupWalk2S
+	MultiSeedResults srs(1, multiseedLen, gNofw, gNorc);
+	MultiSeedAligner als(ebwt, srs);
+	GroupWalkState gwstate(GW_CAT);
+	PerReadMetrics prm;
+	RandomSource rnd; rnd.init(7);
+	std::ifstream in(fq);
+	Fq r; size_t ridx = 0, nw = 0;
+	while(readFq(in, r)) {
+		Read rd(r.name.c_str(), r.seq.c_str(), r.qual.c_str());
+		const size_t rdlen = rd.length();
+		size_t myidx = ridx++;
+		if(rdlen >= 256 || rdlen < 1) continue;
+		const int interval = std::max((int)msIval.f<int>((double)rdlen), 1);
+		const uint32_t nrounds = std::min<uint16_t>(nSeedRounds, interval);
+		for(uint32_t roundi = 0; roundi < nrounds; roundi++) {
+			const uint32_t offset = (interval * roundi) / nrounds;
+			if(offset > 0 && multiseedLen + offset > rdlen) break;
+			srs.clearSeeds();
+			srs.prepareOneSeed(0, offset, interval, &rd);
+			Read* rds[1] = { &rd };
+			srs.instantiateSeeds(rds);
+			als.reserveBuffers();
+			als.prepareSearchAllSeedsOne(0);
+			als.searchAllSeedsDoAll(true);
+			for(size_t k = 0; k < als._bufVec_filled; k++) {
+				const SeedAlignerSearchParams& p = als._paramVec[k];
+				const SeedAlignerSearchData& d = als._dataVec[k];
+				if(!d.need_reporting) continue;
+				const TIndexOffU topf = d.bwt.topf, sz = d.bwt.botf - d.bwt.topf;
+				if(sz == 0) continue;
+				const size_t klen = (size_t)p.cs.n_seed_steps;
+				fprintf(fo, "G %zu %u %d %d %llu %llu %zu\n", myidx, roundi, (int)p.fw, (int)p.seedoffidx,
+				        (unsigned long long)topf, (unsigned long long)d.bwt.botf, klen);
+				if(sz <= (TIndexOffU)TStateVSize) {
+					// GroupWalk2S keeps its walk states in a fixed DList of TStateVSize (6)
+					// (group_walk.h:92, :900); a range of n elements creates at most n
+					// states, so ranges of <= 6 elements walk safely.  Larger ranges can
+					// overflow it (st.expand(), group_walk.h:762, writes past the DList
+					// into hit_) -- for them the W record is Ebwt::getOffset(row), the
+					// value group_walk.h:425-432 asserts the walk produces.
+					// A cache slice pair as AlignmentCache::queryQval makes (aligner_cache.h:636-644)
+					EList<TIndexOffU> salist;
+					salist.resize(2 * sz);
+					TSlice offs(salist, 0, sz), fmap(salist, sz, sz);
+					offs.fill(OFF_MASK); fmap.fill(OFF_MASK);
+					SARangeWithOffs<TSlice> sa(topf, klen, offs, fmap);
+					GroupWalk2S<TSlice> gw;
+					gw.init(*ebwt, ref, sa, rnd);
+					for(TIndexOffU e = 0; e < sz; e++) {
+						WalkResult wr;
+						gw.advanceElement(e, *ebwt, ref, sa, gwstate, wr, prm);
+						fprintf(fo, "W %llu %llu %llu %llu", (unsigned long long)wr.elt.elt,
+						        (unsigned long long)wr.bwrow, (unsigned long long)wr.toff,
+						        (unsigned long long)wr.elt.len);
+						printJ(fo, ebwt, wr.elt.len, wr.toff);
+						fprintf(fo, "\n");
+						nw++;
+					}
+				} else {
+					const TIndexOffU step = sz <= 8 ? 1 : sz / 8;
+					for(TIndexOffU e = 0; e < sz; e += step) {
+						const TIndexOffU row = topf + e, toff = ebwt->getOffset(row);
+						fprintf(fo, "V %llu %llu %llu %llu", (unsigned long long)e, (unsigned long long)row,
+						        (unsigned long long)toff, (unsigned long long)klen);
+						printJ(fo, ebwt, klen, toff);
+						fprintf(fo, "\n");
+						nw++;
+					}
+				}
+			}
+		}
+	}
+	fclose(fo);
+	fprintf(stderr, "resolve: %zu reads, %zu walk results, %zu boundary probes\n", ridx, nw, nj);
+	return 0;
+}
+
 // -------------------------------------------------------------------- bench
 // CPU baseline for bench.py: the reference's own hot path, OpenMP-parallel the way
 // bt2_search.cpp drives it, over a FASTQ sample whose names carry the true origin.
@@ -426,6 +552,7 @@ int main(int argc, char** argv) {
 		if(cmd == "seeds") return harness::cmdSeeds(argc - 1, argv + 1);
 		if(cmd == "dp") return harness::cmdDp(argc - 1, argv + 1);
 		if(cmd == "bench") return harness::cmdBench(argc - 1, argv + 1);
+		if(cmd == "resolve") return harness::cmdResolve(argc - 1, argv + 1);
 	} catch(int e) {
 		fprintf(stderr, "reference threw %d\n", e);
 		return 1;

@@ -239,3 +239,48 @@ def dp_header_scoring(golden: str) -> dict:
     rfc, rfl = (int(v) for v in kv["rfg"].split(","))
     return {"mm_max": mx, "mm_min": mn, "n_pen": int(kv["np"]), "rdg_const": rdc,
             "rdg_linear": rdl, "rfg_const": rfc, "rfg_linear": rfl, "gapbar": int(kv["gapbar"])}
+
+
+class ResolveCase:
+    """tests/golden/resolve_*.txt.xz (refharness resolve): seed-range elements through
+    GroupWalk2S::advanceElement ('W', ranges of <= 6 elements) or Ebwt::getOffset ('V',
+    larger ranges), and joinedToTextOff fragment-boundary probes ('J'); every record
+    carries joinedToTextOff's (tidx, toff, tlen, straddled) for rejectStraddle = false
+    and true (tidx -1 = OFF_MASK)."""
+
+    def __init__(self, path: str):
+        walk, probe = [], []
+        self.kinds = []
+        with open_text(path) as f:
+            for line in f:
+                t = line.split()
+                if not t or t[0] in ("#", "G"):
+                    continue
+                if t[0] in ("W", "V"):
+                    walk.append([int(x) for x in t[2:]])           # row joff qlen + 8
+                    self.kinds.append(t[0])
+                elif t[0] == "J":
+                    probe.append([int(x) for x in t[1:]])          # off qlen + 8
+        w = np.array(walk, dtype=np.int64).reshape(-1, 11)
+        p = np.array(probe, dtype=np.int64).reshape(-1, 10)
+        self.rows, self.joff, self.qlen = w[:, 0].astype(np.uint64), w[:, 1].astype(np.uint64), w[:, 2]
+        self.exp = [self._res(w[:, 3:7]), self._res(w[:, 7:11])]
+        self.j_off, self.j_qlen = p[:, 0].astype(np.uint64), p[:, 1]
+        self.j_exp = [self._res(p[:, 2:6]), self._res(p[:, 6:10])]
+        self.n = len(w)
+
+    @staticmethod
+    def _res(a):
+        tidx = np.where(a[:, 0] < 0, abi.NO_TIDX, a[:, 0]).astype(np.uint32)
+        return {"tidx": tidx, "toff": a[:, 1].astype(np.uint64), "tlen": a[:, 2].astype(np.uint64),
+                "straddled": a[:, 3].astype(np.uint32)}
+
+
+def compare_resolve(out, exp, joff=None):
+    """Mismatch count of RESOLVE_OUT records against a ResolveCase expectation dict."""
+    bad = 0
+    for k, v in exp.items():
+        bad += int((out[k] != v).sum())
+    if joff is not None:
+        bad += int((out["joff"] != joff).sum())
+    return bad

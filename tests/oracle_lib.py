@@ -32,6 +32,8 @@ def lib():
                                     vp, u32, ctypes.POINTER(ctypes.c_uint32),
                                     vp, u32, ctypes.POINTER(ctypes.c_uint32),
                                     ctypes.POINTER(abi.DpDebug), ctypes.POINTER(abi.Counters)]
+        L.bt2o_resolve.argtypes = [ctypes.POINTER(abi.IndexDesc), vp, u32, i32, vp,
+                                   ctypes.POINTER(abi.Counters)]
         L.bt2o_count_side.restype = ctypes.c_uint64
         L.bt2o_count_side.argtypes = [ctypes.POINTER(abi.IndexDesc), ctypes.c_uint64, i32]
         _LIB = L
@@ -63,6 +65,19 @@ def seed_search(idx: OracleIndex, reads: np.ndarray, inp: np.ndarray, do_extend=
     ctr = abi.Counters()
     rc = lib().bt2o_seed_search(ctypes.byref(idx.desc), abi.ptr(reads), abi.ptr(inp), len(inp),
                                 int(do_extend), abi.ptr(out), ctypes.byref(ctr))
+    assert rc == 0, rc
+    return out, ctr.as_dict()
+
+
+def resolve(idx: OracleIndex, rows, qlen, reject_straddle=False):
+    rows = np.asarray(rows, dtype=np.uint64)
+    inp = np.zeros(len(rows), dtype=abi.RESOLVE_IN)
+    inp["row"] = rows
+    inp["qlen"] = qlen
+    out = np.zeros(len(rows), dtype=abi.RESOLVE_OUT)
+    ctr = abi.Counters()
+    rc = lib().bt2o_resolve(ctypes.byref(idx.desc), abi.ptr(inp), len(inp), int(reject_straddle),
+                            abi.ptr(out), ctypes.byref(ctr))
     assert rc == 0, rc
     return out, ctr.as_dict()
 

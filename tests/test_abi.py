@@ -36,6 +36,7 @@ def test_struct_sizes_match_numpy_mirrors():
     assert s[5] == ctypes.sizeof(abi.Scoring)
     assert s[6] == ctypes.sizeof(abi.IndexDesc)
     assert s[7] == ctypes.sizeof(abi.Counters)
+    assert s[8:10] == [abi.RESOLVE_IN.itemsize, abi.RESOLVE_OUT.itemsize]
 
 
 def test_scoring_tables_match_oracle():

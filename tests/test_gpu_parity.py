@@ -313,3 +313,69 @@ def test_empty_batches(ctxs):
     res = ctx.dp_align(np.zeros(1, np.uint8), np.zeros(1, np.uint8), np.zeros(1, np.uint8),
                        np.zeros(0, dtype=abi.DP_IN), debug=False)
     assert len(res[0]) == 0
+
+
+RESOLVE_SETS = [("lambda_virus", "resolve_lambda.txt.xz"), ("rep", "resolve_rep.txt.xz")]
+
+
+def _check_resolve(ctx, oidx, case):
+    for rej in (0, 1):
+        out = ctx.resolve(case.rows, case.qlen, rej)
+        assert g.compare_resolve(out, case.exp[rej], case.joff) == 0
+    # boundary probes through the rows that hold those offsets (oracle SA)
+    n = int(oidx.desc.len) + 1
+    sa, _ = ol.resolve(oidx, np.arange(n, dtype=np.uint64), 0)
+    isa = np.empty(n, dtype=np.uint64)
+    isa[sa["joff"].astype(np.int64)] = np.arange(n, dtype=np.uint64)
+    rows = isa[case.j_off.astype(np.int64)]
+    for rej in (0, 1):
+        for ql in np.unique(case.j_qlen):
+            m = case.j_qlen == ql
+            out = ctx.resolve(rows[m], int(ql), rej)
+            assert g.compare_resolve(out, {k: v[m] for k, v in case.j_exp[rej].items()}, case.j_off[m]) == 0
+    # every row of the index, against the oracle ('$' suffix row included)
+    allrows = np.arange(n, dtype=np.uint64)
+    out = ctx.resolve(allrows, 22, 0)
+    exp, _ = ol.resolve(oidx, allrows, 22, 0)
+    np.testing.assert_array_equal(out, exp)
+
+
+@pytest.mark.parametrize("name,gold", RESOLVE_SETS)
+def test_resolve_matches_reference_golden(ctxs, golden_dir, name, gold):
+    """SA resolution (resident full SA lookup + joinedToTextOff) vs the reference's
+    GroupWalk2S / getOffset / joinedToTextOff outputs and the oracle."""
+    ctx, _ = ctxs[name]
+    base = g.materialize_index(name, str(golden_dir))
+    oidx = ol.OracleIndex(base, load_offs=True)
+    case = g.ResolveCase(os.path.join(g.GOLDEN, gold))
+    _check_resolve(ctx, oidx, case)
+    c = ctx.last_counters(abi.K_RESOLVE)
+    assert c["n_lf1"] == 0 and c["n_problems"] == int(oidx.desc.len) + 1
+    assert ctx.last_kernel_ms(abi.K_RESOLVE) > 0
+
+
+@pytest.mark.parametrize("env", [{"BT2X_FULL_SA": "0"}, {"BT2X_FM_SIDES": "1"}])
+def test_resolve_lf_walk_paths(golden_dir, monkeypatch, env):
+    """Without the full SA the kernel walks LF to the SA sample (blocks, or the .bt2l
+    sides): same results, and the LF step count equals the oracle's."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    base = g.materialize_index("rep", str(golden_dir))
+    ctx = lib.Context(lib.Index(base, load_offs=True))
+    oidx = ol.OracleIndex(base, load_offs=True)
+    case = g.ResolveCase(os.path.join(g.GOLDEN, "resolve_rep.txt.xz"))
+    _check_resolve(ctx, oidx, case)
+    c = ctx.last_counters(abi.K_RESOLVE)
+    _, oc = ol.resolve(oidx, np.arange(int(oidx.desc.len) + 1, dtype=np.uint64), 22)
+    assert c["n_lf1"] == oc["n_lf1"] > 0
+
+
+def test_resolve_argument_errors(ctxs, golden_dir):
+    ctx, oidx = ctxs["rep"]
+    with pytest.raises(lib.Bt2xError):
+        ctx.resolve([int(oidx.desc.len) + 1], 22)            # row beyond the BWT
+    assert len(ctx.resolve([], 22)) == 0
+    base = g.materialize_index("rep", str(golden_dir))
+    noffs = lib.Context(lib.Index(base, load_offs=False))    # no SA sample: no resolution
+    with pytest.raises(lib.Bt2xError):
+        noffs.resolve([0], 22)

@@ -60,3 +60,39 @@ def test_dp_matches_reference(gold):
     assert (out["status"] == 1).sum() > 1000 and (out["status"] == 0).sum() > 100
     assert (recs["gaps"] > 0).sum() > 100 and (recs["ns"] > 0).sum() > 10
     assert (out["nrec"] > 1).sum() > 100
+
+
+RESOLVE_SETS = [("lambda_virus", "resolve_lambda.txt.xz"), ("rep", "resolve_rep.txt.xz")]
+
+
+@pytest.mark.parametrize("name,gold", RESOLVE_SETS)
+def test_resolve_matches_reference(golden_dir, name, gold):
+    """getOffset + joinedToTextOff restatement vs GroupWalk2S / getOffset / joinedToTextOff
+    outputs of the reference (seed-range elements and fragment-boundary probes)."""
+    base = g.materialize_index(name, str(golden_dir))
+    idx = ol.OracleIndex(base, load_offs=True)
+    case = g.ResolveCase(os.path.join(g.GOLDEN, gold))
+    assert case.n > 5000 and "W" in case.kinds
+    for rej in (0, 1):
+        out, ctr = ol.resolve(idx, case.rows, case.qlen, rej)
+        assert g.compare_resolve(out, case.exp[rej], case.joff) == 0
+    assert ctr["n_lf1"] > 0
+    # boundary probes: rows holding those joined offsets, via the oracle's own SA
+    n = int(idx.desc.len) + 1
+    sa, _ = ol.resolve(idx, np.arange(n, dtype=np.uint64), 0)
+    isa = np.empty(n, dtype=np.uint64)
+    isa[sa["joff"].astype(np.int64)] = np.arange(n, dtype=np.uint64)
+    assert sorted(sa["joff"].tolist()) == list(range(n))
+    rows = isa[case.j_off.astype(np.int64)]
+    for rej in (0, 1):
+        for ql in np.unique(case.j_qlen):
+            m = case.j_qlen == ql
+            out, _ = ol.resolve(idx, rows[m], int(ql), rej)
+            exp = {k: v[m] for k, v in case.j_exp[rej].items()}
+            assert g.compare_resolve(out, exp, case.j_off[m]) == 0
+    if name == "rep":       # multi-fragment index: straddles and rejections are covered
+        assert case.j_exp[0]["straddled"].sum() > 10
+        assert (case.j_exp[1]["tidx"] == g.abi.NO_TIDX).sum() > 10
+    # the '$' suffix row (offset len) lies in no fragment
+    out, _ = ol.resolve(idx, [n - 1 if sa["joff"][n - 1] == n - 1 else int(isa[n - 1])], 1)
+    assert out["tidx"][0] == g.abi.NO_TIDX

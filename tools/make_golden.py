@@ -12,6 +12,9 @@ Steps (all outputs xz-compressed under tests/golden/):
      lengths (and an N-rich set); seeds golden + DP golden at the reference defaults,
      DP golden at --dpad 12 (config C3's setting) and DP golden under a non-default
      scoring scheme.
+  4. resolve: the committed lambda and rep indexes/reads through refharness resolve
+     (GroupWalk2S + joinedToTextOff on every reported seed range, fragment-boundary
+     probes).  `make_golden.py resolve` regenerates only these.
 Each golden file starts with a '#' header naming the command that produced it.
 """
 from __future__ import annotations
@@ -47,8 +50,33 @@ def run(cmd, **kw):
     subprocess.run(cmd, check=True, **kw)
 
 
+def xz_unpack(src: str, dst: str) -> None:
+    with lzma.open(src, "rb") as fi, open(dst, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+
+
+def resolve_goldens(tmp: str) -> None:
+    for name, fq in (("lambda_virus", "lambda_longreads.fq"), ("rep", "rep_reads.fq")):
+        base = os.path.join(tmp, name)
+        for k in "1234":
+            xz_unpack(os.path.join(GOLD, f"{name}.{k}.bt2l.xz"), f"{base}.{k}.bt2l")
+        rfq = os.path.join(tmp, fq)
+        xz_unpack(os.path.join(GOLD, fq + ".xz"), rfq)
+        tag = "lambda" if name == "lambda_virus" else name
+        out = os.path.join(tmp, f"resolve_{tag}.txt")
+        run([HARN, "resolve", base, rfq, out])
+        xz_copy(out, os.path.join(GOLD, f"resolve_{tag}.txt.xz"))
+
+
 def main() -> None:
     run(["make", "-C", os.path.join(ROOT, "oracle"), "ref", "oracle"])
+    if sys.argv[1:] == ["resolve"]:
+        tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
+        try:
+            resolve_goldens(tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     os.makedirs(GOLD, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
     try:
@@ -107,6 +135,7 @@ def main() -> None:
         with open(os.path.join(GOLD, "builder_md5.json"), "w") as f:
             json.dump({"tricky": md5, "_note": "md5 of oracle/_ref/bowtie2-build-l tests/golden/tricky.fa "
                        "output (tools/make_golden.py)"}, f, indent=1)
+        resolve_goldens(tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     for f in sorted(os.listdir(GOLD)):
