@@ -132,6 +132,99 @@ private:
 	size_t last_len_ = 0, last_off_ = 0;
 };
 
+// Per-read seed hits after the seed kernel: SeedAligner::searchAllSeedsFinalize
+// (aligner_seed.cpp:508-540) feeds every need_reporting seed to SeedResults::add
+// (aligner_seed.h:603-641) as a QVal of one BW range with botf - topf elements; then
+// rankSeedHits (aligner_seed.h:1000-1061) orders them for extension and hitsByRank
+// (:1120-1145) reads the order back.  Rnd: nextBool(), nextU32() (RandomSource).
+class SeedHitsHip {
+public:
+	struct Hit {
+		uint64_t topf = 0, botf = 0;
+		uint8_t nlex = 0;
+		bool valid = false;
+		uint64_t numElts() const { return botf - topf; }
+	};
+	// SeedResults::clearSeeds + reset: numOffs seed offsets per strand.
+	void reset(uint32_t numOffs) {
+		numOffs_ = numOffs;
+		hits_[0].assign(numOffs, Hit()); hits_[1].assign(numOffs, Hit());
+		sorted_[0].assign(numOffs, false); sorted_[1].assign(numOffs, false);
+		rankOffs_.clear(); rankFws_.clear();
+		nonzTot_ = nonzFw_ = nonzRc_ = uniTot_ = repTot_ = 0;
+		numElts_ = numEltsFw_ = numEltsRc_ = 0;
+	}
+	// searchAllSeedsFinalize's per-seed step: seed i of strand fw, kernel output d.
+	void add(uint32_t seedIdx, bool fw, const bt2x_seed_out& d) {
+		if(!d.need_reporting || seedIdx >= numOffs_) return;
+		Hit& h = hits_[fw ? 0 : 1][seedIdx];
+		h.topf = d.topf; h.botf = d.botf; h.nlex = d.nlex; h.valid = true;
+		const uint64_t n = h.numElts();
+		(fw ? numEltsFw_ : numEltsRc_) += n;
+		(fw ? nonzFw_ : nonzRc_)++;
+		numElts_ += n;
+		nonzTot_++;
+		if(n == 1) uniTot_++; else repTot_++;
+	}
+	template<class Rnd>
+	void rankSeedHits(Rnd& rnd, bool all) {
+		if(all) {
+			for(uint32_t i = 1; i < numOffs_; i++)
+				for(int fwi = 0; fwi <= 1; fwi++)
+					if(hits_[fwi][i].valid && hits_[fwi][i].numElts() > 0) push(i, fwi == 0);
+			if(numOffs_ > 0 && hits_[0][0].valid && hits_[0][0].numElts() > 0) push(0, true);
+			if(numOffs_ > 0 && hits_[1][0].valid && hits_[1][0].numElts() > 0) push(0, false);
+			return;
+		}
+		while(rankOffs_.size() < nonzTot_) {
+			uint64_t minsz = 0xffffffffu;              // MAX_U32 (aligner_seed.h:1024)
+			uint32_t minidx = 0;
+			bool minfw = true;
+			const bool rb = rnd.nextBool();
+			for(int fwi = 0; fwi <= 1; fwi++) {
+				const bool fw = (fwi == (rb ? 1 : 0));
+				const std::vector<Hit>& rrs = hits_[fw ? 0 : 1];
+				const std::vector<bool>& sorted = sorted_[fw ? 0 : 1];
+				uint32_t i = rnd.nextU32() % numOffs_;
+				for(uint32_t ii = 0; ii < numOffs_; ii++) {
+					if(rrs[i].valid && rrs[i].numElts() > 0 && !sorted[i] && rrs[i].numElts() < minsz) {
+						minsz = rrs[i].numElts(); minidx = i; minfw = fw;
+					}
+					if(++i == numOffs_) i = 0;
+				}
+			}
+			if(minsz == 0xffffffffu) throw Error(BT2X_E_ARG, "rankSeedHits: no rankable hit");
+			sorted_[minfw ? 0 : 1][minidx] = true;
+			push(minidx, minfw);
+		}
+	}
+	size_t nonzeroOffsets() const { return nonzTot_; }
+	size_t numOffs() const { return numOffs_; }
+	size_t ranked() const { return rankOffs_.size(); }
+	// hitsByRank(r, offidx, off, fw, seedlen) minus the offset arithmetic
+	const Hit& hitsByRank(size_t r, uint32_t& offidx, bool& fw) const {
+		offidx = rankOffs_[r]; fw = rankFws_[r];
+		return hits_[fw ? 0 : 1][offidx];
+	}
+	const Hit& hit(bool fw, uint32_t i) const { return hits_[fw ? 0 : 1][i]; }
+	size_t nonzFw() const { return nonzFw_; }
+	size_t nonzRc() const { return nonzRc_; }
+	uint64_t numElts() const { return numElts_; }
+	uint64_t numEltsFw() const { return numEltsFw_; }
+	uint64_t numEltsRc() const { return numEltsRc_; }
+	size_t uniTot() const { return uniTot_; }
+	size_t repTot() const { return repTot_; }
+private:
+	void push(uint32_t i, bool fw) { rankOffs_.push_back(i); rankFws_.push_back(fw); }
+	uint32_t numOffs_ = 0;
+	std::vector<Hit> hits_[2];
+	std::vector<bool> sorted_[2];
+	std::vector<uint32_t> rankOffs_;
+	std::vector<bool> rankFws_;
+	size_t nonzTot_ = 0, nonzFw_ = 0, nonzRc_ = 0, uniTot_ = 0, repTot_ = 0;
+	uint64_t numElts_ = 0, numEltsFw_ = 0, numEltsRc_ = 0;
+};
+
 // ------------------------------------------------------------------------ DP
 
 // One alignment out of nextAlignment(): the AlnRes fields the caller copies

@@ -15,6 +15,10 @@
 //           (group_walk.h:917-1005) and Ebwt::joinedToTextOff (bt2_idx.cpp:54) as
 //           SwDriver::extendSeeds calls them (aligner_sw_driver.cpp:383-402), plus
 //           joinedToTextOff at every fragment boundary (straddle / reject cases).
+//   rank    : SeedAligner::searchAllSeedsFinalize (aligner_seed.cpp:508-540) ->
+//           SeedResults::add (aligner_seed.h:603) and rankSeedHits(rnd, all)
+//           (aligner_seed.h:1000-1061) with a per-(read, round) RNG seed -> rank order,
+//           hit counters and the RNG state afterwards.
 //
 // Options (scoring, seed length, --dpad, ...) are parsed by the reference's own
 // parseOptions() (bt2_search.cpp:1578) so every default is the reference's.
@@ -437,6 +441,68 @@ static int cmdResolve(int argc, char** argv) {
 	return 0;
 }
 
+// --------------------------------------------------------------------- rank
+static void printRank(FILE* fo, const char* tag, size_t ridx, uint32_t roundi, uint32_t seed,
+                      const SeedResults& sr, const RandomSource& rnd) {
+	fprintf(fo, "%s %zu %u %u %u %zu %zu %zu %zu %zu %zu %zu %zu %u", tag, ridx, roundi, seed,
+	        (unsigned)sr.numOffs_, (size_t)sr.nonzTot_, (size_t)sr.nonzFw_, (size_t)sr.nonzRc_, (size_t)sr.numElts_,
+	        (size_t)sr.numEltsFw_, (size_t)sr.numEltsRc_, (size_t)sr.uniTot_, (size_t)sr.repTot_,
+	        rnd.last);
+	for(size_t r = 0; r < sr.rankOffs_.size(); r++) {
+		uint32_t offidx = 0, off = 0, seedlen = 0; bool fw = true;
+		const QVal& qv = sr.hitsByRank(r, offidx, off, fw, seedlen);
+		fprintf(fo, " %u,%d,%llu", offidx, (int)fw, (unsigned long long)qv.numElts());
+	}
+	fprintf(fo, "\n");
+}
+
+static int cmdRank(int argc, char** argv) {
+	if(argc < 4) { fprintf(stderr, "rank <idx> <reads.fq> <out> [bt2 opts]\n"); return 2; }
+	std::string idx = argv[1], fq = argv[2], out = argv[3];
+	parseRefOptions(idx, fq, argc - 4, argv + 4);
+	Ebwt* ebwt = loadEbwt(idx);
+	FILE* fo = fopen(out.c_str(), "w");
+	fprintf(fo, "# rank idx=%s reads=%s seedlen=%d rounds=%d\n", idx.c_str(), fq.c_str(),
+	        (int)multiseedLen, (int)nSeedRounds);
+	MultiSeedResults srs(1, multiseedLen, gNofw, gNorc);
+	MultiSeedAligner als(ebwt, srs);
+	std::ifstream in(fq);
+	Fq r; size_t ridx = 0, nk = 0;
+	while(readFq(in, r)) {
+		Read rd(r.name.c_str(), r.seq.c_str(), r.qual.c_str());
+		const size_t rdlen = rd.length();
+		size_t myidx = ridx++;
+		if(rdlen >= 256 || rdlen < 1) continue;
+		const int interval = std::max((int)msIval.f<int>((double)rdlen), 1);
+		const uint32_t nrounds = std::min<uint16_t>(nSeedRounds, interval);
+		for(uint32_t roundi = 0; roundi < nrounds; roundi++) {
+			const uint32_t offset = (interval * roundi) / nrounds;
+			if(offset > 0 && multiseedLen + offset > rdlen) break;
+			srs.clearSeeds();
+			srs.prepareOneSeed(0, offset, interval, &rd);
+			Read* rds[1] = { &rd };
+			srs.instantiateSeeds(rds);
+			als.reserveBuffers();
+			als.prepareSearchAllSeedsOne(0);
+			als.searchAllSeedsDoAll(true);
+			SeedResults& sr = srs.getSR(0);
+			als._als[0].searchAllSeedsFinalize(als.getCache(0), sr);
+			if(sr.nonzeroOffsets() == 0) { fprintf(fo, "Z %zu %u\n", myidx, roundi); continue; }
+			const uint32_t seed = (uint32_t)(myidx * 2654435761u + roundi * 97u + 1u);
+			RandomSource rnd; rnd.init(seed);
+			sr.rankSeedHits(rnd, false);
+			printRank(fo, "K", myidx, roundi, seed, sr, rnd);
+			sr.rankOffs_.clear(); sr.rankFws_.clear();
+			sr.rankSeedHits(rnd, true);
+			printRank(fo, "A", myidx, roundi, seed, sr, rnd);
+			nk++;
+		}
+	}
+	fclose(fo);
+	fprintf(stderr, "rank: %zu reads, %zu ranked rounds\n", ridx, nk);
+	return 0;
+}
+
 // -------------------------------------------------------------------- bench
 // CPU baseline for bench.py: the reference's own hot path, OpenMP-parallel the way
 // bt2_search.cpp drives it, over a FASTQ sample whose names carry the true origin.
@@ -553,6 +619,7 @@ int main(int argc, char** argv) {
 		if(cmd == "dp") return harness::cmdDp(argc - 1, argv + 1);
 		if(cmd == "bench") return harness::cmdBench(argc - 1, argv + 1);
 		if(cmd == "resolve") return harness::cmdResolve(argc - 1, argv + 1);
+		if(cmd == "rank") return harness::cmdRank(argc - 1, argv + 1);
 	} catch(int e) {
 		fprintf(stderr, "reference threw %d\n", e);
 		return 1;

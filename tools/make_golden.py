@@ -14,7 +14,8 @@ Steps (all outputs xz-compressed under tests/golden/):
      scoring scheme.
   4. resolve: the committed lambda and rep indexes/reads through refharness resolve
      (GroupWalk2S + joinedToTextOff on every reported seed range, fragment-boundary
-     probes).  `make_golden.py resolve` regenerates only these.
+     probes) and, for rep, refharness rank (searchAllSeedsFinalize + rankSeedHits).
+     `make_golden.py resolve` regenerates only these.
 Each golden file starts with a '#' header naming the command that produced it.
 """
 from __future__ import annotations
@@ -66,6 +67,10 @@ def resolve_goldens(tmp: str) -> None:
         out = os.path.join(tmp, f"resolve_{tag}.txt")
         run([HARN, "resolve", base, rfq, out])
         xz_copy(out, os.path.join(GOLD, f"resolve_{tag}.txt.xz"))
+        if name == "rep":
+            out = os.path.join(tmp, "rank_rep.txt")
+            run([HARN, "rank", base, rfq, out])
+            xz_copy(out, os.path.join(GOLD, "rank_rep.txt.xz"))
 
 
 def main() -> None:
