@@ -206,8 +206,19 @@ typedef struct {
 	uint16_t refns;          /* AlnRes::refns_                                   */
 	int64_t  refoff;         /* refcoord_.off() = col + rect.refl                */
 	uint32_t edit_off;       /* edits[edit_off .. +nedit), final order of ned()  */
-	uint32_t pad1;
+	uint32_t nbuf;           /* edit-buffer image, see below                     */
 } bt2x_aln_rec;
+
+/* Edit-buffer image.  The reference keeps the edits of every nextAlignment() attempt in
+ * one per-read buffer (SwDriver::resGap_.alres.ned_, a DList whose storage is inline) and
+ * the alignments it reports copy only the pointer to that storage (DList's implicit copy,
+ * ds.h:979-1040).  The SAM record printed at the end of the read therefore shows the
+ * buffer's final contents, not the reported edits.  To reproduce that, each
+ * record carries edits[edit_off .. edit_off + nbuf): the buffer entries written during
+ * the call, as they stand when it returns (a failed backtrace leaves the edits it pushed
+ * in backtrace order; a success leaves its final list, which is also the first nedit
+ * entries).  A caller replays the images of the calls it consumed, in order, over one
+ * buffer per read. */
 
 /* Packed Edit (edit.h:58-310): pos in bits 0-9, type (EDIT_TYPE_*) 12-14,
  * chr 16-23, qchr 24-31 (ASCII, as in Edit::chr/qchr). */

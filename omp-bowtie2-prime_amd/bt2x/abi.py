@@ -21,7 +21,7 @@ DP_OUT = np.dtype([("status", "<i4"), ("best", "<i4"), ("ncand", "<u2"), ("nrec"
 ALN_REC = np.dtype([("ntries", "<u2"), ("ok", "u1"), ("pad0", "u1"), ("score", "<i2"),
                     ("ns", "<u2"), ("gaps", "<u2"), ("nedit", "<u2"),
                     ("bases_aligned", "<u2"), ("refns", "<u2"), ("refoff", "<i8"),
-                    ("edit_off", "<u4"), ("pad1", "<u4")], align=True)
+                    ("edit_off", "<u4"), ("nbuf", "<u4")], align=True)
 RESOLVE_IN = np.dtype([("row", "<u8"), ("qlen", "<u4"), ("pad", "<u4")], align=True)
 RESOLVE_OUT = np.dtype([("joff", "<u8"), ("toff", "<u8"), ("tlen", "<u8"), ("tidx", "<u4"),
                         ("straddled", "<u4")], align=True)

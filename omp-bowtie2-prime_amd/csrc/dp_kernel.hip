@@ -131,6 +131,16 @@ __device__ __forceinline__ uint32_t row_info(int rdc, bool gbar, int mm) {
 	return (uint32_t)rdc | (gbar ? 8u : 0u) | ((uint32_t)mm << 4);
 }
 
+// Copy the edit-buffer entries [0, hi) written by one nextAlignment call to the edits
+// arena; returns their offset (0 when nothing was written).
+__device__ __forceinline__ uint32_t publish_edbuf(const DpLaunch& a, const uint32_t* stage_ed, int lane, int hi) {
+	if(hi <= 0) return 0;
+	const uint32_t eo = atomicAdd(&a.counters[1], (uint32_t)hi);
+	if(eo + (uint32_t)hi <= a.edit_cap)
+		for(int k = 0; k < hi; k++) a.edits[eo + k] = stage_ed[(size_t)k * 64 + lane];
+	return eo;
+}
+
 // SwAligner::nextAlignment until done() for problem pi (lane gl of the group whose fill
 // output starts at gslot): its candidates in order, each not already reportedThrough
 // backtraced over the fill's traceback bytes; records and edits staged per lane.
@@ -153,8 +163,11 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 		const int ncand = o.ncand;
 		const int row0 = R - 1;
 		int ndone = 0, nrec = 0;
+		// stage_ed doubles as the reference's per-read edit buffer (SwResult::alres.ned_,
+		// bt2x.h "edit-buffer image"): attempts write it from index 0, a success leaves its
+		// final list there; hi = entries written during the current call.
 		while(ndone < ncand) {
-			int ntries = 0;
+			int ntries = 0, hi = 0;
 			bool found = false;
 			while(ndone < ncand) {
 				const int col0 = cands[(size_t)ndone * 64 + gl];
@@ -226,7 +239,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 						gaps++;
 					}
 				}
-				if(!ok || !over_core) continue;
+				if(!ok || !over_core) { hi = max(hi, ne); continue; }
 				if(tb_end & TB_MM) {                     // the final (row 0) cell
 					const int rdc = rd[row], refc = rf[col];
 					const bool amb = rdc > 3 || refc > 3;
@@ -237,36 +250,44 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 					bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
 					if(amb) ns++;
 				}
-				if(ns > p.nceil) continue;
+				if(ns > p.nceil) { hi = max(hi, ne); continue; }
 				int refns = 0;
 				for(int k = col; k <= col0; k++) refns += (rf[k] > 3);
 				const int trimBeg = 0;
 				const int extent = R - trimBeg - (R - row0 - 1);
-				// publish the edit list in ned() order: reverse(), pos -= trimBeg, and
-				// for the reverse-complement strand invertEdits() (edit.cpp:50-78)
-				const uint32_t eo = atomicAdd(&a.counters[1], (uint32_t)ne);
-				if(eo + (uint32_t)ne <= a.edit_cap) {
+				// the edit list in ned() order, in place: reverse(), pos -= trimBeg, and for
+				// the reverse-complement strand invertEdits() (reverse again, mirror pos;
+				// edit.cpp:50-78)
+				if(p.fw) {
+					for(int k = 0; k < ne / 2; k++) {
+						const uint32_t x = stage_ed[(size_t)k * 64 + lane];
+						stage_ed[(size_t)k * 64 + lane] = stage_ed[(size_t)(ne - 1 - k) * 64 + lane];
+						stage_ed[(size_t)(ne - 1 - k) * 64 + lane] = x;
+					}
+				} else {
 					for(int k = 0; k < ne; k++) {
-						const uint32_t e = stage_ed[(size_t)(p.fw ? ne - 1 - k : k) * 64 + lane];
-						uint32_t pos = (e & 0x3ffu) - (uint32_t)trimBeg;
-						if(!p.fw) pos = (uint32_t)extent - pos - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
-						a.edits[eo + k] = (e & ~0x3ffu) | (pos & 0x3ffu);
+						const uint32_t e = stage_ed[(size_t)k * 64 + lane];
+						const uint32_t pos = (uint32_t)extent - ((e & 0x3ffu) - (uint32_t)trimBeg)
+						                     - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
+						stage_ed[(size_t)k * 64 + lane] = (e & ~0x3ffu) | (pos & 0x3ffu);
 					}
 				}
+				hi = max(hi, ne);
 				found = true;
 				bt2x_aln_rec r;
 				r.ntries = (uint16_t)ntries; r.ok = 1; r.pad0 = 0;
 				r.score = (int16_t)bscore; r.ns = (uint16_t)ns; r.gaps = (uint16_t)gaps;
 				r.nedit = (uint16_t)ne; r.bases_aligned = (uint16_t)(extent - ne);
 				r.refns = (uint16_t)refns; r.refoff = (int64_t)col + p.refl;
-				r.edit_off = eo; r.pad1 = 0;
+				r.edit_off = publish_edbuf(a, stage_ed, lane, hi); r.nbuf = (uint32_t)hi;
 				stage_rec[(size_t)nrec * 64 + lane] = r;
 				break;
 			}
 			if(!found) {
 				bt2x_aln_rec r;
 				r.ntries = (uint16_t)ntries; r.ok = 0; r.pad0 = 0; r.score = 0; r.ns = 0; r.gaps = 0;
-				r.nedit = 0; r.bases_aligned = 0; r.refns = 0; r.refoff = 0; r.edit_off = 0; r.pad1 = 0;
+				r.nedit = 0; r.bases_aligned = 0; r.refns = 0; r.refoff = 0;
+				r.edit_off = publish_edbuf(a, stage_ed, lane, hi); r.nbuf = (uint32_t)hi;
 				stage_rec[(size_t)nrec * 64 + lane] = r;
 				nrec++;
 				break;

@@ -1,0 +1,129 @@
+// bt2x-align — the MI355X aligner's command line: the subset of bowtie2-align-l's
+// options this fork honours for unpaired end-to-end alignment (bt2_search.cpp:446-643),
+// FASTQ in, SAM out.  All hot-path work runs on one GPU through libbt2x (include/bt2x.h);
+// there is no CPU fallback.
+//
+//   bt2x-align -x <index base> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N]
+//              [-L N] [--mp MX,MN] [--np N] [--rdg O,E] [--rfg O,E] [--gbar N]
+//              [--seed N] [-p threads] [--slots N] [--device N] [--stats]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "bt2x_align.hpp"
+
+using namespace bt2x::host;
+
+namespace {
+
+// Product backend: every request kind is one bt2x C-ABI call on the context's GPU.
+class HipBackend : public Backend {
+public:
+	explicit HipBackend(bt2x_ctx* ctx) : ctx_(ctx) {}
+	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
+	                 std::vector<bt2x_seed_out>& out) override {
+		out.resize(in.size());
+		bt2x::check(bt2x_seed_search(ctx_, reads.data(), reads.size(), in.data(), (uint32_t)in.size(), 1,
+		                             out.data()), "bt2x_seed_search");
+	}
+	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+		out.resize(in.size());
+		bt2x::check(bt2x_resolve(ctx_, in.data(), (uint32_t)in.size(), 0, out.data()), "bt2x_resolve");
+	}
+	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
+	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
+	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
+	              std::vector<uint32_t>& edits) override {
+		const uint32_t n = (uint32_t)in.size();
+		out.resize(n);
+		uint32_t rec_cap = 4 * n + 64, edit_cap = 48 * n + 256;
+		for(int attempt = 0; attempt < 2; attempt++) {
+			recs.resize(rec_cap);
+			edits.resize(edit_cap);
+			uint32_t nrec = 0, ned = 0;
+			const int rc = bt2x_dp_align(ctx_, reads.data(), reads.size(), quals.data(), quals.size(),
+			                             refs.data(), refs.size(), in.data(), n, out.data(), recs.data(), rec_cap,
+			                             &nrec, edits.data(), edit_cap, &ned, nullptr);
+			if(rc == BT2X_E_OVERFLOW && attempt == 0) { rec_cap = nrec; edit_cap = ned; continue; }
+			bt2x::check(rc, "bt2x_dp_align");
+			recs.resize(nrec);
+			edits.resize(ned);
+			return;
+		}
+	}
+private:
+	bt2x_ctx* ctx_;
+};
+
+void usage() {
+	std::fprintf(stderr,
+	             "usage: bt2x-align -x <index> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N] [-L N]\n"
+	             "                  [--mp MX,MN] [--np N] [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N]\n"
+	             "                  [-p threads] [--slots N] [--device N] [--stats]\n");
+}
+
+} // namespace
+
+int main(int argc, char** argv) {
+	std::string idx, fq, outp;
+	Params p;
+	int threads = 16, device = 0;
+	size_t slots = 1 << 18;
+	bool stats = false;
+	for(int i = 1; i < argc; i++) {
+		const std::string a = argv[i];
+		auto val = [&]() -> const char* {
+			if(i + 1 >= argc) { usage(); std::exit(1); }
+			return argv[++i];
+		};
+		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
+		if(a == "-x") idx = val();
+		else if(a == "-U") fq = val();
+		else if(a == "-S") outp = val();
+		else if(a == "-p") threads = std::atoi(val());
+		else if(a == "--slots") slots = (size_t)std::atol(val());
+		else if(a == "--device") device = std::atoi(val());
+		else if(a == "--stats") stats = true;
+		else if(a == "--end-to-end" || a == "--sensitive" || a == "--reorder" || a == "-q") {}
+		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); usage(); return 1; }
+	}
+	if(idx.empty() || fq.empty()) { usage(); return 1; }
+	bt2x_scoring_init(&p.sc);
+	if(p.multiseedLen < 1 || p.multiseedLen > 32) { std::fprintf(stderr, "-L must be in 1..32\n"); return 1; }
+	try {
+		bt2x::Index index(idx.c_str(), true);
+		RefInfo ref;
+		ref.init(index.desc(), idx);
+		bt2x::Device dev(device, index, p.sc);
+		HipBackend be(dev.ctx());
+		Aligner al(p, ref, be);
+		FastqReader reader(fq.c_str());
+		std::FILE* out = outp.empty() ? stdout : std::fopen(outp.c_str(), "wb");
+		if(!out) { std::fprintf(stderr, "cannot open %s\n", outp.c_str()); return 1; }
+		std::vector<char> obuf(1 << 24);
+		std::setvbuf(out, obuf.data(), _IOFBF, obuf.size());
+		const RunStats st = al.run(reader, out, slots, threads);
+		if(out != stdout) std::fclose(out); else std::fflush(out);
+		// alignment summary (AlnSink::printAlSumm, unpaired)
+		auto pct = [&](uint64_t a) { return st.reads ? 100.0 * (double)a / (double)st.reads : 0.0; };
+		std::fprintf(stderr, "%llu reads; of these:\n", (unsigned long long)st.reads);
+		std::fprintf(stderr, "  %llu (100.00%%) were unpaired; of these:\n", (unsigned long long)st.reads);
+		std::fprintf(stderr, "    %llu (%.2f%%) aligned 0 times\n", (unsigned long long)st.unaligned, pct(st.unaligned));
+		std::fprintf(stderr, "    %llu (%.2f%%) aligned exactly 1 time\n", (unsigned long long)(st.aligned - st.rep), pct(st.aligned - st.rep));
+		std::fprintf(stderr, "    %llu (%.2f%%) aligned >1 times\n", (unsigned long long)st.rep, pct(st.rep));
+		std::fprintf(stderr, "%.2f%% overall alignment rate\n", pct(st.aligned));
+		if(stats)
+			std::fprintf(stderr, "BT2X_STATS seed_launches=%llu seeds=%llu t_seed=%.4f resolve_launches=%llu resolves=%llu "
+			             "t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f t_host=%.4f t_io=%.4f\n",
+			             (unsigned long long)st.seed_launches, (unsigned long long)st.seeds, st.t_seed,
+			             (unsigned long long)st.resolve_launches, (unsigned long long)st.resolves, st.t_resolve,
+			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io);
+	} catch(const std::exception& e) {
+		std::fprintf(stderr, "bt2x-align: %s\n", e.what());
+		return 1;
+	}
+	return 0;
+}

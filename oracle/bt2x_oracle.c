@@ -368,6 +368,7 @@ static int cand_cmp(const void* a, const void* b) {
 typedef struct {
 	int ok;
 	int score, ns, gaps, nedit, bases_aligned, refns, off;
+	int nraw;                       /* edit-buffer entries written by the last attempt */
 	uint32_t edits[BT2X_MAX_ROWS + BT2X_MAX_COLS + 8];
 } btres_t;
 
@@ -382,15 +383,17 @@ static inline uint32_t pack_edit(uint32_t pos, int type, int chr, int qchr) {
  * cells that are themselves marked, so unwinding the stack can never resume). */
 static int backtrace(const bt2x_scoring* sc, dpmat_t* m, const uint8_t* rd, const uint8_t* qu,
                      const uint8_t* rf, const bt2x_dp_in* p, int row, int col, btres_t* res,
-                     uint64_t* btcells) {
+                     uint64_t* btcells, uint32_t* raw) {
 	const int R = m->R;
 	const int rdo = sc->rdg_const + sc->rdg_linear, rde = sc->rdg_linear;
 	const int rfo = sc->rfg_const + sc->rfg_linear, rfe = sc->rfg_linear;
 	int ct = MAT_H, score = 0, ns = 0, gaps = 0;
 	int nedit = 0, trimBeg = 0;
 	const int trimEnd = R - row - 1, origCol = col;
-	uint32_t raw[BT2X_MAX_ROWS + BT2X_MAX_COLS + 8];   /* edits in backtrace order */
+	/* raw: the caller's persistent edit buffer (SwResult::alres.ned_ storage), written
+	 * in backtrace order from index 0; res->nraw = entries written by this attempt */
 	int over_core = 0;
+	res->nraw = 0;
 	while(row >= 0) {
 		(*btcells)++;
 		const int rdc = rd[row], refm = 1 << rf[col], q = qu[row] - 33;
@@ -434,7 +437,7 @@ static int backtrace(const bt2x_scoring* sc, dpmat_t* m, const uint8_t* rd, cons
 			}
 		}
 		m->rt[row][col] = 1;
-		if(!canMoveThru) return 0;
+		if(!canMoveThru) { res->nraw = nedit; return 0; }
 		{
 			long long diag = (long long)col - row + p->triml;   /* core diagonal check */
 			if(diag >= 0 && (uint64_t)diag >= p->corel && (uint64_t)diag <= p->corer) over_core = 1;
@@ -465,10 +468,11 @@ static int backtrace(const bt2x_scoring* sc, dpmat_t* m, const uint8_t* rd, cons
 			col--; gaps++;
 			break;
 		default:
+			res->nraw = nedit;
 			return 0;
 		}
 	}
-	if(!over_core) return 0;
+	if(!over_core) { res->nraw = nedit; return 0; }
 	{
 		const int rdc = rd[row], refm = 1 << rf[col], q = qu[row] - 33;
 		int mt = matches_ex(rdc, refm);
@@ -478,7 +482,7 @@ static int backtrace(const bt2x_scoring* sc, dpmat_t* m, const uint8_t* rd, cons
 		}
 		if(mt == -1) ns++;
 	}
-	if(ns > p->nceil) return 0;
+	if(ns > p->nceil) { res->nraw = nedit; return 0; }
 	/* res.reverse(); setShape (pos -= trimBeg); for rc invertEdits (aligner_result.h:852,
 	 * edit.cpp:50-78): reverse again and pos = extent - pos - (readgap ? 0 : 1). */
 	const int extent = R - trimBeg - trimEnd;
@@ -490,6 +494,9 @@ static int backtrace(const bt2x_scoring* sc, dpmat_t* m, const uint8_t* rd, cons
 	}
 	int refns = 0;
 	for(int i = col; i <= origCol; i++) refns += (rf[i] > 3);
+	/* the reference reverses / inverts ned_ in place: the buffer now holds the final list */
+	for(int k = 0; k < nedit; k++) raw[k] = res->edits[k];
+	res->nraw = nedit;
 	res->ok = 1; res->score = score; res->ns = ns; res->gaps = gaps; res->nedit = nedit;
 	res->bases_aligned = extent - nedit; res->refns = refns; res->off = col;
 	return 1;
@@ -575,15 +582,20 @@ int bt2o_dp_align(const bt2x_scoring* sc,
 		if(!o->status) continue;
 		/* nextAlignment() until done() (aligner_sw.cpp:252-375) */
 		int cural = 0;
+		/* SwResult::alres.ned_ storage: every backtrace attempt writes its edits from index
+		 * 0 (failed attempts leave them behind), successes leave the final list in place.
+		 * Each record publishes the entries written during its call (BT2X_REC_NBUF). */
+		uint32_t edbuf[BT2X_MAX_ROWS + BT2X_MAX_COLS + 8];
 		while(cural < ncand) {
-			int ntries = 0, found = 0;
+			int ntries = 0, found = 0, hi = 0;
 			while(cural < ncand) {
 				const cand_t* cd = &cands[cural];
 				if(cd->score < p->minsc) { cural++; continue; }
 				if(m->rt[cd->row][cd->col]) { cural++; continue; }
 				ntries++;
 				uint64_t btc = 0;
-				int ok = backtrace(sc, m, rd, qu, rf, p, cd->row, cd->col, res, &btc);
+				int ok = backtrace(sc, m, rd, qu, rf, p, cd->row, cd->col, res, &btc, edbuf);
+				if(res->nraw > hi) hi = res->nraw;
 				if(ctr) ctr->bt_cells += btc;
 				if(ok) { found = 1; break; }
 				cural++;
@@ -598,13 +610,14 @@ int bt2o_dp_align(const bt2x_scoring* sc,
 					r->gaps = (uint16_t)res->gaps; r->nedit = (uint16_t)res->nedit;
 					r->bases_aligned = (uint16_t)res->bases_aligned; r->refns = (uint16_t)res->refns;
 					r->refoff = (int64_t)res->off + p->refl;
-					r->edit_off = nedit;
-					if(nedit + (uint32_t)res->nedit <= edit_cap)
-						memcpy(edits + nedit, res->edits, sizeof(uint32_t) * (size_t)res->nedit);
-					else overflow = 1;
 				}
+				r->nbuf = (uint32_t)hi;
+				r->edit_off = hi > 0 ? nedit : 0;
+				if(nedit + (uint32_t)hi <= edit_cap)
+					memcpy(edits + nedit, edbuf, sizeof(uint32_t) * (size_t)hi);
+				else overflow = 1;
 			} else overflow = 1;
-			if(found) nedit += (uint32_t)res->nedit;
+			nedit += (uint32_t)hi;
 			nrec++; o->nrec++;
 			if(!found) break;
 			cural++;

@@ -1,0 +1,84 @@
+// test_e2e_oracle.cpp — TEST INFRASTRUCTURE (CPU, no GPU): the end-to-end host driver
+// (omp-bowtie2-prime_amd/host/bt2x_align.cpp: per-read coroutine, prioritizeSATups,
+// extendSeeds, reporting, MAPQ, SAM) run with the CPU oracle standing in for the three
+// kernels, so the host logic can be pinned against the reference's own SAM output
+// (tests/golden/*.sam.xz) on a machine without a GPU.  The product binary
+// (bt2x-align) links only libbt2x.so and is checked against the same goldens on the
+// GPU (tests/test_e2e.py, -m gpu).  The kernels' own parity with the oracle is
+// tested separately (tests/test_gpu_parity.py).
+//
+//   test_e2e_oracle <index base> <reads.fq> [--dpad N] [--slots N] [-p T]
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../omp-bowtie2-prime_amd/host/bt2x_align.hpp"
+#include "../../oracle/bt2x_oracle.h"
+
+using namespace bt2x::host;
+
+namespace {
+class OracleBackend : public Backend {
+public:
+	OracleBackend(const bt2x_index_desc& idx, const bt2x_scoring& sc) : idx_(idx), sc_(sc) {}
+	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
+	                 std::vector<bt2x_seed_out>& out) override {
+		out.resize(in.size());
+		if(bt2o_seed_search(&idx_, reads.data(), in.data(), (uint32_t)in.size(), 1, out.data(), nullptr) != 0)
+			throw std::runtime_error("oracle seed search");
+	}
+	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+		out.resize(in.size());
+		if(bt2o_resolve(&idx_, in.data(), (uint32_t)in.size(), 0, out.data(), nullptr) != 0)
+			throw std::runtime_error("oracle resolve");
+	}
+	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
+	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
+	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
+	              std::vector<uint32_t>& edits) override {
+		const uint32_t n = (uint32_t)in.size();
+		out.resize(n);
+		uint32_t rec_cap = 4 * n + 64, edit_cap = 48 * n + 256;
+		for(int attempt = 0; attempt < 2; attempt++) {
+			recs.resize(rec_cap); edits.resize(edit_cap);
+			uint32_t nrec = 0, ned = 0;
+			const int rc = bt2o_dp_align(&sc_, reads.data(), quals.data(), refs.data(), in.data(), n, out.data(),
+			                             recs.data(), rec_cap, &nrec, edits.data(), edit_cap, &ned, nullptr, nullptr);
+			if(rc == BT2X_E_OVERFLOW && attempt == 0) { rec_cap = nrec; edit_cap = ned; continue; }
+			if(rc != 0) throw std::runtime_error("oracle dp");
+			recs.resize(nrec); edits.resize(ned);
+			return;
+		}
+	}
+private:
+	const bt2x_index_desc& idx_;
+	const bt2x_scoring& sc_;
+};
+}
+
+int main(int argc, char** argv) {
+	if(argc < 3) { std::fprintf(stderr, "usage: test_e2e_oracle <index> <reads.fq> [--dpad N] [--slots N] [-p T]\n"); return 1; }
+	Params p;
+	size_t slots = 4096;
+	int threads = 4;
+	for(int i = 3; i + 1 < argc; i++) {
+		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
+		const std::string a = argv[i];
+		if(a == "--slots") slots = (size_t)std::atol(argv[++i]);
+		else if(a == "-p") threads = std::atoi(argv[++i]);
+		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); return 1; }
+	}
+	bt2x_scoring_init(&p.sc);
+	bt2x::Index index(argv[1], true);
+	RefInfo ref;
+	ref.init(index.desc(), argv[1]);
+	OracleBackend be(index.desc(), p.sc);
+	Aligner al(p, ref, be);
+	FastqReader fq(argv[2]);
+	const RunStats st = al.run(fq, stdout, slots, threads);
+	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu\n",
+	             (unsigned long long)st.reads, (unsigned long long)st.aligned, (unsigned long long)st.seed_launches,
+	             (unsigned long long)st.resolve_launches, (unsigned long long)st.dp_launches, (unsigned long long)st.dps);
+	return 0;
+}

@@ -16,7 +16,10 @@ Steps (all outputs xz-compressed under tests/golden/):
      (GroupWalk2S + joinedToTextOff on every reported seed range, fragment-boundary
      probes) and, for rep, refharness rank (searchAllSeedsFinalize + rankSeedHits).
      `make_golden.py resolve` regenerates only these.
-Each golden file starts with a '#' header naming the command that produced it.
+  5. e2e: the reference aligner (bowtie2-align-l, 1 thread) on the lambda and rep
+     fixtures, default and --dpad 12 / non-default scoring, as sorted @PG-less SAM.
+     `make_golden.py e2e` regenerates only these.
+Each text golden file starts with a '#' header naming the command that produced it.
 """
 from __future__ import annotations
 
@@ -73,8 +76,52 @@ def resolve_goldens(tmp: str) -> None:
             xz_copy(out, os.path.join(GOLD, "rank_rep.txt.xz"))
 
 
+ALIGN = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l")
+
+# end-to-end SAM goldens: (name, index, reads fixture, extra bowtie2-align-l options)
+E2E_SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
+            ("e2e_rep", "rep", "rep_reads.fq", []),
+            ("e2e_rep_dpad12", "rep", "rep_reads.fq", ["--dpad", "12"]),
+            ("e2e_rep_alt", "rep", "rep_reads.fq", ALT_OPTS)]
+
+
+def sam_records(path: str) -> bytes:
+    """SAM minus @PG, records sorted: the reference's own comparison methodology
+    (scripts/sim Sim.pm: sort, strip @PG), which is also independent of how reads
+    finish across seed rounds."""
+    with open(path, "rb") as f:
+        lines = [ln for ln in f.read().split(b"\n") if ln and not ln.startswith(b"@PG")]
+    hdr = [ln for ln in lines if ln.startswith(b"@")]
+    rec = sorted(ln for ln in lines if not ln.startswith(b"@"))
+    return b"\n".join(hdr + rec) + b"\n"
+
+
+def e2e_goldens(tmp: str) -> None:
+    """The reference aligner itself (OMP_NUM_THREADS=1) on the committed fixtures."""
+    for name, idx, fq, opts in E2E_SETS:
+        base = os.path.join(tmp, idx)
+        if not os.path.exists(base + ".4.bt2l"):
+            for k in "1234":
+                xz_unpack(os.path.join(GOLD, f"{idx}.{k}.bt2l.xz"), f"{base}.{k}.bt2l")
+        rfq = os.path.join(tmp, fq)
+        if not os.path.exists(rfq):
+            xz_unpack(os.path.join(GOLD, fq + ".xz"), rfq)
+        sam = os.path.join(tmp, name + ".sam")
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        run([ALIGN, "-x", base, "-U", rfq, "-S", sam] + opts, env=env, stderr=subprocess.DEVNULL)
+        with lzma.open(os.path.join(GOLD, name + ".sam.xz"), "wb", preset=9 | lzma.PRESET_EXTREME) as fo:
+            fo.write(sam_records(sam))
+
+
 def main() -> None:
     run(["make", "-C", os.path.join(ROOT, "oracle"), "ref", "oracle"])
+    if sys.argv[1:] == ["e2e"]:
+        tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
+        try:
+            e2e_goldens(tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     if sys.argv[1:] == ["resolve"]:
         tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
         try:
@@ -141,6 +188,7 @@ def main() -> None:
             json.dump({"tricky": md5, "_note": "md5 of oracle/_ref/bowtie2-build-l tests/golden/tricky.fa "
                        "output (tools/make_golden.py)"}, f, indent=1)
         resolve_goldens(tmp)
+        e2e_goldens(tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     for f in sorted(os.listdir(GOLD)):
