@@ -6,6 +6,7 @@
 //   bt2x-align -x <index base> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N]
 //              [-L N] [--mp MX,MN] [--np N] [--rdg O,E] [--rfg O,E] [--gbar N]
 //              [--seed N] [-p threads] [--slots N] [--device N] [--stats]
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -58,6 +59,43 @@ private:
 	bt2x_ctx* ctx_;
 };
 
+// --dump DIR: record every GPU launch's inputs (bench.py replays them from HBM).
+// File NNNNNN.<kind>: u64 count of each array, then the arrays.
+class DumpBackend : public Backend {
+public:
+	DumpBackend(Backend& inner, const std::string& dir) : in_(inner), dir_(dir) {}
+	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
+	                 std::vector<bt2x_seed_out>& out) override {
+		write("seed", {{reads.data(), reads.size()}, {in.data(), in.size() * sizeof(bt2x_seed_in)}});
+		in_.seed_search(reads, in, out);
+	}
+	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+		write("resolve", {{in.data(), in.size() * sizeof(bt2x_resolve_in)}});
+		in_.resolve(in, out);
+	}
+	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
+	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
+	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
+	              std::vector<uint32_t>& edits) override {
+		write("dp", {{reads.data(), reads.size()}, {quals.data(), quals.size()}, {refs.data(), refs.size()},
+		             {in.data(), in.size() * sizeof(bt2x_dp_in)}});
+		in_.dp_align(reads, quals, refs, in, out, recs, edits);
+	}
+private:
+	void write(const char* kind, std::initializer_list<std::pair<const void*, size_t>> parts) {
+		char name[64];
+		std::snprintf(name, sizeof name, "/%06u.%s", n_++, kind);
+		std::FILE* f = std::fopen((dir_ + name).c_str(), "wb");
+		if(!f) throw std::runtime_error("cannot write " + dir_ + name);
+		for(auto& p : parts) { const uint64_t n = p.second; std::fwrite(&n, 8, 1, f); }
+		for(auto& p : parts) if(p.second) std::fwrite(p.first, 1, p.second, f);
+		std::fclose(f);
+	}
+	Backend& in_;
+	std::string dir_;
+	unsigned n_ = 0;
+};
+
 void usage() {
 	std::fprintf(stderr,
 	             "usage: bt2x-align -x <index> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N] [-L N]\n"
@@ -73,6 +111,7 @@ int main(int argc, char** argv) {
 	int threads = 16, device = 0;
 	size_t slots = 1 << 18;
 	bool stats = false;
+	std::string dump;
 	for(int i = 1; i < argc; i++) {
 		const std::string a = argv[i];
 		auto val = [&]() -> const char* {
@@ -87,6 +126,7 @@ int main(int argc, char** argv) {
 		else if(a == "--slots") slots = (size_t)std::atol(val());
 		else if(a == "--device") device = std::atoi(val());
 		else if(a == "--stats") stats = true;
+		else if(a == "--dump") dump = val();
 		else if(a == "--end-to-end" || a == "--sensitive" || a == "--reorder" || a == "-q") {}
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); usage(); return 1; }
 	}
@@ -98,15 +138,20 @@ int main(int argc, char** argv) {
 		RefInfo ref;
 		ref.init(index.desc(), idx);
 		bt2x::Device dev(device, index, p.sc);
-		HipBackend be(dev.ctx());
+		HipBackend hip(dev.ctx());
+		std::unique_ptr<DumpBackend> dumper;
+		if(!dump.empty()) dumper.reset(new DumpBackend(hip, dump));
+		Backend& be = dumper ? static_cast<Backend&>(*dumper) : static_cast<Backend&>(hip);
 		Aligner al(p, ref, be);
 		FastqReader reader(fq.c_str());
+		const auto t_start = std::chrono::steady_clock::now();
 		std::FILE* out = outp.empty() ? stdout : std::fopen(outp.c_str(), "wb");
 		if(!out) { std::fprintf(stderr, "cannot open %s\n", outp.c_str()); return 1; }
 		std::vector<char> obuf(1 << 24);
 		std::setvbuf(out, obuf.data(), _IOFBF, obuf.size());
 		const RunStats st = al.run(reader, out, slots, threads);
 		if(out != stdout) std::fclose(out); else std::fflush(out);
+		const double t_align = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
 		// alignment summary (AlnSink::printAlSumm, unpaired)
 		auto pct = [&](uint64_t a) { return st.reads ? 100.0 * (double)a / (double)st.reads : 0.0; };
 		std::fprintf(stderr, "%llu reads; of these:\n", (unsigned long long)st.reads);
@@ -116,8 +161,9 @@ int main(int argc, char** argv) {
 		std::fprintf(stderr, "    %llu (%.2f%%) aligned >1 times\n", (unsigned long long)st.rep, pct(st.rep));
 		std::fprintf(stderr, "%.2f%% overall alignment rate\n", pct(st.aligned));
 		if(stats)
-			std::fprintf(stderr, "BT2X_STATS seed_launches=%llu seeds=%llu t_seed=%.4f resolve_launches=%llu resolves=%llu "
-			             "t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f t_host=%.4f t_io=%.4f\n",
+			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "
+			             "resolve_launches=%llu resolves=%llu t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f "
+			             "t_host=%.4f t_io=%.4f\n", (unsigned long long)st.reads, t_align,
 			             (unsigned long long)st.seed_launches, (unsigned long long)st.seeds, st.t_seed,
 			             (unsigned long long)st.resolve_launches, (unsigned long long)st.resolves, st.t_resolve,
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io);
