@@ -1,25 +1,33 @@
 #!/usr/bin/env python3
-"""bench.py — throughput of the MI355X hot path (FM seed search + banded end-to-end DP)
-on BASELINE.json's headline workload: 150 bp single-end reads, u8 DP with --dpad 12
-(config C3; hg38 is not available offline, so a seeded synthetic genome stands in).
+"""bench.py — BASELINE.json's headline metric on MI355X: 150 bp single-end reads,
+end-to-end alignment with --dpad 12 (config C3; hg38 is not available offline, so a
+seeded 1 Gbp synthetic genome stands in), reads/s and the DP kernel's HBM roofline.
 
-One step = the hot path over one batch of synthetic reads already resident in HBM:
-  1. bt2x_seed_search_dev: exact search + left extension of every instantiated seed
-     (18 seeds/read at 150 bp: 9 per strand, MultiSeedAligner::searchAllSeedsDoAll);
-  2. bt2x_dp_align_dev: one framed end-to-end DP problem per read at its seed-hit
-     diagonal (SwAligner::align + every nextAlignment() call), exactly as
-     SwDriver::extendSeeds frames it (the reference measures 1.04 DP/read).
-value = reads of all ranks / max-over-ranks wall time of K steps (M reads/s).
-
-Multi-GPU: one process per GPU, reads sharded (each rank its own seeded batch), index
-replicated per GPU, no collective on the data path ("scaling": "weak"); the only
-collective is the max-of-times reduction for the report.
+Per rank (one process per GPU):
+  1. The aligner itself, bt2x-align (FASTQ -> SAM; host driver + the three gfx950
+     kernels, omp-bowtie2-prime_amd/host), runs once over the batch of --reads reads and
+     records the inputs of every GPU launch it makes (--dump): the seed searches, SA
+     resolutions and DP rounds that SwDriver::extendSeeds generates for these reads.
+     A second, undumped run gives the end-to-end wall time (`end_to_end`, FASTQ parse,
+     host logic, PCIe and SAM formatting included).
+  2. The timed hot path: one step = that exact launch sequence replayed from HBM
+     (inputs resident before the timed region) -- seed_kernel, resolve_kernel and
+     dp_fill_kernel launches in the aligner's order.
+     value = reads of all ranks / max-over-ranks wall time of K steps.
+  3. Rank 0 at N=1: the reference aligner (oracle/_ref/bowtie2-align-l, OpenMP) on a
+     bounded sample of the same FASTQ = cpu_baseline; its SAM is compared with ours
+     record by record (`parity`).
+Multi-GPU: reads sharded (each rank its own seeded batch), index replicated per GPU,
+no collective on the data path ("scaling": "weak"); the only collective is the
+max-of-times reduction for the report.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -31,6 +39,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
+ALIGN = os.path.join(ROOT, "omp-bowtie2-prime_amd", "bt2x", "bt2x-align")
+REF_ALIGN = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l")
 
 
 def parse():
@@ -44,26 +54,26 @@ def parse():
     ap.add_argument("--genome", default="synthetic", help="'synthetic' (default) or 'rep' (fixture)")
     ap.add_argument("--genome-mb", type=float, default=1000.0)
     ap.add_argument("--genome-seed", type=int, default=2024)
+    ap.add_argument("--host-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
+                    help="host threads of bt2x-align (the box's CPU share)")
     ap.add_argument("--cpu-sample", type=int, default=200000,
-                    help="reads timed on the reference's CPU path (oracle/_ref/refharness bench)")
+                    help="reads aligned by the reference aligner for cpu_baseline / parity")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
-                    help="OpenMP threads for the reference CPU baseline (the box's CPU share)")
-    ap.add_argument("--port-sample", type=int, default=20000, help="reads timed on the 1-thread C port")
+                    help="OpenMP threads of the reference CPU baseline (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--overlap", type=int, default=0, help="1: seed and DP stages on two streams")
+    ap.add_argument("--rss-limit-gb", type=float, default=120.0, help="kill bt2x-align above this host RSS")
     return ap.parse_args()
 
 
 def workload_key(args) -> str:
     g = f"synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}" if args.genome == "synthetic" else args.genome
-    return f"{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}"
+    return f"e2e|{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}"
 
 
 def pmc_traffic(args, kernel: str):
-    """Per-launch HBM bytes of `kernel` from the newest committed rocprofv3 PMC summary
+    """Per-step HBM bytes of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_traffic.json, tools/pmc_traffic.py) taken on this same workload;
     (None, None) if there is none."""
-    import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
         with open(path) as f:
             t = json.load(f)
@@ -121,6 +131,132 @@ def load_genome(args, workdir, rank=0, dist=None):
                          f"5% repeat families, low-complexity, N runs)"
 
 
+def mark(msg):
+    rss = 0
+    try:
+        with open("/proc/self/status") as f:
+            rss = next(int(ln.split()[1]) >> 10 for ln in f if ln.startswith("VmRSS"))
+    except (OSError, StopIteration):
+        pass
+    print(f"# {msg} (bench RSS {rss} MiB)", file=sys.stderr, flush=True)
+
+
+def write_fastq(path, reads, quals, first_id=0):
+    """Fixed-length FASTQ, vectorised: '@r<9 digits>' names."""
+    n, R = reads.shape
+    rec = np.empty((n, 11 + 1 + R + 3 + R + 1), dtype=np.uint8)
+    rec[:, 0] = ord("@"); rec[:, 1] = ord("r")
+    ids = np.arange(first_id, first_id + n, dtype=np.int64)
+    for k in range(9):
+        rec[:, 10 - k] = ord("0") + (ids // (10 ** k)) % 10
+    rec[:, 11] = ord("\n")
+    rec[:, 12:12 + R] = np.frombuffer(b"ACGTN", np.uint8)[reads]
+    rec[:, 12 + R] = ord("\n"); rec[:, 13 + R] = ord("+"); rec[:, 14 + R] = ord("\n")
+    rec[:, 15 + R:15 + 2 * R] = quals
+    rec[:, 15 + 2 * R] = ord("\n")
+    with open(path, "wb") as f:
+        f.write(rec.tobytes())
+
+
+def run_aligner(args, base, fq, sam, gpu, dump=None):
+    cmd = [ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad), "--device", str(gpu),
+           "-p", str(args.host_threads), "--slots", str(args.reads), "--stats"]
+    if dump:
+        cmd += ["--dump", dump]
+    t0 = time.perf_counter()
+    errp = os.path.join(os.path.dirname(sam), "align.err")
+    with open(errp, "w") as ferr:
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=ferr)
+        peak = 0
+        while p.poll() is None:          # host-RAM watchdog (the box caps a command's RAM)
+            try:
+                with open(f"/proc/{p.pid}/status") as f:
+                    for ln in f:
+                        if ln.startswith("VmRSS"):
+                            peak = max(peak, int(ln.split()[1]) >> 10)
+            except OSError:
+                pass
+            if peak > args.rss_limit_gb * 1024 or time.perf_counter() - t0 > 1500:
+                p.kill()
+                p.wait()
+                break
+            time.sleep(0.2)
+    wall = time.perf_counter() - t0
+    err = open(errp).read()
+    if p.returncode != 0:
+        raise SystemExit(f"bt2x-align failed (rc {p.returncode}, peak RSS {peak} MiB): {err[-3000:]}")
+    print(f"# bt2x-align {'(dump) ' if dump else ''}{wall:.1f} s, peak RSS {peak} MiB", file=sys.stderr, flush=True)
+    line = [ln for ln in err.splitlines() if ln.startswith("BT2X_STATS")][-1]
+    st = {k: float(v) for k, v in (t.split("=") for t in line.split()[1:])}
+    st["wall_incl_index_load"] = wall
+    st["peak_rss_mib"] = peak
+    st["summary"] = [ln.strip() for ln in err.splitlines() if "aligned" in ln or "overall" in ln]
+    return st
+
+
+def load_dumps(ddir):
+    """-> list of (kind, [arrays]) in launch order (DumpBackend, bt2x_align_main.cpp)."""
+    from bt2x import abi
+    out = []
+    for path in sorted(glob.glob(os.path.join(ddir, "*.*"))):
+        kind = path.rsplit(".", 1)[1]
+        nparts = {"seed": 2, "resolve": 1, "dp": 4}[kind]
+        raw = np.fromfile(path, dtype=np.uint8)
+        sizes = raw[:8 * nparts].view(np.uint64).astype(np.int64)
+        parts, o = [], 8 * nparts
+        for s in sizes:
+            parts.append(raw[o:o + s]); o += s
+        if kind == "seed":
+            parts[1] = parts[1].view(abi.SEED_IN)
+        elif kind == "resolve":
+            parts[0] = parts[0].view(abi.RESOLVE_IN)
+        else:
+            parts[3] = parts[3].view(abi.DP_IN)
+        out.append((kind, parts))
+    return out
+
+
+def sam_records(path, limit_ids=None):
+    recs = []
+    with open(path, "rb") as f:
+        for ln in f:
+            if ln.startswith(b"@"):
+                continue
+            if limit_ids is not None and int(ln[1:10]) >= limit_ids:
+                continue
+            recs.append(ln.rstrip(b"\n"))
+    recs.sort()
+    return recs
+
+
+def cpu_reference(args, base, fq_sample, m, workdir):
+    """The reference aligner (OpenMP, --cpu-threads) on the first m reads; alignment time
+    = wall(m reads) - wall(1 read) (index load cancels)."""
+    if not os.access(REF_ALIGN, os.X_OK):
+        return None, None
+    env = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY="ACTIVE")
+    one = os.path.join(workdir, "one.fq")
+    with open(fq_sample, "rb") as f, open(one, "wb") as g:
+        for _ in range(4):
+            g.write(f.readline())
+    times = []
+    for fq, sam in ((one, os.path.join(workdir, "ref_one.sam")), (fq_sample, os.path.join(workdir, "ref.sam"))):
+        t0 = time.perf_counter()
+        r = subprocess.run([REF_ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad)],
+                           env=env, capture_output=True, text=True, timeout=1200)
+        times.append(time.perf_counter() - t0)
+        if r.returncode != 0:
+            print(r.stderr[-2000:], file=sys.stderr)
+            return None, None
+    dt = max(times[1] - times[0], 1e-6)
+    base_line = {"value": round(m / dt / 1e6, 6), "unit": "M reads/s", "cores": args.cpu_threads,
+                 "kind": "reference",
+                 "sample": f"first {m} reads of this batch through the reference aligner "
+                           f"(oracle/_ref/bowtie2-align-l --dpad {args.dpad}, FASTQ->SAM, OpenMP "
+                           f"{args.cpu_threads} threads): {times[1]:.2f} s minus {times[0]:.2f} s index load"}
+    return base_line, os.path.join(workdir, "ref.sam")
+
+
 def main():
     args = parse()
     import torch
@@ -130,186 +266,178 @@ def main():
     # GPU, BT2X_BENCH_DIST_BACKEND=gloo runs the rank reductions on the host
     gpu = int(os.environ.get("BT2X_BENCH_DEVICE", local))
     backend = os.environ.get("BT2X_BENCH_DIST_BACKEND", "nccl")
-    torch.cuda.set_device(gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
+            torch.cuda.set_device(gpu)
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
 
-    from bt2x import abi, framing, lib, seeds
+    from bt2x import abi, lib
     import simdata as sd
 
     workdir = os.path.join("/tmp", f"bt2x_bench_{os.getuid()}")
     os.makedirs(workdir, exist_ok=True)
     chroms, base, gdesc = load_genome(args, workdir, rank, dist)
     genome, starts = sd.concat_genome(chroms)
-    lens = np.array([len(s) for _, s in chroms], dtype=np.int64)
+    R, n = args.read_len, args.reads
+    reads, quals, _, _, _ = sd.sim_reads_fixed(genome, starts, n, R, seed=bdist.rank_seed(3, rank))
+    del genome
+    rdir = os.path.join(workdir, f"rank{rank}")
+    os.makedirs(rdir, exist_ok=True)
+    fq = os.path.join(rdir, "reads.fq")
+    write_fastq(fq, reads, quals)
+    del reads, quals
+    mark(f"{n} reads written to {fq}")
 
-    R = args.read_len
-    n = args.reads
-    reads, quals, chrom, off, fw = sd.sim_reads_fixed(genome, starts, n, R, seed=bdist.rank_seed(3, rank))
-    # host prep (untimed): seeds and DP problems
-    sbuf, sin, _ = seeds.batch_fixed_length(reads)
-    drd, dqu, drf, dpin, keep = framing.build_dp_batch_fixed(genome, starts, lens, chrom, off, fw,
-                                                             reads, quals, maxhalf=args.dpad)
-    nseed, ndp = len(sin), len(dpin)
+    # ---- 1. the aligner: launch recording run, then the end-to-end timing run
+    ddir = os.path.join(rdir, "dump")
+    for p in glob.glob(os.path.join(ddir, "*")):
+        os.unlink(p)
+    os.makedirs(ddir, exist_ok=True)
+    sam = os.path.join(rdir, "out.sam")
+    run_aligner(args, base, fq, sam, gpu, dump=ddir)
+    e2e = run_aligner(args, base, fq, sam, gpu)
+    launches = load_dumps(ddir)
+    mark(f"{len(launches)} launches loaded")
 
+    # ---- 2. replay the launch sequence from HBM
+    if world == 1 or backend != "nccl":
+        torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     idx = lib.Index(base, load_offs=True)     # SA sample + text: full SA rebuilt in HBM
     ctx = lib.Context(idx, device=gpu)
-    dev = torch.device("cuda", gpu)
 
     def to_dev(a):
         return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
 
-    d_sbuf, d_sin = to_dev(sbuf), to_dev(sin)
-    d_sout = torch.empty(nseed * abi.SEED_OUT.itemsize, dtype=torch.uint8, device=dev)
-    d_rd, d_qu, d_rf, d_dpin = to_dev(drd), to_dev(dqu), to_dev(drf), to_dev(dpin)
-    d_dpout = torch.empty(ndp * abi.DP_OUT.itemsize, dtype=torch.uint8, device=dev)
-    rec_cap, edit_cap = 4 * ndp + 1024, 48 * ndp + 4096
-    d_recs = torch.empty(rec_cap * abi.ALN_REC.itemsize, dtype=torch.uint8, device=dev)
-    d_edits = torch.empty(edit_cap * 4, dtype=torch.uint8, device=dev)
-    d_cnt = torch.zeros(16, dtype=torch.int32, device=dev)
+    plan = []
+    for kind, parts in launches:
+        if kind == "seed":
+            m = len(parts[1])
+            plan.append((kind, m, [to_dev(parts[0]), to_dev(parts[1]),
+                                   torch.empty(m * abi.SEED_OUT.itemsize, dtype=torch.uint8, device=dev)]))
+        elif kind == "resolve":
+            m = len(parts[0])
+            plan.append((kind, m, [to_dev(parts[0]),
+                                   torch.empty(m * abi.RESOLVE_OUT.itemsize, dtype=torch.uint8, device=dev)]))
+        else:
+            m = len(parts[3])
+            rec_cap, edit_cap = 4 * m + 1024, 96 * m + 4096
+            plan.append((kind, m, [to_dev(parts[0]), to_dev(parts[1]), to_dev(parts[2]), to_dev(parts[3]),
+                                   torch.empty(m * abi.DP_OUT.itemsize, dtype=torch.uint8, device=dev),
+                                   torch.empty(rec_cap * abi.ALN_REC.itemsize, dtype=torch.uint8, device=dev),
+                                   torch.empty(edit_cap * 4, dtype=torch.uint8, device=dev),
+                                   torch.zeros(16, dtype=torch.int32, device=dev), rec_cap, edit_cap]))
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    # --overlap: the seed stage and the DP stage on two HIP streams, the way a streaming
-    # aligner pipelines seed(batch k+1) with DP(batch k); the seed kernel is latency-bound
-    # and the DP fill VALU-bound, so they share the CUs well.  Every step still runs both
-    # stages over the whole batch; the timed region waits for both streams.
-    s2 = torch.cuda.Stream(dev) if args.overlap else stream
-    sh2 = s2.cuda_stream
+    kid = {"seed": abi.K_SEED, "resolve": abi.K_RESOLVE, "dp": abi.K_DP}
+    units = {"seed": 0, "resolve": 0, "dp": 0}
+    for kind, m, _ in plan:
+        units[kind] += m
 
-    def step():
-        if args.overlap:
-            s2.wait_stream(stream)
-        ctx.seed_search_dev(d_sbuf.data_ptr(), d_sin.data_ptr(), nseed, d_sout.data_ptr(), True, sh2)
-        ctx.dp_align_dev(d_rd.data_ptr(), d_qu.data_ptr(), d_rf.data_ptr(), d_dpin.data_ptr(), ndp,
-                         d_dpout.data_ptr(), d_recs.data_ptr(), rec_cap, d_edits.data_ptr(),
-                         edit_cap, d_cnt.data_ptr(), sh)
-        if args.overlap:
-            stream.wait_stream(s2)
+    def step(record=None, counters=None):
+        for kind, m, b in plan:
+            if kind == "seed":
+                ctx.seed_search_dev(b[0].data_ptr(), b[1].data_ptr(), m, b[2].data_ptr(), True, sh)
+            elif kind == "resolve":
+                ctx.resolve_dev(b[0].data_ptr(), m, b[1].data_ptr(), False, sh)
+            else:
+                ctx.dp_align_dev(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), b[3].data_ptr(), m,
+                                 b[4].data_ptr(), b[5].data_ptr(), b[8], b[6].data_ptr(), b[9],
+                                 b[7].data_ptr(), sh)
+            if record is not None:
+                # HIP events recorded on this stream around each launch (bt2x_last_kernel_ms)
+                record[kind]["ms"] += ctx.last_kernel_ms(kid[kind])
+            if counters is not None:
+                for k, v in ctx.last_counters(kid[kind]).items():
+                    counters[kind][k] = counters[kind].get(k, 0) + v
 
-    for _ in range(args.warmup):
-        step()
+    ctr = {k: {} for k in kid}          # algorithmic-work counters (deterministic per step)
+    for w in range(max(args.warmup, 1)):
+        step(counters=ctr if w == 0 else None)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    seed_ms, dp_ms = [], []
+    recs = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        # per-kernel durations from HIP events recorded on this stream around each launch
-        seed_ms.append(ctx.last_kernel_ms(abi.K_SEED))
-        dp_ms.append(ctx.last_kernel_ms(abi.K_DP))
+        rec = {k: {"ms": 0.0} for k in kid}
+        step(rec)
+        recs.append(rec)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    e2e_t = e2e["t_align"]
     if dist:
         dist.barrier()
-        elapsed = bdist.max_over_ranks(elapsed, dist, dev if backend == "nccl" else None)
-    used = d_cnt[:2].cpu().numpy()
-    if used[0] > rec_cap or used[1] > edit_cap:
-        raise SystemExit(f"result arena overflow {used} vs {(rec_cap, edit_cap)}")
-    cs, cd = ctx.last_counters(abi.K_SEED), ctx.last_counters(abi.K_DP)
-
-    # sanity: outputs of the last step
-    sout = d_sout.cpu().numpy().view(abi.SEED_OUT)
-    dout = d_dpout.cpu().numpy().view(abi.DP_OUT)
-    aligned_frac = float((dout["status"] == 1).mean())
+        red_dev = dev if backend == "nccl" else None
+        elapsed = bdist.max_over_ranks(elapsed, dist, red_dev)
+        e2e_t = bdist.max_over_ranks(e2e_t, dist, red_dev)
+    for kind, m, b in plan:           # overflow check on the last step's arenas
+        if kind == "dp":
+            used = b[7][:2].cpu().numpy()
+            if used[0] > b[8] or used[1] > b[9]:
+                raise SystemExit(f"DP result arena overflow {used} vs {(b[8], b[9])}")
 
     value = n * world * args.steps / elapsed / 1e6
-    seed_avg, dp_avg = float(np.mean(seed_ms)), float(np.mean(dp_ms))
-    # algorithmic bytes: FM = 128*(2*BiLF + LF1) + 16*ftab;
-    # DP = 3*R*C (E,F,H) + C (window) + 10*ceil(R/16)*16 (profile) per problem
-    fm_bytes = 128 * (2 * cs["n_bilf"] + cs["n_lf1"]) + 16 * cs["n_ftab"]
-    dp_bytes = 3 * cd["dp_cells"] + cd["dp_cols"] + ndp * 10 * ((R + 15) // 16) * 16
-    kern = {"seed": (seed_avg, fm_bytes), "dp": (dp_avg, dp_bytes)}
+    kms = {k: float(np.mean([r[k]["ms"] for r in recs])) for k in kid}
+    # algorithmic bytes: FM = 128*(2*BiLF + LF1) + 16*ftab (+ 128*LF1 + 8 per
+    # SA sample for the GroupWalk resolve); DP = 3*R*C (E,F,H) + C (window) + 10*ceil(R/16)*16
+    cs, cr, cd = ctr["seed"], ctr["resolve"], ctr["dp"]
+    fm_bytes = 128 * (2 * cs.get("n_bilf", 0) + cs.get("n_lf1", 0)) + 16 * cs.get("n_ftab", 0)
+    res_bytes = cr.get("alg_bytes", 0)
+    dp_bytes = 3 * cd.get("dp_cells", 0) + cd.get("dp_cols", 0) + units["dp"] * 10 * ((R + 15) // 16) * 16
+    kern = {"seed": (kms["seed"], fm_bytes), "resolve": (kms["resolve"], res_bytes), "dp": (kms["dp"], dp_bytes)}
     dom = max(kern, key=lambda k: kern[k][0])
-    ach = kern[dom][1] / (kern[dom][0] / 1e3) / 1e9
+    ach = kern[dom][1] / (kern[dom][0] / 1e3) / 1e9 if kern[dom][0] > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args, dom)
+    nl = {k: sum(1 for kk, _, _ in plan if kk == k) for k in kid}
     line = {
         "metric": "M reads/s aligned (150 bp SE vs hg38) at 1/2/4/8 MI355X; % HBM-roofline",
         "value": round(value, 4), "unit": "M reads/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded genome + simulated 150 bp reads, BASELINE.md error model)",
-        "config": {"workload": f"C3 stand-in: {R} bp SE, --dpad {args.dpad}, genome {gdesc}; "
-                               f"step = seed search+extend ({nseed} seeds) + DP ({ndp} problems)"
-                               + (", the two stages on two streams" if args.overlap else ""),
+        "config": {"workload": f"C3 stand-in: {R} bp SE, --dpad {args.dpad}, genome {gdesc}; step = the "
+                               f"GPU launch sequence bt2x-align issues to align {n} reads end to end "
+                               f"({nl['seed']} seed, {nl['resolve']} resolve, {nl['dp']} DP launches: "
+                               f"{units['seed']} seeds, {units['resolve']} SA elements, {units['dp']} DP "
+                               f"problems), replayed from HBM",
                    "reads_per_gpu_step": n, "read_len": R, "parallelism": f"dp{world} (read shards)",
                    "key": workload_key(args)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes": kern[dom][1], "traffic_src": traffic_src},
-        "kernels": {"seed_ms": round(seed_avg, 3), "dp_ms": round(dp_avg, 3),
-                    "seed_alg_bytes": fm_bytes, "dp_alg_bytes": dp_bytes,
-                    "dp_traceback_bytes": cd["dp_cells"], "counters_seed": cs, "counters_dp": cd},
-        "checks": {"dp_aligned_frac": round(aligned_frac, 4),
-                   "seed_reported_frac": round(float(sout["need_reporting"].mean()), 4)},
+                     "alg_bytes": kern[dom][1], "launches_per_step": nl[dom], "traffic_src": traffic_src},
+        "kernels": {"seed_ms": round(kms["seed"], 3), "resolve_ms": round(kms["resolve"], 3),
+                    "dp_ms": round(kms["dp"], 3), "seed_alg_bytes": fm_bytes, "resolve_alg_bytes": res_bytes,
+                    "dp_alg_bytes": dp_bytes, "launches": nl, "units": units,
+                    "counters_seed": cs, "counters_resolve": cr, "counters_dp": cd},
+        "end_to_end": {"value": round(n * world / e2e_t / 1e6, 4), "unit": "M reads/s",
+                       "what": "bt2x-align FASTQ->SAM wall time (host driver, PCIe, SAM formatting; "
+                               "index load excluded), max over ranks",
+                       "t_align_s": round(e2e_t, 3), "summary": e2e["summary"],
+                       "stats": {k: v for k, v in e2e.items() if k not in ("summary",)}},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        ref = cpu_baseline_reference(args, reads, quals, chrom, off, fw, base, workdir)
-        port = cpu_baseline_port(args, sbuf, sin, drd, dqu, drf, dpin, base, n)
-        line["cpu_baseline"] = ref if ref is not None else port
+        m = min(args.cpu_sample, n)
+        fqs = os.path.join(rdir, "sample.fq")
+        with open(fq, "rb") as f, open(fqs, "wb") as g:
+            rec_len = 11 + 1 + R + 3 + R + 1
+            g.write(f.read(rec_len * m))
+        ref, ref_sam = cpu_reference(args, base, fqs, m, rdir)
         if ref is not None:
-            line["cpu_port"] = port
+            line["cpu_baseline"] = ref
+            ours, theirs = sam_records(sam, limit_ids=m), sam_records(ref_sam)
+            diff = sum(1 for a, b in zip(ours, theirs) if a != b) + abs(len(ours) - len(theirs))
+            line["parity"] = {"sample_reads": m, "records_differ": diff,
+                              "what": "sorted SAM records of bt2x-align vs the reference aligner on the sample"}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
-
-
-def cpu_baseline_reference(args, reads, quals, chrom, off, fw, base, workdir):
-    """The reference's own seed search + DP (oracle/_ref/refharness bench: its
-    MultiSeedAligner::searchAllSeedsDoAll and SwAligner::align/nextAlignment, OpenMP
-    over --cpu-threads host cores) on the first --cpu-sample reads of this batch.
-    None when the reference build did not travel with the snapshot."""
-    import subprocess
-    exe = os.path.join(ROOT, "oracle", "_ref", "refharness")
-    if not os.access(exe, os.X_OK):
-        return None
-    m = min(args.cpu_sample, len(reads))
-    fq = os.path.join(workdir, "cpu_sample.fq")
-    alpha = np.frombuffer(b"ACGTN", dtype=np.uint8)
-    with open(fq, "wb") as f:
-        seqs, qs = alpha[reads[:m]], quals[:m]
-        for i in range(m):
-            f.write(b"@r%d:%d:%d:%d\n%s\n+\n%s\n" % (i, chrom[i], off[i], int(fw[i]),
-                                                        seqs[i].tobytes(), qs[i].tobytes()))
-    env = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY="ACTIVE")
-    out = subprocess.run([exe, "bench", base, fq, "--dpad", str(args.dpad)], env=env,
-                         capture_output=True, text=True, timeout=900)
-    if out.returncode != 0:
-        print(out.stderr[-2000:], file=sys.stderr)
-        return None
-    kv = dict(t.split("=") for t in out.stdout.split("BENCH", 1)[1].split())
-    dt = float(kv["seed_s"]) + float(kv["dp_s"])
-    return {"value": round(m / dt / 1e6, 6), "unit": "M reads/s", "cores": int(kv["threads"]),
-            "kind": "reference",
-            "sample": f"{m} reads of this batch: {kv['seeds']} seeds searched+extended "
-                      f"({float(kv['seed_s']):.2f} s) + {kv['dp_probs']} DP problems, "
-                      f"{kv['dp_alns']} alignments ({float(kv['dp_s']):.2f} s); reference "
-                      f"searchAllSeedsDoAll + SwAligner (oracle/_ref/refharness bench), "
-                      f"OpenMP {kv['threads']} threads"}
-
-
-def cpu_baseline_port(args, sbuf, sin, drd, dqu, drf, dpin, base, n):
-    """The oracle ("port", 1 thread) on a bounded sample of the same workload."""
-    import oracle_lib as ol
-    m = min(args.port_sample, n)
-    spr = len(sin) / n
-    sseeds = sin[: int(round(spr * m))]
-    sdp = dpin[: int(round(len(dpin) / n * m))]
-    oidx = ol.OracleIndex(base)
-    t0 = time.perf_counter()
-    ol.seed_search(oidx, sbuf, sseeds, True)
-    ol.dp_align(ol.default_scoring(), drd, dqu, drf, sdp, debug=False)
-    dt = time.perf_counter() - t0
-    return {"value": round(m / dt / 1e6, 6), "unit": "M reads/s", "cores": 1, "kind": "port",
-            "sample": f"{m} reads: {len(sseeds)} seeds + {len(sdp)} DP problems, oracle/bt2x_oracle.c, "
-                      f"{dt:.1f} s"}
 
 
 if __name__ == "__main__":

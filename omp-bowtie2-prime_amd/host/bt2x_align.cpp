@@ -725,70 +725,99 @@ bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st, int threads) {
 		else if(c->req == REQ_DP) wd.push_back(c);
 	}
 	if(ws.empty() && wr.empty() && wd.empty()) return false;
-	if(!ws.empty()) {
+	static const bool trace = std::getenv("BT2X_TRACE") != nullptr;
+	if(trace) {
+		long rss = 0;
+		if(std::FILE* f = std::fopen("/proc/self/statm", "r")) { long a = 0; if(std::fscanf(f, "%ld %ld", &a, &rss) != 2) rss = 0; std::fclose(f); }
+		std::fprintf(stderr, "BT2X_TRACE active=%zu seed=%zu resolve=%zu dp=%zu rss_mb=%ld\n", act.size(), ws.size(),
+		             wr.size(), wd.size(), rss * 4096 / (1 << 20));
+	}
+	const long nws = (long)ws.size(), nwr = (long)wr.size(), nwd = (long)wd.size();
+	if(nws) {
+		// one launch for every waiting read's seeds: patFw+patRc of each read, then its
+		// seeds with read_off rebased (gather/scatter in parallel over reads)
 		double t0 = now_s();
-		std::vector<uint8_t> reads;
-		std::vector<bt2x_seed_in> in;
-		for(ReadCtx* c : ws) {
-			const uint64_t base = reads.size();
-			reads.insert(reads.end(), c->rd.fw.begin(), c->rd.fw.end());
-			reads.insert(reads.end(), c->rd.rc.begin(), c->rd.rc.end());
-			for(bt2x_seed_in s : c->seed.in) { s.read_off += base; in.push_back(s); }
+		std::vector<uint64_t> rb(nws + 1, 0), sb(nws + 1, 0);
+		for(long i = 0; i < nws; i++) {
+			rb[i + 1] = rb[i] + 2 * ws[i]->rd.length();
+			sb[i + 1] = sb[i] + ws[i]->seed.in.size();
+		}
+		std::vector<uint8_t> reads(rb[nws]);
+		std::vector<bt2x_seed_in> in(sb[nws]);
+#pragma omp parallel for schedule(static, 256) num_threads(threads)
+		for(long i = 0; i < nws; i++) {
+			const ReadCtx* c = ws[i];
+			const size_t L = c->rd.length();
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), reads.begin() + (long)rb[i]);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), reads.begin() + (long)(rb[i] + L));
+			for(size_t k = 0; k < c->seed.in.size(); k++) {
+				bt2x_seed_in s = c->seed.in[k];
+				s.read_off += rb[i];
+				in[sb[i] + k] = s;
+			}
 		}
 		std::vector<bt2x_seed_out> out;
 		be_.seed_search(reads, in, out);
-		size_t k = 0;
-		for(ReadCtx* c : ws) {
-			c->seed.out.assign(out.begin() + k, out.begin() + k + c->seed.in.size());
-			k += c->seed.in.size();
-		}
+#pragma omp parallel for schedule(static, 256) num_threads(threads)
+		for(long i = 0; i < nws; i++)
+			ws[i]->seed.out.assign(out.begin() + (long)sb[i], out.begin() + (long)sb[i + 1]);
 		st.seed_launches++; st.seeds += in.size(); st.t_seed += now_s() - t0;
 	}
-	if(!wr.empty()) {
+	if(nwr) {
 		double t0 = now_s();
-		std::vector<bt2x_resolve_in> in;
-		for(ReadCtx* c : wr) in.insert(in.end(), c->resolve.in.begin(), c->resolve.in.end());
+		std::vector<uint64_t> ib(nwr + 1, 0);
+		for(long i = 0; i < nwr; i++) ib[i + 1] = ib[i] + wr[i]->resolve.in.size();
+		std::vector<bt2x_resolve_in> in(ib[nwr]);
+#pragma omp parallel for schedule(static, 256) num_threads(threads)
+		for(long i = 0; i < nwr; i++)
+			std::copy(wr[i]->resolve.in.begin(), wr[i]->resolve.in.end(), in.begin() + (long)ib[i]);
 		std::vector<bt2x_resolve_out> out;
 		be_.resolve(in, out);
-		size_t k = 0;
-		for(ReadCtx* c : wr) {
-			c->resolve.out.assign(out.begin() + k, out.begin() + k + c->resolve.in.size());
-			k += c->resolve.in.size();
-		}
+#pragma omp parallel for schedule(static, 256) num_threads(threads)
+		for(long i = 0; i < nwr; i++)
+			wr[i]->resolve.out.assign(out.begin() + (long)ib[i], out.begin() + (long)ib[i + 1]);
 		st.resolve_launches++; st.resolves += in.size(); st.t_resolve += now_s() - t0;
 	}
-	if(!wd.empty()) {
+	if(nwd) {
 		double t0 = now_s();
-		std::vector<uint8_t> reads, quals, refs;
-		std::vector<bt2x_dp_in> in;
-		in.reserve(wd.size());
-		for(ReadCtx* c : wd) {
+		// one DP problem per waiting read: oriented read, qualities, reference window
+		std::vector<uint64_t> qb(nwd + 1, 0), fb(nwd + 1, 0);
+		for(long i = 0; i < nwd; i++) {
+			qb[i + 1] = qb[i] + wd[i]->rd.length();
+			fb[i + 1] = fb[i] + wd[i]->dp.window.size();
+		}
+		std::vector<uint8_t> reads(qb[nwd]), quals(qb[nwd]), refs(fb[nwd]);
+		std::vector<bt2x_dp_in> in(nwd);
+#pragma omp parallel for schedule(static, 256) num_threads(threads)
+		for(long i = 0; i < nwd; i++) {
+			const ReadCtx* c = wd[i];
 			bt2x_dp_in p = c->dp.in;
-			p.read_off = reads.size();
-			p.qual_off = quals.size();
-			p.ref_off = refs.size();
+			p.read_off = qb[i];
+			p.qual_off = qb[i];
+			p.ref_off = fb[i];
 			const std::vector<uint8_t>& s = c->dp.fw ? c->rd.fw : c->rd.rc;
 			const std::string& q = c->dp.fw ? c->rd.qual : c->rd.qualRev;
-			reads.insert(reads.end(), s.begin(), s.end());
-			quals.insert(quals.end(), q.begin(), q.end());
-			refs.insert(refs.end(), c->dp.window.begin(), c->dp.window.end());
-			in.push_back(p);
+			std::copy(s.begin(), s.end(), reads.begin() + (long)qb[i]);
+			std::copy(q.begin(), q.end(), quals.begin() + (long)qb[i]);
+			std::copy(c->dp.window.begin(), c->dp.window.end(), refs.begin() + (long)fb[i]);
+			in[i] = p;
 		}
 		std::vector<bt2x_dp_out> out;
 		std::vector<bt2x_aln_rec> recs;
 		std::vector<uint32_t> edits;
 		be_.dp_align(reads, quals, refs, in, out, recs, edits);
-		for(size_t k = 0; k < wd.size(); k++) {
+#pragma omp parallel for schedule(static, 256) num_threads(threads)
+		for(long k = 0; k < nwd; k++) {
 			DpWork& d = wd[k]->dp;
 			d.out = out[k];
 			d.recs.assign(recs.begin() + out[k].rec_off, recs.begin() + out[k].rec_off + out[k].nrec);
-			// edit offsets stay global: rebase them onto this problem's copy
-			uint32_t lo = UINT32_MAX, hi = 0;
-			for(const bt2x_aln_rec& r : d.recs) if(r.nbuf) { lo = std::min(lo, r.edit_off); hi = std::max(hi, r.edit_off + r.nbuf); }
-			if(lo == UINT32_MAX) { d.edits.clear(); }
-			else {
-				d.edits.assign(edits.begin() + lo, edits.begin() + hi);
-				for(bt2x_aln_rec& r : d.recs) r.edit_off -= lo;
+			// gather each record's edit-buffer image (arena offsets are allocated by the
+			// kernel's atomics, so one problem's images are not contiguous)
+			d.edits.clear();
+			for(bt2x_aln_rec& r : d.recs) {
+				const uint32_t o = (uint32_t)d.edits.size();
+				d.edits.insert(d.edits.end(), edits.begin() + r.edit_off, edits.begin() + r.edit_off + r.nbuf);
+				r.edit_off = o;
 			}
 		}
 		st.dp_launches++; st.dps += in.size(); st.t_dp += now_s() - t0;

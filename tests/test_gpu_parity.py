@@ -111,12 +111,14 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     for i in np.nonzero(out["nrec"])[0]:
         a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
         b = erecs[eo["rec_off"][i]: eo["rec_off"][i] + eo["nrec"][i]]
-        fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff"]
+        fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff", "nbuf"]
         assert (a[fields] == b[fields]).all(), i
         for ra, rb in zip(a, b):
-            np.testing.assert_array_equal(edits[ra["edit_off"]: ra["edit_off"] + ra["nedit"]],
-                                          eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
+            # the edit-buffer image (bt2x.h): the alignment's edits are its prefix
+            np.testing.assert_array_equal(edits[ra["edit_off"]: ra["edit_off"] + ra["nbuf"]],
+                                          eedits[rb["edit_off"]: rb["edit_off"] + rb["nbuf"]])
     assert (out["status"] == 1).sum() > 20000
+    assert (recs["nbuf"] > recs["nedit"]).sum() > 1000      # failed attempts' leftovers are exercised
 
 
 def test_dp_rejects_shapes_outside_reference_limits(ctxs):
