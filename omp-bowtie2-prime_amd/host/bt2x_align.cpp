@@ -10,6 +10,11 @@
 #include <map>
 #include <memory>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -27,6 +32,27 @@ const uint8_t kAsc2Dna[256] = {   // alphabet.cpp:142 (A/C/G/T, either case; all
 	N4, N4, N4, N4, N4, N4, N4, N4
 #undef N4
 };
+
+// ---------------------------------------------------------------- FastqReader
+
+FastqReader::FastqReader(const char* path) {
+	fd_ = ::open(path, O_RDONLY);
+	if(fd_ < 0) throw std::runtime_error(std::string("cannot open reads file ") + path);
+	struct stat sb;
+	if(::fstat(fd_, &sb) != 0) throw std::runtime_error(std::string("cannot stat ") + path);
+	len_ = (size_t)sb.st_size;
+	if(len_) {
+		void* m = ::mmap(nullptr, len_, PROT_READ, MAP_PRIVATE, fd_, 0);
+		if(m == MAP_FAILED) throw std::runtime_error(std::string("cannot map ") + path);
+		::madvise(m, len_, MADV_SEQUENTIAL);
+		map_ = (const char*)m;
+	}
+}
+
+FastqReader::~FastqReader() {
+	if(map_) ::munmap((void*)map_, len_);
+	if(fd_ >= 0) ::close(fd_);
+}
 
 // ------------------------------------------------------------------- RefInfo
 
@@ -65,7 +91,13 @@ void RefInfo::init(const bt2x_index_desc& d, const std::string& base) {
 
 void RefInfo::stretch(uint32_t tidx, int64_t off, size_t n, uint8_t* out) const {
 	std::memset(out, 4, n);
-	for(const Frag& fr : frags_[tidx]) {
+	const std::vector<Frag>& fs = frags_[tidx];
+	// fragments are in text order: start at the last one beginning at or before `off`
+	size_t k = (size_t)(std::upper_bound(fs.begin(), fs.end(), off,
+	                                     [](int64_t o, const Frag& f) { return o < f.toff; }) - fs.begin());
+	if(k > 0) k--;
+	for(; k < fs.size() && fs[k].toff < off + (int64_t)n; k++) {
+		const Frag& fr = fs[k];
 		const int64_t a = std::max<int64_t>(off, fr.toff);
 		const int64_t b = std::min<int64_t>(off + (int64_t)n, fr.toff + (int64_t)fr.len);
 		for(int64_t p = a; p < b; p++) {
@@ -852,20 +884,29 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		// refill the pool
 		double t0 = now_s();
 		std::vector<ReadCtx*> fresh;
-		while(!eof && act.size() + fresh.size() < slots) {
-			std::unique_ptr<ReadCtx> c(new ReadCtx());
-			if(!fq.next(c->rd, rdid, p_.randSeed)) { eof = true; break; }
-			rdid++;
-			c->task = align_read(c.get());
-			fresh.push_back(c.get());
-			window.push_back(std::move(c));
+		std::vector<FastqReader::Raw> raw;
+		if(!eof && act.size() < slots) {
+			const size_t want = slots - act.size();
+			if(fq.take(want, raw) < want) eof = true;
 		}
 		st.t_io += now_s() - t0;
-		if(!fresh.empty()) {
+		const long nf = (long)raw.size();
+		if(nf) {
 			t0 = now_s();
-			const long nf = (long)fresh.size();
+			fresh.resize((size_t)nf);
+			for(long i = 0; i < nf; i++) {
+				window.emplace_back(new ReadCtx());
+				fresh[(size_t)i] = window.back().get();
+			}
+			// decode + run each new read up to its first request, in parallel
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-			for(long i = 0; i < nf; i++) fresh[i]->task.h.resume();
+			for(long i = 0; i < nf; i++) {
+				ReadCtx* c = fresh[(size_t)i];
+				FastqReader::decode(raw[(size_t)i], c->rd, rdid + (uint64_t)i, p_.randSeed);
+				c->task = align_read(c);
+				c->task.h.resume();
+			}
+			rdid += (uint64_t)nf;
 			st.t_host += now_s() - t0;
 			act.insert(act.end(), fresh.begin(), fresh.end());
 		}

@@ -267,17 +267,45 @@ struct AlnRes {                     // the AlnRes fields the unpaired SAM path r
 };
 
 // RedundantAlns (aligner_result.cpp:821-914): DP cells already used by an alignment.
+// The reference keeps one ESet per read row; here one open-addressing set of
+// (ref, strand, column, row) cells, empty (and never walked) until the first add.
 class RedundantAlns {
 public:
-	void init(size_t npos) { cells_.assign(npos, {}); }
+	void init(size_t) { slots_.clear(); n_ = 0; }
 	void add(const AlnRes& r) { walk(r, true); }
-	bool overlap(const AlnRes& r) { return walk(r, false); }
+	bool overlap(const AlnRes& r) { return n_ != 0 && walk(r, false); }
 private:
-	struct Cell { int64_t rfid; bool fw; int64_t rfoff; };
+	struct Cell { int64_t rfid = -1; int64_t rfoff = 0; uint32_t row = 0; bool fw = false; };
+	static uint64_t hash(int64_t rfid, bool fw, int64_t rfoff, uint32_t row) {
+		uint64_t z = (uint64_t)rfoff * 0x9e3779b97f4a7c15ULL ^ ((uint64_t)rfid << 20) ^ ((uint64_t)row << 1) ^ (fw ? 1u : 0u);
+		z ^= z >> 29; z *= 0xbf58476d1ce4e5b9ULL; z ^= z >> 32;
+		return z;
+	}
+	bool find_or_insert(int64_t rfid, bool fw, int64_t rfoff, uint32_t row, bool insert) {
+		if(slots_.empty()) { if(!insert) return false; slots_.resize(512); }
+		else if(insert && (n_ + 1) * 2 > slots_.size()) {
+			std::vector<Cell> old;
+			old.swap(slots_);
+			slots_.resize(old.size() * 2);
+			n_ = 0;
+			for(const Cell& c : old) if(c.rfid >= 0) find_or_insert(c.rfid, c.fw, c.rfoff, c.row, true);
+		}
+		const size_t mask = slots_.size() - 1;
+		for(size_t h = hash(rfid, fw, rfoff, row) & mask;; h = (h + 1) & mask) {
+			Cell& c = slots_[h];
+			if(c.rfid < 0) {
+				if(insert) { c.rfid = rfid; c.fw = fw; c.rfoff = rfoff; c.row = row; n_++; }
+				return false;
+			}
+			if(c.rfid == rfid && c.fw == fw && c.rfoff == rfoff && c.row == row) return true;
+		}
+	}
 	bool walk(const AlnRes& r, bool insert) {
 		int64_t left = r.refoff, right;
 		const size_t len = r.rdlen;
-		const std::vector<uint32_t> ned = r.fw ? r.ned : invert_poss(r.ned, r.rdlen);
+		std::vector<uint32_t> inv;
+		if(!r.fw) inv = invert_poss(r.ned, r.rdlen);
+		const std::vector<uint32_t>& ned = r.fw ? r.ned : inv;
 		size_t ni = 0;
 		for(size_t i = 0; i < len; i++) {
 			size_t diff = 1;
@@ -294,17 +322,15 @@ private:
 				}
 			}
 			for(int64_t j = left; j < right; j++) {
-				std::vector<Cell>& row = cells_[i];
-				bool found = false;
-				for(const Cell& c : row) if(c.rfid == r.refid && c.fw == r.fw && c.rfoff == j) { found = true; break; }
-				if(insert) { if(!found) row.push_back({r.refid, r.fw, j}); }
-				else if(found) return true;
+				const bool found = find_or_insert(r.refid, r.fw, j, (uint32_t)i, insert);
+				if(!insert && found) return true;
 			}
 			left = right + diff - 1;
 		}
 		return false;
 	}
-	std::vector<std::vector<Cell>> cells_;
+	std::vector<Cell> slots_;
+	size_t n_ = 0;
 };
 
 // ------------------------------------------------------------------------ parameters
@@ -407,70 +433,68 @@ inline uint32_t gen_rand_seed(const Read& r, uint32_t seed) {
 	return rseed;
 }
 
-// Streaming FASTQ reader (FastqPatternSource light parse + parse, pat.cpp:1124-1220),
-// Phred+33 only; '.' is N, non-alphabetic sequence characters are skipped.
+// FASTQ input (FastqPatternSource light parse + parse, pat.cpp:1124-1220), Phred+33
+// only; '.' is N, non-alphabetic sequence characters are skipped.  The file is mapped:
+// take() finds record boundaries (four lines each) serially with memchr, decode() builds
+// the Read (codes, reverse complement, genRandSeed) and runs in parallel over records.
 class FastqReader {
 public:
-	explicit FastqReader(const char* path) {
-		f_ = std::fopen(path, "rb");
-		if(!f_) throw std::runtime_error(std::string("cannot open reads file ") + path);
-		buf_.resize(1 << 22);
-	}
-	~FastqReader() { if(f_) std::fclose(f_); }
+	struct Raw { const char* l[4]; size_t n[4]; };
+	explicit FastqReader(const char* path);
+	~FastqReader();
 	FastqReader(const FastqReader&) = delete;
 	FastqReader& operator=(const FastqReader&) = delete;
-	// false at end of input
-	bool next(Read& r, uint64_t rdid, uint32_t randSeed) {
-		std::string l1, l2, l3, l4;
-		do { if(!line(l1)) return false; } while(l1.empty());
-		if(l1[0] != '@') throw std::runtime_error("FASTQ record does not start with '@'");
-		line(l2); line(l3); line(l4);
+	// up to `max` more records appended to `out`; returns how many
+	size_t take(size_t max, std::vector<Raw>& out) {
+		size_t k = 0;
+		while(k < max) {
+			Raw r;
+			const char* s;
+			size_t n;
+			do { if(!line(s, n)) return k; } while(n == 0);
+			r.l[0] = s; r.n[0] = n;
+			for(int j = 1; j < 4; j++) { if(!line(s, n)) { s = map_ + len_; n = 0; } r.l[j] = s; r.n[j] = n; }
+			out.push_back(r);
+			k++;
+		}
+		return k;
+	}
+	static void decode(const Raw& raw, Read& r, uint64_t rdid, uint32_t randSeed) {
+		if(raw.l[0][0] != '@') throw std::runtime_error("FASTQ record does not start with '@'");
 		r = Read();
 		r.rdid = rdid;
-		r.name = l1.substr(1);
-		for(char ch : l2) {
-			unsigned char c = (unsigned char)(ch == '.' ? 'N' : ch);
+		r.name.assign(raw.l[0] + 1, raw.n[0] - 1);
+		r.fw.reserve(raw.n[1]);
+		for(size_t i = 0; i < raw.n[1]; i++) {
+			const unsigned char c = (unsigned char)(raw.l[1][i] == '.' ? 'N' : raw.l[1][i]);
 			if(std::isalpha(c)) r.fw.push_back(kAsc2Dna[c]);
 		}
-		if(!l2.empty() || !l4.empty()) r.qual = l4;
+		if(raw.n[1] || raw.n[3]) r.qual.assign(raw.l[3], raw.n[3]);
 		if(r.qual.size() != r.fw.size())
 			throw std::runtime_error("read " + r.name + ": qualities and sequence differ in length");
 		if(r.name.empty()) r.name = std::to_string(rdid);
-		r.rc.resize(r.fw.size());
-		for(size_t i = 0; i < r.fw.size(); i++) {
-			const uint8_t c = r.fw[r.fw.size() - 1 - i];
+		const size_t L = r.fw.size();
+		r.rc.resize(L);
+		for(size_t i = 0; i < L; i++) {
+			const uint8_t c = r.fw[L - 1 - i];
 			r.rc[i] = c < 4 ? (uint8_t)(3 - c) : (uint8_t)4;
 		}
 		r.qualRev.assign(r.qual.rbegin(), r.qual.rend());
 		r.seed = gen_rand_seed(r, randSeed);
-		return true;
 	}
 private:
-	bool line(std::string& s) {
-		s.clear();
-		bool any = false;
-		while(true) {
-			if(pos_ == len_) {
-				len_ = std::fread(buf_.data(), 1, buf_.size(), f_);
-				pos_ = 0;
-				if(len_ == 0) return any;
-			}
-			const char* b = buf_.data() + pos_;
-			const char* nl = (const char*)std::memchr(b, '\n', len_ - pos_);
-			const size_t n = nl ? (size_t)(nl - b) : len_ - pos_;
-			s.append(b, n);
-			any = true;
-			pos_ += n;
-			if(nl) {
-				pos_++;
-				while(!s.empty() && s.back() == '\r') s.pop_back();
-				return true;
-			}
-		}
+	bool line(const char*& s, size_t& n) {
+		if(pos_ >= len_) return false;
+		s = map_ + pos_;
+		const char* nl = (const char*)std::memchr(s, '\n', len_ - pos_);
+		n = nl ? (size_t)(nl - s) : len_ - pos_;
+		pos_ += n + (nl ? 1 : 0);
+		while(n > 0 && s[n - 1] == '\r') n--;
+		return true;
 	}
-	std::FILE* f_ = nullptr;
-	std::vector<char> buf_;
-	size_t pos_ = 0, len_ = 0;
+	const char* map_ = nullptr;
+	size_t len_ = 0, pos_ = 0;
+	int fd_ = -1;
 };
 
 // ------------------------------------------------------------------- reference

@@ -8,6 +8,7 @@
 // tested separately (tests/test_gpu_parity.py).
 //
 //   test_e2e_oracle <index base> <reads.fq> [--dpad N] [--slots N] [-p T]
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -55,6 +56,35 @@ private:
 	const bt2x_index_desc& idx_;
 	const bt2x_scoring& sc_;
 };
+
+// --host-timing: the second run answers every launch from the first run's recorded
+// outputs (the driver is deterministic), so its wall time is the host driver's alone.
+class ReplayBackend : public Backend {
+public:
+	explicit ReplayBackend(Backend* rec) : rec_(rec) {}
+	void rewind() { rec_ = nullptr; k_ = 0; }
+	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
+	                 std::vector<bt2x_seed_out>& out) override {
+		if(rec_) { rec_->seed_search(reads, in, out); seeds_.push_back(out); } else out = seeds_[k_++];
+	}
+	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+		if(rec_) { rec_->resolve(in, out); res_.push_back(out); } else out = res_[kr_++];
+	}
+	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
+	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
+	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
+	              std::vector<uint32_t>& edits) override {
+		if(rec_) { rec_->dp_align(reads, quals, refs, in, out, recs, edits); dp_.push_back({out, recs, edits}); }
+		else { const auto& d = dp_[kd_++]; out = d.out; recs = d.recs; edits = d.edits; }
+	}
+private:
+	struct Dp { std::vector<bt2x_dp_out> out; std::vector<bt2x_aln_rec> recs; std::vector<uint32_t> edits; };
+	Backend* rec_;
+	size_t k_ = 0, kr_ = 0, kd_ = 0;
+	std::vector<std::vector<bt2x_seed_out>> seeds_;
+	std::vector<std::vector<bt2x_resolve_out>> res_;
+	std::vector<Dp> dp_;
+};
 }
 
 int main(int argc, char** argv) {
@@ -62,11 +92,13 @@ int main(int argc, char** argv) {
 	Params p;
 	size_t slots = 4096;
 	int threads = 4;
-	for(int i = 3; i + 1 < argc; i++) {
+	bool host_timing = false;
+	for(int i = 3; i < argc; i++) {
 		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
 		const std::string a = argv[i];
-		if(a == "--slots") slots = (size_t)std::atol(argv[++i]);
-		else if(a == "-p") threads = std::atoi(argv[++i]);
+		if(a == "--slots" && i + 1 < argc) slots = (size_t)std::atol(argv[++i]);
+		else if(a == "-p" && i + 1 < argc) threads = std::atoi(argv[++i]);
+		else if(a == "--host-timing") host_timing = true;
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); return 1; }
 	}
 	bt2x_scoring_init(&p.sc);
@@ -74,6 +106,21 @@ int main(int argc, char** argv) {
 	RefInfo ref;
 	ref.init(index.desc(), argv[1]);
 	OracleBackend be(index.desc(), p.sc);
+	if(host_timing) {
+		ReplayBackend rb(&be);
+		Aligner al(p, ref, rb);
+		{ FastqReader fq(argv[2]); std::FILE* nul = std::fopen("/dev/null", "wb"); al.run(fq, nul, slots, threads); std::fclose(nul); }
+		rb.rewind();
+		FastqReader fq(argv[2]);
+		const auto t0 = std::chrono::steady_clock::now();
+		const RunStats st = al.run(fq, stdout, slots, threads);
+		const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+		std::fprintf(stderr, "HOST_TIMING reads=%llu wall=%.3f t_host=%.3f t_io=%.3f t_seed=%.3f t_resolve=%.3f t_dp=%.3f "
+		             "launches=%llu/%llu/%llu\n", (unsigned long long)st.reads, t, st.t_host, st.t_io, st.t_seed,
+		             st.t_resolve, st.t_dp, (unsigned long long)st.seed_launches,
+		             (unsigned long long)st.resolve_launches, (unsigned long long)st.dp_launches);
+		return 0;
+	}
 	Aligner al(p, ref, be);
 	FastqReader fq(argv[2]);
 	const RunStats st = al.run(fq, stdout, slots, threads);
