@@ -449,6 +449,115 @@ struct RowSampler {
 	}
 };
 
+// The candidate walk of extendSeeds (aligner_sw_driver.cpp:278-631) as a resumable
+// iterator: next() runs the loop up to its next DP problem (PROBLEM, the problem's key)
+// or to the loop's exit (an EXTEND_* code); failed() applies a DP that found nothing.
+// The walk's own state (position, per-range samplers, elements left) is a value and the
+// per-read state it advances (RNG, limit metrics, seen diagonals) is bound by pointer,
+// so a copy bound to copies of those runs ahead of the real walk on the assumption
+// that every DP fails: the lookahead the scheduler batches (DpKey, bt2x_align.hpp).
+class ExtendWalk {
+public:
+	static constexpr int PROBLEM = 0;
+	ExtendWalk(const Params& P, const std::vector<SatPos>& sat, const std::vector<uint32_t>& rand_ns,
+	           const std::vector<size_t>& firstRow, const std::vector<bt2x_resolve_out>& res, size_t nelt,
+	           size_t rdlen)
+		: P_(&P), sat_(&sat), firstRow_(&firstRow), res_(&res), neltLeft_(nelt), rdlen_(rdlen) {
+		rands_.resize(sat.size());
+		for(size_t i = 0; i < sat.size(); i++) rands_[i].init((uint16_t)rand_ns[i], false);
+	}
+	void bind(Rng* rnd, Prm* prm, SeenDiags* seen) { rnd_ = rnd; prm_ = prm; seen_ = seen; }
+	int next(int64_t minsc, DpKey& k) {
+		const Params& P = *P_;
+		const size_t n = (uint16_t)sat_->size();                // gws_size is a uint16_t
+		for(;;) {
+			if(!inPass_) {                                       // while(neltLeft > 0)
+				if(neltLeft_ == 0) return EXTEND_EXHAUSTED_CANDIDATES;
+				if(minsc == 0) return EXTEND_PERFECT_SCORE;
+				inPass_ = true; i_ = 0; first_ = true;
+			}
+			if(i_ >= n) { inPass_ = false; continue; }
+			const SatPos& sp = (*sat_)[i_];
+			const bool is_small = sp.size < kNsm;
+			if(rands_[i_].done() || !(first_ || is_small)) { i_++; first_ = true; continue; }
+			if(minsc == 0) return EXTEND_PERFECT_SCORE;
+			if(prm_->nExDps >= P.mxDp || prm_->nMateDps >= P.mxDp) return EXTEND_EXCEEDED_HARD_LIMIT;
+			if(prm_->nExUgs >= P.mxUg || prm_->nMateUgs >= P.mxUg) return EXTEND_EXCEEDED_HARD_LIMIT;
+			if(prm_->nExIters >= P.mxIter) return EXTEND_EXCEEDED_HARD_LIMIT;
+			prm_->nExIters++;
+			first_ = false;
+			const bool fw = sp.fw;
+			uint32_t rdoff = sp.rdoff;
+			if(!fw) rdoff = (uint32_t)(rdlen_ - rdoff - sp.seedlen);
+			const uint16_t elt = rands_[i_].next(*rnd_);
+			const bt2x_resolve_out& wr = (*res_)[(*firstRow_)[i_] + elt];
+			neltLeft_--;
+			const int64_t tidx = wr.tidx == BT2X_NO_TIDX ? 0 : (int64_t)wr.tidx;
+			const int64_t toff = (int64_t)wr.toff, tlen = (int64_t)wr.tlen;
+			const int64_t refoff = toff - (int64_t)rdoff;
+			const Coord refcoord(tidx, refoff, fw);
+			if(seen_->locusPresent(refcoord)) { prm_->nRedundants++; continue; }
+			// DynProgFramer::frameSeedExtensionRect, trimToRef (dp_framer.cpp:81-129)
+			const int readGaps = P.maxReadGaps(minsc), refGaps = P.maxRefGaps(minsc);
+			const size_t maxgap = std::min((size_t)std::max(readGaps, refGaps), P.maxhalf);
+			const int64_t refl_pre = refoff - 2 * (int64_t)maxgap;
+			const int64_t refr_pre = refoff + ((int64_t)rdlen_ - 1) + 2 * (int64_t)maxgap;
+			size_t triml = 0, trimr = 0;
+			if(refr_pre >= tlen) trimr = (size_t)(refr_pre - (tlen - 1));
+			if(refl_pre < 0) triml = (size_t)(-refl_pre);
+			const int64_t refl = refl_pre + (int64_t)triml, refr = refr_pre - (int64_t)trimr;
+			const size_t corel = maxgap, corer = corel + 2 * maxgap;
+			seen_->add(Interval(refcoord, 1));
+			if(refr < refl) continue;                            // entirely trimmed
+			// SwAligner::initRef (aligner_sw.cpp:117-229)
+			const size_t ncol = (size_t)(refr - refl + 1);
+			if(ncol + 1 > BT2X_MAX_COLS) {
+				prm_->nExDpFails++; prm_->nDpFail++;
+				return EXTEND_EXCEEDED_HARD_LIMIT;
+			}
+			seen_->add(Interval(Coord(tidx, refl_pre + (int64_t)corel, fw), (int64_t)(corer - corel + 1)));
+			k.tidx = tidx; k.refl = refl; k.minsc = minsc; k.ncol = (uint32_t)ncol;
+			k.triml = (uint32_t)triml; k.corel = (uint32_t)corel; k.corer = (uint32_t)corer; k.fw = fw;
+			return PROBLEM;
+		}
+	}
+	// the DP of the last next() found no alignment; false: the fail streak ends the walk
+	bool failed() {
+		prm_->nExDps++; prm_->nExDpFails++; prm_->nDpFail++;
+		return prm_->nDpFail < P_->streak;
+	}
+private:
+	static constexpr uint64_t kNsm = 5;                          // prioritizeSATups' nsm
+	const Params* P_;
+	const std::vector<SatPos>* sat_;
+	const std::vector<size_t>* firstRow_;
+	const std::vector<bt2x_resolve_out>* res_;
+	size_t neltLeft_, rdlen_;
+	std::vector<Random1toN> rands_;
+	size_t i_ = 0;
+	bool first_ = true, inPass_ = false;
+	Rng* rnd_ = nullptr;
+	Prm* prm_ = nullptr;
+	SeenDiags* seen_ = nullptr;
+};
+
+// SwAligner::initRef's problem for key k (window = BitPairReference::getStretch).
+void pose_dp(std::vector<DpWork>& dps, const RefInfo& ref, const DpKey& k, size_t rdlen, int nceil) {
+	dps.emplace_back();
+	DpWork& d = dps.back();
+	d.key = k;
+	std::memset(&d.in, 0, sizeof(d.in));
+	d.in.refl = k.refl;
+	d.in.rdlen = (uint16_t)rdlen;
+	d.in.ncol = (uint16_t)k.ncol;
+	d.in.minsc = (int16_t)std::max<int64_t>(k.minsc, -254);
+	d.in.nceil = (int16_t)nceil;
+	d.in.triml = (uint16_t)k.triml; d.in.corel = (uint16_t)k.corel; d.in.corer = (uint16_t)k.corer;
+	d.in.fw = k.fw ? 1 : 0;
+	d.window.resize(k.ncol);
+	ref.stretch((uint32_t)k.tidx, k.refl, k.ncol, d.window.data());
+}
+
 } // namespace
 
 // ---------------------------------------------------------------- SAM header
@@ -484,6 +593,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 	RedundantAlns redAnchor;
 	redAnchor.init(rdlen);
 	std::vector<uint32_t> edbuf;         // SwDriver::resGap_.alres.ned_ storage
+	std::unordered_map<DpKey, DpResult, DpKeyHash> memo;   // this read's DP results (lookahead)
 	std::vector<ExtendRange> exRange[2];
 	Prm prm;
 	const uint32_t nrounds = (uint32_t)std::min<int>(P.nSeedRounds, interval);
@@ -605,126 +715,95 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		if(!c->resolve.in.empty()) co_await Awaiter{c, REQ_RESOLVE};
 
 		// -------------------------------------------------- extendSeeds (:278-631)
-		int ret = EXTEND_EXHAUSTED_CANDIDATES;
+		int ret;
 		{
 			prm.nDpFail = 0;
 			const int64_t perfectScore = 0;
-			const uint16_t gws_size = (uint16_t)satpos.size();
-			std::vector<Random1toN> rands(gws_size);
-			for(uint16_t i = 0; i < gws_size; i++) rands[i].init((uint16_t)rand_ns[i], false);
-			size_t neltLeft = nelt_;
-			while(neltLeft > 0) {
-				if(minsc == perfectScore) { ret = EXTEND_PERFECT_SCORE; goto extend_done; }
-				for(uint16_t i = 0; i < gws_size; i++) {
-					const bool is_small = satpos[i].size < nsm;
-					const bool fw = satpos[i].fw;
-					uint32_t rdoff = satpos[i].rdoff;
-					const uint32_t seedhitlen = satpos[i].seedlen;
-					if(!fw) rdoff = (uint32_t)(rdlen - rdoff - seedhitlen);
-					bool first = true;
-					while(!rands[i].done() && (first || is_small)) {
-						if(minsc == perfectScore) { ret = EXTEND_PERFECT_SCORE; goto extend_done; }
-						if(prm.nExDps >= P.mxDp || prm.nMateDps >= P.mxDp) { ret = EXTEND_EXCEEDED_HARD_LIMIT; goto extend_done; }
-						if(prm.nExUgs >= P.mxUg || prm.nMateUgs >= P.mxUg) { ret = EXTEND_EXCEEDED_HARD_LIMIT; goto extend_done; }
-						if(prm.nExIters >= P.mxIter) { ret = EXTEND_EXCEEDED_HARD_LIMIT; goto extend_done; }
-						prm.nExIters++;
-						first = false;
-						const uint16_t elt = rands[i].next(rnd);
-						const bt2x_resolve_out& wr = c->resolve.out[firstRow[i] + elt];
-						neltLeft--;
-						const int64_t tidx = wr.tidx == BT2X_NO_TIDX ? 0 : (int64_t)wr.tidx;
-						const int64_t toff = (int64_t)wr.toff, tlen = (int64_t)wr.tlen;
-						const int64_t refoff = toff - (int64_t)rdoff;
-						const Coord refcoord(tidx, refoff, fw);
-						if(seenDiags.locusPresent(refcoord)) { prm.nRedundants++; continue; }
-						// DynProgFramer::frameSeedExtensionRect, trimToRef (dp_framer.cpp:81-129)
-						const int readGaps = P.maxReadGaps(minsc), refGaps = P.maxRefGaps(minsc);
-						const size_t maxgap = std::min((size_t)std::max(readGaps, refGaps), P.maxhalf);
-						const int64_t refl_pre = refoff - 2 * (int64_t)maxgap;
-						const int64_t refr_pre = refoff + ((int64_t)rdlen - 1) + 2 * (int64_t)maxgap;
-						size_t triml = 0, trimr = 0;
-						if(refr_pre >= tlen) trimr = (size_t)(refr_pre - (tlen - 1));
-						if(refl_pre < 0) triml = (size_t)(-refl_pre);
-						const int64_t refl = refl_pre + (int64_t)triml, refr = refr_pre - (int64_t)trimr;
-						const size_t corel = maxgap, corer = corel + 2 * maxgap;
-						seenDiags.add(Interval(refcoord, 1));
-						if(refr < refl) continue;                            // entirely trimmed
-						// SwAligner::initRef (aligner_sw.cpp:117-229)
-						const size_t ncol = (size_t)(refr - refl + 1);
-						if(ncol + 1 > BT2X_MAX_COLS) {
-							prm.nExDpFails++; prm.nDpFail++;
-							ret = EXTEND_EXCEEDED_HARD_LIMIT; goto extend_done;
-						}
-						seenDiags.add(Interval(Coord(tidx, refl_pre + (int64_t)corel, fw), (int64_t)(corer - corel + 1)));
-						// ---- the DP problem (SwAligner::align + nextAlignment sequence)
-						{
-							DpWork& d = c->dp;
-							std::memset(&d.in, 0, sizeof(d.in));
-							d.in.read_off = 0; d.in.qual_off = 0; d.in.ref_off = 0;
-							d.in.refl = refl;
-							d.in.rdlen = (uint16_t)rdlen;
-							d.in.ncol = (uint16_t)ncol;
-							d.in.minsc = (int16_t)std::max<int64_t>(minsc, -254);
-							d.in.nceil = (int16_t)swNceil;
-							d.in.triml = (uint16_t)triml; d.in.corel = (uint16_t)corel; d.in.corer = (uint16_t)corer;
-							d.in.fw = fw ? 1 : 0;
-							d.fw = fw;
-							d.window.resize(ncol);
-							ref_.stretch((uint32_t)tidx, refl, ncol, d.window.data());
-						}
-						co_await Awaiter{c, REQ_DP};
-						{
-							DpWork& d = c->dp;
-							prm.nExDps++;
-							if(d.out.status == 0) {
-								prm.nExDpFails++; prm.nDpFail++;
-								if(prm.nDpFail >= P.streak) { ret = EXTEND_EXCEEDED_SOFT_LIMIT; goto extend_done; }
+			ExtendWalk walk(P, satpos, rand_ns, firstRow, c->resolve.out, nelt_, rdlen);
+			walk.bind(&rnd, &prm, &seenDiags);
+			for(;;) {
+				DpKey key;
+				ret = walk.next(minsc, key);
+				if(ret != ExtendWalk::PROBLEM) break;
+				auto hit = memo.find(key);
+				if(hit == memo.end()) {
+					// pose this problem and the ones the walk reaches next if each of them
+					// fails (a copy of the walk over copies of the state it advances)
+					c->dps.clear();
+					pose_dp(c->dps, ref_, key, rdlen, swNceil);
+					if(P.lookahead > 1) {
+						Rng rnd2 = rnd;
+						Prm prm2 = prm;
+						SeenDiags seen2 = seenDiags;
+						ExtendWalk ahead = walk;
+						ahead.bind(&rnd2, &prm2, &seen2);
+						while(c->dps.size() < P.lookahead && ahead.failed()) {
+							DpKey k2;
+							if(ahead.next(minsc, k2) != ExtendWalk::PROBLEM) break;
+							const auto m = memo.find(k2);
+							if(m != memo.end()) {
+								if(m->second.out.status != 0) break;    // a known success: stop guessing
 								continue;
 							}
-							prm.nExDpSuccs++;
-							if(prm.nDpFail > prm.nDpFailStreak) prm.nDpFailStreak = prm.nDpFail;
-							prm.nDpFail = 0;
-							for(uint32_t k = 0; k < d.out.nrec; k++) {        // while(!swa.done()) nextAlignment
-								const bt2x_aln_rec& rec = d.recs[k];
-								replay_backtrace_draws(rnd, rec.ntries);
-								// the call's writes to the read's edit buffer (bt2x.h)
-								if(edbuf.size() < rec.nbuf) edbuf.resize(rec.nbuf);
-								std::copy(d.edits.begin() + rec.edit_off, d.edits.begin() + rec.edit_off + rec.nbuf, edbuf.begin());
-								if(!rec.ok) break;
-								AlnRes res;
-								res.score = rec.score;
-								res.bases_aligned = rec.bases_aligned;
-								res.refid = tidx;
-								res.refoff = rec.refoff;
-								res.fw = fw;
-								res.rdlen = rdlen;
-								res.refns = rec.refns;
-								res.ned.assign(d.edits.begin() + rec.edit_off, d.edits.begin() + rec.edit_off + rec.nedit);
-								// (the alignment lies inside [0, tlen): the rectangle is trimmed to the reference)
-								if(redAnchor.overlap(res)) continue;
-								redAnchor.add(res);
-								if(sink.report(res)) { ret = EXTEND_POLICY_FULFILLED; goto extend_done; }
-								if(P.tighten > 0 && sink.hasSecondBest()) {
-									if(P.tighten == 1) {
-										if(sink.best >= minsc) {
-											minsc = sink.best;
-											if(minsc < perfectScore && sink.best == sink.best2) minsc++;
-										}
-									} else if(P.tighten == 2) {
-										if(sink.best2 >= minsc) { minsc = sink.best2; if(minsc < perfectScore) minsc++; }
-									} else {
-										const int64_t diff = sink.best - sink.best2;
-										const int64_t bot = sink.best2 + ((diff * 3) / 4);
-										if(bot >= minsc) { minsc = bot; if(minsc < perfectScore) minsc++; }
-									}
-								}
+							bool dup = false;
+							for(const DpWork& d : c->dps) dup = dup || d.key == k2;
+							if(!dup) pose_dp(c->dps, ref_, k2, rdlen, swNceil);
+						}
+					}
+					co_await Awaiter{c, REQ_DP};
+					for(DpWork& d : c->dps) memo.emplace(d.key, std::move(d.res));
+					c->dps.clear();
+					hit = memo.find(key);
+				}
+				c->ndp_used++;
+				const DpResult& d = hit->second;
+				if(d.out.status == 0) {
+					if(!walk.failed()) { ret = EXTEND_EXCEEDED_SOFT_LIMIT; break; }
+					continue;
+				}
+				prm.nExDps++;
+				prm.nExDpSuccs++;
+				if(prm.nDpFail > prm.nDpFailStreak) prm.nDpFailStreak = prm.nDpFail;
+				prm.nDpFail = 0;
+				bool fulfilled = false;
+				for(uint32_t k = 0; k < d.out.nrec; k++) {            // while(!swa.done()) nextAlignment
+					const bt2x_aln_rec& rec = d.recs[k];
+					replay_backtrace_draws(rnd, rec.ntries);
+					// the call's writes to the read's edit buffer (bt2x.h)
+					if(edbuf.size() < rec.nbuf) edbuf.resize(rec.nbuf);
+					std::copy(d.edits.begin() + rec.edit_off, d.edits.begin() + rec.edit_off + rec.nbuf, edbuf.begin());
+					if(!rec.ok) break;
+					AlnRes res;
+					res.score = rec.score;
+					res.bases_aligned = rec.bases_aligned;
+					res.refid = key.tidx;
+					res.refoff = rec.refoff;
+					res.fw = key.fw;
+					res.rdlen = rdlen;
+					res.refns = rec.refns;
+					res.ned.assign(d.edits.begin() + rec.edit_off, d.edits.begin() + rec.edit_off + rec.nedit);
+					// (the alignment lies inside [0, tlen): the rectangle is trimmed to the reference)
+					if(redAnchor.overlap(res)) continue;
+					redAnchor.add(res);
+					if(sink.report(res)) { fulfilled = true; break; }
+					if(P.tighten > 0 && sink.hasSecondBest()) {
+						if(P.tighten == 1) {
+							if(sink.best >= minsc) {
+								minsc = sink.best;
+								if(minsc < perfectScore && sink.best == sink.best2) minsc++;
 							}
+						} else if(P.tighten == 2) {
+							if(sink.best2 >= minsc) { minsc = sink.best2; if(minsc < perfectScore) minsc++; }
+						} else {
+							const int64_t diff = sink.best - sink.best2;
+							const int64_t bot = sink.best2 + ((diff * 3) / 4);
+							if(bot >= minsc) { minsc = bot; if(minsc < perfectScore) minsc++; }
 						}
 					}
 				}
+				if(fulfilled) { ret = EXTEND_POLICY_FULFILLED; break; }
 			}
 		}
-	extend_done:
 		if(ret == EXTEND_EXHAUSTED_CANDIDATES || ret == EXTEND_EXCEEDED_SOFT_LIMIT || ret == EXTEND_POLICY_FULFILLED) {
 			if(hits.numElts() / hits.nonzeroOffsets() < P.seedBoostThresh) break;   // averageHitsPerSeed
 			if(sink.done()) break;                                                  // doneWithMate
@@ -812,47 +891,60 @@ bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st, int threads) {
 	}
 	if(nwd) {
 		double t0 = now_s();
-		// one DP problem per waiting read: oriented read, qualities, reference window
-		std::vector<uint64_t> qb(nwd + 1, 0), fb(nwd + 1, 0);
+		// every waiting read's posed problems in one launch: the read's two orientations
+		// (codes and qualities) once per read, one reference window per problem
+		std::vector<uint64_t> qb(nwd + 1, 0), pb(nwd + 1, 0);
 		for(long i = 0; i < nwd; i++) {
-			qb[i + 1] = qb[i] + wd[i]->rd.length();
-			fb[i + 1] = fb[i] + wd[i]->dp.window.size();
+			qb[i + 1] = qb[i] + 2 * wd[i]->rd.length();
+			pb[i + 1] = pb[i] + wd[i]->dps.size();
 		}
-		std::vector<uint8_t> reads(qb[nwd]), quals(qb[nwd]), refs(fb[nwd]);
-		std::vector<bt2x_dp_in> in(nwd);
+		const uint64_t np = pb[nwd];
+		std::vector<uint64_t> fb(np + 1, 0);
+		for(long i = 0; i < nwd; i++)
+			for(size_t j = 0; j < wd[i]->dps.size(); j++)
+				fb[pb[i] + j + 1] = fb[pb[i] + j] + wd[i]->dps[j].window.size();
+		std::vector<uint8_t> reads(qb[nwd]), quals(qb[nwd]), refs(fb[np]);
+		std::vector<bt2x_dp_in> in(np);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nwd; i++) {
 			const ReadCtx* c = wd[i];
-			bt2x_dp_in p = c->dp.in;
-			p.read_off = qb[i];
-			p.qual_off = qb[i];
-			p.ref_off = fb[i];
-			const std::vector<uint8_t>& s = c->dp.fw ? c->rd.fw : c->rd.rc;
-			const std::string& q = c->dp.fw ? c->rd.qual : c->rd.qualRev;
-			std::copy(s.begin(), s.end(), reads.begin() + (long)qb[i]);
-			std::copy(q.begin(), q.end(), quals.begin() + (long)qb[i]);
-			std::copy(c->dp.window.begin(), c->dp.window.end(), refs.begin() + (long)fb[i]);
-			in[i] = p;
+			const size_t L = c->rd.length();
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), reads.begin() + (long)qb[i]);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), reads.begin() + (long)(qb[i] + L));
+			std::copy(c->rd.qual.begin(), c->rd.qual.end(), quals.begin() + (long)qb[i]);
+			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), quals.begin() + (long)(qb[i] + L));
+			for(size_t j = 0; j < c->dps.size(); j++) {
+				const DpWork& d = c->dps[j];
+				const uint64_t k = pb[i] + j;
+				bt2x_dp_in p = d.in;
+				p.read_off = p.qual_off = qb[i] + (d.key.fw ? 0 : L);
+				p.ref_off = fb[k];
+				std::copy(d.window.begin(), d.window.end(), refs.begin() + (long)fb[k]);
+				in[k] = p;
+			}
 		}
 		std::vector<bt2x_dp_out> out;
 		std::vector<bt2x_aln_rec> recs;
 		std::vector<uint32_t> edits;
 		be_.dp_align(reads, quals, refs, in, out, recs, edits);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
-		for(long k = 0; k < nwd; k++) {
-			DpWork& d = wd[k]->dp;
-			d.out = out[k];
-			d.recs.assign(recs.begin() + out[k].rec_off, recs.begin() + out[k].rec_off + out[k].nrec);
-			// gather each record's edit-buffer image (arena offsets are allocated by the
-			// kernel's atomics, so one problem's images are not contiguous)
-			d.edits.clear();
-			for(bt2x_aln_rec& r : d.recs) {
-				const uint32_t o = (uint32_t)d.edits.size();
-				d.edits.insert(d.edits.end(), edits.begin() + r.edit_off, edits.begin() + r.edit_off + r.nbuf);
-				r.edit_off = o;
+		for(long i = 0; i < nwd; i++) {
+			for(size_t j = 0; j < wd[i]->dps.size(); j++) {
+				const uint64_t k = pb[i] + j;
+				DpResult& r = wd[i]->dps[j].res;
+				r.out = out[k];
+				r.recs.assign(recs.begin() + out[k].rec_off, recs.begin() + out[k].rec_off + out[k].nrec);
+				// gather each record's edit-buffer image (arena offsets are allocated by the
+				// kernel's atomics, so one problem's images are not contiguous)
+				r.edits.clear();
+				for(bt2x_aln_rec& a : r.recs) {
+					const uint32_t o = (uint32_t)r.edits.size();
+					r.edits.insert(r.edits.end(), edits.begin() + a.edit_off, edits.begin() + a.edit_off + a.nbuf);
+					a.edit_off = o;
+				}
 			}
 		}
-		st.dp_launches++; st.dps += in.size(); st.t_dp += now_s() - t0;
+		st.dp_launches++; st.dps += np; st.t_dp += now_s() - t0;
 	}
 	// resume the reads whose requests were served
 	std::vector<ReadCtx*> run;
@@ -931,6 +1023,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			st.reads++;
 			if(c->aligned) st.aligned++; else st.unaligned++;
 			if(c->repetitive) st.rep++;
+			st.dps_used += c->ndp_used;
 			window[head].reset();
 			head++;
 		}
@@ -974,6 +1067,7 @@ std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threa
 			out += ctx[head]->sam;
 			st.reads++;
 			if(ctx[head]->aligned) st.aligned++; else st.unaligned++;
+			st.dps_used += ctx[head]->ndp_used;
 			ctx[head].reset();
 			head++;
 		}

@@ -44,6 +44,7 @@
 #include <limits>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -363,6 +364,8 @@ struct Params {
 	int tighten = 3;
 	uint32_t randSeed = 0;          // --seed
 	bool nofw = false, norc = false;
+	size_t lookahead = 8;           // DP problems posed per request (not a reference option;
+	                                // results do not depend on it)
 	Params() {
 		bt2x_scoring_default(&sc);
 		scoreMin.type = 2; scoreMin.C = (double)-0.6f; scoreMin.L = (double)-0.6f;       // L,-0.6,-0.6
@@ -404,6 +407,7 @@ inline int parse_align_option(Params& p, int argc, char** argv, int i) {
 	if(a == "--rdg") { pair(p.sc.rdg_const, p.sc.rdg_linear); return 2; }
 	if(a == "--rfg") { pair(p.sc.rfg_const, p.sc.rfg_linear); return 2; }
 	if(a == "--gbar") { p.sc.gapbar = std::atoi(argv[i + 1]); return 2; }
+	if(a == "--lookahead") { p.lookahead = (size_t)std::max(1L, std::atol(argv[i + 1])); return 2; }
 	return 0;
 }
 
@@ -528,13 +532,37 @@ struct ResolveWork {
 	std::vector<bt2x_resolve_in> in;
 	std::vector<bt2x_resolve_out> out;
 };
-struct DpWork {                     // one SwAligner problem and its nextAlignment records
-	bt2x_dp_in in;                  // read_off / qual_off / ref_off relative to this problem
+// A DP problem of one read is fixed by its rectangle and floor: the read, its
+// qualities and the N ceiling do not change within the read, and the kernel draws no
+// random numbers (it reports how many the reference's backtrace draws, bt2x.h).  So a
+// read's results can be memoised by this key and posed ahead of need (lookahead).
+struct DpKey {
+	int64_t tidx = 0, refl = 0, minsc = 0;
+	uint32_t ncol = 0, triml = 0, corel = 0, corer = 0;
 	bool fw = true;
-	std::vector<uint8_t> window;
+	bool operator==(const DpKey& o) const {
+		return tidx == o.tidx && refl == o.refl && minsc == o.minsc && ncol == o.ncol && triml == o.triml &&
+		       corel == o.corel && corer == o.corer && fw == o.fw;
+	}
+};
+struct DpKeyHash {
+	size_t operator()(const DpKey& k) const {
+		uint64_t z = (uint64_t)k.refl * 0x9e3779b97f4a7c15ULL ^ ((uint64_t)k.tidx << 32) ^ ((uint64_t)k.minsc << 16) ^
+		             ((uint64_t)k.ncol << 1) ^ (k.fw ? 1u : 0u) ^ ((uint64_t)k.triml << 40) ^ ((uint64_t)k.corel << 48);
+		z ^= z >> 29; z *= 0xbf58476d1ce4e5b9ULL; z ^= z >> 32;
+		return (size_t)z;
+	}
+};
+struct DpResult {                   // SwAligner::align + its nextAlignment sequence
 	bt2x_dp_out out;
-	std::vector<bt2x_aln_rec> recs;
-	std::vector<uint32_t> edits;
+	std::vector<bt2x_aln_rec> recs; // edit_off relative to `edits`
+	std::vector<uint32_t> edits;    // each record's edit-buffer image (nbuf entries)
+};
+struct DpWork {                     // one posed problem
+	DpKey key;
+	bt2x_dp_in in;                  // read_off / qual_off / ref_off are set by the scheduler
+	std::vector<uint8_t> window;
+	DpResult res;
 };
 
 enum ReqKind { REQ_NONE = 0, REQ_SEED = 1, REQ_RESOLVE = 2, REQ_DP = 3 };
@@ -571,11 +599,12 @@ struct ReadCtx {
 	int req = REQ_NONE;
 	SeedWork seed;
 	ResolveWork resolve;
-	DpWork dp;
+	std::vector<DpWork> dps;        // the problems posed by the current DP request
 	std::string sam;                // the finished record(s)
 	ReadTask task;
 	// statistics for the run summary
 	bool aligned = false, repetitive = false;
+	uint64_t ndp_used = 0;          // DP results the walk consumed (the rest were lookahead)
 };
 
 inline void Awaiter::await_suspend(std::coroutine_handle<>) noexcept { c->req = kind; }
@@ -600,7 +629,7 @@ public:
 struct RunStats {
 	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0;
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
-	uint64_t seeds = 0, resolves = 0, dps = 0;
+	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0;
 	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0;
 };
 

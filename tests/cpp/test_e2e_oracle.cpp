@@ -116,9 +116,9 @@ int main(int argc, char** argv) {
 		const RunStats st = al.run(fq, stdout, slots, threads);
 		const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 		std::fprintf(stderr, "HOST_TIMING reads=%llu wall=%.3f t_host=%.3f t_io=%.3f t_seed=%.3f t_resolve=%.3f t_dp=%.3f "
-		             "launches=%llu/%llu/%llu\n", (unsigned long long)st.reads, t, st.t_host, st.t_io, st.t_seed,
+		             "launches=%llu/%llu/%llu dps=%llu dps_used=%llu\n", (unsigned long long)st.reads, t, st.t_host, st.t_io, st.t_seed,
 		             st.t_resolve, st.t_dp, (unsigned long long)st.seed_launches,
-		             (unsigned long long)st.resolve_launches, (unsigned long long)st.dp_launches);
+		             (unsigned long long)st.resolve_launches, (unsigned long long)st.dp_launches, (unsigned long long)st.dps, (unsigned long long)st.dps_used);
 		return 0;
 	}
 	Aligner al(p, ref, be);

@@ -92,3 +92,16 @@ def test_host_driver_slot_count_invariance(fixtures):
 def test_bt2x_align_vs_reference_sam(fixtures, name, idx, fq, opts):
     """The product binary (kernels on the MI355X) == the reference's SAM."""
     check([ALIGN, "-x", fixtures[idx], "-U", fixtures[fq], "--slots", "1000"] + opts, name)
+
+
+def test_host_driver_lookahead_invariance(fixtures):
+    """DP lookahead (problems posed ahead of need and memoised by DpKey) changes the
+    number of launches, never the records."""
+    outs = []
+    for la in ("1", "8", "64"):
+        r = subprocess.run([ORACLE_DRIVER, fixtures["rep"], fixtures["rep_reads.fq"], "--slots", "3000", "-p", "3",
+                            "--dpad", "12", "--lookahead", la], capture_output=True, timeout=600, check=True)
+        outs.append(sam_records(r.stdout))
+    assert outs[0] == outs[1] == outs[2]
+    with lzma.open(os.path.join(g.GOLDEN, "e2e_rep_dpad12.sam.xz"), "rb") as f:
+        assert outs[0] == sam_records(f.read())
