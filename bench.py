@@ -61,13 +61,14 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
                     help="OpenMP threads of the reference CPU baseline (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lookahead", type=int, default=8, help="bt2x-align --lookahead (DP problems posed per request)")
     ap.add_argument("--rss-limit-gb", type=float, default=120.0, help="kill bt2x-align above this host RSS")
     return ap.parse_args()
 
 
 def workload_key(args) -> str:
     g = f"synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}" if args.genome == "synthetic" else args.genome
-    return f"e2e|{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}"
+    return f"e2e|{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}|la{args.lookahead}"
 
 
 def pmc_traffic(args, kernel: str):
@@ -160,7 +161,7 @@ def write_fastq(path, reads, quals, first_id=0):
 
 def run_aligner(args, base, fq, sam, gpu, dump=None):
     cmd = [ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad), "--device", str(gpu),
-           "-p", str(args.host_threads), "--slots", str(args.reads), "--stats"]
+           "-p", str(args.host_threads), "--slots", str(args.reads), "--lookahead", str(args.lookahead), "--stats"]
     if dump:
         cmd += ["--dump", dump]
     t0 = time.perf_counter()
@@ -200,7 +201,7 @@ def load_dumps(ddir):
     out = []
     for path in sorted(glob.glob(os.path.join(ddir, "*.*"))):
         kind = path.rsplit(".", 1)[1]
-        nparts = {"seed": 2, "resolve": 1, "dp": 4}[kind]
+        nparts = {"seed": 2, "resolve": 1, "dp": 5}[kind]
         raw = np.fromfile(path, dtype=np.uint8)
         sizes = raw[:8 * nparts].view(np.uint64).astype(np.int64)
         parts, o = [], 8 * nparts
@@ -212,6 +213,7 @@ def load_dumps(ddir):
             parts[0] = parts[0].view(abi.RESOLVE_IN)
         else:
             parts[3] = parts[3].view(abi.DP_IN)
+            parts[4] = parts[4].view(np.uint64)
         out.append((kind, parts))
     return out
 
@@ -325,7 +327,7 @@ def main():
                                    torch.empty(m * abi.RESOLVE_OUT.itemsize, dtype=torch.uint8, device=dev)]))
         else:
             m = len(parts[3])
-            rec_cap, edit_cap = 4 * m + 1024, 96 * m + 4096
+            rec_cap, edit_cap = int(parts[4][0]) + 1024, int(parts[4][1]) + 4096   # sizes the aligner saw
             plan.append((kind, m, [to_dev(parts[0]), to_dev(parts[1]), to_dev(parts[2]), to_dev(parts[3]),
                                    torch.empty(m * abi.DP_OUT.itemsize, dtype=torch.uint8, device=dev),
                                    torch.empty(rec_cap * abi.ALN_REC.itemsize, dtype=torch.uint8, device=dev),

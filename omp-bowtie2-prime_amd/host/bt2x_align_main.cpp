@@ -77,9 +77,10 @@ public:
 	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
 	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
 	              std::vector<uint32_t>& edits) override {
-		write("dp", {{reads.data(), reads.size()}, {quals.data(), quals.size()}, {refs.data(), refs.size()},
-		             {in.data(), in.size() * sizeof(bt2x_dp_in)}});
 		in_.dp_align(reads, quals, refs, in, out, recs, edits);
+		const uint64_t used[2] = {recs.size(), edits.size()};      // arena sizes the replay needs
+		write("dp", {{reads.data(), reads.size()}, {quals.data(), quals.size()}, {refs.data(), refs.size()},
+		             {in.data(), in.size() * sizeof(bt2x_dp_in)}, {used, sizeof used}});
 	}
 private:
 	void write(const char* kind, std::initializer_list<std::pair<const void*, size_t>> parts) {

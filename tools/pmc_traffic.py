@@ -20,7 +20,8 @@ import shutil
 from collections import defaultdict
 
 # logical op -> the kernels one call launches (per-launch figures are summed over them)
-KERNELS = {"seed": ("seed_init_kernel", "seed_kernel"), "dp": ("dp_fill_kernel", "dp_walk_kernel", "dp_kernel")}
+KERNELS = {"seed": ("seed_init_kernel", "seed_kernel"), "resolve": ("sa_resolve_kernel",),
+           "dp": ("dp_fill_kernel", "dp_walk_kernel", "dp_kernel")}
 
 
 def short(name: str) -> str | None:
@@ -43,6 +44,9 @@ def main() -> None:
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--workload", required=True, help="bench.py workload key of the profiled run")
     ap.add_argument("--cmd", default="python3 bench.py --steps 5 --warmup 2 --no-cpu")
+    ap.add_argument("--replays", type=int, default=0,
+                    help="bench steps in the profiled run (warmup + steps): traffic is then reported per step "
+                         "(all launches of the op in one replay), as bench.py times it")
     a = ap.parse_args()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.path.join(root, "profiles")
@@ -90,11 +94,16 @@ def main() -> None:
         w = ctr[k].get("WRITE_SIZE", {})
         if not f or not w:
             continue
-        fetch = per_call(f) * 1024 * 2
-        write = per_call(w) * 1024
+        if a.replays:           # per step: every dispatch of the op over the replays
+            fetch = sum(sum(v) for v in f.values()) * 1024 * 2 / a.replays
+            write = sum(sum(v) for v in w.values()) * 1024 / a.replays
+        else:
+            fetch = per_call(f) * 1024 * 2
+            write = per_call(w) * 1024
         res["kernels"][k] = {"fetch_bytes": round(fetch), "write_bytes": round(write),
                              "traffic_bytes": round(fetch + write),
                              "kernels": sorted(set(f) | set(w)),
+                             "per": "step" if a.replays else "launch",
                              "avg_duration_ms": round(per_call(dur[k]) / 1e6, 4) if dur.get(k) else None,
                              "per_kernel_ms": {n: round(sum(v) / len(v) / 1e6, 4) for n, v in dur[k].items()}}
     with open(os.path.join(out, f"{a.tag}_traffic.json"), "w") as g:
