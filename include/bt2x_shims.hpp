@@ -234,6 +234,10 @@ struct AlnView {
 	int64_t refoff = 0;
 	bool fw = true;
 	std::vector<uint32_t> edits;   // packed, BT2X_EDIT_* accessors, final ned() order
+	// The call's writes to the read's edit buffer (bt2x.h "edit-buffer image"),
+	// set by every nextAlignment() call, also one that returns false.  A caller that needs
+	// the reference's printed CIGAR/MD copies it into its SwResult's ned() storage.
+	std::vector<uint32_t> image;
 };
 
 class SwBatch {
@@ -350,6 +354,7 @@ public:
 		if(o.status == 0 || k >= o.nrec) return false;
 		const bt2x_aln_rec& r = recs_[o.rec_off + k++];
 		replay_backtrace_draws(rnd, r.ntries);
+		res.image.assign(edits_.begin() + r.edit_off, edits_.begin() + r.edit_off + r.nbuf);
 		if(!r.ok) { cursor_[(size_t)prob] = o.nrec; return false; }
 		res.score = r.score; res.ns = r.ns; res.gaps = r.gaps; res.bases_aligned = r.bases_aligned;
 		res.refns = r.refns; res.refoff = r.refoff; res.fw = in_[(size_t)prob].fw != 0;
