@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
                     help="OpenMP threads of the reference CPU baseline (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--lookahead", type=int, default=8, help="bt2x-align --lookahead (DP problems posed per request)")
+    ap.add_argument("--lookahead", type=int, default=16, help="bt2x-align --lookahead (DP problems posed per request)")
     ap.add_argument("--rss-limit-gb", type=float, default=120.0, help="kill bt2x-align above this host RSS")
     return ap.parse_args()
 

@@ -645,6 +645,9 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		// ---------------------------------------------- prioritizeSATups (:61-260)
 		std::vector<SatPos> satpos2, satpos;
 		std::vector<uint32_t> rand_ns;
+		satpos2.reserve(hits.nonzeroOffsets());
+		satpos.reserve(std::min<size_t>(P.mxIter, 64));
+		rand_ns.reserve(std::min<size_t>(P.mxIter, 64));
 		size_t nrange = 0, nelt = 0, nsmall = 0, nsmall_elts = 0;
 		const size_t nsm = 5, maxelt = P.mxIter;
 		for(size_t r = 0; r < hits.nonzeroOffsets(); r++) {

@@ -276,29 +276,38 @@ public:
 	void add(const AlnRes& r) { walk(r, true); }
 	bool overlap(const AlnRes& r) { return n_ != 0 && walk(r, false); }
 private:
-	struct Cell { int64_t rfid = -1; int64_t rfoff = 0; uint32_t row = 0; bool fw = false; };
-	static uint64_t hash(int64_t rfid, bool fw, int64_t rfoff, uint32_t row) {
-		uint64_t z = (uint64_t)rfoff * 0x9e3779b97f4a7c15ULL ^ ((uint64_t)rfid << 20) ^ ((uint64_t)row << 1) ^ (fw ? 1u : 0u);
+	// one cell in 16 bytes: reference offset, and (ref id, row, strand) packed; kEmpty marks a
+	// free slot (ref ids < 2^40, rows < 2^11)
+	struct Cell { int64_t rfoff = 0; uint64_t tag = kEmpty; };
+	static constexpr uint64_t kEmpty = ~0ULL;
+	static uint64_t tag_of(int64_t rfid, bool fw, uint32_t row) {
+		return ((uint64_t)rfid << 12) | ((uint64_t)row << 1) | (fw ? 1u : 0u);
+	}
+	static uint64_t hash(int64_t rfoff, uint64_t tag) {
+		uint64_t z = (uint64_t)rfoff * 0x9e3779b97f4a7c15ULL ^ tag;
 		z ^= z >> 29; z *= 0xbf58476d1ce4e5b9ULL; z ^= z >> 32;
 		return z;
 	}
 	bool find_or_insert(int64_t rfid, bool fw, int64_t rfoff, uint32_t row, bool insert) {
-		if(slots_.empty()) { if(!insert) return false; slots_.resize(512); }
+		return probe(rfoff, tag_of(rfid, fw, row), insert);
+	}
+	bool probe(int64_t rfoff, uint64_t tag, bool insert) {
+		if(slots_.empty()) { if(!insert) return false; slots_.resize(256); }
 		else if(insert && (n_ + 1) * 2 > slots_.size()) {
 			std::vector<Cell> old;
 			old.swap(slots_);
 			slots_.resize(old.size() * 2);
 			n_ = 0;
-			for(const Cell& c : old) if(c.rfid >= 0) find_or_insert(c.rfid, c.fw, c.rfoff, c.row, true);
+			for(const Cell& c : old) if(c.tag != kEmpty) probe(c.rfoff, c.tag, true);
 		}
 		const size_t mask = slots_.size() - 1;
-		for(size_t h = hash(rfid, fw, rfoff, row) & mask;; h = (h + 1) & mask) {
+		for(size_t h = hash(rfoff, tag) & mask;; h = (h + 1) & mask) {
 			Cell& c = slots_[h];
-			if(c.rfid < 0) {
-				if(insert) { c.rfid = rfid; c.fw = fw; c.rfoff = rfoff; c.row = row; n_++; }
+			if(c.tag == kEmpty) {
+				if(insert) { c.rfoff = rfoff; c.tag = tag; n_++; }
 				return false;
 			}
-			if(c.rfid == rfid && c.fw == fw && c.rfoff == rfoff && c.row == row) return true;
+			if(c.tag == tag && c.rfoff == rfoff) return true;
 		}
 	}
 	bool walk(const AlnRes& r, bool insert) {
@@ -364,7 +373,7 @@ struct Params {
 	int tighten = 3;
 	uint32_t randSeed = 0;          // --seed
 	bool nofw = false, norc = false;
-	size_t lookahead = 8;           // DP problems posed per request (not a reference option;
+	size_t lookahead = 16;          // DP problems posed per request (not a reference option;
 	                                // results do not depend on it)
 	Params() {
 		bt2x_scoring_default(&sc);
