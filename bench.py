@@ -410,9 +410,15 @@ def main():
                                f"problems), replayed from HBM",
                    "reads_per_gpu_step": n, "read_len": R, "parallelism": f"dp{world} (read shards)",
                    "key": workload_key(args)},
+        # achieved = algorithmic bytes per launch / average launch time (= per-step bytes / per-step
+        # kernel time); traffic (PMC, committed per step) is reported per launch to match.
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes": kern[dom][1], "launches_per_step": nl[dom], "traffic_src": traffic_src},
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": None if traffic is None else int(traffic / max(nl[dom], 1)),
+                     "alg_bytes": int(kern[dom][1] / max(nl[dom], 1)),
+                     "avg_launch_ms": round(kern[dom][0] / max(nl[dom], 1), 4), "per": "launch",
+                     "alg_bytes_per_step": kern[dom][1], "traffic_per_step": traffic,
+                     "launches_per_step": nl[dom], "traffic_src": traffic_src},
         "kernels": {"seed_ms": round(kms["seed"], 3), "resolve_ms": round(kms["resolve"], 3),
                     "dp_ms": round(kms["dp"], 3), "seed_alg_bytes": fm_bytes, "resolve_alg_bytes": res_bytes,
                     "dp_alg_bytes": dp_bytes, "launches": nl, "units": units,
