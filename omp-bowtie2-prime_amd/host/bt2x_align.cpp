@@ -769,8 +769,16 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 				if(prm.nDpFail > prm.nDpFailStreak) prm.nDpFailStreak = prm.nDpFail;
 				prm.nDpFail = 0;
 				bool fulfilled = false;
+				const int64_t minsc_posed = minsc;
 				for(uint32_t k = 0; k < d.out.nrec; k++) {            // while(!swa.done()) nextAlignment
 					const bt2x_aln_rec& rec = d.recs[k];
+					// -M tightening below raises minsc between the calls of this problem, but the
+					// record sequence needs no re-filtering: nextAlignment's score filter compares
+					// the candidate's raw u8 cell value (DpBtCandidate::score = lr in 0..255,
+					// aligner_swsse_ee_u8.cpp:519) with minsc <= 0 (aligner_sw.cpp:274), so it
+					// never fires and the calls proceed exactly as posed (tests/test_e2e.py,
+					// tandem-repeat fixture).
+					if(minsc != minsc_posed) c->ntight++;
 					replay_backtrace_draws(rnd, rec.ntries);
 					// the call's writes to the read's edit buffer (bt2x.h)
 					if(edbuf.size() < rec.nbuf) edbuf.resize(rec.nbuf);
@@ -1027,6 +1035,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			if(c->aligned) st.aligned++; else st.unaligned++;
 			if(c->repetitive) st.rep++;
 			st.dps_used += c->ndp_used;
+			st.tight_recs += c->ntight;
 			window[head].reset();
 			head++;
 		}
@@ -1071,6 +1080,7 @@ std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threa
 			st.reads++;
 			if(ctx[head]->aligned) st.aligned++; else st.unaligned++;
 			st.dps_used += ctx[head]->ndp_used;
+			st.tight_recs += ctx[head]->ntight;
 			ctx[head].reset();
 			head++;
 		}

@@ -614,6 +614,8 @@ struct ReadCtx {
 	// statistics for the run summary
 	bool aligned = false, repetitive = false;
 	uint64_t ndp_used = 0;          // DP results the walk consumed (the rest were lookahead)
+	uint64_t ntight = 0;            // nextAlignment records consumed after -M tightened minsc
+	                                // within the same DP problem
 };
 
 inline void Awaiter::await_suspend(std::coroutine_handle<>) noexcept { c->req = kind; }
@@ -638,7 +640,7 @@ public:
 struct RunStats {
 	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0;
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
-	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0;
+	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
 	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0;
 };
 

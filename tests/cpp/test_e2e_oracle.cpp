@@ -124,8 +124,10 @@ int main(int argc, char** argv) {
 	Aligner al(p, ref, be);
 	FastqReader fq(argv[2]);
 	const RunStats st = al.run(fq, stdout, slots, threads);
-	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu\n",
+	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu "
+	             "tight_recs=%llu\n",
 	             (unsigned long long)st.reads, (unsigned long long)st.aligned, (unsigned long long)st.seed_launches,
-	             (unsigned long long)st.resolve_launches, (unsigned long long)st.dp_launches, (unsigned long long)st.dps);
+	             (unsigned long long)st.resolve_launches, (unsigned long long)st.dp_launches, (unsigned long long)st.dps,
+	             (unsigned long long)st.tight_recs);
 	return 0;
 }

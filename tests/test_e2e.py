@@ -31,7 +31,9 @@ ALT_OPTS = ["--mp", "5,1", "--np", "2", "--rdg", "4,2", "--rfg", "6,3", "--gbar"
 SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
         ("e2e_rep", "rep", "rep_reads.fq", []),
         ("e2e_rep_dpad12", "rep", "rep_reads.fq", ["--dpad", "12"]),
-        ("e2e_rep_alt", "rep", "rep_reads.fq", ALT_OPTS)]
+        ("e2e_rep_alt", "rep", "rep_reads.fq", ALT_OPTS),
+        ("e2e_tandem", "tandem", "tandem_reads.fq", []),
+        ("e2e_tandem_dpad12", "tandem", "tandem_reads.fq", ["--dpad", "12"])]
 
 
 def sam_records(data: bytes) -> list[bytes]:
@@ -64,17 +66,22 @@ def check(cmd: list[str], golden: str):
     assert len(got) == len(exp) and not bad, \
         f"{len(bad)} of {len(exp)} records differ; first:\n ours {bad[0][0][:300]!r}\n ref  {bad[0][1][:300]!r}" \
         if bad else f"{len(got)} records vs {len(exp)}"
-    return got
+    return got, r.stderr
 
 
 @pytest.mark.parametrize("name,idx,fq,opts", SETS, ids=[s[0] for s in SETS])
 def test_host_driver_vs_reference_sam(fixtures, name, idx, fq, opts):
     """Host driver + CPU oracle kernels == the reference's SAM (no GPU)."""
     assert os.access(ORACLE_DRIVER, os.X_OK), "build first: make -C tests/cpp"
-    got = check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4"] + opts, name)
+    got, err = check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4"] + opts, name)
     n_al = sum(1 for ln in got if not ln.startswith(b"@") and ln.split(b"\t")[1] != b"4")
     # (150 bp reads need --dpad <= 12 to fit ALN_MAX_COLS: SURVEY F2)
-    assert n_al > (400 if idx == "lambda_virus" else 2000)
+    assert n_al > {"lambda_virus": 400, "rep": 2000, "tandem": 1400}[idx]
+    if idx == "tandem":
+        # the fixture's point: -M tightens minsc between nextAlignment calls of one DP
+        # problem (records consumed after a tightening in the same problem)
+        tight = int(err.split(b"tight_recs=")[1].split()[0])
+        assert tight > 100, tight
 
 
 def test_host_driver_slot_count_invariance(fixtures):

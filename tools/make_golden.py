@@ -113,8 +113,42 @@ def e2e_goldens(tmp: str) -> None:
             fo.write(sam_records(sam))
 
 
+TANDEM_SETS = [("e2e_tandem", []), ("e2e_tandem_dpad12", ["--dpad", "12"])]
+
+
+def tandem_goldens(tmp: str) -> None:
+    """Tandem-repeat fixture: reads whose DP windows hold several alignments, so -M's
+    score tightening (aligner_sw_driver.cpp:589-619) happens between nextAlignment calls
+    of one DP problem.  Index by the reference builder, SAM by the reference aligner."""
+    g, arrays = sd.gen_tandem_genome(nchrom=4, chrom_len=40000, arrays_per_chrom=12, seed=21)
+    fa = os.path.join(tmp, "tandem.fa")
+    sd.write_fasta(fa, g)
+    base = os.path.join(tmp, "tandem")
+    run([BUILD, fa, base], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    for k in "1234":
+        xz_copy(f"{base}.{k}.bt2l", os.path.join(GOLD, f"tandem.{k}.bt2l.xz"))
+    reads = (sd.sim_reads_in(g, arrays, 1200, 100, seed=31) + sd.sim_reads_in(g, arrays, 800, 150, seed=32)
+             + sd.sim_reads_in(g, arrays, 300, 60, seed=33, sub_rate=0.03))
+    rfq = os.path.join(tmp, "tandem_reads.fq")
+    sd.write_fastq(rfq, reads)
+    xz_copy(rfq, os.path.join(GOLD, "tandem_reads.fq.xz"))
+    for name, opts in TANDEM_SETS:
+        sam = os.path.join(tmp, name + ".sam")
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        run([ALIGN, "-x", base, "-U", rfq, "-S", sam] + opts, env=env, stderr=subprocess.DEVNULL)
+        with lzma.open(os.path.join(GOLD, name + ".sam.xz"), "wb", preset=9 | lzma.PRESET_EXTREME) as fo:
+            fo.write(sam_records(sam))
+
+
 def main() -> None:
     run(["make", "-C", os.path.join(ROOT, "oracle"), "ref", "oracle"])
+    if sys.argv[1:] == ["tandem"]:
+        tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
+        try:
+            tandem_goldens(tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     if sys.argv[1:] == ["e2e"]:
         tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
         try:

@@ -60,6 +60,50 @@ def gen_genome(total_len: int, nchrom: int = 1, seed: int = 0, repeat_frac: floa
     return out
 
 
+def gen_tandem_genome(nchrom: int = 4, chrom_len: int = 40000, arrays_per_chrom: int = 12,
+                      seed: int = 0, div: float = 0.02):
+    """Random chromosomes carrying tandem-repeat arrays (unit 2-40 bp, 200-1500 bp long,
+    ~div divergence per base).  A read from an array aligns at several unit shifts inside
+    one DP window, so one DP problem yields several alignments and the -M score
+    tightening (aligner_sw_driver.cpp:589-619) acts between nextAlignment calls of the
+    same problem.  Returns (chroms, arrays) with arrays = [(chrom index, start, end)]."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    chroms, arrays = [], []
+    for c in range(nchrom):
+        s = rng.integers(0, 4, size=chrom_len, dtype=np.uint8)
+        slot = chrom_len // arrays_per_chrom
+        for a in range(arrays_per_chrom):
+            u = int(rng.integers(2, 41))
+            ln = int(rng.integers(200, min(1500, slot - 100)))
+            p = a * slot + int(rng.integers(0, slot - ln))
+            unit = rng.integers(0, 4, size=u, dtype=np.uint8)
+            arr = np.resize(unit, ln)
+            mut = rng.random(ln) < div
+            arr[mut] = rng.integers(0, 4, size=int(mut.sum()), dtype=np.uint8)
+            s[p:p + ln] = arr
+            arrays.append((c, p, p + ln))
+        chroms.append((f"tr{c + 1}", ACGT[s].tobytes()))
+    return chroms, arrays
+
+
+def sim_reads_in(chroms, arrays, n: int, rdlen: int, seed: int, **kw):
+    """sim_reads with origins drawn from the given (chrom, start, end) intervals (a read
+    may run past an interval's end by up to half its length)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    for i in range(n):
+        c, a, b = arrays[int(rng.integers(0, len(arrays)))]
+        ref = chroms[c][1]
+        lo = max(0, a - rdlen // 4)
+        hi = max(lo + 1, min(len(ref) - rdlen - 2, b - rdlen // 2))
+        p = int(rng.integers(lo, hi))
+        sub = [(chroms[c][0], ref[p:p + rdlen + 2])]
+        name, seq, q = sim_reads(sub, 1, rdlen, seed=int(rng.integers(0, 2**31)), **kw)[0]
+        fields = name.split(":")
+        out.append((f"t{i}:{c}:{p + int(fields[2])}:{fields[3]}", seq, q))
+    return out
+
+
 def write_fasta(path: str, chroms: list[tuple[str, bytes]], width: int = 60) -> None:
     with open(path, "wb") as f:
         for name, seq in chroms:
