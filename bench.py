@@ -62,6 +62,7 @@ def parse():
                     help="OpenMP threads of the reference CPU baseline (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--lookahead", type=int, default=16, help="bt2x-align --lookahead (DP problems posed per request)")
+    ap.add_argument("--slots", type=int, default=1 << 18, help="bt2x-align --slots (reads in flight)")
     ap.add_argument("--rss-limit-gb", type=float, default=120.0, help="kill bt2x-align above this host RSS")
     return ap.parse_args()
 
@@ -161,7 +162,7 @@ def write_fastq(path, reads, quals, first_id=0):
 
 def run_aligner(args, base, fq, sam, gpu, dump=None):
     cmd = [ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad), "--device", str(gpu),
-           "-p", str(args.host_threads), "--slots", str(args.reads), "--lookahead", str(args.lookahead), "--stats"]
+           "-p", str(args.host_threads), "--slots", str(args.slots), "--lookahead", str(args.lookahead), "--stats"]
     if dump:
         cmd += ["--dump", dump]
     t0 = time.perf_counter()

@@ -6,9 +6,13 @@
 #include "bt2x_align.hpp"
 
 #include <cctype>
+#include <charconv>
 #include <chrono>
-#include <map>
+#include <condition_variable>
+#include <deque>
 #include <memory>
+#include <mutex>
+#include <thread>
 
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -17,6 +21,37 @@
 
 #ifdef _OPENMP
 #include <omp.h>
+#endif
+
+#ifdef BT2X_PHASE_PROF
+// Development-only phase profiler of the per-read coroutine (-DBT2X_PHASE_PROF): TSC
+// cycles per phase summed over threads, printed at the end of run().
+#include <mutex>
+#include <x86intrin.h>
+namespace {
+constexpr int kPhases = 10;
+const char* kPhaseName[kPhases] = {"init", "seeds", "rank", "prioritize", "resolve_in", "walk", "lookahead",
+                                   "records", "finish", "scatter"};
+struct PhaseAcc { uint64_t c[kPhases] = {}; uint64_t last = 0; PhaseAcc(); };
+std::mutex g_ph_mu;
+std::vector<PhaseAcc*> g_ph_all;
+PhaseAcc::PhaseAcc() { std::lock_guard<std::mutex> g(g_ph_mu); g_ph_all.push_back(this); }
+thread_local PhaseAcc t_ph;
+inline void ph_start() { t_ph.last = __rdtsc(); }
+inline void ph(int k) { const uint64_t n = __rdtsc(); t_ph.c[k] += n - t_ph.last; t_ph.last = n; }
+void ph_print() {
+	uint64_t tot[kPhases] = {}, all = 0;
+	for(PhaseAcc* a : g_ph_all) for(int k = 0; k < kPhases; k++) tot[k] += a->c[k];
+	for(int k = 0; k < kPhases; k++) all += tot[k];
+	for(int k = 0; k < kPhases; k++)
+		std::fprintf(stderr, "PHASE %-11s %7.3f Gcyc %5.1f%%\n", kPhaseName[k], tot[k] / 1e9, 100.0 * tot[k] / (all ? all : 1));
+}
+}
+#define PH_START() ph_start()
+#define PH(k) ph(k)
+#else
+#define PH_START() ((void)0)
+#define PH(k) ((void)0)
 #endif
 
 namespace bt2x {
@@ -89,6 +124,18 @@ void RefInfo::init(const bt2x_index_desc& d, const std::string& base) {
 	names_.resize(d.npat);
 }
 
+namespace {
+// byte of the packed text (4 bases, LSB first) -> its 4 codes as bytes
+struct Unpack4 {
+	uint32_t t[256];
+	Unpack4() {
+		for(uint32_t b = 0; b < 256; b++)
+			t[b] = (b & 3) | (((b >> 2) & 3) << 8) | (((b >> 4) & 3) << 16) | (((b >> 6) & 3) << 24);
+	}
+};
+const Unpack4 kUnpack4;
+}
+
 void RefInfo::stretch(uint32_t tidx, int64_t off, size_t n, uint8_t* out) const {
 	std::memset(out, 4, n);
 	const std::vector<Frag>& fs = frags_[tidx];
@@ -100,10 +147,14 @@ void RefInfo::stretch(uint32_t tidx, int64_t off, size_t n, uint8_t* out) const 
 		const Frag& fr = fs[k];
 		const int64_t a = std::max<int64_t>(off, fr.toff);
 		const int64_t b = std::min<int64_t>(off + (int64_t)n, fr.toff + (int64_t)fr.len);
-		for(int64_t p = a; p < b; p++) {
-			const uint64_t j = fr.joff + (uint64_t)(p - fr.toff);
-			out[p - off] = (text_[j >> 2] >> ((j & 3) << 1)) & 3;
-		}
+		if(a >= b) continue;
+		uint8_t* o = out + (a - off);
+		uint64_t j = fr.joff + (uint64_t)(a - fr.toff);
+		size_t m = (size_t)(b - a);
+		while(m && (j & 3)) { *o++ = (text_[j >> 2] >> ((j & 3) << 1)) & 3; j++; m--; }
+		const uint8_t* t = text_ + (j >> 2);
+		for(; m >= 4; m -= 4, o += 4, j += 4) std::memcpy(o, &kUnpack4.t[*t++], 4);
+		while(m) { *o++ = (text_[j >> 2] >> ((j & 3) << 1)) & 3; j++; m--; }
 	}
 }
 
@@ -111,48 +162,32 @@ void RefInfo::stretch(uint32_t tidx, int64_t off, size_t n, uint8_t* out) const 
 
 namespace {
 
-enum { EXIT_DID_NOT_EXIT = 1, EXIT_SHORT_CIRCUIT_k, EXIT_SHORT_CIRCUIT_M, EXIT_SHORT_CIRCUIT_TRUMPED,
-       EXIT_NO_ALIGNMENTS, EXIT_WITH_ALIGNMENTS };
-
 enum { EXTEND_EXHAUSTED_CANDIDATES = 1, EXTEND_POLICY_FULFILLED, EXTEND_PERFECT_SCORE,
        EXTEND_EXCEEDED_SOFT_LIMIT, EXTEND_EXCEEDED_HARD_LIMIT };
 
-constexpr int64_t kMinScore = std::numeric_limits<int64_t>::min();
+template<class T> inline void append_int(std::string& o, T v) {
+	char b[24];
+	const auto r = std::to_chars(b, b + sizeof b, v);
+	o.append(b, (size_t)(r.ptr - b));
+}
 
-// AlnSinkWrap for an unpaired read (aln_sink.cpp:583-643, 1395-1445) with its
-// ReportingState (aln_sink.cpp:33-210) under -k 1 -M mhits.
-struct Sink {
-	int64_t mhits = 50;
-	std::vector<AlnRes> rs;
-	int64_t best = kMinScore, best2 = kMinScore;
-	uint64_t n = 0;
-	bool doneUnpair = false;
-	int exitUnpair = EXIT_DID_NOT_EXIT;
-	bool done() const { return doneUnpair; }            // doneConcord_/doneDiscord_ are true
-	bool report(const AlnRes& r) {
-		n++;
-		if(!doneUnpair && n > (uint64_t)mhits) { doneUnpair = true; exitUnpair = EXIT_SHORT_CIRCUIT_M; }
-		rs.push_back(r);
-		if(r.score > best) { best2 = best; best = r.score; }
-		else if(r.score > best2) best2 = r.score;
-		return done();
-	}
-	bool hasSecondBest() const { return best2 != kMinScore; }
-};
-
-// StackedAln (aligner_result.cpp:448-770) over the Watson-strand read.
-std::string cigar_md(const Read& rd, const AlnRes& r, std::string& md) {
-	const std::vector<uint8_t>& s = r.fw ? rd.fw : rd.rc;
-	const std::vector<uint32_t> ed = r.fw ? r.ned : invert_poss(r.ned, rd.length());
-	std::vector<char> ref, rel, rdc;
-	ref.reserve(s.size() + 16); rel.reserve(s.size() + 16); rdc.reserve(s.size() + 16);
+// StackedAln (aligner_result.cpp:448-770) over the Watson-strand read: CIGAR appended to
+// `cig`, MD:Z value to `md`.  ned: the printed edits (ned() order, 5'-relative for rc).
+void cigar_md(const Read& rd, bool fw, const uint32_t* ned0, size_t nedn, std::string& cig, std::string& md) {
+	thread_local std::vector<uint32_t> inv;
+	thread_local std::string ref, rel, rdc;
+	const std::vector<uint8_t>& s = fw ? rd.fw : rd.rc;
+	const uint32_t* ed = ned0;
+	if(!fw) { invert_poss(ned0, nedn, rd.length(), inv); ed = inv.data(); }
+	ref.clear(); rel.clear(); rdc.clear();
 	size_t rdoff = 0;
 	static const char kAcgtn[] = "ACGTN";
 	// The printed edits come from the read's shared edit buffer and may step
 	// past the read's end; the reference then reads stale bytes of its read buffer, which
 	// only ever reach the output through left-alignment of an adjacent gap.  N stands in.
 	auto at = [&](size_t i) -> int { return i < s.size() ? s[i] : 4; };
-	for(uint32_t e : ed) {
+	for(size_t q = 0; q < nedn; q++) {
+		const uint32_t e = ed[q];
 		const size_t pos = e_pos(e);
 		while(rdoff < pos) { const int c = at(rdoff++); ref.push_back(kAcgtn[c]); rel.push_back('='); rdc.push_back(kAcgtn[c]); }
 		const uint32_t t = e_type(e);
@@ -170,8 +205,8 @@ std::string cigar_md(const Read& rd, const AlnRes& r, std::string& md) {
 		for(size_t j = i + 1; j < ln; j++) { if(rel[j] != g) break; glen++; }
 		if(i >= 1) {   // i == 0 would index [-1] in the reference; a gap never opens row 0
 			size_t l = i - 1, r2 = l + glen;
-			std::vector<char>& gp = (g == 'I') ? ref : rdc;
-			const std::vector<char>& ngp = (g == 'I') ? rdc : ref;
+			std::string& gp = (g == 'I') ? ref : rdc;
+			const std::string& ngp = (g == 'I') ? rdc : ref;
 			while(l > 0 && ngp[l] == ngp[r2]) {
 				if(rel[l] == 'X') break;
 				std::swap(gp[l], gp[r2]);
@@ -182,7 +217,6 @@ std::string cigar_md(const Read& rd, const AlnRes& r, std::string& md) {
 		i += glen - 1;
 	}
 	// CIGAR (xeq = false)
-	std::string cig;
 	for(size_t i = 0; i < ln; i++) {
 		char op = rel[i] == 'X' || rel[i] == '=' ? 'M' : rel[i];
 		size_t run = 1;
@@ -191,11 +225,10 @@ std::string cigar_md(const Read& rd, const AlnRes& r, std::string& md) {
 			if(op2 != op) break;
 		}
 		i += run - 1;
-		cig += std::to_string(run);
+		append_int(cig, run);
 		cig.push_back(op);
 	}
 	// MD:Z (buildMdz + writeMdz)
-	md.clear();
 	bool mm_last = false, rdgap_last = false, first_print = true;
 	for(size_t i = 0; i < ln; i++) {
 		const char op = rel[i];
@@ -208,7 +241,7 @@ std::string cigar_md(const Read& rd, const AlnRes& r, std::string& md) {
 			}
 			i += run - 1;
 			if(run - nins > 0) {
-				md += std::to_string(run - nins);
+				append_int(md, run - nins);
 				first_print = false; mm_last = false; rdgap_last = false;
 			}
 		} else if(op == 'X') {
@@ -223,7 +256,6 @@ std::string cigar_md(const Read& rd, const AlnRes& r, std::string& md) {
 		}
 	}
 	if(mm_last || rdgap_last) md.push_back('0');
-	return cig;
 }
 
 // BowtieMapq2::mapq, monotone (end-to-end) branch, unpaired (unique.h:187-330).
@@ -297,36 +329,42 @@ void append_refname(std::string& o, const std::string& name) {   // SamConfig::p
 
 void append_seq(std::string& o, const std::vector<uint8_t>& s) {
 	if(s.empty()) { o.push_back('*'); return; }
-	for(uint8_t c : s) o.push_back("ACGTN"[c]);
+	const size_t b = o.size();
+	o.resize(b + s.size());
+	for(size_t i = 0; i < s.size(); i++) o[b + i] = "ACGTN"[s[i]];
 }
 
-// AlnSinkWrap::finishRead, unpaired branch (aln_sink.cpp:643-1384) -> one SAM record
-// (AlnSinkSam::appendMate, aln_sink.cpp:1889-2090; tags per sam.cpp:121-730).
-std::string finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, Rng& rnd,
-                        const std::vector<uint32_t>& edbuf, bool* aligned, bool* rep) {
+// AlnSinkWrap::finishRead, unpaired branch (aln_sink.cpp:643-1384) -> one SAM record in
+// `o` (AlnSinkSam::appendMate, aln_sink.cpp:1889-2090; tags per sam.cpp:121-730).
+void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, Rng& rnd,
+                 const std::vector<uint32_t>& edbuf, bool* aligned, bool* rep, std::string& o) {
 	// ReportingState::finish + getReport
-	if(!sk.doneUnpair) { sk.doneUnpair = true; sk.exitUnpair = sk.n > 0 ? EXIT_WITH_ALIGNMENTS : EXIT_NO_ALIGNMENTS; }
+	if(!sk.doneUnpair) {
+		sk.doneUnpair = true;
+		sk.exitUnpair = sk.n > 0 ? Sink::EXIT_WITH_ALIGNMENTS : Sink::EXIT_NO_ALIGNMENTS;
+	}
 	uint64_t nunpair = 0;
 	bool unpairMax = false;
 	if(sk.n > 0) {
-		if(sk.exitUnpair == EXIT_SHORT_CIRCUIT_M) { unpairMax = true; nunpair = 1; }
-		else if(sk.exitUnpair == EXIT_WITH_ALIGNMENTS) nunpair = std::min<uint64_t>(sk.n, 1);
+		if(sk.exitUnpair == Sink::EXIT_SHORT_CIRCUIT_M) { unpairMax = true; nunpair = 1; }
+		else if(sk.exitUnpair == Sink::EXIT_WITH_ALIGNMENTS) nunpair = std::min<uint64_t>(sk.n, 1);
 	}
-	std::string o;
+	o.clear();
 	append_name(o, rd.name);
 	if(nunpair == 0) {
 		*aligned = false; *rep = unpairMax;
 		o += "\t4\t*\t0\t0\t*\t*\t0\t0\t";
 		append_seq(o, rd.fw);
 		o.push_back('\t');
-		o += rd.qual.empty() ? std::string("*") : rd.qual;
+		if(rd.qual.empty()) o.push_back('*'); else o += rd.qual;
 		o += "\tYT:Z:UU\tYF:Z:LN\n";
-		return o;
+		return;
 	}
 	// selectByScore (aln_sink.cpp:1477-1640): sort by score desc (ties by index desc),
 	// shuffle equal-score streaks with the read's RNG
 	const size_t sz = sk.rs.size();
-	std::vector<std::pair<int64_t, size_t>> buf(sz);
+	thread_local std::vector<std::pair<int64_t, size_t>> buf;
+	buf.resize(sz);
 	for(size_t i = 0; i < sz; i++) buf[i] = {sk.rs[i].score, i};
 	std::stable_sort(buf.begin(), buf.end());
 	std::reverse(buf.begin(), buf.end());
@@ -348,201 +386,55 @@ std::string finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sin
 	// Every reported AlnRes shares the read's edit buffer (DList copies keep the source's
 	// storage pointer, ds.h:979-1040): the record shows its first ned().size() entries as
 	// they stand now.
-	AlnRes r = sk.rs[buf[0].second];
-	const size_t nshow = r.ned.size();
-	r.ned.assign(edbuf.begin(), edbuf.begin() + (long)std::min(nshow, edbuf.size()));
+	const AlnRes& r = sk.rs[buf[0].second];
+	const uint32_t* ned = edbuf.data();
+	const size_t nedn = std::min<size_t>(r.nedit, edbuf.size());
 	const int64_t bestU = r.score;
 	const bool hasSec = buf.size() > 1;
 	const int64_t secU = hasSec ? sk.rs[buf[1].second].score : 0;
 	*aligned = true; *rep = unpairMax;
+	thread_local std::string cig, md;
+	cig.clear(); md.clear();
+	cigar_md(rd, r.fw, ned, nedn, cig, md);
 	// record
-	o.push_back('\t');
-	o += r.fw ? "0" : "16";
-	o.push_back('\t');
+	o += r.fw ? "\t0\t" : "\t16\t";
 	append_refname(o, ref.name((size_t)r.refid));
 	o.push_back('\t');
-	o += std::to_string(r.refoff + 1);
+	append_int(o, r.refoff + 1);
 	o.push_back('\t');
-	o += std::to_string(mapq_v2(p, rd.length(), bestU, hasSec, secU));
+	append_int(o, mapq_v2(p, rd.length(), bestU, hasSec, secU));
 	o.push_back('\t');
-	std::string md;
-	o += cigar_md(rd, r, md);
+	o += cig;
 	o += "\t*\t0\t0\t";
 	append_seq(o, r.fw ? rd.fw : rd.rc);
 	o.push_back('\t');
 	o += (r.fw ? rd.qual : rd.qualRev);
-	o += "\tAS:i:" + std::to_string(r.score);
-	if(hasSec) o += "\tXS:i:" + std::to_string(secU);
-	o += "\tXN:i:" + std::to_string(r.refns);
+	o += "\tAS:i:"; append_int(o, r.score);
+	if(hasSec) { o += "\tXS:i:"; append_int(o, secU); }
+	o += "\tXN:i:"; append_int(o, r.refns);
 	size_t num_mm = 0, num_go = 0, num_gx = 0;
-	const std::vector<uint32_t>& ned = r.ned;
-	for(size_t i = 0; i < ned.size(); i++) {
+	for(size_t i = 0; i < nedn; i++) {
 		const uint32_t t = e_type(ned[i]);
 		if(t == ET_MM) num_mm++;
 		else if(t == ET_READ_GAP) {
 			num_go++; num_gx++;
-			while(i < ned.size() - 1 && e_pos(ned[i + 1]) == e_pos(ned[i]) && e_type(ned[i + 1]) == ET_READ_GAP) { i++; num_gx++; }
+			while(i < nedn - 1 && e_pos(ned[i + 1]) == e_pos(ned[i]) && e_type(ned[i + 1]) == ET_READ_GAP) { i++; num_gx++; }
 		} else if(t == ET_REF_GAP) {
 			num_go++; num_gx++;
-			while(i < ned.size() - 1 && e_pos(ned[i + 1]) == e_pos(ned[i]) + 1 && e_type(ned[i + 1]) == ET_REF_GAP) { i++; num_gx++; }
+			while(i < nedn - 1 && e_pos(ned[i + 1]) == e_pos(ned[i]) + 1 && e_type(ned[i + 1]) == ET_REF_GAP) { i++; num_gx++; }
 		}
 	}
-	o += "\tXM:i:" + std::to_string(num_mm);
-	o += "\tXO:i:" + std::to_string(num_go);
-	o += "\tXG:i:" + std::to_string(num_gx);
-	o += "\tNM:i:" + std::to_string(ned.size());
-	o += "\tMD:Z:" + md;
+	o += "\tXM:i:"; append_int(o, num_mm);
+	o += "\tXO:i:"; append_int(o, num_go);
+	o += "\tXG:i:"; append_int(o, num_gx);
+	o += "\tNM:i:"; append_int(o, nedn);
+	o += "\tMD:Z:"; o += md;
 	o += "\tYT:Z:UU\tYF:Z:LN\n";
-	return o;
 }
 
-struct SatPos {                     // SATupleAndPos (aligner_sw_driver.h:118-180)
-	uint64_t topf = 0, size = 0;    // SATuple: BW top and #elements (offs.size())
-	uint64_t key = 0;               // identity of the cache entry (its BW top)
-	uint8_t nlex = 0;
-	uint64_t origSz = 0;
-	bool fw = true;                 // SeedPos
-	uint32_t offidx = 0, rdoff = 0, seedlen = 0;
-	bool operator<(const SatPos& o) const {
-		if(size != o.size) return size < o.size;
-		if(topf != o.topf) return topf < o.topf;
-		if(offidx != o.offidx) return offidx < o.offidx;
-		if(rdoff != o.rdoff) return rdoff < o.rdoff;
-		if(seedlen != o.seedlen) return seedlen < o.seedlen;
-		return fw && !o.fw;
-	}
-};
-
-struct ExtendRange { size_t off, len, sz; };
-
-// RowSampler (aligner_sw_driver.h:176-267), lensq = szsq = true
-struct RowSampler {
-	double mass = 0;
-	std::vector<double> masses;
-	std::vector<bool> elim;
-	void init(const std::vector<SatPos>& sl, size_t sai, size_t saf) {
-		elim.assign(saf - sai, false);
-		mass = 0.0f;
-		masses.assign(saf - sai, 0.0);
-		for(size_t i = sai; i < saf; i++) {
-			double num = (double)(sl[i].nlex + 1);
-			num *= num;
-			double den = (double)sl[i].size;
-			den *= den;
-			masses[i - sai] = num / den;
-			mass += masses[i - sai];
-		}
-	}
-	void finishedRange(size_t i) { elim[i] = true; mass -= masses[i]; }
-	size_t next(Rng& rnd) {
-		const double rd = rnd.nextFloat() * mass;
-		double sofar = 0.0f;
-		size_t last = std::numeric_limits<size_t>::max();
-		for(size_t i = 0; i < masses.size(); i++) {
-			if(!elim[i]) {
-				last = i;
-				sofar += masses[i];
-				if(rd < sofar) return i;
-			}
-		}
-		return last;
-	}
-};
-
-// The candidate walk of extendSeeds (aligner_sw_driver.cpp:278-631) as a resumable
-// iterator: next() runs the loop up to its next DP problem (PROBLEM, the problem's key)
-// or to the loop's exit (an EXTEND_* code); failed() applies a DP that found nothing.
-// The walk's own state (position, per-range samplers, elements left) is a value and the
-// per-read state it advances (RNG, limit metrics, seen diagonals) is bound by pointer,
-// so a copy bound to copies of those runs ahead of the real walk on the assumption
-// that every DP fails: the lookahead the scheduler batches (DpKey, bt2x_align.hpp).
-class ExtendWalk {
-public:
-	static constexpr int PROBLEM = 0;
-	ExtendWalk(const Params& P, const std::vector<SatPos>& sat, const std::vector<uint32_t>& rand_ns,
-	           const std::vector<size_t>& firstRow, const std::vector<bt2x_resolve_out>& res, size_t nelt,
-	           size_t rdlen)
-		: P_(&P), sat_(&sat), firstRow_(&firstRow), res_(&res), neltLeft_(nelt), rdlen_(rdlen) {
-		rands_.resize(sat.size());
-		for(size_t i = 0; i < sat.size(); i++) rands_[i].init((uint16_t)rand_ns[i], false);
-	}
-	void bind(Rng* rnd, Prm* prm, SeenDiags* seen) { rnd_ = rnd; prm_ = prm; seen_ = seen; }
-	int next(int64_t minsc, DpKey& k) {
-		const Params& P = *P_;
-		const size_t n = (uint16_t)sat_->size();                // gws_size is a uint16_t
-		for(;;) {
-			if(!inPass_) {                                       // while(neltLeft > 0)
-				if(neltLeft_ == 0) return EXTEND_EXHAUSTED_CANDIDATES;
-				if(minsc == 0) return EXTEND_PERFECT_SCORE;
-				inPass_ = true; i_ = 0; first_ = true;
-			}
-			if(i_ >= n) { inPass_ = false; continue; }
-			const SatPos& sp = (*sat_)[i_];
-			const bool is_small = sp.size < kNsm;
-			if(rands_[i_].done() || !(first_ || is_small)) { i_++; first_ = true; continue; }
-			if(minsc == 0) return EXTEND_PERFECT_SCORE;
-			if(prm_->nExDps >= P.mxDp || prm_->nMateDps >= P.mxDp) return EXTEND_EXCEEDED_HARD_LIMIT;
-			if(prm_->nExUgs >= P.mxUg || prm_->nMateUgs >= P.mxUg) return EXTEND_EXCEEDED_HARD_LIMIT;
-			if(prm_->nExIters >= P.mxIter) return EXTEND_EXCEEDED_HARD_LIMIT;
-			prm_->nExIters++;
-			first_ = false;
-			const bool fw = sp.fw;
-			uint32_t rdoff = sp.rdoff;
-			if(!fw) rdoff = (uint32_t)(rdlen_ - rdoff - sp.seedlen);
-			const uint16_t elt = rands_[i_].next(*rnd_);
-			const bt2x_resolve_out& wr = (*res_)[(*firstRow_)[i_] + elt];
-			neltLeft_--;
-			const int64_t tidx = wr.tidx == BT2X_NO_TIDX ? 0 : (int64_t)wr.tidx;
-			const int64_t toff = (int64_t)wr.toff, tlen = (int64_t)wr.tlen;
-			const int64_t refoff = toff - (int64_t)rdoff;
-			const Coord refcoord(tidx, refoff, fw);
-			if(seen_->locusPresent(refcoord)) { prm_->nRedundants++; continue; }
-			// DynProgFramer::frameSeedExtensionRect, trimToRef (dp_framer.cpp:81-129)
-			const int readGaps = P.maxReadGaps(minsc), refGaps = P.maxRefGaps(minsc);
-			const size_t maxgap = std::min((size_t)std::max(readGaps, refGaps), P.maxhalf);
-			const int64_t refl_pre = refoff - 2 * (int64_t)maxgap;
-			const int64_t refr_pre = refoff + ((int64_t)rdlen_ - 1) + 2 * (int64_t)maxgap;
-			size_t triml = 0, trimr = 0;
-			if(refr_pre >= tlen) trimr = (size_t)(refr_pre - (tlen - 1));
-			if(refl_pre < 0) triml = (size_t)(-refl_pre);
-			const int64_t refl = refl_pre + (int64_t)triml, refr = refr_pre - (int64_t)trimr;
-			const size_t corel = maxgap, corer = corel + 2 * maxgap;
-			seen_->add(Interval(refcoord, 1));
-			if(refr < refl) continue;                            // entirely trimmed
-			// SwAligner::initRef (aligner_sw.cpp:117-229)
-			const size_t ncol = (size_t)(refr - refl + 1);
-			if(ncol + 1 > BT2X_MAX_COLS) {
-				prm_->nExDpFails++; prm_->nDpFail++;
-				return EXTEND_EXCEEDED_HARD_LIMIT;
-			}
-			seen_->add(Interval(Coord(tidx, refl_pre + (int64_t)corel, fw), (int64_t)(corer - corel + 1)));
-			k.tidx = tidx; k.refl = refl; k.minsc = minsc; k.ncol = (uint32_t)ncol;
-			k.triml = (uint32_t)triml; k.corel = (uint32_t)corel; k.corer = (uint32_t)corer; k.fw = fw;
-			return PROBLEM;
-		}
-	}
-	// the DP of the last next() found no alignment; false: the fail streak ends the walk
-	bool failed() {
-		prm_->nExDps++; prm_->nExDpFails++; prm_->nDpFail++;
-		return prm_->nDpFail < P_->streak;
-	}
-private:
-	static constexpr uint64_t kNsm = 5;                          // prioritizeSATups' nsm
-	const Params* P_;
-	const std::vector<SatPos>* sat_;
-	const std::vector<size_t>* firstRow_;
-	const std::vector<bt2x_resolve_out>* res_;
-	size_t neltLeft_, rdlen_;
-	std::vector<Random1toN> rands_;
-	size_t i_ = 0;
-	bool first_ = true, inPass_ = false;
-	Rng* rnd_ = nullptr;
-	Prm* prm_ = nullptr;
-	SeenDiags* seen_ = nullptr;
-};
-
-// SwAligner::initRef's problem for key k (window = BitPairReference::getStretch).
-void pose_dp(std::vector<DpWork>& dps, const RefInfo& ref, const DpKey& k, size_t rdlen, int nceil) {
+// SwAligner::initRef's problem for key k (the window, BitPairReference::getStretch, is
+// fetched when the scheduler gathers the launch).
+void pose_dp(std::vector<DpWork>& dps, const DpKey& k, size_t rdlen, int nceil) {
 	dps.emplace_back();
 	DpWork& d = dps.back();
 	d.key = k;
@@ -554,11 +446,69 @@ void pose_dp(std::vector<DpWork>& dps, const RefInfo& ref, const DpKey& k, size_
 	d.in.nceil = (int16_t)nceil;
 	d.in.triml = (uint16_t)k.triml; d.in.corel = (uint16_t)k.corel; d.in.corer = (uint16_t)k.corer;
 	d.in.fw = k.fw ? 1 : 0;
-	d.window.resize(k.ncol);
-	ref.stretch((uint32_t)k.tidx, k.refl, k.ncol, d.window.data());
+}
+
+long find_memo(const std::vector<DpMemo>& memo, const DpKey& k) {
+	for(size_t i = 0; i < memo.size(); i++) if(memo[i].key == k) return (long)i;
+	return -1;
 }
 
 } // namespace
+
+int ExtendWalk::next(int64_t minsc, DpKey& k) {
+	const Params& P = *P_;
+	const size_t n = (uint16_t)sat_->size();                // gws_size is a uint16_t
+	for(;;) {
+		if(!inPass_) {                                       // while(neltLeft > 0)
+			if(neltLeft_ == 0) return EXTEND_EXHAUSTED_CANDIDATES;
+			if(minsc == 0) return EXTEND_PERFECT_SCORE;
+			inPass_ = true; i_ = 0; first_ = true;
+		}
+		if(i_ >= n) { inPass_ = false; continue; }
+		const SatPos& sp = (*sat_)[i_];
+		const bool is_small = sp.size < kNsm;
+		if(rands_[i_].done() || !(first_ || is_small)) { i_++; first_ = true; continue; }
+		if(minsc == 0) return EXTEND_PERFECT_SCORE;
+		if(prm_->nExDps >= P.mxDp || prm_->nMateDps >= P.mxDp) return EXTEND_EXCEEDED_HARD_LIMIT;
+		if(prm_->nExUgs >= P.mxUg || prm_->nMateUgs >= P.mxUg) return EXTEND_EXCEEDED_HARD_LIMIT;
+		if(prm_->nExIters >= P.mxIter) return EXTEND_EXCEEDED_HARD_LIMIT;
+		prm_->nExIters++;
+		first_ = false;
+		const bool fw = sp.fw;
+		uint32_t rdoff = sp.rdoff;
+		if(!fw) rdoff = (uint32_t)(rdlen_ - rdoff - sp.seedlen);
+		const uint16_t elt = rands_[i_].next(*rnd_);
+		const bt2x_resolve_out& wr = (*res_)[(*firstRow_)[i_] + elt];
+		neltLeft_--;
+		const int64_t tidx = wr.tidx == BT2X_NO_TIDX ? 0 : (int64_t)wr.tidx;
+		const int64_t toff = (int64_t)wr.toff, tlen = (int64_t)wr.tlen;
+		const int64_t refoff = toff - (int64_t)rdoff;
+		const Coord refcoord(tidx, refoff, fw);
+		if(seen_->locusPresent(refcoord)) { prm_->nRedundants++; continue; }
+		// DynProgFramer::frameSeedExtensionRect, trimToRef (dp_framer.cpp:81-129)
+		const int readGaps = P.maxReadGaps(minsc), refGaps = P.maxRefGaps(minsc);
+		const size_t maxgap = std::min((size_t)std::max(readGaps, refGaps), P.maxhalf);
+		const int64_t refl_pre = refoff - 2 * (int64_t)maxgap;
+		const int64_t refr_pre = refoff + ((int64_t)rdlen_ - 1) + 2 * (int64_t)maxgap;
+		size_t triml = 0, trimr = 0;
+		if(refr_pre >= tlen) trimr = (size_t)(refr_pre - (tlen - 1));
+		if(refl_pre < 0) triml = (size_t)(-refl_pre);
+		const int64_t refl = refl_pre + (int64_t)triml, refr = refr_pre - (int64_t)trimr;
+		const size_t corel = maxgap, corer = corel + 2 * maxgap;
+		seen_->add(Interval(refcoord, 1));
+		if(refr < refl) continue;                            // entirely trimmed
+		// SwAligner::initRef (aligner_sw.cpp:117-229)
+		const size_t ncol = (size_t)(refr - refl + 1);
+		if(ncol + 1 > BT2X_MAX_COLS) {
+			prm_->nExDpFails++; prm_->nDpFail++;
+			return EXTEND_EXCEEDED_HARD_LIMIT;
+		}
+		seen_->add(Interval(Coord(tidx, refl_pre + (int64_t)corel, fw), (int64_t)(corer - corel + 1)));
+		k.tidx = tidx; k.refl = refl; k.minsc = minsc; k.ncol = (uint32_t)ncol;
+		k.triml = (uint32_t)triml; k.corel = (uint32_t)corel; k.corer = (uint32_t)corer; k.fw = fw;
+		return PROBLEM;
+	}
+}
 
 // ---------------------------------------------------------------- SAM header
 
@@ -582,31 +532,33 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 	int64_t minsc = P.scoreMin.f<int64_t>((double)rdlen);
 	if(minsc > 0) minsc = 0;
 	else if(minsc < -254) minsc = -254;
+	PH_START();
 	Rng rnd;
 	rnd.init(rd.seed);
 	const int interval = std::max(P.msIval.f<int>((double)rdlen), 1);
-	const int nceil = std::min(P.nCeil.f<int>((double)rdlen), (int)rdlen);
 	const int swNceil = P.nCeil.f<int>((double)rdlen);      // SwAligner::initRead's nceil
-	Sink sink;
-	sink.mhits = P.mhits;
-	SeenDiags seenDiags;
-	RedundantAlns redAnchor;
-	redAnchor.init(rdlen);
-	std::vector<uint32_t> edbuf;         // SwDriver::resGap_.alres.ned_ storage
-	std::unordered_map<DpKey, DpResult, DpKeyHash> memo;   // this read's DP results (lookahead)
-	std::vector<ExtendRange> exRange[2];
+	Sink& sink = c->sink;
+	sink.reset(P.mhits);
+	c->seenDiags.clear();
+	c->redAnchor.init(rdlen);
+	c->edbuf.clear();
+	c->memo.clear(); c->recs.clear(); c->edits.clear();
+	c->exRange[0].clear(); c->exRange[1].clear();
+	c->ndp_used = c->ntight = 0;
+	c->aligned = c->repetitive = false;
 	Prm prm;
 	const uint32_t nrounds = (uint32_t)std::min<int>(P.nSeedRounds, interval);
 	const uint32_t L = (uint32_t)std::min<size_t>((size_t)P.multiseedLen, rdlen);
 	// reads the u8 DP cannot hold never align (initRead, aligner_sw.cpp:59)
 	const bool dpOk = rdlen >= 1 && rdlen <= BT2X_MAX_ROWS;
+	PH(0);
 	for(uint32_t roundi = 0; roundi < nrounds && dpOk; roundi++) {
 		const uint32_t offset = (uint32_t)((interval * roundi) / nrounds);
 		if(offset > 0 && (size_t)P.multiseedLen + offset > rdlen) break;
 		// instantiateSeeds (aligner_seed.cpp:411-447): fw seed i at depth, rc seed at rdlen-depth-L
 		const uint32_t nseeds = (rdlen - offset > L) ? 1 + (uint32_t)((rdlen - offset - L) / interval) : 1;
-		c->seed.in.clear();
-		std::vector<std::pair<uint8_t, uint32_t>> seedIds;          // (fw, idx) of each searched seed
+		c->seed_in.clear();
+		c->seedIds.clear();
 		for(int fwi = 0; fwi < 2; fwi++) {
 			const bool fw = fwi == 0;
 			if((fw && P.nofw) || (!fw && P.norc)) continue;
@@ -622,32 +574,34 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 				si.read_off = fw ? 0 : rdlen;
 				si.seed_off = (uint8_t)st;
 				si.seed_len = (uint8_t)L;
-				c->seed.in.push_back(si);
-				seedIds.push_back({(uint8_t)fw, i});
+				c->seed_in.push_back(si);
+				c->seedIds.push_back({(uint8_t)fw, i});
 			}
 		}
-		if(!c->seed.in.empty()) co_await Awaiter{c, REQ_SEED};
+		PH(1);
+		if(!c->seed_in.empty()) co_await Awaiter{c, REQ_SEED};
+		PH_START();
 		// searchAllSeedsFinalize + SeedResults::add (aligner_seed.cpp:508-540)
-		SeedHitsHip hits;
+		SeedHitsHip& hits = c->hits;
 		hits.reset(nseeds);
-		std::vector<std::pair<uint64_t, uint8_t>> cacheNlex;        // AlignmentCache: key -> nlex of the first add
-		for(size_t k = 0; k < seedIds.size(); k++) {
-			const bt2x_seed_out& d = c->seed.out[k];
+		c->cacheNlex.clear();
+		for(size_t k = 0; k < c->seedIds.size(); k++) {
+			const bt2x_seed_out& d = c->seed_out[k];
 			if(!d.need_reporting) continue;
-			hits.add(seedIds[k].second, seedIds[k].first != 0, d);
+			hits.add(c->seedIds[k].second, c->seedIds[k].first != 0, d);
 			bool have = false;
-			for(auto& e : cacheNlex) if(e.first == d.topf) { have = true; break; }
-			if(!have) cacheNlex.push_back({d.topf, d.nlex});
+			for(auto& e : c->cacheNlex) if(e.first == d.topf) { have = true; break; }
+			if(!have) c->cacheNlex.push_back({d.topf, d.nlex});
 		}
 		if(hits.nonzeroOffsets() == 0) break;                        // no seed hits: done
 		hits.rankSeedHits(rnd, false);
+		PH(2);
 
 		// ---------------------------------------------- prioritizeSATups (:61-260)
-		std::vector<SatPos> satpos2, satpos;
-		std::vector<uint32_t> rand_ns;
-		satpos2.reserve(hits.nonzeroOffsets());
-		satpos.reserve(std::min<size_t>(P.mxIter, 64));
-		rand_ns.reserve(std::min<size_t>(P.mxIter, 64));
+		std::vector<SatPos>& satpos2 = c->satpos2;
+		std::vector<SatPos>& satpos = c->satpos;
+		std::vector<uint32_t>& rand_ns = c->rand_ns;
+		satpos2.clear(); satpos.clear(); rand_ns.clear();
 		size_t nrange = 0, nelt = 0, nsmall = 0, nsmall_elts = 0;
 		const size_t nsm = 5, maxelt = P.mxIter;
 		for(size_t r = 0; r < hits.nonzeroOffsets(); r++) {
@@ -657,11 +611,11 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			const uint32_t seedlen = L;
 			SatPos sp;
 			sp.topf = h.topf; sp.size = h.numElts(); sp.key = h.topf;
-			for(auto& e : cacheNlex) if(e.first == h.topf) { sp.nlex = e.second; break; }
+			for(auto& e : c->cacheNlex) if(e.first == h.topf) { sp.nlex = e.second; break; }
 			if(sp.size == 0) continue;
 			nrange++; nelt += sp.size;
 			bool skip = false;
-			for(const ExtendRange& er : exRange[fw ? 0 : 1]) {
+			for(const ExtendRange& er : c->exRange[fw ? 0 : 1]) {
 				if(er.off <= rdoff && er.off + er.len >= rdoff + seedlen && sp.size <= er.sz) { skip = true; break; }
 			}
 			if(!skip) for(const SatPos& q : satpos2) skip |= (q.key == sp.key);
@@ -672,7 +626,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			if(sp.size <= nsm) { nsmall++; nsmall_elts += sp.size; }
 			if(sp.nlex > 0) {
 				const size_t p5 = rdoff - (fw ? sp.nlex : 0);
-				exRange[fw ? 0 : 1].push_back({p5, (size_t)seedlen + sp.nlex, sp.size});
+				c->exRange[fw ? 0 : 1].push_back({p5, (size_t)seedlen + sp.nlex, sp.size});
 			}
 		}
 		std::stable_sort(satpos2.begin(), satpos2.end());
@@ -683,14 +637,15 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			nelt_added += satpos2[j].size;
 		}
 		if(!(nelt_added >= maxelt || nsmall == satpos2.size())) {
-			RowSampler rows;
-			rows.init(satpos2, nsmall, satpos2.size());
-			std::vector<Random1toN> rands(satpos2.size());
+			c->rows.init(satpos2, nsmall, satpos2.size());
+			std::vector<Random1toN>& rands = c->prioRands;
+			if(rands.size() < satpos2.size()) rands.resize(satpos2.size());
+			for(size_t q = 0; q < satpos2.size(); q++) rands[q].reset();
 			while(nelt_added < maxelt && nelt_added < nelt) {
-				const size_t ri = rows.next(rnd) + nsmall;
+				const size_t ri = c->rows.next(rnd) + nsmall;
 				if(!rands[ri].inited()) rands[ri].init((uint16_t)satpos2[ri].size, false);
 				const size_t rr = rands[ri].next(rnd);
-				if(rands[ri].done()) rows.finishedRange(ri - nsmall);
+				if(rands[ri].done()) c->rows.finishedRange(ri - nsmall);
 				SatPos sp = satpos2[ri];
 				sp.topf = satpos2[ri].topf + rr;
 				sp.size = 1;
@@ -701,67 +656,72 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			}
 		}
 		const size_t nelt_ = nelt_added;
+		PH(3);
 
 		// ----------------------- SA resolution of every element extendSeeds may visit
-		c->resolve.in.clear();
-		std::vector<size_t> firstRow(satpos.size());
+		c->res_in.clear();
+		c->firstRow.resize(satpos.size());
 		for(size_t i = 0; i < satpos.size(); i++) {
-			firstRow[i] = c->resolve.in.size();
+			c->firstRow[i] = (uint32_t)c->res_in.size();
 			for(uint32_t e = 0; e < rand_ns[i]; e++) {
 				bt2x_resolve_in ri;
 				std::memset(&ri, 0, sizeof(ri));
 				ri.row = satpos[i].topf + e;
 				ri.qlen = satpos[i].seedlen;
-				c->resolve.in.push_back(ri);
+				c->res_in.push_back(ri);
 			}
 		}
-		if(!c->resolve.in.empty()) co_await Awaiter{c, REQ_RESOLVE};
+		PH(4);
+		if(!c->res_in.empty()) co_await Awaiter{c, REQ_RESOLVE};
+		PH_START();
 
 		// -------------------------------------------------- extendSeeds (:278-631)
 		int ret;
 		{
 			prm.nDpFail = 0;
 			const int64_t perfectScore = 0;
-			ExtendWalk walk(P, satpos, rand_ns, firstRow, c->resolve.out, nelt_, rdlen);
-			walk.bind(&rnd, &prm, &seenDiags);
+			c->walk.reset(P, satpos, rand_ns, c->firstRow, c->res_out, nelt_, rdlen);
+			c->walk.bind(&rnd, &prm, &c->seenDiags);
 			for(;;) {
 				DpKey key;
-				ret = walk.next(minsc, key);
+				ret = c->walk.next(minsc, key);
 				if(ret != ExtendWalk::PROBLEM) break;
-				auto hit = memo.find(key);
-				if(hit == memo.end()) {
+				long mi = find_memo(c->memo, key);
+				PH(5);
+				if(mi < 0) {
 					// pose this problem and the ones the walk reaches next if each of them
 					// fails (a copy of the walk over copies of the state it advances)
 					c->dps.clear();
-					pose_dp(c->dps, ref_, key, rdlen, swNceil);
+					pose_dp(c->dps, key, rdlen, swNceil);
 					if(P.lookahead > 1) {
 						Rng rnd2 = rnd;
 						Prm prm2 = prm;
-						SeenDiags seen2 = seenDiags;
-						ExtendWalk ahead = walk;
-						ahead.bind(&rnd2, &prm2, &seen2);
-						while(c->dps.size() < P.lookahead && ahead.failed()) {
+						c->seen2 = c->seenDiags;
+						c->ahead = c->walk;
+						c->ahead.bind(&rnd2, &prm2, &c->seen2);
+						while(c->dps.size() < P.lookahead && c->ahead.failed()) {
 							DpKey k2;
-							if(ahead.next(minsc, k2) != ExtendWalk::PROBLEM) break;
-							const auto m = memo.find(k2);
-							if(m != memo.end()) {
-								if(m->second.out.status != 0) break;    // a known success: stop guessing
+							if(c->ahead.next(minsc, k2) != ExtendWalk::PROBLEM) break;
+							const long m = find_memo(c->memo, k2);
+							if(m >= 0) {
+								if(c->memo[(size_t)m].out.status != 0) break;    // a known success: stop guessing
 								continue;
 							}
 							bool dup = false;
 							for(const DpWork& d : c->dps) dup = dup || d.key == k2;
-							if(!dup) pose_dp(c->dps, ref_, k2, rdlen, swNceil);
+							if(!dup) pose_dp(c->dps, k2, rdlen, swNceil);
 						}
 					}
+					PH(6);
 					co_await Awaiter{c, REQ_DP};
-					for(DpWork& d : c->dps) memo.emplace(d.key, std::move(d.res));
+					PH_START();
 					c->dps.clear();
-					hit = memo.find(key);
+					mi = find_memo(c->memo, key);
 				}
 				c->ndp_used++;
-				const DpResult& d = hit->second;
+				const DpMemo d = c->memo[(size_t)mi];
 				if(d.out.status == 0) {
-					if(!walk.failed()) { ret = EXTEND_EXCEEDED_SOFT_LIMIT; break; }
+					if(!c->walk.failed()) { ret = EXTEND_EXCEEDED_SOFT_LIMIT; break; }
 					continue;
 				}
 				prm.nExDps++;
@@ -771,7 +731,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 				bool fulfilled = false;
 				const int64_t minsc_posed = minsc;
 				for(uint32_t k = 0; k < d.out.nrec; k++) {            // while(!swa.done()) nextAlignment
-					const bt2x_aln_rec& rec = d.recs[k];
+					const bt2x_aln_rec& rec = c->recs[d.rec0 + k];
 					// -M tightening below raises minsc between the calls of this problem, but the
 					// record sequence needs no re-filtering: nextAlignment's score filter compares
 					// the candidate's raw u8 cell value (DpBtCandidate::score = lr in 0..255,
@@ -781,21 +741,20 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 					if(minsc != minsc_posed) c->ntight++;
 					replay_backtrace_draws(rnd, rec.ntries);
 					// the call's writes to the read's edit buffer (bt2x.h)
-					if(edbuf.size() < rec.nbuf) edbuf.resize(rec.nbuf);
-					std::copy(d.edits.begin() + rec.edit_off, d.edits.begin() + rec.edit_off + rec.nbuf, edbuf.begin());
+					if(c->edbuf.size() < rec.nbuf) c->edbuf.resize(rec.nbuf);
+					std::copy(c->edits.begin() + rec.edit_off, c->edits.begin() + rec.edit_off + rec.nbuf, c->edbuf.begin());
 					if(!rec.ok) break;
 					AlnRes res;
 					res.score = rec.score;
-					res.bases_aligned = rec.bases_aligned;
 					res.refid = key.tidx;
 					res.refoff = rec.refoff;
 					res.fw = key.fw;
-					res.rdlen = rdlen;
+					res.nedit = rec.nedit;
 					res.refns = rec.refns;
-					res.ned.assign(d.edits.begin() + rec.edit_off, d.edits.begin() + rec.edit_off + rec.nedit);
+					const uint32_t* ned = c->edits.data() + rec.edit_off;
 					// (the alignment lies inside [0, tlen): the rectangle is trimmed to the reference)
-					if(redAnchor.overlap(res)) continue;
-					redAnchor.add(res);
+					if(c->redAnchor.overlap(res, ned, rec.nedit)) continue;
+					c->redAnchor.add(res, ned, rec.nedit);
 					if(sink.report(res)) { fulfilled = true; break; }
 					if(P.tighten > 0 && sink.hasSecondBest()) {
 						if(P.tighten == 1) {
@@ -812,6 +771,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 						}
 					}
 				}
+				PH(7);
 				if(fulfilled) { ret = EXTEND_POLICY_FULFILLED; break; }
 			}
 		}
@@ -822,9 +782,11 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			break;
 		}
 	}
-	(void)nceil;
-	c->sam = finish_read(P, ref_, rd, sink, rnd, edbuf, &c->aligned, &c->repetitive);
+	PH(5);
+	finish_read(P, ref_, rd, sink, rnd, c->edbuf, &c->aligned, &c->repetitive, c->sam);
+	PH(8);
 	c->req = REQ_NONE;
+	c->done = true;
 	co_return;
 }
 
@@ -855,103 +817,109 @@ bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st, int threads) {
 		             wr.size(), wd.size(), rss * 4096 / (1 << 20));
 	}
 	const long nws = (long)ws.size(), nwr = (long)wr.size(), nwd = (long)wd.size();
+	std::vector<uint64_t>& ob = b_off_;
+	std::vector<uint64_t>& ob2 = b_off2_;
 	if(nws) {
 		// one launch for every waiting read's seeds: patFw+patRc of each read, then its
 		// seeds with read_off rebased (gather/scatter in parallel over reads)
 		double t0 = now_s();
-		std::vector<uint64_t> rb(nws + 1, 0), sb(nws + 1, 0);
+		ob.assign(nws + 1, 0); ob2.assign(nws + 1, 0);
 		for(long i = 0; i < nws; i++) {
-			rb[i + 1] = rb[i] + 2 * ws[i]->rd.length();
-			sb[i + 1] = sb[i] + ws[i]->seed.in.size();
+			ob[i + 1] = ob[i] + 2 * ws[i]->rd.length();
+			ob2[i + 1] = ob2[i] + ws[i]->seed_in.size();
 		}
-		std::vector<uint8_t> reads(rb[nws]);
-		std::vector<bt2x_seed_in> in(sb[nws]);
+		b_reads_.resize(ob[nws]);
+		b_seed_in_.resize(ob2[nws]);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nws; i++) {
 			const ReadCtx* c = ws[i];
 			const size_t L = c->rd.length();
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), reads.begin() + (long)rb[i]);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), reads.begin() + (long)(rb[i] + L));
-			for(size_t k = 0; k < c->seed.in.size(); k++) {
-				bt2x_seed_in s = c->seed.in[k];
-				s.read_off += rb[i];
-				in[sb[i] + k] = s;
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), b_reads_.begin() + (long)ob[i]);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), b_reads_.begin() + (long)(ob[i] + L));
+			for(size_t k = 0; k < c->seed_in.size(); k++) {
+				bt2x_seed_in s = c->seed_in[k];
+				s.read_off += ob[i];
+				b_seed_in_[ob2[i] + k] = s;
 			}
 		}
-		std::vector<bt2x_seed_out> out;
-		be_.seed_search(reads, in, out);
+		be_.seed_search(b_reads_, b_seed_in_, b_seed_out_);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nws; i++)
-			ws[i]->seed.out.assign(out.begin() + (long)sb[i], out.begin() + (long)sb[i + 1]);
-		st.seed_launches++; st.seeds += in.size(); st.t_seed += now_s() - t0;
+			ws[i]->seed_out.assign(b_seed_out_.begin() + (long)ob2[i], b_seed_out_.begin() + (long)ob2[i + 1]);
+		st.seed_launches++; st.seeds += b_seed_in_.size(); st.t_seed += now_s() - t0;
 	}
 	if(nwr) {
 		double t0 = now_s();
-		std::vector<uint64_t> ib(nwr + 1, 0);
-		for(long i = 0; i < nwr; i++) ib[i + 1] = ib[i] + wr[i]->resolve.in.size();
-		std::vector<bt2x_resolve_in> in(ib[nwr]);
+		ob.assign(nwr + 1, 0);
+		for(long i = 0; i < nwr; i++) ob[i + 1] = ob[i] + wr[i]->res_in.size();
+		b_res_in_.resize(ob[nwr]);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nwr; i++)
-			std::copy(wr[i]->resolve.in.begin(), wr[i]->resolve.in.end(), in.begin() + (long)ib[i]);
-		std::vector<bt2x_resolve_out> out;
-		be_.resolve(in, out);
+			std::copy(wr[i]->res_in.begin(), wr[i]->res_in.end(), b_res_in_.begin() + (long)ob[i]);
+		be_.resolve(b_res_in_, b_res_out_);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nwr; i++)
-			wr[i]->resolve.out.assign(out.begin() + (long)ib[i], out.begin() + (long)ib[i + 1]);
-		st.resolve_launches++; st.resolves += in.size(); st.t_resolve += now_s() - t0;
+			wr[i]->res_out.assign(b_res_out_.begin() + (long)ob[i], b_res_out_.begin() + (long)ob[i + 1]);
+		st.resolve_launches++; st.resolves += b_res_in_.size(); st.t_resolve += now_s() - t0;
 	}
 	if(nwd) {
 		double t0 = now_s();
 		// every waiting read's posed problems in one launch: the read's two orientations
 		// (codes and qualities) once per read, one reference window per problem
-		std::vector<uint64_t> qb(nwd + 1, 0), pb(nwd + 1, 0);
+		std::vector<uint64_t>& qb = ob;
+		std::vector<uint64_t>& pb = ob2;
+		std::vector<uint64_t>& fb = b_off3_;
+		qb.assign(nwd + 1, 0); pb.assign(nwd + 1, 0);
 		for(long i = 0; i < nwd; i++) {
 			qb[i + 1] = qb[i] + 2 * wd[i]->rd.length();
 			pb[i + 1] = pb[i] + wd[i]->dps.size();
 		}
 		const uint64_t np = pb[nwd];
-		std::vector<uint64_t> fb(np + 1, 0);
+		fb.assign(np + 1, 0);
 		for(long i = 0; i < nwd; i++)
 			for(size_t j = 0; j < wd[i]->dps.size(); j++)
-				fb[pb[i] + j + 1] = fb[pb[i] + j] + wd[i]->dps[j].window.size();
-		std::vector<uint8_t> reads(qb[nwd]), quals(qb[nwd]), refs(fb[np]);
-		std::vector<bt2x_dp_in> in(np);
+				fb[pb[i] + j + 1] = fb[pb[i] + j] + wd[i]->dps[j].key.ncol;
+		b_reads_.resize(qb[nwd]); b_quals_.resize(qb[nwd]); b_refs_.resize(fb[np]);
+		b_dp_in_.resize(np);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nwd; i++) {
 			const ReadCtx* c = wd[i];
 			const size_t L = c->rd.length();
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), reads.begin() + (long)qb[i]);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), reads.begin() + (long)(qb[i] + L));
-			std::copy(c->rd.qual.begin(), c->rd.qual.end(), quals.begin() + (long)qb[i]);
-			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), quals.begin() + (long)(qb[i] + L));
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), b_reads_.begin() + (long)qb[i]);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), b_reads_.begin() + (long)(qb[i] + L));
+			std::copy(c->rd.qual.begin(), c->rd.qual.end(), b_quals_.begin() + (long)qb[i]);
+			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), b_quals_.begin() + (long)(qb[i] + L));
 			for(size_t j = 0; j < c->dps.size(); j++) {
 				const DpWork& d = c->dps[j];
 				const uint64_t k = pb[i] + j;
 				bt2x_dp_in p = d.in;
 				p.read_off = p.qual_off = qb[i] + (d.key.fw ? 0 : L);
 				p.ref_off = fb[k];
-				std::copy(d.window.begin(), d.window.end(), refs.begin() + (long)fb[k]);
-				in[k] = p;
+				ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, b_refs_.data() + fb[k]);
+				b_dp_in_[k] = p;
 			}
 		}
-		std::vector<bt2x_dp_out> out;
-		std::vector<bt2x_aln_rec> recs;
-		std::vector<uint32_t> edits;
-		be_.dp_align(reads, quals, refs, in, out, recs, edits);
+		be_.dp_align(b_reads_, b_quals_, b_refs_, b_dp_in_, b_dp_out_, b_recs_, b_edits_);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nwd; i++) {
-			for(size_t j = 0; j < wd[i]->dps.size(); j++) {
+			ReadCtx* c = wd[i];
+			for(size_t j = 0; j < c->dps.size(); j++) {
 				const uint64_t k = pb[i] + j;
-				DpResult& r = wd[i]->dps[j].res;
-				r.out = out[k];
-				r.recs.assign(recs.begin() + out[k].rec_off, recs.begin() + out[k].rec_off + out[k].nrec);
-				// gather each record's edit-buffer image (arena offsets are allocated by the
-				// kernel's atomics, so one problem's images are not contiguous)
-				r.edits.clear();
-				for(bt2x_aln_rec& a : r.recs) {
-					const uint32_t o = (uint32_t)r.edits.size();
-					r.edits.insert(r.edits.end(), edits.begin() + a.edit_off, edits.begin() + a.edit_off + a.nbuf);
-					a.edit_off = o;
+				const bt2x_dp_out& o = b_dp_out_[k];
+				DpMemo m;
+				m.key = c->dps[j].key;
+				m.out = o;
+				m.rec0 = (uint32_t)c->recs.size();
+				c->memo.push_back(m);
+				// each record's edit-buffer image moves to the read's edit arena (arena
+				// offsets are allocated by the kernel's atomics, so one problem's images are
+				// not contiguous)
+				for(uint32_t q = 0; q < o.nrec; q++) {
+					bt2x_aln_rec a = b_recs_[o.rec_off + q];
+					const uint32_t eo = (uint32_t)c->edits.size();
+					c->edits.insert(c->edits.end(), b_edits_.begin() + a.edit_off, b_edits_.begin() + a.edit_off + a.nbuf);
+					a.edit_off = eo;
+					c->recs.push_back(a);
 				}
 			}
 		}
@@ -974,20 +942,167 @@ bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st, int threads) {
 	return true;
 }
 
-RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads) {
+namespace {
+// Finished records by read id until they can be written in input order.
+class OutRing {
+public:
+	OutRing() : slot_(1 << 12), ready_(1 << 12, 0) {}
+	// make room for ids below `end`
+	void reserve(uint64_t end) {
+		if(end - base_ <= slot_.size()) return;
+		size_t cap = slot_.size();
+		while(end - base_ > cap) cap *= 2;
+		std::vector<std::string> s(cap);
+		std::vector<uint8_t> r(cap, 0);
+		for(uint64_t id = base_; id < base_ + slot_.size(); id++) {
+			s[id & (cap - 1)].swap(slot_[id & (slot_.size() - 1)]);
+			r[id & (cap - 1)] = ready_[id & (slot_.size() - 1)];
+		}
+		slot_.swap(s); ready_.swap(r);
+	}
+	// hand over read id's record (the caller gets back an empty buffer with capacity)
+	void put(uint64_t id, std::string& rec) {
+		const size_t k = id & (slot_.size() - 1);
+		slot_[k].swap(rec);
+		rec.clear();
+		ready_[k] = 1;
+	}
+	template<class F> void drain(F&& write) {
+		for(;;) {
+			const size_t k = base_ & (slot_.size() - 1);
+			if(!ready_[k]) return;
+			write(slot_[k]);
+			slot_[k].clear();
+			ready_[k] = 0;
+			base_++;
+		}
+	}
+private:
+	std::vector<std::string> slot_;
+	std::vector<uint8_t> ready_;
+	uint64_t base_ = 0;
+};
+
+// SAM output off the scheduler's thread: records are appended to 4 MiB chunks that a
+// writer thread fwrites in order.
+class SamWriter {
+public:
+	explicit SamWriter(std::FILE* f) : f_(f), th_([this] { loop(); }) { cur_.reserve(kChunk + 4096); }
+	~SamWriter() { finish(); }
+	void append(const std::string& rec) {
+		cur_ += rec;
+		if(cur_.size() >= kChunk) flush();
+	}
+	void finish() {
+		if(!th_.joinable()) return;
+		flush();
+		{ std::lock_guard<std::mutex> g(mu_); stop_ = true; }
+		cv_.notify_all();
+		th_.join();
+	}
+private:
+	static constexpr size_t kChunk = 4u << 20;
+	void flush() {
+		if(cur_.empty()) return;
+		std::string next;
+		{
+			std::unique_lock<std::mutex> g(mu_);
+			full_.push_back(std::move(cur_));
+			if(!spare_.empty()) { next = std::move(spare_.back()); spare_.pop_back(); }
+		}
+		cv_.notify_all();
+		cur_ = std::move(next);
+		cur_.clear();
+		cur_.reserve(kChunk + 4096);
+	}
+	void loop() {
+		for(;;) {
+			std::string buf;
+			{
+				std::unique_lock<std::mutex> g(mu_);
+				cv_.wait(g, [&] { return stop_ || !full_.empty(); });
+				if(full_.empty()) return;
+				buf = std::move(full_.front());
+				full_.pop_front();
+			}
+			std::fwrite(buf.data(), 1, buf.size(), f_);
+			buf.clear();
+			std::lock_guard<std::mutex> g(mu_);
+			if(spare_.size() < 4) spare_.push_back(std::move(buf));
+		}
+	}
+	std::FILE* f_;
+	std::string cur_;
+	std::mutex mu_;
+	std::condition_variable cv_;
+	std::deque<std::string> full_;
+	std::vector<std::string> spare_;
+	bool stop_ = false;
+	std::thread th_;
+};
+
+void count(RunStats& st, const ReadCtx* c) {
+	st.reads++;
+	if(c->aligned) st.aligned++; else st.unaligned++;
+	if(c->repetitive) st.rep++;
+	st.dps_used += c->ndp_used;
+	st.tight_recs += c->ntight;
+}
+}
+
+ReadCtx* Aligner::take_ctx() {
+	if(free_.empty()) {
+		pool_.emplace_back(new ReadCtx);
+		return pool_.back().get();
+	}
+	ReadCtx* c = free_.back();
+	free_.pop_back();
+	return c;
+}
+
+Aligner::~Aligner() {
+	// contexts hold tens of buffers each: release them in parallel
+	const long n = (long)pool_.size();
+#pragma omp parallel for schedule(static, 256)
+	for(long i = 0; i < n; i++) pool_[(size_t)i].reset();
+}
+
+// Retire the finished reads of `act` (their records go to the ring, their contexts back
+// to the pool); the others stay in `act`.
+void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, void* ringp) {
+	OutRing& ring = *static_cast<OutRing*>(ringp);
+	size_t w = 0;
+	for(ReadCtx* c : act) {
+		if(c->done) {
+			c->task.h.destroy();
+			c->task.h = nullptr;
+			c->done = false;
+			count(st, c);
+			ring.put(c->rd.rdid, c->sam);
+			free_.push_back(c);
+		} else {
+			act[w++] = c;
+		}
+	}
+	act.resize(w);
+}
+
+RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads, double* t_run) {
 	RunStats st;
+	const double t_start = now_s();
 	const std::string hdr = header();
 	std::fwrite(hdr.data(), 1, hdr.size(), out);
 	uint64_t rdid = 0;
 	bool eof = false;
-	std::vector<std::unique_ptr<ReadCtx>> window;   // reads in input order, not yet written
-	size_t head = 0;                                // first unwritten read in `window`
-	std::vector<ReadCtx*> act;
+	std::vector<ReadCtx*> act, fresh;
+	std::vector<FastqReader::Raw> raw;
+	OutRing ring;
+	SamWriter writer(out);
+	if(slots < 1) slots = 1;
 	while(true) {
 		// refill the pool
 		double t0 = now_s();
-		std::vector<ReadCtx*> fresh;
-		std::vector<FastqReader::Raw> raw;
+		raw.clear();
 		if(!eof && act.size() < slots) {
 			const size_t want = slots - act.size();
 			if(fq.take(want, raw) < want) eof = true;
@@ -997,10 +1112,9 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		if(nf) {
 			t0 = now_s();
 			fresh.resize((size_t)nf);
-			for(long i = 0; i < nf; i++) {
-				window.emplace_back(new ReadCtx());
-				fresh[(size_t)i] = window.back().get();
-			}
+			for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
+			ring.reserve(rdid + (uint64_t)nf);
+			st.t_alloc += now_s() - t0;
 			// decode + run each new read up to its first request, in parallel
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
 			for(long i = 0; i < nf; i++) {
@@ -1014,76 +1128,50 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			act.insert(act.end(), fresh.begin(), fresh.end());
 		}
 		if(act.empty()) break;
-		step(act, st, threads);
-		// retire finished reads; write records in input order
-		std::vector<ReadCtx*> still;
-		still.reserve(act.size());
-		for(ReadCtx* c : act) {
-			if(c->task.h.done()) {
-				c->task.h.destroy();
-				c->task.h = nullptr;
-			} else {
-				still.push_back(c);
-			}
-		}
-		act.swap(still);
 		t0 = now_s();
-		while(head < window.size() && window[head] && !window[head]->task.h) {
-			ReadCtx* c = window[head].get();
-			std::fwrite(c->sam.data(), 1, c->sam.size(), out);
-			st.reads++;
-			if(c->aligned) st.aligned++; else st.unaligned++;
-			if(c->repetitive) st.rep++;
-			st.dps_used += c->ndp_used;
-			st.tight_recs += c->ntight;
-			window[head].reset();
-			head++;
-		}
-		if(head > (1u << 16) && head * 2 > window.size()) {
-			window.erase(window.begin(), window.begin() + (long)head);
-			head = 0;
-		}
+		step(act, st, threads);
+		st.t_step += now_s() - t0;
+		t0 = now_s();
+		retire(act, st, &ring);
+		ring.drain([&](const std::string& s) { writer.append(s); });
 		st.t_io += now_s() - t0;
 	}
+	writer.finish();
+	if(t_run) *t_run = now_s() - t_start;
+#ifdef BT2X_PHASE_PROF
+	ph_print();
+#endif
 	return st;
 }
 
 std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threads, RunStats* stp) {
 	RunStats st;
-	std::vector<std::unique_ptr<ReadCtx>> ctx(reads.size());
+	std::vector<ReadCtx*> act, fresh;
+	OutRing ring;
 	std::string out;
-	size_t next = 0, head = 0;
-	std::vector<ReadCtx*> act;
+	size_t next = 0;
+	if(slots < 1) slots = 1;
 	while(true) {
-		std::vector<ReadCtx*> fresh;
+		fresh.clear();
 		while(next < reads.size() && act.size() + fresh.size() < slots) {
-			ctx[next].reset(new ReadCtx());
-			ctx[next]->rd = reads[next];
-			ctx[next]->task = align_read(ctx[next].get());
-			fresh.push_back(ctx[next].get());
+			ReadCtx* c = take_ctx();
+			c->rd = reads[next];
+			c->rd.rdid = next;
+			fresh.push_back(c);
 			next++;
 		}
+		ring.reserve(next);
 		const long nf = (long)fresh.size();
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-		for(long i = 0; i < nf; i++) fresh[i]->task.h.resume();
+		for(long i = 0; i < nf; i++) {
+			fresh[i]->task = align_read(fresh[i]);
+			fresh[i]->task.h.resume();
+		}
 		act.insert(act.end(), fresh.begin(), fresh.end());
 		if(act.empty()) break;
 		step(act, st, threads);
-		std::vector<ReadCtx*> still;
-		for(ReadCtx* c : act) {
-			if(c->task.h.done()) { c->task.h.destroy(); c->task.h = nullptr; }
-			else still.push_back(c);
-		}
-		act.swap(still);
-		while(head < next && !ctx[head]->task.h) {
-			out += ctx[head]->sam;
-			st.reads++;
-			if(ctx[head]->aligned) st.aligned++; else st.unaligned++;
-			st.dps_used += ctx[head]->ndp_used;
-			st.tight_recs += ctx[head]->ntight;
-			ctx[head].reset();
-			head++;
-		}
+		retire(act, st, &ring);
+		ring.drain([&](const std::string& s) { out += s; });
 	}
 	if(stp) *stp = st;
 	return out;

@@ -17,6 +17,10 @@
 // launch.  Per-read state (RNG, seen diagonals, redundancy sets, -M tightening, limits)
 // never crosses reads, so batching preserves the reference's results read by read.
 //
+// Host throughput: a read's state lives in a pooled ReadCtx whose buffers keep their
+// capacity from one read to the next (the coroutine frame too, ReadCtx::frame_), so the
+// steady state allocates almost nothing per read; DP results sit in per-read arenas.
+//
 // Host semantics restated here (file:line of the reference):
 //   RandomSource            random_source.h:34-140
 //   Random1toN              random_util.h:32-230
@@ -37,14 +41,16 @@
 #include <cctype>
 #include <cmath>
 #include <coroutine>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
+#include <new>
 #include <stdexcept>
 #include <string>
-#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -144,6 +150,31 @@ private:
 	std::vector<uint16_t> list_, seen_;
 };
 
+// Random1toN over the ranges extendSeeds walks.  prioritizeSATups keeps whole only the
+// ranges of at most nsm = 5 elements and samples larger ones element by element
+// (aligner_sw_driver.cpp:176-257), so every range the walk draws from has <= 5 elements:
+// swap-list mode (n < 128) with inline storage, trivially copyable (the DP lookahead
+// copies the walk).
+struct SmallRandom1toN {
+	static constexpr uint32_t kMax = 8;
+	uint8_t n = 0, cur = 0;
+	uint8_t list[kMax] = {};
+	void init(uint32_t nn) {
+		if(nn > kMax) throw std::logic_error("SmallRandom1toN: range larger than prioritizeSATups keeps whole");
+		n = (uint8_t)nn; cur = 0;
+	}
+	uint16_t next(Rng& rnd) {
+		if(cur == 0) {
+			if(n == 1) { cur = 1; return 0; }
+			for(uint8_t i = 0; i < n; i++) list[i] = i;
+		}
+		const uint32_t r = cur + rnd.nextU32() % (uint32_t)(n - cur);
+		if(r != cur) std::swap(list[cur], list[r]);
+		return list[cur++];
+	}
+	bool done() const { return n > 0 && cur >= n; }
+};
+
 // ------------------------------------------------------------ coordinates & intervals
 
 struct Coord {                      // ref_coord.h Coord: order (ref, orient, off)
@@ -166,76 +197,55 @@ struct Interval {                   // ref_coord.h Interval
 	int64_t len = 0;
 	Interval() = default;
 	Interval(const Coord& u, int64_t l) : up(u), len(l) {}
-	bool operator<(const Interval& o) const {
-		if(up < o.up) return true;
-		if(up > o.up) return false;
-		return len < o.len;
-	}
-	Coord downstream() const { Coord c = up; c.off += len; return c; }
 	bool contains(const Coord& c) const {
 		return c.ref == up.ref && c.orient == up.orient && c.off >= up.off && c.off < up.off + len;
 	}
 };
 
-// EIvalMergeList (ival_list.h): 16 unsorted intervals, then sort + merge on flush.
-class IvalMergeList {
+// SwDriver::seenDiags1_ (EIvalMergeListBinned over EIvalMergeList, ival_list.h).  The
+// driver only ever asks locusPresent(), i.e. membership in the union of the intervals
+// added so far: the reference's sort + merge of every 16 unsorted adds (and its 128 bins
+// by reference id) keep exactly that union.  One flat list does the same: an unsorted
+// tail of up to 16 intervals, then a sorted run of disjoint merged intervals searched by
+// bisection.  Two vectors of PODs, so the DP lookahead's copy reuses capacity.
+class SeenDiags {
 public:
+	void clear() { sorted_.clear(); tail_.clear(); }
 	void add(const Interval& i) {
-		if(unsorted_.size() < 16) unsorted_.push_back(i);
-		if(unsorted_.size() == 16) flush();
+		tail_.push_back(i);
+		if(tail_.size() == 16) flush();
 	}
-	bool locusPresent(const Coord& loc) const {
-		for(const Interval& iv : unsorted_) if(iv.contains(loc)) return true;
+	bool locusPresent(const Coord& c) const {
+		for(const Interval& iv : tail_) if(iv.contains(c)) return true;
 		if(sorted_.empty()) return false;
-		const size_t beg = (size_t)(std::lower_bound(lhs_.begin(), lhs_.end(), loc) - lhs_.begin());
-		if(beg == lhs_.size() || lhs_[beg] > loc) {
-			if(beg == 0) return false;
-			return sorted_[beg - 1].contains(loc);
+		// last interval whose start is <= c
+		size_t lo = 0, hi = sorted_.size();
+		while(lo < hi) {
+			const size_t mid = (lo + hi) >> 1;
+			if(c < sorted_[mid].up) hi = mid; else lo = mid + 1;
 		}
-		return true;
+		return lo > 0 && sorted_[lo - 1].contains(c);
 	}
 private:
 	void flush() {
-		for(const Interval& iv : unsorted_) sorted_.push_back(iv);
-		std::stable_sort(sorted_.begin(), sorted_.end());
-		size_t nmerged = 0;
-		for(size_t i = 1; i < sorted_.size(); i++) {
-			if(sorted_[i - 1].downstream() >= sorted_[i].up) {
-				nmerged++;
-				const Coord up = std::min(sorted_[i - 1].up, sorted_[i].up);
-				const Coord dn = std::max(sorted_[i - 1].downstream(), sorted_[i].downstream());
-				sorted_[i].up = up;
-				sorted_[i].len = dn.off - up.off;
-				sorted_[i - 1] = Interval();
+		sorted_.insert(sorted_.end(), tail_.begin(), tail_.end());
+		tail_.clear();
+		std::sort(sorted_.begin(), sorted_.end(), [](const Interval& a, const Interval& b) { return a.up < b.up; });
+		size_t w = 0;
+		for(size_t i = 0; i < sorted_.size(); i++) {
+			const Interval& iv = sorted_[i];
+			if(w > 0) {
+				Interval& p = sorted_[w - 1];
+				if(p.up.ref == iv.up.ref && p.up.orient == iv.up.orient && iv.up.off <= p.up.off + p.len) {
+					p.len = std::max(p.up.off + p.len, iv.up.off + iv.len) - p.up.off;
+					continue;
+				}
 			}
+			sorted_[w++] = iv;
 		}
-		std::stable_sort(sorted_.begin(), sorted_.end());
-		sorted_.resize(sorted_.size() - nmerged);
-		lhs_.clear();
-		for(const Interval& iv : sorted_) lhs_.push_back(iv.up);
-		unsorted_.clear();
+		sorted_.resize(w);
 	}
-	std::vector<Interval> sorted_, unsorted_;
-	std::vector<Coord> lhs_;
-};
-
-// EIvalMergeListBinned: 128 bins by reference id; bins are created on first use.
-class SeenDiags {
-public:
-	void clear() { bins_.clear(); }
-	void add(const Interval& i) { bin((uint32_t)(i.up.ref & 127), true)->add(i); }
-	bool locusPresent(const Coord& c) const {
-		const IvalMergeList* b = const_cast<SeenDiags*>(this)->bin((uint32_t)(c.ref & 127), false);
-		return b != nullptr && b->locusPresent(c);
-	}
-private:
-	IvalMergeList* bin(uint32_t k, bool create) {
-		for(auto& p : bins_) if(p.first == k) return &p.second;
-		if(!create) return nullptr;
-		bins_.emplace_back(k, IvalMergeList());
-		return &bins_.back().second;
-	}
-	std::vector<std::pair<uint32_t, IvalMergeList>> bins_;
+	std::vector<Interval> sorted_, tail_;
 };
 
 // ----------------------------------------------------------------------- alignments
@@ -247,100 +257,83 @@ inline char e_chr(uint32_t e) { return BT2X_EDIT_CHR(e); }
 inline uint32_t e_setpos(uint32_t e, uint32_t p) { return (e & ~0x3ffu) | (p & 0x3ffu); }
 
 // Edit::invertPoss(edits, sz, sort=false) (edit.cpp:50-80): reverse, then mirror pos.
-inline std::vector<uint32_t> invert_poss(const std::vector<uint32_t>& ed, size_t sz) {
-	std::vector<uint32_t> out(ed.rbegin(), ed.rend());
+inline void invert_poss(const uint32_t* ed, size_t n, size_t sz, std::vector<uint32_t>& out) {
+	out.assign(ed, ed + n);
+	std::reverse(out.begin(), out.end());
 	for(uint32_t& e : out) {
 		const uint32_t p = e_pos(e);
 		e = e_setpos(e, (uint32_t)(sz - p - (e_type(e) == ET_READ_GAP ? 0 : 1)));
 	}
-	return out;
 }
 
-// AlnScore: only the score orders alignments (aligner_result.h:57-255).
-struct AlnRes {                     // the AlnRes fields the unpaired SAM path reads
+// A reported alignment as the sink keeps it: AlnScore orders by score only
+// (aligner_result.h:57-255); its edits are printed from the read's shared edit buffer
+// (SURVEY F11), so only their count is kept.
+struct AlnRes {
 	int64_t score = 0;
-	int bases_aligned = 0;
 	int64_t refid = 0, refoff = 0;
 	bool fw = true;
-	size_t rdlen = 0;               // rdexrows_ (end-to-end: the whole read)
-	size_t refns = 0;
-	std::vector<uint32_t> ned;      // edits in ned() order (5'-relative after invertEdits)
+	uint32_t nedit = 0;
+	uint32_t refns = 0;
 };
 
-// RedundantAlns (aligner_result.cpp:821-914): DP cells already used by an alignment.
-// The reference keeps one ESet per read row; here one open-addressing set of
-// (ref, strand, column, row) cells, empty (and never walked) until the first add.
+// RedundantAlns (aligner_result.cpp:821-914): DP cells (ref, strand, row, ref offset)
+// already used by a reported alignment.  A reported alignment's cells in row i are the
+// contiguous reference run [left_i, right_i), so it is kept as one run per row; a new
+// alignment overlaps iff on some row its run intersects the run of an earlier one on
+// the same reference and strand.
 class RedundantAlns {
 public:
-	void init(size_t) { slots_.clear(); n_ = 0; }
-	void add(const AlnRes& r) { walk(r, true); }
-	bool overlap(const AlnRes& r) { return n_ != 0 && walk(r, false); }
-private:
-	// one cell in 16 bytes: reference offset, and (ref id, row, strand) packed; kEmpty marks a
-	// free slot (ref ids < 2^40, rows < 2^11)
-	struct Cell { int64_t rfoff = 0; uint64_t tag = kEmpty; };
-	static constexpr uint64_t kEmpty = ~0ULL;
-	static uint64_t tag_of(int64_t rfid, bool fw, uint32_t row) {
-		return ((uint64_t)rfid << 12) | ((uint64_t)row << 1) | (fw ? 1u : 0u);
-	}
-	static uint64_t hash(int64_t rfoff, uint64_t tag) {
-		uint64_t z = (uint64_t)rfoff * 0x9e3779b97f4a7c15ULL ^ tag;
-		z ^= z >> 29; z *= 0xbf58476d1ce4e5b9ULL; z ^= z >> 32;
-		return z;
-	}
-	bool find_or_insert(int64_t rfid, bool fw, int64_t rfoff, uint32_t row, bool insert) {
-		return probe(rfoff, tag_of(rfid, fw, row), insert);
-	}
-	bool probe(int64_t rfoff, uint64_t tag, bool insert) {
-		if(slots_.empty()) { if(!insert) return false; slots_.resize(256); }
-		else if(insert && (n_ + 1) * 2 > slots_.size()) {
-			std::vector<Cell> old;
-			old.swap(slots_);
-			slots_.resize(old.size() * 2);
-			n_ = 0;
-			for(const Cell& c : old) if(c.tag != kEmpty) probe(c.rfoff, c.tag, true);
-		}
-		const size_t mask = slots_.size() - 1;
-		for(size_t h = hash(rfoff, tag) & mask;; h = (h + 1) & mask) {
-			Cell& c = slots_[h];
-			if(c.tag == kEmpty) {
-				if(insert) { c.rfoff = rfoff; c.tag = tag; n_++; }
-				return false;
+	void init(size_t rdlen) { rdlen_ = rdlen; alns_.clear(); runs_.clear(); }
+	// ned: the alignment's own edits in ned() order (5'-relative for rc)
+	bool overlap(const AlnRes& r, const uint32_t* ned, size_t n) {
+		if(alns_.empty()) return false;
+		rows(r, ned, n, tmp_);
+		for(const Aln& a : alns_) {
+			if(a.refid != r.refid || a.fw != r.fw) continue;
+			const int64_t* o = runs_.data() + a.run0;
+			for(size_t i = 0; i < rdlen_; i++) {
+				const int64_t l = std::max(o[2 * i], tmp_[2 * i]), rr = std::min(o[2 * i + 1], tmp_[2 * i + 1]);
+				if(l < rr) return true;
 			}
-			if(c.tag == tag && c.rfoff == rfoff) return true;
 		}
+		return false;
 	}
-	bool walk(const AlnRes& r, bool insert) {
+	void add(const AlnRes& r, const uint32_t* ned, size_t n) {
+		rows(r, ned, n, tmp_);
+		alns_.push_back({r.refid, r.fw, runs_.size()});
+		runs_.insert(runs_.end(), tmp_.begin(), tmp_.end());
+	}
+private:
+	struct Aln { int64_t refid; bool fw; size_t run0; };
+	void rows(const AlnRes& r, const uint32_t* ned0, size_t n, std::vector<int64_t>& out) {
+		const uint32_t* ned = ned0;
+		if(!r.fw) { invert_poss(ned0, n, rdlen_, inv_); ned = inv_.data(); }
+		out.resize(2 * rdlen_);
 		int64_t left = r.refoff, right;
-		const size_t len = r.rdlen;
-		std::vector<uint32_t> inv;
-		if(!r.fw) inv = invert_poss(r.ned, r.rdlen);
-		const std::vector<uint32_t>& ned = r.fw ? r.ned : inv;
 		size_t ni = 0;
-		for(size_t i = 0; i < len; i++) {
+		for(size_t i = 0; i < rdlen_; i++) {
 			size_t diff = 1;
 			right = left + 1;
-			while(ni < ned.size() && e_pos(ned[ni]) == i) {
+			while(ni < n && e_pos(ned[ni]) == i) {
 				if(e_type(ned[ni]) == ET_REF_GAP) diff = 0;
 				ni++;
 			}
-			if(i < len - 1) {
+			if(i < rdlen_ - 1) {
 				size_t nn = ni;
-				while(nn < ned.size() && e_pos(ned[nn]) == i + 1) {
+				while(nn < n && e_pos(ned[nn]) == i + 1) {
 					if(e_type(ned[nn]) == ET_READ_GAP) right++;
 					nn++;
 				}
 			}
-			for(int64_t j = left; j < right; j++) {
-				const bool found = find_or_insert(r.refid, r.fw, j, (uint32_t)i, insert);
-				if(!insert && found) return true;
-			}
-			left = right + diff - 1;
+			out[2 * i] = left; out[2 * i + 1] = right;
+			left = right + (int64_t)diff - 1;
 		}
-		return false;
 	}
-	std::vector<Cell> slots_;
-	size_t n_ = 0;
+	size_t rdlen_ = 0;
+	std::vector<Aln> alns_;
+	std::vector<int64_t> runs_, tmp_;
+	std::vector<uint32_t> inv_;
 };
 
 // ------------------------------------------------------------------------ parameters
@@ -472,16 +465,18 @@ public:
 		}
 		return k;
 	}
+	// decodes into r, reusing its buffers
 	static void decode(const Raw& raw, Read& r, uint64_t rdid, uint32_t randSeed) {
 		if(raw.l[0][0] != '@') throw std::runtime_error("FASTQ record does not start with '@'");
-		r = Read();
 		r.rdid = rdid;
 		r.name.assign(raw.l[0] + 1, raw.n[0] - 1);
+		r.fw.clear();
 		r.fw.reserve(raw.n[1]);
 		for(size_t i = 0; i < raw.n[1]; i++) {
 			const unsigned char c = (unsigned char)(raw.l[1][i] == '.' ? 'N' : raw.l[1][i]);
 			if(std::isalpha(c)) r.fw.push_back(kAsc2Dna[c]);
 		}
+		r.qual.clear();
 		if(raw.n[1] || raw.n[3]) r.qual.assign(raw.l[3], raw.n[3]);
 		if(r.qual.size() != r.fw.size())
 			throw std::runtime_error("read " + r.name + ": qualities and sequence differ in length");
@@ -533,14 +528,6 @@ private:
 
 // -------------------------------------------------------------- GPU requests
 
-struct SeedWork {                   // one seed round of one read
-	std::vector<bt2x_seed_in> in;   // read_off: 0 = patFw, rdlen = patRc
-	std::vector<bt2x_seed_out> out;
-};
-struct ResolveWork {
-	std::vector<bt2x_resolve_in> in;
-	std::vector<bt2x_resolve_out> out;
-};
 // A DP problem of one read is fixed by its rectangle and floor: the read, its
 // qualities and the N ceiling do not change within the read, and the kernel draws no
 // random numbers (it reports how many the reference's backtrace draws, bt2x.h).  So a
@@ -554,27 +541,21 @@ struct DpKey {
 		       corel == o.corel && corer == o.corer && fw == o.fw;
 	}
 };
-struct DpKeyHash {
-	size_t operator()(const DpKey& k) const {
-		uint64_t z = (uint64_t)k.refl * 0x9e3779b97f4a7c15ULL ^ ((uint64_t)k.tidx << 32) ^ ((uint64_t)k.minsc << 16) ^
-		             ((uint64_t)k.ncol << 1) ^ (k.fw ? 1u : 0u) ^ ((uint64_t)k.triml << 40) ^ ((uint64_t)k.corel << 48);
-		z ^= z >> 29; z *= 0xbf58476d1ce4e5b9ULL; z ^= z >> 32;
-		return (size_t)z;
-	}
-};
-struct DpResult {                   // SwAligner::align + its nextAlignment sequence
+// One memoised DP result: align()'s outcome and its nextAlignment records, which live in
+// the read's arenas (ReadCtx::recs; their edit_off index ReadCtx::edits).
+struct DpMemo {
+	DpKey key;
 	bt2x_dp_out out;
-	std::vector<bt2x_aln_rec> recs; // edit_off relative to `edits`
-	std::vector<uint32_t> edits;    // each record's edit-buffer image (nbuf entries)
+	uint32_t rec0 = 0;
 };
-struct DpWork {                     // one posed problem
+struct DpWork {                     // one posed problem (its window is fetched at gather)
 	DpKey key;
 	bt2x_dp_in in;                  // read_off / qual_off / ref_off are set by the scheduler
-	std::vector<uint8_t> window;
-	DpResult res;
 };
 
 enum ReqKind { REQ_NONE = 0, REQ_SEED = 1, REQ_RESOLVE = 2, REQ_DP = 3 };
+
+struct ReadCtx;
 
 struct ReadTask {
 	struct promise_type {
@@ -583,11 +564,13 @@ struct ReadTask {
 		std::suspend_always final_suspend() noexcept { return {}; }
 		void return_void() {}
 		void unhandled_exception() { throw; }
+		// the frame lives in the read's pooled context (Aligner::align_read(ReadCtx*))
+		template<class Self> static void* operator new(std::size_t sz, Self&, ReadCtx* c);
+		static void operator delete(void* p, std::size_t sz);
 	};
 	std::coroutine_handle<promise_type> h;
 };
 
-struct ReadCtx;
 struct Awaiter {
 	ReadCtx* c;
 	int kind;
@@ -603,20 +586,178 @@ struct Prm {
 	int64_t bestLtMinscMate1 = std::numeric_limits<int64_t>::min();
 };
 
+// SATupleAndPos (aligner_sw_driver.h:118-180)
+struct SatPos {
+	uint64_t topf = 0, size = 0;    // SATuple: BW top and #elements (offs.size())
+	uint64_t key = 0;               // identity of the cache entry (its BW top)
+	uint8_t nlex = 0;
+	uint64_t origSz = 0;
+	bool fw = true;                 // SeedPos
+	uint32_t offidx = 0, rdoff = 0, seedlen = 0;
+	bool operator<(const SatPos& o) const {
+		if(size != o.size) return size < o.size;
+		if(topf != o.topf) return topf < o.topf;
+		if(offidx != o.offidx) return offidx < o.offidx;
+		if(rdoff != o.rdoff) return rdoff < o.rdoff;
+		if(seedlen != o.seedlen) return seedlen < o.seedlen;
+		return fw && !o.fw;
+	}
+};
+
+struct ExtendRange { size_t off, len, sz; };
+
+// RowSampler (aligner_sw_driver.h:176-267), lensq = szsq = true
+struct RowSampler {
+	double mass = 0;
+	std::vector<double> masses;
+	std::vector<uint8_t> elim;
+	void init(const std::vector<SatPos>& sl, size_t sai, size_t saf) {
+		elim.assign(saf - sai, 0);
+		mass = 0.0f;
+		masses.assign(saf - sai, 0.0);
+		for(size_t i = sai; i < saf; i++) {
+			double num = (double)(sl[i].nlex + 1);
+			num *= num;
+			double den = (double)sl[i].size;
+			den *= den;
+			masses[i - sai] = num / den;
+			mass += masses[i - sai];
+		}
+	}
+	void finishedRange(size_t i) { elim[i] = 1; mass -= masses[i]; }
+	size_t next(Rng& rnd) {
+		const double rd = rnd.nextFloat() * mass;
+		double sofar = 0.0f;
+		size_t last = std::numeric_limits<size_t>::max();
+		for(size_t i = 0; i < masses.size(); i++) {
+			if(!elim[i]) {
+				last = i;
+				sofar += masses[i];
+				if(rd < sofar) return i;
+			}
+		}
+		return last;
+	}
+};
+
+// The candidate walk of extendSeeds (aligner_sw_driver.cpp:278-631) as a resumable
+// iterator: next() runs the loop up to its next DP problem (PROBLEM, the problem's key)
+// or to the loop's exit (an EXTEND_* code); failed() applies a DP that found nothing.
+// The walk's own state (position, per-range samplers, elements left) is a value and the
+// per-read state it advances (RNG, limit metrics, seen diagonals) is bound by pointer,
+// so a copy bound to copies of those runs ahead of the real walk on the assumption
+// that every DP fails: the lookahead the scheduler batches (DpKey).
+class ExtendWalk {
+public:
+	static constexpr int PROBLEM = 0;
+	void reset(const Params& P, const std::vector<SatPos>& sat, const std::vector<uint32_t>& rand_ns,
+	           const std::vector<uint32_t>& firstRow, const std::vector<bt2x_resolve_out>& res, size_t nelt,
+	           size_t rdlen) {
+		P_ = &P; sat_ = &sat; firstRow_ = &firstRow; res_ = &res; neltLeft_ = nelt; rdlen_ = rdlen;
+		rands_.resize(sat.size());
+		for(size_t i = 0; i < sat.size(); i++) rands_[i].init(rand_ns[i]);
+		i_ = 0; first_ = true; inPass_ = false;
+	}
+	void bind(Rng* rnd, Prm* prm, SeenDiags* seen) { rnd_ = rnd; prm_ = prm; seen_ = seen; }
+	int next(int64_t minsc, DpKey& k);
+	// the DP of the last next() found no alignment; false: the fail streak ends the walk
+	bool failed() {
+		prm_->nExDps++; prm_->nExDpFails++; prm_->nDpFail++;
+		return prm_->nDpFail < P_->streak;
+	}
+private:
+	static constexpr uint64_t kNsm = 5;                          // prioritizeSATups' nsm
+	const Params* P_ = nullptr;
+	const std::vector<SatPos>* sat_ = nullptr;
+	const std::vector<uint32_t>* firstRow_ = nullptr;
+	const std::vector<bt2x_resolve_out>* res_ = nullptr;
+	size_t neltLeft_ = 0, rdlen_ = 0;
+	std::vector<SmallRandom1toN> rands_;
+	size_t i_ = 0;
+	bool first_ = true, inPass_ = false;
+	Rng* rnd_ = nullptr;
+	Prm* prm_ = nullptr;
+	SeenDiags* seen_ = nullptr;
+};
+
+// AlnSinkWrap for an unpaired read (aln_sink.cpp:583-643, 1395-1445) with its
+// ReportingState (aln_sink.cpp:33-210) under -k 1 -M mhits.
+struct Sink {
+	static constexpr int64_t kMinScore = std::numeric_limits<int64_t>::min();
+	enum { EXIT_DID_NOT_EXIT = 1, EXIT_SHORT_CIRCUIT_k, EXIT_SHORT_CIRCUIT_M, EXIT_SHORT_CIRCUIT_TRUMPED,
+	       EXIT_NO_ALIGNMENTS, EXIT_WITH_ALIGNMENTS };
+	int64_t mhits = 50;
+	std::vector<AlnRes> rs;
+	int64_t best = kMinScore, best2 = kMinScore;
+	uint64_t n = 0;
+	bool doneUnpair = false;
+	int exitUnpair = EXIT_DID_NOT_EXIT;
+	void reset(int64_t m) {
+		mhits = m; rs.clear(); best = best2 = kMinScore; n = 0; doneUnpair = false; exitUnpair = EXIT_DID_NOT_EXIT;
+	}
+	bool done() const { return doneUnpair; }            // doneConcord_/doneDiscord_ are true
+	bool report(const AlnRes& r) {
+		n++;
+		if(!doneUnpair && n > (uint64_t)mhits) { doneUnpair = true; exitUnpair = EXIT_SHORT_CIRCUIT_M; }
+		rs.push_back(r);
+		if(r.score > best) { best2 = best; best = r.score; }
+		else if(r.score > best2) best2 = r.score;
+		return done();
+	}
+	bool hasSecondBest() const { return best2 != kMinScore; }
+};
+
+// One read in flight: its input, its pending request and every per-read buffer of the
+// reference's per-slot objects (SwDriver, SeedResults, AlnSinkWrap, RandomSource).
+// Contexts are pooled: buffers keep their capacity from read to read.
 struct ReadCtx {
 	Read rd;
 	int req = REQ_NONE;
-	SeedWork seed;
-	ResolveWork resolve;
-	std::vector<DpWork> dps;        // the problems posed by the current DP request
-	std::string sam;                // the finished record(s)
+	// request payloads (gathered / scattered by the scheduler)
+	std::vector<bt2x_seed_in> seed_in;   // read_off: 0 = patFw, rdlen = patRc
+	std::vector<bt2x_seed_out> seed_out;
+	std::vector<bt2x_resolve_in> res_in;
+	std::vector<bt2x_resolve_out> res_out;
+	std::vector<DpWork> dps;             // the problems posed by the current DP request
+	// DP results of this read (memo by DpKey; records and edit images in arenas)
+	std::vector<DpMemo> memo;
+	std::vector<bt2x_aln_rec> recs;
+	std::vector<uint32_t> edits;
+	// seed round scratch
+	std::vector<std::pair<uint8_t, uint32_t>> seedIds;      // (fw, idx) of each searched seed
+	std::vector<std::pair<uint64_t, uint8_t>> cacheNlex;    // AlignmentCache: key -> nlex of the first add
+	SeedHitsHip hits;
+	std::vector<SatPos> satpos2, satpos;
+	std::vector<uint32_t> rand_ns, firstRow;
+	std::vector<ExtendRange> exRange[2];
+	RowSampler rows;
+	std::vector<Random1toN> prioRands;
+	// extendSeeds state
+	SeenDiags seenDiags, seen2;
+	ExtendWalk walk, ahead;
+	RedundantAlns redAnchor;
+	Sink sink;
+	std::vector<uint32_t> edbuf;         // SwDriver::resGap_.alres.ned_ storage
+	std::string sam;                     // the finished record
 	ReadTask task;
+	bool done = false;                   // finished, record not yet handed to the writer
 	// statistics for the run summary
 	bool aligned = false, repetitive = false;
 	uint64_t ndp_used = 0;          // DP results the walk consumed (the rest were lookahead)
 	uint64_t ntight = 0;            // nextAlignment records consumed after -M tightened minsc
 	                                // within the same DP problem
+	// the coroutine frame (ReadTask::promise_type::operator new)
+	static constexpr size_t kFrameBytes = 4096;
+	alignas(std::max_align_t) unsigned char frame_[kFrameBytes];
 };
+
+template<class Self>
+inline void* ReadTask::promise_type::operator new(std::size_t sz, Self&, ReadCtx* c) {
+	return sz <= ReadCtx::kFrameBytes ? static_cast<void*>(c->frame_) : ::operator new(sz);
+}
+inline void ReadTask::promise_type::operator delete(void* p, std::size_t sz) {
+	if(sz > ReadCtx::kFrameBytes) ::operator delete(p);
+}
 
 inline void Awaiter::await_suspend(std::coroutine_handle<>) noexcept { c->req = kind; }
 
@@ -641,24 +782,44 @@ struct RunStats {
 	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0;
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
 	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
-	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0;
+	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0;
 };
 
 class Aligner {
 public:
 	Aligner(const Params& p, const RefInfo& ref, Backend& be) : p_(p), ref_(ref), be_(be) {}
+	~Aligner();
+	Aligner(const Aligner&) = delete;
+	Aligner& operator=(const Aligner&) = delete;
 	// SAM header (@HD, @SQ; sam.cpp:47-80)
 	std::string header() const;
 	// Align every read of `fq`, writing SAM records in input order to `out`.
-	RunStats run(FastqReader& fq, std::FILE* out, size_t slots, int threads);
+	// t_run (optional): wall time of the run before its buffers are released
+	RunStats run(FastqReader& fq, std::FILE* out, size_t slots, int threads, double* t_run = nullptr);
 	// Align a vector of reads (tests); records in input order.
 	std::string align_all(std::vector<Read>& reads, size_t slots, int threads, RunStats* st = nullptr);
 private:
 	ReadTask align_read(ReadCtx* c);
 	bool step(std::vector<ReadCtx*>& active, RunStats& st, int threads);
+	ReadCtx* take_ctx();
+	void retire(std::vector<ReadCtx*>& act, RunStats& st, void* ring);
+	// pooled read contexts (kept across runs; released by the destructor)
+	std::vector<std::unique_ptr<ReadCtx>> pool_;
+	std::vector<ReadCtx*> free_;
 	const Params& p_;
 	const RefInfo& ref_;
 	Backend& be_;
+	// launch buffers, reused across steps
+	std::vector<uint8_t> b_reads_, b_quals_, b_refs_;
+	std::vector<uint64_t> b_off_, b_off2_, b_off3_;
+	std::vector<bt2x_seed_in> b_seed_in_;
+	std::vector<bt2x_seed_out> b_seed_out_;
+	std::vector<bt2x_resolve_in> b_res_in_;
+	std::vector<bt2x_resolve_out> b_res_out_;
+	std::vector<bt2x_dp_in> b_dp_in_;
+	std::vector<bt2x_dp_out> b_dp_out_;
+	std::vector<bt2x_aln_rec> b_recs_;
+	std::vector<uint32_t> b_edits_;
 };
 
 } // namespace host
