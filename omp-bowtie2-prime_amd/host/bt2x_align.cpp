@@ -179,6 +179,31 @@ void cigar_md(const Read& rd, bool fw, const uint32_t* ned0, size_t nedn, std::s
 	const std::vector<uint8_t>& s = fw ? rd.fw : rd.rc;
 	const uint32_t* ed = ned0;
 	if(!fw) { invert_poss(ned0, nedn, rd.length(), inv); ed = inv.data(); }
+	// Fast path: mismatches only, in increasing read order inside the read (no gap to
+	// left-align): the CIGAR is one M run and MD interleaves match runs and reference bases
+	// exactly as buildMdz/writeMdz do below.
+	{
+		bool simple = !s.empty();
+		for(size_t q = 0; q < nedn && simple; q++)
+			simple = e_type(ed[q]) == ET_MM && e_pos(ed[q]) < s.size() && (q == 0 || e_pos(ed[q]) > e_pos(ed[q - 1]));
+		if(simple) {
+			append_int(cig, s.size());
+			cig.push_back('M');
+			size_t prev = 0;
+			bool mm_last = false, first = true;
+			for(size_t q = 0; q < nedn; q++) {
+				const size_t p = e_pos(ed[q]);
+				if(p > prev) { append_int(md, p - prev); mm_last = false; first = false; }
+				if(mm_last || first) md.push_back('0');
+				md.push_back(e_chr(ed[q]));
+				mm_last = true; first = false;
+				prev = p + 1;
+			}
+			if(s.size() > prev) append_int(md, s.size() - prev);
+			else if(mm_last) md.push_back('0');
+			return;
+		}
+	}
 	ref.clear(); rel.clear(); rdc.clear();
 	size_t rdoff = 0;
 	static const char kAcgtn[] = "ACGTN";
@@ -486,8 +511,12 @@ int ExtendWalk::next(int64_t minsc, DpKey& k) {
 		const Coord refcoord(tidx, refoff, fw);
 		if(seen_->locusPresent(refcoord)) { prm_->nRedundants++; continue; }
 		// DynProgFramer::frameSeedExtensionRect, trimToRef (dp_framer.cpp:81-129)
-		const int readGaps = P.maxReadGaps(minsc), refGaps = P.maxRefGaps(minsc);
-		const size_t maxgap = std::min((size_t)std::max(readGaps, refGaps), P.maxhalf);
+		if(minsc != gapMinsc_) {
+			const int readGaps = P.maxReadGaps(minsc), refGaps = P.maxRefGaps(minsc);
+			maxgap_ = std::min((size_t)std::max(readGaps, refGaps), P.maxhalf);
+			gapMinsc_ = minsc;
+		}
+		const size_t maxgap = maxgap_;
 		const int64_t refl_pre = refoff - 2 * (int64_t)maxgap;
 		const int64_t refr_pre = refoff + ((int64_t)rdlen_ - 1) + 2 * (int64_t)maxgap;
 		size_t triml = 0, trimr = 0;
@@ -798,147 +827,164 @@ double now_s() {
 }
 }
 
-// One scheduler iteration: run the GPU launch for every request kind some read is
-// waiting on, then resume those reads (in parallel) until each waits again or finishes.
-// Returns false when no read is waiting.
-bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st, int threads) {
-	std::vector<ReadCtx*> ws, wr, wd;
-	for(ReadCtx* c : act) {
-		if(c->req == REQ_SEED) ws.push_back(c);
-		else if(c->req == REQ_RESOLVE) wr.push_back(c);
-		else if(c->req == REQ_DP) wd.push_back(c);
+// ----- one launch: gather a cohort's waiting requests, run them, scatter the results
+
+// Classify the cohort's reads by pending request and fill the launch's input buffers
+// (one seed, one resolve and one DP launch; gathers in parallel over reads).
+void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort, int threads) {
+	L.ws.clear(); L.wr.clear(); L.wd.clear();
+	for(ReadCtx* c : cohort) {
+		if(c->req == REQ_SEED) L.ws.push_back(c);
+		else if(c->req == REQ_RESOLVE) L.wr.push_back(c);
+		else if(c->req == REQ_DP) L.wd.push_back(c);
 	}
-	if(ws.empty() && wr.empty() && wd.empty()) return false;
-	static const bool trace = std::getenv("BT2X_TRACE") != nullptr;
-	if(trace) {
-		long rss = 0;
-		if(std::FILE* f = std::fopen("/proc/self/statm", "r")) { long a = 0; if(std::fscanf(f, "%ld %ld", &a, &rss) != 2) rss = 0; std::fclose(f); }
-		std::fprintf(stderr, "BT2X_TRACE active=%zu seed=%zu resolve=%zu dp=%zu rss_mb=%ld\n", act.size(), ws.size(),
-		             wr.size(), wd.size(), rss * 4096 / (1 << 20));
-	}
-	const long nws = (long)ws.size(), nwr = (long)wr.size(), nwd = (long)wd.size();
-	std::vector<uint64_t>& ob = b_off_;
-	std::vector<uint64_t>& ob2 = b_off2_;
+	const long nws = (long)L.ws.size(), nwr = (long)L.wr.size(), nwd = (long)L.wd.size();
 	if(nws) {
-		// one launch for every waiting read's seeds: patFw+patRc of each read, then its
-		// seeds with read_off rebased (gather/scatter in parallel over reads)
-		double t0 = now_s();
-		ob.assign(nws + 1, 0); ob2.assign(nws + 1, 0);
+		// patFw+patRc of each read, then its seeds with read_off rebased
+		L.sr.assign(nws + 1, 0); L.sk.assign(nws + 1, 0);
 		for(long i = 0; i < nws; i++) {
-			ob[i + 1] = ob[i] + 2 * ws[i]->rd.length();
-			ob2[i + 1] = ob2[i] + ws[i]->seed_in.size();
+			L.sr[i + 1] = L.sr[i] + 2 * L.ws[i]->rd.length();
+			L.sk[i + 1] = L.sk[i] + L.ws[i]->seed_in.size();
 		}
-		b_reads_.resize(ob[nws]);
-		b_seed_in_.resize(ob2[nws]);
+		L.seed_reads.resize(L.sr[nws]);
+		L.seed_in.resize(L.sk[nws]);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nws; i++) {
-			const ReadCtx* c = ws[i];
-			const size_t L = c->rd.length();
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), b_reads_.begin() + (long)ob[i]);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), b_reads_.begin() + (long)(ob[i] + L));
+			const ReadCtx* c = L.ws[i];
+			const size_t n = c->rd.length();
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.seed_reads.begin() + (long)L.sr[i]);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.seed_reads.begin() + (long)(L.sr[i] + n));
 			for(size_t k = 0; k < c->seed_in.size(); k++) {
-				bt2x_seed_in s = c->seed_in[k];
-				s.read_off += ob[i];
-				b_seed_in_[ob2[i] + k] = s;
+				bt2x_seed_in q = c->seed_in[k];
+				q.read_off += L.sr[i];
+				L.seed_in[L.sk[i] + k] = q;
 			}
 		}
-		be_.seed_search(b_reads_, b_seed_in_, b_seed_out_);
-#pragma omp parallel for schedule(static, 256) num_threads(threads)
-		for(long i = 0; i < nws; i++)
-			ws[i]->seed_out.assign(b_seed_out_.begin() + (long)ob2[i], b_seed_out_.begin() + (long)ob2[i + 1]);
-		st.seed_launches++; st.seeds += b_seed_in_.size(); st.t_seed += now_s() - t0;
 	}
 	if(nwr) {
-		double t0 = now_s();
-		ob.assign(nwr + 1, 0);
-		for(long i = 0; i < nwr; i++) ob[i + 1] = ob[i] + wr[i]->res_in.size();
-		b_res_in_.resize(ob[nwr]);
+		L.rk.assign(nwr + 1, 0);
+		for(long i = 0; i < nwr; i++) L.rk[i + 1] = L.rk[i] + L.wr[i]->res_in.size();
+		L.res_in.resize(L.rk[nwr]);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nwr; i++)
-			std::copy(wr[i]->res_in.begin(), wr[i]->res_in.end(), b_res_in_.begin() + (long)ob[i]);
-		be_.resolve(b_res_in_, b_res_out_);
-#pragma omp parallel for schedule(static, 256) num_threads(threads)
-		for(long i = 0; i < nwr; i++)
-			wr[i]->res_out.assign(b_res_out_.begin() + (long)ob[i], b_res_out_.begin() + (long)ob[i + 1]);
-		st.resolve_launches++; st.resolves += b_res_in_.size(); st.t_resolve += now_s() - t0;
+			std::copy(L.wr[i]->res_in.begin(), L.wr[i]->res_in.end(), L.res_in.begin() + (long)L.rk[i]);
 	}
 	if(nwd) {
-		double t0 = now_s();
-		// every waiting read's posed problems in one launch: the read's two orientations
-		// (codes and qualities) once per read, one reference window per problem
-		std::vector<uint64_t>& qb = ob;
-		std::vector<uint64_t>& pb = ob2;
-		std::vector<uint64_t>& fb = b_off3_;
-		qb.assign(nwd + 1, 0); pb.assign(nwd + 1, 0);
+		// the read's two orientations (codes and qualities) once per read, one reference
+		// window per posed problem (BitPairReference::getStretch)
+		L.qb.assign(nwd + 1, 0); L.pb.assign(nwd + 1, 0);
 		for(long i = 0; i < nwd; i++) {
-			qb[i + 1] = qb[i] + 2 * wd[i]->rd.length();
-			pb[i + 1] = pb[i] + wd[i]->dps.size();
+			L.qb[i + 1] = L.qb[i] + 2 * L.wd[i]->rd.length();
+			L.pb[i + 1] = L.pb[i] + L.wd[i]->dps.size();
 		}
-		const uint64_t np = pb[nwd];
-		fb.assign(np + 1, 0);
+		const uint64_t np = L.pb[nwd];
+		L.fb.assign(np + 1, 0);
 		for(long i = 0; i < nwd; i++)
-			for(size_t j = 0; j < wd[i]->dps.size(); j++)
-				fb[pb[i] + j + 1] = fb[pb[i] + j] + wd[i]->dps[j].key.ncol;
-		b_reads_.resize(qb[nwd]); b_quals_.resize(qb[nwd]); b_refs_.resize(fb[np]);
-		b_dp_in_.resize(np);
+			for(size_t j = 0; j < L.wd[i]->dps.size(); j++)
+				L.fb[L.pb[i] + j + 1] = L.fb[L.pb[i] + j] + L.wd[i]->dps[j].key.ncol;
+		L.dp_reads.resize(L.qb[nwd]); L.dp_quals.resize(L.qb[nwd]); L.dp_refs.resize(L.fb[np]);
+		L.dp_in.resize(np);
 #pragma omp parallel for schedule(static, 256) num_threads(threads)
 		for(long i = 0; i < nwd; i++) {
-			const ReadCtx* c = wd[i];
-			const size_t L = c->rd.length();
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), b_reads_.begin() + (long)qb[i]);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), b_reads_.begin() + (long)(qb[i] + L));
-			std::copy(c->rd.qual.begin(), c->rd.qual.end(), b_quals_.begin() + (long)qb[i]);
-			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), b_quals_.begin() + (long)(qb[i] + L));
+			const ReadCtx* c = L.wd[i];
+			const size_t n = c->rd.length();
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)L.qb[i]);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.dp_reads.begin() + (long)(L.qb[i] + n));
+			std::copy(c->rd.qual.begin(), c->rd.qual.end(), L.dp_quals.begin() + (long)L.qb[i]);
+			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), L.dp_quals.begin() + (long)(L.qb[i] + n));
 			for(size_t j = 0; j < c->dps.size(); j++) {
 				const DpWork& d = c->dps[j];
-				const uint64_t k = pb[i] + j;
-				bt2x_dp_in p = d.in;
-				p.read_off = p.qual_off = qb[i] + (d.key.fw ? 0 : L);
-				p.ref_off = fb[k];
-				ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, b_refs_.data() + fb[k]);
-				b_dp_in_[k] = p;
+				const uint64_t k = L.pb[i] + j;
+				bt2x_dp_in q = d.in;
+				q.read_off = q.qual_off = L.qb[i] + (d.key.fw ? 0 : n);
+				q.ref_off = L.fb[k];
+				ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, L.dp_refs.data() + L.fb[k]);
+				L.dp_in[k] = q;
 			}
 		}
-		be_.dp_align(b_reads_, b_quals_, b_refs_, b_dp_in_, b_dp_out_, b_recs_, b_edits_);
-#pragma omp parallel for schedule(static, 256) num_threads(threads)
-		for(long i = 0; i < nwd; i++) {
-			ReadCtx* c = wd[i];
+	}
+}
+
+// The launch's backend calls (on the GPU thread when pipelined).
+void Aligner::execute(Launch& L) {
+	L.t_seed = L.t_resolve = L.t_dp = 0;
+	if(!L.ws.empty()) {
+		const double t0 = now_s();
+		be_.seed_search(L.seed_reads, L.seed_in, L.seed_out);
+		L.t_seed = now_s() - t0;
+	}
+	if(!L.wr.empty()) {
+		const double t0 = now_s();
+		be_.resolve(L.res_in, L.res_out);
+		L.t_resolve = now_s() - t0;
+	}
+	if(!L.wd.empty()) {
+		const double t0 = now_s();
+		be_.dp_align(L.dp_reads, L.dp_quals, L.dp_refs, L.dp_in, L.dp_out, L.recs, L.edits);
+		L.t_dp = now_s() - t0;
+	}
+}
+
+// Hand every served read its results and resume it until it waits again or finishes.
+void Aligner::scatter_resume(Launch& L, RunStats& st, int threads) {
+	const long nws = (long)L.ws.size(), nwr = (long)L.wr.size(), nwd = (long)L.wd.size();
+	if(nws) { st.seed_launches++; st.seeds += L.seed_in.size(); st.t_seed += L.t_seed; }
+	if(nwr) { st.resolve_launches++; st.resolves += L.res_in.size(); st.t_resolve += L.t_resolve; }
+	if(nwd) { st.dp_launches++; st.dps += L.dp_in.size(); st.t_dp += L.t_dp; }
+	st.t_backend += L.t_seed + L.t_resolve + L.t_dp;
+	L.run.clear();
+	L.run.insert(L.run.end(), L.ws.begin(), L.ws.end());
+	L.run.insert(L.run.end(), L.wr.begin(), L.wr.end());
+	L.run.insert(L.run.end(), L.wd.begin(), L.wd.end());
+	const long nrun = (long)L.run.size();
+	const double t0 = now_s();
+#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
+	for(long i = 0; i < nrun; i++) {
+		ReadCtx* c = L.run[(size_t)i];
+		if(i < nws) {
+			c->seed_out.assign(L.seed_out.begin() + (long)L.sk[i], L.seed_out.begin() + (long)L.sk[i + 1]);
+		} else if(i < nws + nwr) {
+			const long r = i - nws;
+			c->res_out.assign(L.res_out.begin() + (long)L.rk[r], L.res_out.begin() + (long)L.rk[r + 1]);
+		} else {
+			const long r = i - nws - nwr;
 			for(size_t j = 0; j < c->dps.size(); j++) {
-				const uint64_t k = pb[i] + j;
-				const bt2x_dp_out& o = b_dp_out_[k];
+				const uint64_t k = L.pb[r] + j;
+				const bt2x_dp_out& o = L.dp_out[k];
 				DpMemo m;
 				m.key = c->dps[j].key;
 				m.out = o;
 				m.rec0 = (uint32_t)c->recs.size();
 				c->memo.push_back(m);
 				// each record's edit-buffer image moves to the read's edit arena (arena
-				// offsets are allocated by the kernel's atomics, so one problem's images are
-				// not contiguous)
+				// offsets are allocated by the kernel's atomics, so one problem's images
+				// are not contiguous)
 				for(uint32_t q = 0; q < o.nrec; q++) {
-					bt2x_aln_rec a = b_recs_[o.rec_off + q];
+					bt2x_aln_rec a = L.recs[o.rec_off + q];
 					const uint32_t eo = (uint32_t)c->edits.size();
-					c->edits.insert(c->edits.end(), b_edits_.begin() + a.edit_off, b_edits_.begin() + a.edit_off + a.nbuf);
+					c->edits.insert(c->edits.end(), L.edits.begin() + a.edit_off, L.edits.begin() + a.edit_off + a.nbuf);
 					a.edit_off = eo;
 					c->recs.push_back(a);
 				}
 			}
 		}
-		st.dp_launches++; st.dps += np; st.t_dp += now_s() - t0;
-	}
-	// resume the reads whose requests were served
-	std::vector<ReadCtx*> run;
-	run.reserve(ws.size() + wr.size() + wd.size());
-	run.insert(run.end(), ws.begin(), ws.end());
-	run.insert(run.end(), wr.begin(), wr.end());
-	run.insert(run.end(), wd.begin(), wd.end());
-	double t0 = now_s();
-	const long nrun = (long)run.size();
-#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-	for(long i = 0; i < nrun; i++) {
-		run[i]->req = REQ_NONE;
-		run[i]->task.h.resume();
+		c->req = REQ_NONE;
+		c->task.h.resume();
 	}
 	st.t_host += now_s() - t0;
+}
+
+// One scheduler iteration over `act`: every pending request in one launch per kind,
+// then the served reads resume.  Returns false when no read is waiting.
+bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st, int threads) {
+	Launch& L = launch_[0];
+	gather(L, act, threads);
+	if(L.ws.empty() && L.wr.empty() && L.wd.empty()) return false;
+	static const bool trace = std::getenv("BT2X_TRACE") != nullptr;
+	if(trace) std::fprintf(stderr, "BT2X_TRACE active=%zu seed=%zu resolve=%zu dp=%zu\n", act.size(), L.ws.size(),
+	                       L.wr.size(), L.wd.size());
+	execute(L);
+	scatter_resume(L, st, threads);
 	return true;
 }
 
@@ -1094,47 +1140,86 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	std::fwrite(hdr.data(), 1, hdr.size(), out);
 	uint64_t rdid = 0;
 	bool eof = false;
-	std::vector<ReadCtx*> act, fresh;
 	std::vector<FastqReader::Raw> raw;
+	std::vector<ReadCtx*> fresh;
 	OutRing ring;
 	SamWriter writer(out);
-	if(slots < 1) slots = 1;
-	while(true) {
-		// refill the pool
+	if(slots < 2) slots = 2;
+	// New reads join cohort `co` (up to `cap` reads in it): decoded and run up to their
+	// first request, in parallel.
+	auto refill = [&](std::vector<ReadCtx*>& co, size_t cap) {
 		double t0 = now_s();
 		raw.clear();
-		if(!eof && act.size() < slots) {
-			const size_t want = slots - act.size();
+		if(!eof && co.size() < cap) {
+			const size_t want = cap - co.size();
 			if(fq.take(want, raw) < want) eof = true;
 		}
 		st.t_io += now_s() - t0;
 		const long nf = (long)raw.size();
-		if(nf) {
-			t0 = now_s();
-			fresh.resize((size_t)nf);
-			for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
-			ring.reserve(rdid + (uint64_t)nf);
-			st.t_alloc += now_s() - t0;
-			// decode + run each new read up to its first request, in parallel
+		if(!nf) return;
+		t0 = now_s();
+		fresh.resize((size_t)nf);
+		for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
+		ring.reserve(rdid + (uint64_t)nf);
+		st.t_alloc += now_s() - t0;
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-			for(long i = 0; i < nf; i++) {
-				ReadCtx* c = fresh[(size_t)i];
-				FastqReader::decode(raw[(size_t)i], c->rd, rdid + (uint64_t)i, p_.randSeed);
-				c->task = align_read(c);
-				c->task.h.resume();
-			}
-			rdid += (uint64_t)nf;
-			st.t_host += now_s() - t0;
-			act.insert(act.end(), fresh.begin(), fresh.end());
+		for(long i = 0; i < nf; i++) {
+			ReadCtx* c = fresh[(size_t)i];
+			FastqReader::decode(raw[(size_t)i], c->rd, rdid + (uint64_t)i, p_.randSeed);
+			c->task = align_read(c);
+			c->task.h.resume();
 		}
-		if(act.empty()) break;
-		t0 = now_s();
-		step(act, st, threads);
-		st.t_step += now_s() - t0;
-		t0 = now_s();
-		retire(act, st, &ring);
+		rdid += (uint64_t)nf;
+		st.t_host += now_s() - t0;
+		co.insert(co.end(), fresh.begin(), fresh.end());
+	};
+	auto retire_write = [&](std::vector<ReadCtx*>& co) {
+		const double t0 = now_s();
+		retire(co, st, &ring);
 		ring.drain([&](const std::string& s) { writer.append(s); });
 		st.t_io += now_s() - t0;
+	};
+	if(!pipeline_) {
+		std::vector<ReadCtx*> act;
+		while(true) {
+			refill(act, slots);
+			if(act.empty()) break;
+			const double t0 = now_s();
+			step(act, st, threads);
+			st.t_step += now_s() - t0;
+			retire_write(act);
+		}
+	} else {
+		// Two cohorts of up to slots/2 reads alternate: while the GPU thread runs one
+		// cohort's launches, the host threads resume the other with its previous results,
+		// retire and refill it, and gather its next launch.
+		std::vector<ReadCtx*> co[2];
+		const size_t cap = slots / 2;
+		auto empty = [](const Launch& L) { return L.ws.empty() && L.wr.empty() && L.wd.empty(); };
+		int a = 0;
+		refill(co[0], cap);
+		gather(launch_[0], co[0], threads);
+		std::thread gpu([this] { execute(launch_[0]); });
+		refill(co[1], cap);
+		gather(launch_[1], co[1], threads);
+		while(true) {
+			// invariant: the GPU thread runs launch a (cohort a waits on it); launch b is
+			// gathered from cohort b
+			const double t0 = now_s();
+			gpu.join();
+			st.t_wait += now_s() - t0;
+			const int b = 1 - a;
+			gpu = std::thread([this, b] { execute(launch_[b]); });
+			const double t1 = now_s();
+			scatter_resume(launch_[a], st, threads);
+			retire_write(co[a]);
+			refill(co[a], cap);
+			gather(launch_[a], co[a], threads);
+			st.t_step += now_s() - t1;
+			if(eof && co[a].empty() && co[b].empty() && empty(launch_[a]) && empty(launch_[b])) break;
+			a = b;
+		}
+		if(gpu.joinable()) gpu.join();
 	}
 	writer.finish();
 	if(t_run) *t_run = now_s() - t_start;

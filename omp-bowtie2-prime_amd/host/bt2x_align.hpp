@@ -97,6 +97,7 @@ public:
 		list_.clear();
 		seen_.clear();
 		thresh_ = std::max<uint16_t>(16, (uint16_t)(0.10f * n));
+		if(!swaplist_) seenBits_.assign(((size_t)n + 63) / 64, 0);
 	}
 	void reset() {
 		sz_ = n_ = cur_ = 0; swaplist_ = converted_ = false;
@@ -115,14 +116,14 @@ public:
 			if(r != cur_) std::swap(list_[cur_], list_[r]);
 			return list_[cur_++];
 		}
-		bool again = true;
+		// seen-list mode: redraw until unseen (membership by bitset; the reference scans
+		// the list, same answers)
 		uint16_t rn = 0;
 		const uint16_t seenSz = (uint16_t)seen_.size();
-		while(again) {
+		do {
 			rn = (uint16_t)(rnd.nextU32() % (uint32_t)n_);
-			again = false;
-			for(uint16_t i = 0; i < seenSz; i++) if(seen_[i] == rn) { again = true; break; }
-		}
+		} while((seenBits_[rn >> 6] >> (rn & 63)) & 1);
+		seenBits_[rn >> 6] |= 1ULL << (rn & 63);
 		seen_.push_back(rn);
 		cur_++;
 		if(seen_.size() >= thresh_ && cur_ < n_) {
@@ -148,6 +149,7 @@ private:
 	uint16_t sz_ = 0, n_ = 0, cur_ = 0, thresh_ = 0;
 	bool swaplist_ = false, converted_ = false;
 	std::vector<uint16_t> list_, seen_;
+	std::vector<uint64_t> seenBits_;
 };
 
 // Random1toN over the ranges extendSeeds walks.  prioritizeSATups keeps whole only the
@@ -210,6 +212,9 @@ struct Interval {                   // ref_coord.h Interval
 // bisection.  Two vectors of PODs, so the DP lookahead's copy reuses capacity.
 class SeenDiags {
 public:
+	SeenDiags() = default;
+	SeenDiags(const SeenDiags& o) : sorted_(o.sorted_), tail_(o.tail_) {}
+	SeenDiags& operator=(const SeenDiags& o) { sorted_ = o.sorted_; tail_ = o.tail_; return *this; }   // (not the scratch)
 	void clear() { sorted_.clear(); tail_.clear(); }
 	void add(const Interval& i) {
 		tail_.push_back(i);
@@ -227,25 +232,30 @@ public:
 		return lo > 0 && sorted_[lo - 1].contains(c);
 	}
 private:
+	// sort the tail, merge it into the sorted run and coalesce overlapping or touching
+	// intervals (same union)
 	void flush() {
-		sorted_.insert(sorted_.end(), tail_.begin(), tail_.end());
+		auto byUp = [](const Interval& a, const Interval& b) { return a.up < b.up; };
+		std::sort(tail_.begin(), tail_.end(), byUp);
+		merged_.resize(sorted_.size() + tail_.size());
+		std::merge(sorted_.begin(), sorted_.end(), tail_.begin(), tail_.end(), merged_.begin(), byUp);
 		tail_.clear();
-		std::sort(sorted_.begin(), sorted_.end(), [](const Interval& a, const Interval& b) { return a.up < b.up; });
 		size_t w = 0;
-		for(size_t i = 0; i < sorted_.size(); i++) {
-			const Interval& iv = sorted_[i];
+		for(size_t i = 0; i < merged_.size(); i++) {
+			const Interval& iv = merged_[i];
 			if(w > 0) {
-				Interval& p = sorted_[w - 1];
+				Interval& p = merged_[w - 1];
 				if(p.up.ref == iv.up.ref && p.up.orient == iv.up.orient && iv.up.off <= p.up.off + p.len) {
 					p.len = std::max(p.up.off + p.len, iv.up.off + iv.len) - p.up.off;
 					continue;
 				}
 			}
-			sorted_[w++] = iv;
+			merged_[w++] = iv;
 		}
-		sorted_.resize(w);
+		merged_.resize(w);
+		sorted_.swap(merged_);
 	}
-	std::vector<Interval> sorted_, tail_;
+	std::vector<Interval> sorted_, tail_, merged_;
 };
 
 // ----------------------------------------------------------------------- alignments
@@ -606,15 +616,19 @@ struct SatPos {
 
 struct ExtendRange { size_t off, len, sz; };
 
-// RowSampler (aligner_sw_driver.h:176-267), lensq = szsq = true
+// RowSampler (aligner_sw_driver.h:176-267), lensq = szsq = true.  next() is the
+// reference's linear dart walk over the non-eliminated ranges; here the running sums it
+// accumulates are kept (same order of double additions, so the same values) and the dart
+// is placed by bisection; they are rebuilt when a range is eliminated.
 struct RowSampler {
 	double mass = 0;
 	std::vector<double> masses;
-	std::vector<uint8_t> elim;
+	std::vector<uint32_t> live;     // non-eliminated ranges, in order
+	std::vector<double> pre;        // pre[k] = masses[live[0]] + ... + masses[live[k]]
 	void init(const std::vector<SatPos>& sl, size_t sai, size_t saf) {
-		elim.assign(saf - sai, 0);
 		mass = 0.0f;
 		masses.assign(saf - sai, 0.0);
+		live.resize(saf - sai);
 		for(size_t i = sai; i < saf; i++) {
 			double num = (double)(sl[i].nlex + 1);
 			num *= num;
@@ -622,21 +636,27 @@ struct RowSampler {
 			den *= den;
 			masses[i - sai] = num / den;
 			mass += masses[i - sai];
+			live[i - sai] = (uint32_t)(i - sai);
 		}
+		rebuild();
 	}
-	void finishedRange(size_t i) { elim[i] = 1; mass -= masses[i]; }
+	void finishedRange(size_t i) {
+		mass -= masses[i];
+		const auto it = std::lower_bound(live.begin(), live.end(), (uint32_t)i);
+		if(it != live.end() && *it == (uint32_t)i) live.erase(it);
+		rebuild();
+	}
 	size_t next(Rng& rnd) {
 		const double rd = rnd.nextFloat() * mass;
+		if(live.empty()) return std::numeric_limits<size_t>::max();
+		const size_t k = (size_t)(std::upper_bound(pre.begin(), pre.end(), rd) - pre.begin());   // rd < pre[k]
+		return k < pre.size() ? live[k] : live.back();
+	}
+private:
+	void rebuild() {
+		pre.resize(live.size());
 		double sofar = 0.0f;
-		size_t last = std::numeric_limits<size_t>::max();
-		for(size_t i = 0; i < masses.size(); i++) {
-			if(!elim[i]) {
-				last = i;
-				sofar += masses[i];
-				if(rd < sofar) return i;
-			}
-		}
-		return last;
+		for(size_t k = 0; k < live.size(); k++) { sofar += masses[live[k]]; pre[k] = sofar; }
 	}
 };
 
@@ -675,6 +695,8 @@ private:
 	std::vector<SmallRandom1toN> rands_;
 	size_t i_ = 0;
 	bool first_ = true, inPass_ = false;
+	int64_t gapMinsc_ = 1;          // minsc of the cached maxgap (1: none)
+	size_t maxgap_ = 0;
 	Rng* rnd_ = nullptr;
 	Prm* prm_ = nullptr;
 	SeenDiags* seen_ = nullptr;
@@ -782,13 +804,15 @@ struct RunStats {
 	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0;
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
 	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
-	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0;
+	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0, t_wait = 0;
 };
 
 class Aligner {
 public:
 	Aligner(const Params& p, const RefInfo& ref, Backend& be) : p_(p), ref_(ref), be_(be) {}
 	~Aligner();
+	// run(): overlap one cohort's GPU launches with the host work of another (default on)
+	void set_pipeline(bool on) { pipeline_ = on; }
 	Aligner(const Aligner&) = delete;
 	Aligner& operator=(const Aligner&) = delete;
 	// SAM header (@HD, @SQ; sam.cpp:47-80)
@@ -799,8 +823,28 @@ public:
 	// Align a vector of reads (tests); records in input order.
 	std::string align_all(std::vector<Read>& reads, size_t slots, int threads, RunStats* st = nullptr);
 private:
+	// one cohort's requests as one seed, one resolve and one DP launch
+	struct Launch {
+		std::vector<ReadCtx*> ws, wr, wd, run;          // reads waiting on each kind
+		std::vector<uint64_t> sr, sk, rk, qb, pb, fb;  // per-read offsets into the buffers
+		std::vector<uint8_t> seed_reads, dp_reads, dp_quals, dp_refs;
+		std::vector<bt2x_seed_in> seed_in;
+		std::vector<bt2x_seed_out> seed_out;
+		std::vector<bt2x_resolve_in> res_in;
+		std::vector<bt2x_resolve_out> res_out;
+		std::vector<bt2x_dp_in> dp_in;
+		std::vector<bt2x_dp_out> dp_out;
+		std::vector<bt2x_aln_rec> recs;
+		std::vector<uint32_t> edits;
+		double t_seed = 0, t_resolve = 0, t_dp = 0;
+	};
 	ReadTask align_read(ReadCtx* c);
 	bool step(std::vector<ReadCtx*>& active, RunStats& st, int threads);
+	void gather(Launch& L, const std::vector<ReadCtx*>& cohort, int threads);
+	void execute(Launch& L);
+	void scatter_resume(Launch& L, RunStats& st, int threads);
+	Launch launch_[2];
+	bool pipeline_ = true;
 	ReadCtx* take_ctx();
 	void retire(std::vector<ReadCtx*>& act, RunStats& st, void* ring);
 	// pooled read contexts (kept across runs; released by the destructor)
@@ -809,17 +853,6 @@ private:
 	const Params& p_;
 	const RefInfo& ref_;
 	Backend& be_;
-	// launch buffers, reused across steps
-	std::vector<uint8_t> b_reads_, b_quals_, b_refs_;
-	std::vector<uint64_t> b_off_, b_off2_, b_off3_;
-	std::vector<bt2x_seed_in> b_seed_in_;
-	std::vector<bt2x_seed_out> b_seed_out_;
-	std::vector<bt2x_resolve_in> b_res_in_;
-	std::vector<bt2x_resolve_out> b_res_out_;
-	std::vector<bt2x_dp_in> b_dp_in_;
-	std::vector<bt2x_dp_out> b_dp_out_;
-	std::vector<bt2x_aln_rec> b_recs_;
-	std::vector<uint32_t> b_edits_;
 };
 
 } // namespace host

@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
 	Params p;
 	int threads = 16, device = 0;
 	size_t slots = 1 << 18;
-	bool stats = false;
+	bool stats = false, pipeline = true;
 	std::string dump;
 	for(int i = 1; i < argc; i++) {
 		const std::string a = argv[i];
@@ -128,6 +128,7 @@ int main(int argc, char** argv) {
 		else if(a == "--device") device = std::atoi(val());
 		else if(a == "--stats") stats = true;
 		else if(a == "--dump") dump = val();
+		else if(a == "--no-pipeline") pipeline = false;
 		else if(a == "--end-to-end" || a == "--sensitive" || a == "--reorder" || a == "-q") {}
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); usage(); return 1; }
 	}
@@ -144,6 +145,7 @@ int main(int argc, char** argv) {
 		if(!dump.empty()) dumper.reset(new DumpBackend(hip, dump));
 		Backend& be = dumper ? static_cast<Backend&>(*dumper) : static_cast<Backend&>(hip);
 		Aligner al(p, ref, be);
+		al.set_pipeline(pipeline);
 		FastqReader reader(fq.c_str());
 		const auto t_start = std::chrono::steady_clock::now();
 		std::FILE* out = outp.empty() ? stdout : std::fopen(outp.c_str(), "wb");
@@ -164,11 +166,11 @@ int main(int argc, char** argv) {
 		if(stats)
 			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "
 			             "resolve_launches=%llu resolves=%llu t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f "
-			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu\n", (unsigned long long)st.reads, t_align,
+			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu t_backend=%.4f t_step=%.4f t_wait=%.4f\n", (unsigned long long)st.reads, t_align,
 			             (unsigned long long)st.seed_launches, (unsigned long long)st.seeds, st.t_seed,
 			             (unsigned long long)st.resolve_launches, (unsigned long long)st.resolves, st.t_resolve,
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io, (unsigned long long)st.dps_used,
-			             (unsigned long long)st.tight_recs);
+			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait);
 	} catch(const std::exception& e) {
 		std::fprintf(stderr, "bt2x-align: %s\n", e.what());
 		return 1;

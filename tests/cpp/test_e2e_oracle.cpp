@@ -92,13 +92,14 @@ int main(int argc, char** argv) {
 	Params p;
 	size_t slots = 4096;
 	int threads = 4;
-	bool host_timing = false;
+	bool host_timing = false, pipeline = true;
 	for(int i = 3; i < argc; i++) {
 		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
 		const std::string a = argv[i];
 		if(a == "--slots" && i + 1 < argc) slots = (size_t)std::atol(argv[++i]);
 		else if(a == "-p" && i + 1 < argc) threads = std::atoi(argv[++i]);
 		else if(a == "--host-timing") host_timing = true;
+		else if(a == "--no-pipeline") pipeline = false;
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); return 1; }
 	}
 	bt2x_scoring_init(&p.sc);
@@ -110,6 +111,7 @@ int main(int argc, char** argv) {
 		ReplayBackend rb(&be);
 		{
 			Aligner al0(p, ref, rb);
+			al0.set_pipeline(pipeline);
 			FastqReader fq(argv[2]);
 			std::FILE* nul = std::fopen("/dev/null", "wb");
 			al0.run(fq, nul, slots, threads);
@@ -118,12 +120,14 @@ int main(int argc, char** argv) {
 		rb.rewind();
 		// the timed run starts from an empty context pool, as bt2x-align does
 		Aligner al(p, ref, rb);
+		al.set_pipeline(pipeline);
 		FastqReader fq(argv[2]);
 		const auto t0 = std::chrono::steady_clock::now();
 		double t_run = 0;
 		const RunStats st = al.run(fq, stdout, slots, threads, &t_run);
 		const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-		std::fprintf(stderr, "HOST_TIMING t_alloc=%.3f t_step=%.3f t_run=%.3f\n", st.t_alloc, st.t_step, t_run);
+		std::fprintf(stderr, "HOST_TIMING t_alloc=%.3f t_step=%.3f t_wait=%.3f t_backend=%.3f t_run=%.3f\n", st.t_alloc,
+		             st.t_step, st.t_wait, st.t_backend, t_run);
 		std::fprintf(stderr, "HOST_TIMING reads=%llu wall=%.3f t_host=%.3f t_io=%.3f t_seed=%.3f t_resolve=%.3f t_dp=%.3f "
 		             "launches=%llu/%llu/%llu dps=%llu dps_used=%llu\n", (unsigned long long)st.reads, t, st.t_host, st.t_io, st.t_seed,
 		             st.t_resolve, st.t_dp, (unsigned long long)st.seed_launches,
@@ -131,6 +135,7 @@ int main(int argc, char** argv) {
 		return 0;
 	}
 	Aligner al(p, ref, be);
+	al.set_pipeline(pipeline);
 	FastqReader fq(argv[2]);
 	const RunStats st = al.run(fq, stdout, slots, threads);
 	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu "

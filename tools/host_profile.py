@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--slots", type=int, default=65536)
     ap.add_argument("--dpad", type=int, default=12)
     ap.add_argument("--check", action="store_true", help="also compare with the reference aligner's SAM")
+    ap.add_argument("--nchrom", type=int, default=8)
+    ap.add_argument("--gseed", type=int, default=2024)
+    ap.add_argument("--driver", default=os.path.join(ROOT, "tests", "cpp", "test_e2e_oracle"))
     args, extra = ap.parse_known_args()
     import numpy as np
     import simdata as sd
@@ -40,9 +43,9 @@ def main():
 
     wd = "/tmp/bt2x_hostprof"
     os.makedirs(wd, exist_ok=True)
-    tag = f"g{int(args.mb * 1e6)}"
+    tag = f"g{int(args.mb * 1e6)}" + (f"_c{args.nchrom}" if args.nchrom != 8 else "")
     base = os.path.join(wd, tag)
-    chroms = sd.gen_genome(int(args.mb * 1e6), nchrom=8, seed=2024)
+    chroms = sd.gen_genome(int(args.mb * 1e6), nchrom=args.nchrom, seed=args.gseed)
     if not os.path.exists(base + ".4.bt2l"):
         fa = base + ".fa"
         sd.write_fasta(fa, chroms)
@@ -55,7 +58,7 @@ def main():
         reads, quals, _, _, _ = sd.sim_reads_fixed(genome, starts, args.reads, args.read_len, seed=3)
         bench.write_fastq(fq, reads, quals)
     sam = os.path.join(wd, "out.sam")
-    cmd = [os.path.join(ROOT, "tests", "cpp", "test_e2e_oracle"), base, fq, "--host-timing", "-p", str(args.p),
+    cmd = [args.driver, base, fq, "--host-timing", "-p", str(args.p),
            "--slots", str(args.slots), "--dpad", str(args.dpad)] + extra
     t0 = time.time()
     with open(sam, "wb") as f:
