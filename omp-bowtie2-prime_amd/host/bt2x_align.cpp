@@ -725,7 +725,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 					if(P.lookahead > 1) {
 						Rng rnd2 = rnd;
 						Prm prm2 = prm;
-						c->seen2 = c->seenDiags;
+						c->seen2.clear(&c->seenDiags);
 						c->ahead = c->walk;
 						c->ahead.bind(&rnd2, &prm2, &c->seen2);
 						while(c->dps.size() < P.lookahead && c->ahead.failed()) {

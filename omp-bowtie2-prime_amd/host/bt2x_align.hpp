@@ -212,15 +212,15 @@ struct Interval {                   // ref_coord.h Interval
 // bisection.  Two vectors of PODs, so the DP lookahead's copy reuses capacity.
 class SeenDiags {
 public:
-	SeenDiags() = default;
-	SeenDiags(const SeenDiags& o) : sorted_(o.sorted_), tail_(o.tail_) {}
-	SeenDiags& operator=(const SeenDiags& o) { sorted_ = o.sorted_; tail_ = o.tail_; return *this; }   // (not the scratch)
-	void clear() { sorted_.clear(); tail_.clear(); }
+	// clear; with `base`, this set is an overlay: it answers for base's intervals plus its
+	// own (the DP lookahead's walk adds to an overlay over the read's real set)
+	void clear(const SeenDiags* base = nullptr) { sorted_.clear(); tail_.clear(); base_ = base; }
 	void add(const Interval& i) {
 		tail_.push_back(i);
 		if(tail_.size() == 16) flush();
 	}
 	bool locusPresent(const Coord& c) const {
+		if(base_ && base_->locusPresent(c)) return true;
 		for(const Interval& iv : tail_) if(iv.contains(c)) return true;
 		if(sorted_.empty()) return false;
 		// last interval whose start is <= c
@@ -256,6 +256,7 @@ private:
 		sorted_.swap(merged_);
 	}
 	std::vector<Interval> sorted_, tail_, merged_;
+	const SeenDiags* base_ = nullptr;
 };
 
 // ----------------------------------------------------------------------- alignments
@@ -769,7 +770,7 @@ struct ReadCtx {
 	uint64_t ntight = 0;            // nextAlignment records consumed after -M tightened minsc
 	                                // within the same DP problem
 	// the coroutine frame (ReadTask::promise_type::operator new)
-	static constexpr size_t kFrameBytes = 4096;
+	static constexpr size_t kFrameBytes = 1536;     // align_read's frame is ~1.25 KiB
 	alignas(std::max_align_t) unsigned char frame_[kFrameBytes];
 };
 

@@ -14,6 +14,8 @@
 #include <string>
 #include <vector>
 
+#include <sys/resource.h>
+
 #include "bt2x_align.hpp"
 
 using namespace bt2x::host;
@@ -163,6 +165,13 @@ int main(int argc, char** argv) {
 		std::fprintf(stderr, "    %llu (%.2f%%) aligned exactly 1 time\n", (unsigned long long)(st.aligned - st.rep), pct(st.aligned - st.rep));
 		std::fprintf(stderr, "    %llu (%.2f%%) aligned >1 times\n", (unsigned long long)st.rep, pct(st.rep));
 		std::fprintf(stderr, "%.2f%% overall alignment rate\n", pct(st.aligned));
+		if(stats) {
+			struct rusage ru;
+			getrusage(RUSAGE_SELF, &ru);
+			std::fprintf(stderr, "BT2X_RUSAGE user=%.3f sys=%.3f maxrss_mib=%ld minflt=%ld majflt=%ld vcsw=%ld ivcsw=%ld\n",
+			             ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6, ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6,
+			             ru.ru_maxrss / 1024, ru.ru_minflt, ru.ru_majflt, ru.ru_nvcsw, ru.ru_nivcsw);
+		}
 		if(stats)
 			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "
 			             "resolve_launches=%llu resolves=%llu t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f "

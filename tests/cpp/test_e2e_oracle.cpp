@@ -62,7 +62,7 @@ private:
 class ReplayBackend : public Backend {
 public:
 	explicit ReplayBackend(Backend* rec) : rec_(rec) {}
-	void rewind() { rec_ = nullptr; k_ = 0; }
+	void rewind() { rec_ = nullptr; k_ = kr_ = kd_ = 0; }
 	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
 	                 std::vector<bt2x_seed_out>& out) override {
 		if(rec_) { rec_->seed_search(reads, in, out); seeds_.push_back(out); } else out = seeds_[k_++];
@@ -93,6 +93,7 @@ int main(int argc, char** argv) {
 	size_t slots = 4096;
 	int threads = 4;
 	bool host_timing = false, pipeline = true;
+	int reps = 1;
 	for(int i = 3; i < argc; i++) {
 		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
 		const std::string a = argv[i];
@@ -100,6 +101,7 @@ int main(int argc, char** argv) {
 		else if(a == "-p" && i + 1 < argc) threads = std::atoi(argv[++i]);
 		else if(a == "--host-timing") host_timing = true;
 		else if(a == "--no-pipeline") pipeline = false;
+		else if(a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); return 1; }
 	}
 	bt2x_scoring_init(&p.sc);
@@ -117,6 +119,7 @@ int main(int argc, char** argv) {
 			al0.run(fq, nul, slots, threads);
 			std::fclose(nul);
 		}
+		for(int rep = 0; rep < reps; rep++) {
 		rb.rewind();
 		// the timed run starts from an empty context pool, as bt2x-align does
 		Aligner al(p, ref, rb);
@@ -132,6 +135,7 @@ int main(int argc, char** argv) {
 		             "launches=%llu/%llu/%llu dps=%llu dps_used=%llu\n", (unsigned long long)st.reads, t, st.t_host, st.t_io, st.t_seed,
 		             st.t_resolve, st.t_dp, (unsigned long long)st.seed_launches,
 		             (unsigned long long)st.resolve_launches, (unsigned long long)st.dp_launches, (unsigned long long)st.dps, (unsigned long long)st.dps_used);
+		}
 		return 0;
 	}
 	Aligner al(p, ref, be);

@@ -8,5 +8,5 @@ ALIGN=$(dirname "$0")/../omp-bowtie2-prime_amd/bt2x/bt2x-align
 for opts in "$@"; do
   echo "== $opts"
   timeout -k 10 300 "$ALIGN" -x "$W/syn1000000000_s2024" -U "$W/rank0/reads.fq" -S "$W/sweep.sam" --dpad 12 \
-      -p "${OMP_NUM_THREADS:-16}" --stats $opts 2>&1 | grep -E "BT2X_STATS|overall" || exit 1
+      -p "${OMP_NUM_THREADS:-16}" --stats $opts 2>&1 | grep -E "BT2X_STATS|BT2X_RUSAGE|overall" || exit 1
 done

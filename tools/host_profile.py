@@ -63,7 +63,7 @@ def main():
     t0 = time.time()
     with open(sam, "wb") as f:
         r = subprocess.run(cmd, stdout=f, stderr=subprocess.PIPE, text=True)
-    print(r.stderr[-2000:], file=sys.stderr)
+    print("\n".join(ln for ln in r.stderr.splitlines() if "HOST_TIMING" in ln or "PHASE" in ln or "error" in ln.lower())[-6000:], file=sys.stderr)
     print(f"# total {time.time() - t0:.1f} s", file=sys.stderr)
     if r.returncode:
         raise SystemExit(r.returncode)
