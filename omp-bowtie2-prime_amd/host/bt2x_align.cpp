@@ -14,14 +14,14 @@
 #include <mutex>
 #include <thread>
 
+#include <climits>
+
 #include <fcntl.h>
+#include <malloc.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
-#ifdef _OPENMP
-#include <omp.h>
-#endif
 
 #ifdef BT2X_PHASE_PROF
 // Development-only phase profiler of the per-read coroutine (-DBT2X_PHASE_PROF): TSC
@@ -56,6 +56,12 @@ void ph_print() {
 
 namespace bt2x {
 namespace host {
+
+void tune_malloc() {
+	mallopt(M_TRIM_THRESHOLD, INT_MAX);
+	mallopt(M_TOP_PAD, 64 << 20);
+	mallopt(M_MMAP_THRESHOLD, 32 << 20);
+}
 
 const uint8_t kAsc2Dna[256] = {   // alphabet.cpp:142 (A/C/G/T, either case; all else N)
 #define N4 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4
@@ -831,7 +837,7 @@ double now_s() {
 
 // Classify the cohort's reads by pending request and fill the launch's input buffers
 // (one seed, one resolve and one DP launch; gathers in parallel over reads).
-void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort, int threads) {
+void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 	L.ws.clear(); L.wr.clear(); L.wd.clear();
 	for(ReadCtx* c : cohort) {
 		if(c->req == REQ_SEED) L.ws.push_back(c);
@@ -848,8 +854,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort, int threads
 		}
 		L.seed_reads.resize(L.sr[nws]);
 		L.seed_in.resize(L.sk[nws]);
-#pragma omp parallel for schedule(static, 256) num_threads(threads)
-		for(long i = 0; i < nws; i++) {
+		pool().parallel_for(nws, 256, [&](long i) {
 			const ReadCtx* c = L.ws[i];
 			const size_t n = c->rd.length();
 			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.seed_reads.begin() + (long)L.sr[i]);
@@ -859,15 +864,13 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort, int threads
 				q.read_off += L.sr[i];
 				L.seed_in[L.sk[i] + k] = q;
 			}
-		}
+		});
 	}
 	if(nwr) {
 		L.rk.assign(nwr + 1, 0);
 		for(long i = 0; i < nwr; i++) L.rk[i + 1] = L.rk[i] + L.wr[i]->res_in.size();
 		L.res_in.resize(L.rk[nwr]);
-#pragma omp parallel for schedule(static, 256) num_threads(threads)
-		for(long i = 0; i < nwr; i++)
-			std::copy(L.wr[i]->res_in.begin(), L.wr[i]->res_in.end(), L.res_in.begin() + (long)L.rk[i]);
+		pool().parallel_for(nwr, 256, [&](long i) { std::copy(L.wr[i]->res_in.begin(), L.wr[i]->res_in.end(), L.res_in.begin() + (long)L.rk[i]); });
 	}
 	if(nwd) {
 		// the read's two orientations (codes and qualities) once per read, one reference
@@ -884,8 +887,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort, int threads
 				L.fb[L.pb[i] + j + 1] = L.fb[L.pb[i] + j] + L.wd[i]->dps[j].key.ncol;
 		L.dp_reads.resize(L.qb[nwd]); L.dp_quals.resize(L.qb[nwd]); L.dp_refs.resize(L.fb[np]);
 		L.dp_in.resize(np);
-#pragma omp parallel for schedule(static, 256) num_threads(threads)
-		for(long i = 0; i < nwd; i++) {
+		pool().parallel_for(nwd, 256, [&](long i) {
 			const ReadCtx* c = L.wd[i];
 			const size_t n = c->rd.length();
 			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)L.qb[i]);
@@ -901,7 +903,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort, int threads
 				ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, L.dp_refs.data() + L.fb[k]);
 				L.dp_in[k] = q;
 			}
-		}
+		});
 	}
 }
 
@@ -926,7 +928,7 @@ void Aligner::execute(Launch& L) {
 }
 
 // Hand every served read its results and resume it until it waits again or finishes.
-void Aligner::scatter_resume(Launch& L, RunStats& st, int threads) {
+void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	const long nws = (long)L.ws.size(), nwr = (long)L.wr.size(), nwd = (long)L.wd.size();
 	if(nws) { st.seed_launches++; st.seeds += L.seed_in.size(); st.t_seed += L.t_seed; }
 	if(nwr) { st.resolve_launches++; st.resolves += L.res_in.size(); st.t_resolve += L.t_resolve; }
@@ -938,8 +940,7 @@ void Aligner::scatter_resume(Launch& L, RunStats& st, int threads) {
 	L.run.insert(L.run.end(), L.wd.begin(), L.wd.end());
 	const long nrun = (long)L.run.size();
 	const double t0 = now_s();
-#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-	for(long i = 0; i < nrun; i++) {
+	pool().parallel_for(nrun, 64, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
 		if(i < nws) {
 			c->seed_out.assign(L.seed_out.begin() + (long)L.sk[i], L.seed_out.begin() + (long)L.sk[i + 1]);
@@ -970,21 +971,21 @@ void Aligner::scatter_resume(Launch& L, RunStats& st, int threads) {
 		}
 		c->req = REQ_NONE;
 		c->task.h.resume();
-	}
+	});
 	st.t_host += now_s() - t0;
 }
 
 // One scheduler iteration over `act`: every pending request in one launch per kind,
 // then the served reads resume.  Returns false when no read is waiting.
-bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st, int threads) {
+bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st) {
 	Launch& L = launch_[0];
-	gather(L, act, threads);
+	gather(L, act);
 	if(L.ws.empty() && L.wr.empty() && L.wd.empty()) return false;
 	static const bool trace = std::getenv("BT2X_TRACE") != nullptr;
 	if(trace) std::fprintf(stderr, "BT2X_TRACE active=%zu seed=%zu resolve=%zu dp=%zu\n", act.size(), L.ws.size(),
 	                       L.wr.size(), L.wd.size());
 	execute(L);
-	scatter_resume(L, st, threads);
+	scatter_resume(L, st);
 	return true;
 }
 
@@ -1096,10 +1097,16 @@ void count(RunStats& st, const ReadCtx* c) {
 }
 }
 
+WorkPool& Aligner::pool() { return *pool_; }
+
+void Aligner::use_threads(int threads) {
+	if(!pool_ || pool_->threads() != std::max(1, threads)) pool_.reset(new WorkPool(threads));
+}
+
 ReadCtx* Aligner::take_ctx() {
 	if(free_.empty()) {
-		pool_.emplace_back(new ReadCtx);
-		return pool_.back().get();
+		ctxs_.emplace_back(new ReadCtx);
+		return ctxs_.back().get();
 	}
 	ReadCtx* c = free_.back();
 	free_.pop_back();
@@ -1108,9 +1115,8 @@ ReadCtx* Aligner::take_ctx() {
 
 Aligner::~Aligner() {
 	// contexts hold tens of buffers each: release them in parallel
-	const long n = (long)pool_.size();
-#pragma omp parallel for schedule(static, 256)
-	for(long i = 0; i < n; i++) pool_[(size_t)i].reset();
+	const long n = (long)ctxs_.size();
+	if(pool_) pool().parallel_for(n, 256, [&](long i) { ctxs_[(size_t)i].reset(); });
 }
 
 // Retire the finished reads of `act` (their records go to the ring, their contexts back
@@ -1135,6 +1141,7 @@ void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, void* ringp) {
 
 RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads, double* t_run) {
 	RunStats st;
+	use_threads(threads);
 	const double t_start = now_s();
 	const std::string hdr = header();
 	std::fwrite(hdr.data(), 1, hdr.size(), out);
@@ -1162,13 +1169,12 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
 		ring.reserve(rdid + (uint64_t)nf);
 		st.t_alloc += now_s() - t0;
-#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-		for(long i = 0; i < nf; i++) {
+		pool().parallel_for(nf, 64, [&](long i) {
 			ReadCtx* c = fresh[(size_t)i];
 			FastqReader::decode(raw[(size_t)i], c->rd, rdid + (uint64_t)i, p_.randSeed);
 			c->task = align_read(c);
 			c->task.h.resume();
-		}
+		});
 		rdid += (uint64_t)nf;
 		st.t_host += now_s() - t0;
 		co.insert(co.end(), fresh.begin(), fresh.end());
@@ -1185,7 +1191,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			refill(act, slots);
 			if(act.empty()) break;
 			const double t0 = now_s();
-			step(act, st, threads);
+			step(act, st);
 			st.t_step += now_s() - t0;
 			retire_write(act);
 		}
@@ -1198,10 +1204,10 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		auto empty = [](const Launch& L) { return L.ws.empty() && L.wr.empty() && L.wd.empty(); };
 		int a = 0;
 		refill(co[0], cap);
-		gather(launch_[0], co[0], threads);
+		gather(launch_[0], co[0]);
 		std::thread gpu([this] { execute(launch_[0]); });
 		refill(co[1], cap);
-		gather(launch_[1], co[1], threads);
+		gather(launch_[1], co[1]);
 		while(true) {
 			// invariant: the GPU thread runs launch a (cohort a waits on it); launch b is
 			// gathered from cohort b
@@ -1211,10 +1217,10 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			const int b = 1 - a;
 			gpu = std::thread([this, b] { execute(launch_[b]); });
 			const double t1 = now_s();
-			scatter_resume(launch_[a], st, threads);
+			scatter_resume(launch_[a], st);
 			retire_write(co[a]);
 			refill(co[a], cap);
-			gather(launch_[a], co[a], threads);
+			gather(launch_[a], co[a]);
 			st.t_step += now_s() - t1;
 			if(eof && co[a].empty() && co[b].empty() && empty(launch_[a]) && empty(launch_[b])) break;
 			a = b;
@@ -1231,6 +1237,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 
 std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threads, RunStats* stp) {
 	RunStats st;
+	use_threads(threads);
 	std::vector<ReadCtx*> act, fresh;
 	OutRing ring;
 	std::string out;
@@ -1247,14 +1254,13 @@ std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threa
 		}
 		ring.reserve(next);
 		const long nf = (long)fresh.size();
-#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-		for(long i = 0; i < nf; i++) {
+		pool().parallel_for(nf, 64, [&](long i) {
 			fresh[i]->task = align_read(fresh[i]);
 			fresh[i]->task.h.resume();
-		}
+		});
 		act.insert(act.end(), fresh.begin(), fresh.end());
 		if(act.empty()) break;
-		step(act, st, threads);
+		step(act, st);
 		retire(act, st, &ring);
 		ring.drain([&](const std::string& s) { out += s; });
 	}

@@ -109,6 +109,7 @@ void usage() {
 } // namespace
 
 int main(int argc, char** argv) {
+	tune_malloc();
 	std::string idx, fq, outp;
 	Params p;
 	int threads = 16, device = 0;
@@ -149,6 +150,8 @@ int main(int argc, char** argv) {
 		Aligner al(p, ref, be);
 		al.set_pipeline(pipeline);
 		FastqReader reader(fq.c_str());
+		struct rusage ru0;
+		getrusage(RUSAGE_SELF, &ru0);
 		const auto t_start = std::chrono::steady_clock::now();
 		std::FILE* out = outp.empty() ? stdout : std::fopen(outp.c_str(), "wb");
 		if(!out) { std::fprintf(stderr, "cannot open %s\n", outp.c_str()); return 1; }
@@ -157,6 +160,8 @@ int main(int argc, char** argv) {
 		const RunStats st = al.run(reader, out, slots, threads);
 		if(out != stdout) std::fclose(out); else std::fflush(out);
 		const double t_align = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+		struct rusage ru_end;
+		getrusage(RUSAGE_SELF, &ru_end);
 		// alignment summary (AlnSink::printAlSumm, unpaired)
 		auto pct = [&](uint64_t a) { return st.reads ? 100.0 * (double)a / (double)st.reads : 0.0; };
 		std::fprintf(stderr, "%llu reads; of these:\n", (unsigned long long)st.reads);
@@ -166,11 +171,16 @@ int main(int argc, char** argv) {
 		std::fprintf(stderr, "    %llu (%.2f%%) aligned >1 times\n", (unsigned long long)st.rep, pct(st.rep));
 		std::fprintf(stderr, "%.2f%% overall alignment rate\n", pct(st.aligned));
 		if(stats) {
+			// the whole process, then the alignment window alone
 			struct rusage ru;
 			getrusage(RUSAGE_SELF, &ru);
+			auto sec = [](const timeval& t) { return t.tv_sec + t.tv_usec * 1e-6; };
 			std::fprintf(stderr, "BT2X_RUSAGE user=%.3f sys=%.3f maxrss_mib=%ld minflt=%ld majflt=%ld vcsw=%ld ivcsw=%ld\n",
-			             ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6, ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6,
-			             ru.ru_maxrss / 1024, ru.ru_minflt, ru.ru_majflt, ru.ru_nvcsw, ru.ru_nivcsw);
+			             sec(ru.ru_utime), sec(ru.ru_stime), ru.ru_maxrss / 1024, ru.ru_minflt, ru.ru_majflt, ru.ru_nvcsw,
+			             ru.ru_nivcsw);
+			std::fprintf(stderr, "BT2X_RUSAGE_ALIGN user=%.3f sys=%.3f minflt=%ld vcsw=%ld ivcsw=%ld\n",
+			             sec(ru_end.ru_utime) - sec(ru0.ru_utime), sec(ru_end.ru_stime) - sec(ru0.ru_stime),
+			             ru_end.ru_minflt - ru0.ru_minflt, ru_end.ru_nvcsw - ru0.ru_nvcsw, ru_end.ru_nivcsw - ru0.ru_nivcsw);
 		}
 		if(stats)
 			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "

@@ -9,6 +9,7 @@
 //
 //   test_e2e_oracle <index base> <reads.fq> [--dpad N] [--slots N] [-p T]
 #include <chrono>
+#include <sys/resource.h>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -88,6 +89,7 @@ private:
 }
 
 int main(int argc, char** argv) {
+	tune_malloc();
 	if(argc < 3) { std::fprintf(stderr, "usage: test_e2e_oracle <index> <reads.fq> [--dpad N] [--slots N] [-p T]\n"); return 1; }
 	Params p;
 	size_t slots = 4096;
@@ -125,10 +127,16 @@ int main(int argc, char** argv) {
 		Aligner al(p, ref, rb);
 		al.set_pipeline(pipeline);
 		FastqReader fq(argv[2]);
+		struct rusage ru0, ru1;
+		getrusage(RUSAGE_SELF, &ru0);
 		const auto t0 = std::chrono::steady_clock::now();
 		double t_run = 0;
 		const RunStats st = al.run(fq, stdout, slots, threads, &t_run);
 		const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+		getrusage(RUSAGE_SELF, &ru1);
+		auto sec = [](const timeval& a, const timeval& b) { return (b.tv_sec - a.tv_sec) + (b.tv_usec - a.tv_usec) * 1e-6; };
+		std::fprintf(stderr, "HOST_TIMING rusage user=%.3f sys=%.3f minflt=%ld vcsw=%ld\n", sec(ru0.ru_utime, ru1.ru_utime),
+		             sec(ru0.ru_stime, ru1.ru_stime), ru1.ru_minflt - ru0.ru_minflt, ru1.ru_nvcsw - ru0.ru_nvcsw);
 		std::fprintf(stderr, "HOST_TIMING t_alloc=%.3f t_step=%.3f t_wait=%.3f t_backend=%.3f t_run=%.3f\n", st.t_alloc,
 		             st.t_step, st.t_wait, st.t_backend, t_run);
 		std::fprintf(stderr, "HOST_TIMING reads=%llu wall=%.3f t_host=%.3f t_io=%.3f t_seed=%.3f t_resolve=%.3f t_dp=%.3f "

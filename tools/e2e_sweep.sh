@@ -7,6 +7,9 @@ W=/tmp/bt2x_bench_$(id -u)
 ALIGN=$(dirname "$0")/../omp-bowtie2-prime_amd/bt2x/bt2x-align
 for opts in "$@"; do
   echo "== $opts"
-  timeout -k 10 300 "$ALIGN" -x "$W/syn1000000000_s2024" -U "$W/rank0/reads.fq" -S "$W/sweep.sam" --dpad 12 \
+  # an option set may start with VAR=value environment settings
+  envs=()
+  while [[ "$opts" =~ ^([A-Z_]+=[^ ]*)\ (.*)$ ]]; do envs+=("${BASH_REMATCH[1]}"); opts="${BASH_REMATCH[2]}"; done
+  timeout -k 10 300 env "${envs[@]}" "$ALIGN" -x "$W/syn1000000000_s2024" -U "$W/rank0/reads.fq" -S "$W/sweep.sam" --dpad 12 \
       -p "${OMP_NUM_THREADS:-16}" --stats $opts 2>&1 | grep -E "BT2X_STATS|BT2X_RUSAGE|overall" || exit 1
 done
