@@ -134,10 +134,13 @@ struct DevBuf {
 	void release() { if(p) (void)hipFree(p); p = nullptr; cap = 0; }
 };
 
+// Every resource the context holds is released by its destructor, so bt2x_open's early
+// error returns (through HIPCHK and friends) leak nothing.
 struct bt2x_ctx {
+	~bt2x_ctx();
 	int device = 0;
 	hipStream_t stream = nullptr;
-	hipEvent_t ev[BT2X_K_COUNT][2];
+	hipEvent_t ev[BT2X_K_COUNT][2] = {};
 	bool ev_valid[BT2X_K_COUNT] = {};
 	DevIndex ix{};
 	DevScoring sc{};
@@ -153,6 +156,27 @@ struct bt2x_ctx {
 	uint32_t* d_counters = nullptr;
 	uint64_t n_seed_last = 0, n_dp_last = 0, n_resolve_last = 0;
 };
+
+bt2x_ctx::~bt2x_ctx() {
+	(void)hipSetDevice(device);
+	if(stream) (void)hipStreamSynchronize(stream);
+	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch})
+		b->release();
+	for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen, (void*)d_stats,
+	               (void*)d_counters, (void*)d_queue})
+		if(p) (void)hipFree(p);
+	for(int k = 0; k < BT2X_K_COUNT; k++)
+		for(int j = 0; j < 2; j++) if(ev[k][j]) (void)hipEventDestroy(ev[k][j]);
+	if(stream) (void)hipStreamDestroy(stream);
+}
+
+namespace {
+// a temporary device allocation freed on every exit path
+struct DevTmp {
+	void* p = nullptr;
+	~DevTmp() { if(p) (void)hipFree(p); }
+};
+}
 
 namespace {
 DevScoring to_dev(const bt2x_scoring& s) {
@@ -227,12 +251,11 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 			HIPCHK(hipMemset(c->d_text, 0, tbytes));
 			HIPCHK(hipMemcpy(c->d_text, idx->text2, idx->text2_bytes, hipMemcpyHostToDevice));
 			HIPCHK(hipMalloc(&c->d_sa, (idx->len + 1) * sizeof(uint32_t) + 64));
-			void* d_offs = nullptr;
-			HIPCHK(hipMalloc(&d_offs, idx->offs_len * sizeof(uint64_t)));
-			HIPCHK(hipMemcpy(d_offs, idx->offs, idx->offs_len * sizeof(uint64_t), hipMemcpyHostToDevice));
-			const int rc = bt2x_build_sa(c->ix, (const uint64_t*)d_offs, idx->offs_len, (uint32_t*)c->d_sa, c->stream);
+			DevTmp d_offs;
+			HIPCHK(hipMalloc(&d_offs.p, idx->offs_len * sizeof(uint64_t)));
+			HIPCHK(hipMemcpy(d_offs.p, idx->offs, idx->offs_len * sizeof(uint64_t), hipMemcpyHostToDevice));
+			const int rc = bt2x_build_sa(c->ix, (const uint64_t*)d_offs.p, idx->offs_len, (uint32_t*)c->d_sa, c->stream);
 			HIPCHK(hipStreamSynchronize(c->stream));
-			(void)hipFree(d_offs);
 			if(rc) return rc;
 			c->ix.sa = (const uint32_t*)c->d_sa;
 			c->ix.text = (const uint32_t*)c->d_text;
@@ -273,18 +296,7 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 }
 
 extern "C" void bt2x_close(bt2x_ctx* c) {
-	if(!c) return;
-	(void)hipSetDevice(c->device);
-	(void)hipStreamSynchronize(c->stream);
-	for(DevBuf* b : {&c->b_reads, &c->b_quals, &c->b_refs, &c->b_in, &c->b_out, &c->b_recs,
-	                 &c->b_edits, &c->b_dbg_dig, &c->b_dbg_cand, &c->scratch}) b->release();
-	(void)hipFree(c->d_ebwt); (void)hipFree(c->d_ftab); (void)hipFree(c->d_eftab); (void)hipFree(c->d_blk);
-	(void)hipFree(c->d_sa); (void)hipFree(c->d_text);
-	(void)hipFree(c->d_offs); (void)hipFree(c->d_rstarts); (void)hipFree(c->d_plen);
-	(void)hipFree(c->d_stats); (void)hipFree(c->d_counters); (void)hipFree(c->d_queue);
-	for(int k = 0; k < BT2X_K_COUNT; k++) { (void)hipEventDestroy(c->ev[k][0]); (void)hipEventDestroy(c->ev[k][1]); }
-	(void)hipStreamDestroy(c->stream);
-	delete c;
+	delete c;        // ~bt2x_ctx releases everything
 }
 
 extern "C" double bt2x_last_kernel_ms(const bt2x_ctx* c, int k) {

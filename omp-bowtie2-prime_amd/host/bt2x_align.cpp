@@ -29,9 +29,10 @@
 #include <mutex>
 #include <x86intrin.h>
 namespace {
-constexpr int kPhases = 10;
+constexpr int kPhases = 16;
 const char* kPhaseName[kPhases] = {"init", "seeds", "rank", "prioritize", "resolve_in", "walk", "lookahead",
-                                   "records", "finish", "scatter"};
+                                   "records", "finish", "scatter", "g_pass1", "g_bases", "g_pass2", "prio_hits",
+                                   "prio_small", "n_samples"};
 struct PhaseAcc { uint64_t c[kPhases] = {}; uint64_t last = 0; PhaseAcc(); };
 std::mutex g_ph_mu;
 std::vector<PhaseAcc*> g_ph_all;
@@ -664,6 +665,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 				c->exRange[fw ? 0 : 1].push_back({p5, (size_t)seedlen + sp.nlex, sp.size});
 			}
 		}
+		PH(13);
 		std::stable_sort(satpos2.begin(), satpos2.end());
 		size_t nelt_added = 0;
 		for(size_t j = 0; j < nsmall && nelt_added < maxelt; j++) {
@@ -671,12 +673,16 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			rand_ns.push_back((uint32_t)satpos2[j].size);
 			nelt_added += satpos2[j].size;
 		}
+		PH(14);
 		if(!(nelt_added >= maxelt || nsmall == satpos2.size())) {
 			c->rows.init(satpos2, nsmall, satpos2.size());
 			std::vector<Random1toN>& rands = c->prioRands;
 			if(rands.size() < satpos2.size()) rands.resize(satpos2.size());
 			for(size_t q = 0; q < satpos2.size(); q++) rands[q].reset();
 			while(nelt_added < maxelt && nelt_added < nelt) {
+#ifdef BT2X_PHASE_PROF
+				t_ph.c[kPhases - 1]++;
+#endif
 				const size_t ri = c->rows.next(rnd) + nsmall;
 				if(!rands[ri].inited()) rands[ri].init((uint16_t)satpos2[ri].size, false);
 				const size_t rr = rands[ri].next(rnd);
@@ -836,75 +842,101 @@ double now_s() {
 // ----- one launch: gather a cohort's waiting requests, run them, scatter the results
 
 // Classify the cohort's reads by pending request and fill the launch's input buffers
-// (one seed, one resolve and one DP launch; gathers in parallel over reads).
+// (one seed, one resolve and one DP launch).  Two parallel passes over chunks of the
+// cohort: sizes per chunk, then (after a prefix sum over chunks) the copies; the
+// waiting lists keep cohort order, so a launch's layout is deterministic.
 void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
-	L.ws.clear(); L.wr.clear(); L.wd.clear();
-	for(ReadCtx* c : cohort) {
-		if(c->req == REQ_SEED) L.ws.push_back(c);
-		else if(c->req == REQ_RESOLVE) L.wr.push_back(c);
-		else if(c->req == REQ_DP) L.wd.push_back(c);
-	}
-	const long nws = (long)L.ws.size(), nwr = (long)L.wr.size(), nwd = (long)L.wd.size();
-	if(nws) {
-		// patFw+patRc of each read, then its seeds with read_off rebased
-		L.sr.assign(nws + 1, 0); L.sk.assign(nws + 1, 0);
-		for(long i = 0; i < nws; i++) {
-			L.sr[i + 1] = L.sr[i] + 2 * L.ws[i]->rd.length();
-			L.sk[i + 1] = L.sk[i] + L.ws[i]->seed_in.size();
-		}
-		L.seed_reads.resize(L.sr[nws]);
-		L.seed_in.resize(L.sk[nws]);
-		pool().parallel_for(nws, 256, [&](long i) {
-			const ReadCtx* c = L.ws[i];
-			const size_t n = c->rd.length();
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.seed_reads.begin() + (long)L.sr[i]);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.seed_reads.begin() + (long)(L.sr[i] + n));
-			for(size_t k = 0; k < c->seed_in.size(); k++) {
-				bt2x_seed_in q = c->seed_in[k];
-				q.read_off += L.sr[i];
-				L.seed_in[L.sk[i] + k] = q;
+	const double tg = now_s();
+	constexpr long kChunk = 1024;
+	const long n = (long)cohort.size();
+	const long nch = (n + kChunk - 1) / kChunk;
+	if((long)L.chunks.size() < nch) L.chunks.resize((size_t)nch);
+	PH_START();
+	pool().parallel_for(nch, 1, [&](long ch) {
+		Launch::Chunk& C = L.chunks[(size_t)ch];
+		C.ws.clear(); C.wr.clear(); C.wd.clear();
+		C.sbytes = C.nseed = C.nres = C.dbytes = C.nprob = C.rbytes = 0;
+		const long e = std::min(n, (ch + 1) * kChunk);
+		for(long i = ch * kChunk; i < e; i++) {
+			ReadCtx* c = cohort[(size_t)i];
+			if(c->req == REQ_SEED) {
+				C.ws.push_back(c); C.sbytes += 2 * c->rd.length(); C.nseed += c->seed_in.size();
+			} else if(c->req == REQ_RESOLVE) {
+				C.wr.push_back(c); C.nres += c->res_in.size();
+			} else if(c->req == REQ_DP) {
+				C.wd.push_back(c); C.dbytes += 2 * c->rd.length(); C.nprob += c->dps.size();
+				for(const DpWork& d : c->dps) C.rbytes += d.key.ncol;
 			}
-		});
-	}
-	if(nwr) {
-		L.rk.assign(nwr + 1, 0);
-		for(long i = 0; i < nwr; i++) L.rk[i + 1] = L.rk[i] + L.wr[i]->res_in.size();
-		L.res_in.resize(L.rk[nwr]);
-		pool().parallel_for(nwr, 256, [&](long i) { std::copy(L.wr[i]->res_in.begin(), L.wr[i]->res_in.end(), L.res_in.begin() + (long)L.rk[i]); });
-	}
-	if(nwd) {
-		// the read's two orientations (codes and qualities) once per read, one reference
-		// window per posed problem (BitPairReference::getStretch)
-		L.qb.assign(nwd + 1, 0); L.pb.assign(nwd + 1, 0);
-		for(long i = 0; i < nwd; i++) {
-			L.qb[i + 1] = L.qb[i] + 2 * L.wd[i]->rd.length();
-			L.pb[i + 1] = L.pb[i] + L.wd[i]->dps.size();
 		}
-		const uint64_t np = L.pb[nwd];
-		L.fb.assign(np + 1, 0);
-		for(long i = 0; i < nwd; i++)
-			for(size_t j = 0; j < L.wd[i]->dps.size(); j++)
-				L.fb[L.pb[i] + j + 1] = L.fb[L.pb[i] + j] + L.wd[i]->dps[j].key.ncol;
-		L.dp_reads.resize(L.qb[nwd]); L.dp_quals.resize(L.qb[nwd]); L.dp_refs.resize(L.fb[np]);
-		L.dp_in.resize(np);
-		pool().parallel_for(nwd, 256, [&](long i) {
-			const ReadCtx* c = L.wd[i];
-			const size_t n = c->rd.length();
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)L.qb[i]);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.dp_reads.begin() + (long)(L.qb[i] + n));
-			std::copy(c->rd.qual.begin(), c->rd.qual.end(), L.dp_quals.begin() + (long)L.qb[i]);
-			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), L.dp_quals.begin() + (long)(L.qb[i] + n));
-			for(size_t j = 0; j < c->dps.size(); j++) {
-				const DpWork& d = c->dps[j];
-				const uint64_t k = L.pb[i] + j;
+	});
+	PH(10);
+	// chunk bases
+	uint64_t nws = 0, nwr = 0, nwd = 0, sb = 0, sk = 0, rk = 0, db = 0, pk = 0, rb = 0;
+	for(long ch = 0; ch < nch; ch++) {
+		Launch::Chunk& C = L.chunks[(size_t)ch];
+		C.ws0 = nws; C.sb0 = sb; C.sk0 = sk; C.wr0 = nwr; C.rk0 = rk; C.wd0 = nwd; C.db0 = db; C.pk0 = pk; C.rb0 = rb;
+		nws += C.ws.size(); sb += C.sbytes; sk += C.nseed;
+		nwr += C.wr.size(); rk += C.nres;
+		nwd += C.wd.size(); db += C.dbytes; pk += C.nprob; rb += C.rbytes;
+	}
+	L.ws.resize(nws); L.wr.resize(nwr); L.wd.resize(nwd);
+	L.sr.resize(nws + 1); L.sk.resize(nws + 1); L.rk.resize(nwr + 1);
+	L.qb.resize(nwd + 1); L.pb.resize(nwd + 1); L.fb.resize(pk + 1);
+	L.sr[nws] = sb; L.sk[nws] = sk; L.rk[nwr] = rk; L.qb[nwd] = db; L.pb[nwd] = pk; L.fb[pk] = rb;
+	PH(11);
+	L.seed_reads.resize(sb); L.seed_in.resize(sk);
+	L.res_in.resize(rk);
+	L.dp_reads.resize(db); L.dp_quals.resize(db); L.dp_refs.resize(rb); L.dp_in.resize(pk);
+	pool().parallel_for(nch, 1, [&](long ch) {
+		const Launch::Chunk& C = L.chunks[(size_t)ch];
+		// seeds: patFw+patRc of each read, then its seeds with read_off rebased
+		uint64_t sbo = C.sb0, sko = C.sk0;
+		for(size_t k = 0; k < C.ws.size(); k++) {
+			ReadCtx* c = C.ws[k];
+			const size_t i = C.ws0 + k, len = c->rd.length();
+			L.ws[i] = c; L.sr[i] = sbo; L.sk[i] = sko;
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.seed_reads.begin() + (long)sbo);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.seed_reads.begin() + (long)(sbo + len));
+			for(const bt2x_seed_in& q0 : c->seed_in) {
+				bt2x_seed_in q = q0;
+				q.read_off += sbo;
+				L.seed_in[sko++] = q;
+			}
+			sbo += 2 * len;
+		}
+		// SA elements
+		uint64_t rko = C.rk0;
+		for(size_t k = 0; k < C.wr.size(); k++) {
+			ReadCtx* c = C.wr[k];
+			L.wr[C.wr0 + k] = c; L.rk[C.wr0 + k] = rko;
+			std::copy(c->res_in.begin(), c->res_in.end(), L.res_in.begin() + (long)rko);
+			rko += c->res_in.size();
+		}
+		// DP: the read's two orientations (codes and qualities) once per read, one
+		// reference window per posed problem (BitPairReference::getStretch)
+		uint64_t dbo = C.db0, pko = C.pk0, rbo = C.rb0;
+		for(size_t k = 0; k < C.wd.size(); k++) {
+			ReadCtx* c = C.wd[k];
+			const size_t i = C.wd0 + k, len = c->rd.length();
+			L.wd[i] = c; L.qb[i] = dbo; L.pb[i] = pko;
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)dbo);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.dp_reads.begin() + (long)(dbo + len));
+			std::copy(c->rd.qual.begin(), c->rd.qual.end(), L.dp_quals.begin() + (long)dbo);
+			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), L.dp_quals.begin() + (long)(dbo + len));
+			for(const DpWork& d : c->dps) {
 				bt2x_dp_in q = d.in;
-				q.read_off = q.qual_off = L.qb[i] + (d.key.fw ? 0 : n);
-				q.ref_off = L.fb[k];
-				ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, L.dp_refs.data() + L.fb[k]);
-				L.dp_in[k] = q;
+				q.read_off = q.qual_off = dbo + (d.key.fw ? 0 : len);
+				q.ref_off = rbo;
+				L.fb[pko] = rbo;
+				ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, L.dp_refs.data() + rbo);
+				L.dp_in[pko++] = q;
+				rbo += d.key.ncol;
 			}
-		});
-	}
+			dbo += 2 * len;
+		}
+	});
+	PH(12);
+	L.t_gather = now_s() - tg;
 }
 
 // The launch's backend calls (on the GPU thread when pipelined).
@@ -940,6 +972,7 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	L.run.insert(L.run.end(), L.wd.begin(), L.wd.end());
 	const long nrun = (long)L.run.size();
 	const double t0 = now_s();
+	st.t_gather += L.t_gather;
 	pool().parallel_for(nrun, 64, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
 		if(i < nws) {
@@ -1182,8 +1215,10 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	auto retire_write = [&](std::vector<ReadCtx*>& co) {
 		const double t0 = now_s();
 		retire(co, st, &ring);
+		const double t1 = now_s();
 		ring.drain([&](const std::string& s) { writer.append(s); });
 		st.t_io += now_s() - t0;
+		st.t_retire += t1 - t0;
 	};
 	if(!pipeline_) {
 		std::vector<ReadCtx*> act;

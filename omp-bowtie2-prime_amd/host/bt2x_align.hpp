@@ -815,7 +815,7 @@ struct RunStats {
 	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0;
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
 	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
-	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0, t_wait = 0;
+	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0, t_wait = 0, t_gather = 0, t_retire = 0;
 };
 
 class Aligner {
@@ -847,7 +847,14 @@ private:
 		std::vector<bt2x_dp_out> dp_out;
 		std::vector<bt2x_aln_rec> recs;
 		std::vector<uint32_t> edits;
-		double t_seed = 0, t_resolve = 0, t_dp = 0;
+		double t_seed = 0, t_resolve = 0, t_dp = 0, t_gather = 0;
+		// gather's per-chunk lists, sizes and bases
+		struct Chunk {
+			std::vector<ReadCtx*> ws, wr, wd;
+			uint64_t sbytes = 0, nseed = 0, nres = 0, dbytes = 0, nprob = 0, rbytes = 0;
+			uint64_t ws0 = 0, sb0 = 0, sk0 = 0, wr0 = 0, rk0 = 0, wd0 = 0, db0 = 0, pk0 = 0, rb0 = 0;
+		};
+		std::vector<Chunk> chunks;
 	};
 	ReadTask align_read(ReadCtx* c);
 	bool step(std::vector<ReadCtx*>& active, RunStats& st);

@@ -185,11 +185,11 @@ int main(int argc, char** argv) {
 		if(stats)
 			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "
 			             "resolve_launches=%llu resolves=%llu t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f "
-			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu t_backend=%.4f t_step=%.4f t_wait=%.4f\n", (unsigned long long)st.reads, t_align,
+			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu t_backend=%.4f t_step=%.4f t_wait=%.4f t_gather=%.4f t_retire=%.4f\n", (unsigned long long)st.reads, t_align,
 			             (unsigned long long)st.seed_launches, (unsigned long long)st.seeds, st.t_seed,
 			             (unsigned long long)st.resolve_launches, (unsigned long long)st.resolves, st.t_resolve,
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io, (unsigned long long)st.dps_used,
-			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait);
+			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait, st.t_gather, st.t_retire);
 	} catch(const std::exception& e) {
 		std::fprintf(stderr, "bt2x-align: %s\n", e.what());
 		return 1;

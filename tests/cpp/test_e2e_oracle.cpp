@@ -137,8 +137,8 @@ int main(int argc, char** argv) {
 		auto sec = [](const timeval& a, const timeval& b) { return (b.tv_sec - a.tv_sec) + (b.tv_usec - a.tv_usec) * 1e-6; };
 		std::fprintf(stderr, "HOST_TIMING rusage user=%.3f sys=%.3f minflt=%ld vcsw=%ld\n", sec(ru0.ru_utime, ru1.ru_utime),
 		             sec(ru0.ru_stime, ru1.ru_stime), ru1.ru_minflt - ru0.ru_minflt, ru1.ru_nvcsw - ru0.ru_nvcsw);
-		std::fprintf(stderr, "HOST_TIMING t_alloc=%.3f t_step=%.3f t_wait=%.3f t_backend=%.3f t_run=%.3f\n", st.t_alloc,
-		             st.t_step, st.t_wait, st.t_backend, t_run);
+		std::fprintf(stderr, "HOST_TIMING t_alloc=%.3f t_step=%.3f t_wait=%.3f t_backend=%.3f t_gather=%.3f t_retire=%.3f t_run=%.3f\n",
+		             st.t_alloc, st.t_step, st.t_wait, st.t_backend, st.t_gather, st.t_retire, t_run);
 		std::fprintf(stderr, "HOST_TIMING reads=%llu wall=%.3f t_host=%.3f t_io=%.3f t_seed=%.3f t_resolve=%.3f t_dp=%.3f "
 		             "launches=%llu/%llu/%llu dps=%llu dps_used=%llu\n", (unsigned long long)st.reads, t, st.t_host, st.t_io, st.t_seed,
 		             st.t_resolve, st.t_dp, (unsigned long long)st.seed_launches,
