@@ -71,7 +71,7 @@ def parse():
 
 def workload_key(args) -> str:
     g = f"synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}" if args.genome == "synthetic" else args.genome
-    return f"e2e|{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}|la{args.lookahead}"
+    return f"e2e|{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}|la{args.lookahead}|round"
 
 
 def pmc_traffic(args, kernel: str):
@@ -211,7 +211,7 @@ def load_dumps(ddir):
     out = []
     for path in sorted(glob.glob(os.path.join(ddir, "*.*"))):
         kind = path.rsplit(".", 1)[1]
-        nparts = {"seed": 2, "resolve": 1, "dp": 5}[kind]
+        nparts = {"seed": 2, "resolve": 1, "dp": 5, "round": 5}[kind]
         raw = np.fromfile(path, dtype=np.uint8)
         sizes = raw[:8 * nparts].view(np.uint64).astype(np.int64)
         parts, o = [], 8 * nparts
@@ -221,6 +221,11 @@ def load_dumps(ddir):
             parts[1] = parts[1].view(abi.SEED_IN)
         elif kind == "resolve":
             parts[0] = parts[0].view(abi.RESOLVE_IN)
+        elif kind == "round":
+            parts[1] = parts[1].view(abi.SEED_IN)
+            parts[2] = parts[2].view(abi.ROUND_IN)
+            parts[3] = parts[3].view(abi.EXRANGE)
+            parts[4] = parts[4].view(np.uint64)
         else:
             parts[3] = parts[3].view(abi.DP_IN)
             parts[4] = parts[4].view(np.uint64)
@@ -335,6 +340,18 @@ def main():
             m = len(parts[0])
             plan.append((kind, m, [to_dev(parts[0]),
                                    torch.empty(m * abi.RESOLVE_OUT.itemsize, dtype=torch.uint8, device=dev)]))
+        elif kind == "round":
+            m = len(parts[2])
+            meta = parts[4]
+            caps = [int(meta[1]) + 1024, int(meta[2]) + 1024, int(meta[3]) + 256]   # sizes the aligner saw
+            exr = parts[3] if len(parts[3]) else np.zeros(1, dtype=abi.EXRANGE)
+            plan.append((kind, m, [to_dev(parts[0]), to_dev(parts[1]), len(parts[1]), to_dev(parts[2]), to_dev(exr),
+                                   int(meta[0]),
+                                   torch.empty(m * abi.ROUND_OUT.itemsize, dtype=torch.uint8, device=dev),
+                                   torch.empty(caps[0] * abi.SAT.itemsize, dtype=torch.uint8, device=dev), caps[0],
+                                   torch.empty(caps[1] * abi.RESOLVE_OUT.itemsize, dtype=torch.uint8, device=dev), caps[1],
+                                   torch.empty(caps[2] * abi.EXRANGE.itemsize, dtype=torch.uint8, device=dev), caps[2],
+                                   torch.zeros(4, dtype=torch.int32, device=dev)]))
         else:
             m = len(parts[3])
             rec_cap, edit_cap = int(parts[4][0]) + 1024, int(parts[4][1]) + 4096   # sizes the aligner saw
@@ -345,10 +362,12 @@ def main():
                                    torch.zeros(16, dtype=torch.int32, device=dev), rec_cap, edit_cap]))
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
-    kid = {"seed": abi.K_SEED, "resolve": abi.K_RESOLVE, "dp": abi.K_DP}
-    units = {"seed": 0, "resolve": 0, "dp": 0}
-    for kind, m, _ in plan:
+    kid = {"seed": abi.K_SEED, "resolve": abi.K_RESOLVE, "dp": abi.K_DP, "round": abi.K_ROUND}
+    units = {"seed": 0, "resolve": 0, "dp": 0, "round": 0}
+    for kind, m, b in plan:
         units[kind] += m
+        if kind == "round":
+            units["seed"] += b[2]
 
     def step(record=None, counters=None):
         for kind, m, b in plan:
@@ -356,16 +375,25 @@ def main():
                 ctx.seed_search_dev(b[0].data_ptr(), b[1].data_ptr(), m, b[2].data_ptr(), True, sh)
             elif kind == "resolve":
                 ctx.resolve_dev(b[0].data_ptr(), m, b[1].data_ptr(), False, sh)
+            elif kind == "round":
+                ctx.seed_round_dev(b[0].data_ptr(), b[1].data_ptr(), b[2], b[3].data_ptr(), m, b[4].data_ptr(), b[5],
+                                   b[6].data_ptr(), b[7].data_ptr(), b[8], b[9].data_ptr(), b[10], b[11].data_ptr(),
+                                   b[12], b[13].data_ptr(), sh)
             else:
                 ctx.dp_align_dev(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), b[3].data_ptr(), m,
                                  b[4].data_ptr(), b[5].data_ptr(), b[8], b[6].data_ptr(), b[9],
                                  b[7].data_ptr(), sh)
             if record is not None:
-                # HIP events recorded on this stream around each launch (bt2x_last_kernel_ms)
+                # HIP events recorded on this stream around each launch (bt2x_last_kernel_ms);
+                # a round's seed kernel and ranking+resolution are also booked as seed / resolve
                 record[kind]["ms"] += ctx.last_kernel_ms(kid[kind])
+                if kind == "round":
+                    record["seed"]["ms"] += ctx.last_kernel_ms(abi.K_SEED)
+                    record["resolve"]["ms"] += ctx.last_kernel_ms(abi.K_RESOLVE)
             if counters is not None:
-                for k, v in ctx.last_counters(kid[kind]).items():
-                    counters[kind][k] = counters[kind].get(k, 0) + v
+                for kk in (("seed", "resolve") if kind == "round" else (kind,)):
+                    for k, v in ctx.last_counters(kid[kk]).items():
+                        counters[kk][k] = counters[kk].get(k, 0) + v
 
     ctr = {k: {} for k in kid}          # algorithmic-work counters (deterministic per step)
     for w in range(max(args.warmup, 1)):
@@ -403,6 +431,7 @@ def main():
     res_bytes = cr.get("alg_bytes", 0)
     dp_bytes = 3 * cd.get("dp_cells", 0) + cd.get("dp_cols", 0) + units["dp"] * 10 * ((R + 15) // 16) * 16
     kern = {"seed": (kms["seed"], fm_bytes), "resolve": (kms["resolve"], res_bytes), "dp": (kms["dp"], dp_bytes)}
+    # (round launches are booked above as their seed and resolve parts)
     dom = max(kern, key=lambda k: kern[k][0])
     ach = kern[dom][1] / (kern[dom][0] / 1e3) / 1e9 if kern[dom][0] > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args, dom)
@@ -412,6 +441,8 @@ def main():
     own = {"seed": cs.get("alg_bytes", 0), "resolve": cr.get("alg_bytes", 0), "dp": cd.get("alg_bytes", 0)}[dom]
     ach_own = own / (kern[dom][0] / 1e3) / 1e9 if kern[dom][0] > 0 else 0.0
     nl = {k: sum(1 for kk, _, _ in plan if kk == k) for k in kid}
+    nl["seed"] += nl["round"]
+    nl["resolve"] += nl["round"]
     line = {
         "metric": "M reads/s aligned (150 bp SE vs hg38) at 1/2/4/8 MI355X; % HBM-roofline",
         "value": round(value, 4), "unit": "M reads/s", "n_gpus": world, "steps": args.steps,
@@ -420,9 +451,10 @@ def main():
         "data": "synthetic (seeded genome + simulated 150 bp reads, BASELINE.md error model)",
         "config": {"workload": f"C3 stand-in: {R} bp SE, --dpad {args.dpad}, genome {gdesc}; step = the "
                                f"GPU launch sequence bt2x-align issues to align {n} reads end to end "
-                               f"({nl['seed']} seed, {nl['resolve']} resolve, {nl['dp']} DP launches: "
-                               f"{units['seed']} seeds, {units['resolve']} SA elements, {units['dp']} DP "
-                               f"problems), replayed from HBM",
+                               f"({nl['round']} seed-round launches (seed search + ranking/prioritization + SA "
+                               f"resolution), {nl['seed'] - nl['round']} seed, {nl['resolve'] - nl['round']} resolve, "
+                               f"{nl['dp']} DP launches: {units['seed']} seeds, {cr.get('n_problems', 0)} SA "
+                               f"elements, {units['dp']} DP problems), replayed from HBM",
                    "reads_per_gpu_step": n, "read_len": R, "parallelism": f"dp{world} (read shards)",
                    "key": workload_key(args)},
         # achieved = algorithmic bytes per launch / average launch time (= per-step bytes / per-step

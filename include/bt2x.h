@@ -121,7 +121,7 @@ typedef struct bt2x_ctx bt2x_ctx;
 int  bt2x_open(int hip_device, const bt2x_index_desc* idx, const bt2x_scoring* sc, bt2x_ctx** out);
 void bt2x_close(bt2x_ctx* ctx);
 /* Last kernel's duration in ms (HIP events on the launching stream), by kernel id. */
-enum { BT2X_K_SEED = 0, BT2X_K_DP = 1, BT2X_K_RESOLVE = 2, BT2X_K_COUNT = 3 };
+enum { BT2X_K_SEED = 0, BT2X_K_DP = 1, BT2X_K_RESOLVE = 2, BT2X_K_ROUND = 3, BT2X_K_COUNT = 4 };
 double bt2x_last_kernel_ms(const bt2x_ctx* ctx, int kernel);
 /* Algorithmic bytes / counters of the last call, by kernel id. */
 typedef struct {
@@ -304,6 +304,96 @@ int bt2x_resolve(bt2x_ctx* ctx, const bt2x_resolve_in* in, uint32_t n, int rejec
                  bt2x_resolve_out* out);
 int bt2x_resolve_dev(bt2x_ctx* ctx, const bt2x_resolve_in* d_in, uint32_t n, int reject_straddle,
                      bt2x_resolve_out* d_out, void* stream);
+
+/* ------------------------------------------------------------- seed round */
+
+/* One read's seed round: its seeds (searched as bt2x_seed_search does), then the rest of
+ * the round up to the first DP, per read on the GPU:
+ *   SeedAligner::searchAllSeedsFinalize + SeedResults::add  aligner_seed.cpp:508-540,
+ *                                                            aligner_seed.h:603-641
+ *   SeedResults::rankSeedHits                               aligner_seed.h:1000-1061
+ *   SwDriver::prioritizeSATups                               aligner_sw_driver.cpp:61-260
+ *     (RowSampler aligner_sw_driver.h:176-267, Random1toN random_util.h:32-230)
+ *   GroupWalk2S::advanceElement + joinedToTextOff for every   group_walk.h:969,
+ *     element extendSeeds may visit (as bt2x_resolve)        bt2_idx.cpp:54
+ * The read's RandomSource is carried in and out (rnd_last / rnd_lastoff = the LCG state
+ * and bit offset, random_source.h:34-140).  Seeds: in[r].nseeds entries of `seeds`
+ * starting at in[r].seed0, patFw seeds (read_off == in[r].read_off) and patRc seeds
+ * (read_off == in[r].read_off + rdlen) instantiated at depth i*interval + offset as in
+ * MultiSeedResults::instantiateSeeds (aligner_seed.cpp:411-447). */
+typedef struct {
+	uint64_t read_off;       /* patFw at reads[read_off], patRc right after it           */
+	uint64_t seed0;          /* first seed of the read in `seeds`                         */
+	uint32_t rnd_last;       /* RandomSource state before rankSeedHits                    */
+	int32_t  rnd_lastoff;
+	uint32_t exr0;           /* exRange entries of earlier rounds: exr[exr0 .. +nexr)     */
+	uint16_t nexr;
+	uint16_t nseeds;         /* seeds searched for the read                               */
+	uint16_t num_offs;       /* SeedResults::numOffs(): seed offsets per strand            */
+	uint16_t rdlen;
+	uint16_t interval;       /* msIval(rdlen)                                             */
+	uint16_t offset;         /* this round's offset: interval * round / nrounds           */
+	uint16_t seedlen;        /* multiseedLen clipped to rdlen                              */
+	uint16_t pad[3];
+} bt2x_round_in;
+
+/* extendSeeds' exRange entry: a read span [off, off+len) of strand fw already covered by
+ * a unique-extended range of sz elements (aligner_sw_driver.cpp:97-144). */
+typedef struct {
+	uint64_t sz;
+	uint32_t off;
+	uint16_t len;
+	uint8_t  fw;
+	uint8_t  pad;
+} bt2x_exrange;
+
+/* One SATupleAndPos of the read's extension list, in prioritizeSATups order: rand_n BW
+ * elements (the whole range when it has <= 5 elements, else one sampled element), seed
+ * at read offset rdoff of strand fw. */
+typedef struct {
+	uint32_t rdoff;
+	uint16_t rand_n;
+	uint8_t  fw;
+	uint8_t  seedlen;
+} bt2x_sat;
+
+enum { BT2X_ROUND_OK = 0, BT2X_ROUND_NO_HITS = 1, BT2X_ROUND_REDO = 2 };
+
+typedef struct {
+	uint32_t rnd_last;       /* RandomSource state after ranking and sampling             */
+	int32_t  rnd_lastoff;
+	uint64_t num_elts;       /* SeedResults::numElts()                                    */
+	uint32_t nonz;           /* SeedResults::nonzeroOffsets()                             */
+	uint32_t status;         /* BT2X_ROUND_OK; NO_HITS (no seed hit: the read's seed rounds
+	                            end); REDO: the read exceeded the kernel's per-read workspace
+	                            (more than 64 seed offsets per strand or very repetitive
+	                            sampling) -- the caller runs this round with
+	                            bt2x_seed_search + its own prioritization + bt2x_resolve    */
+	uint32_t sat0, nsat;     /* sats[sat0 .. +nsat)                                       */
+	uint32_t elt0, nelt;     /* elts[elt0 .. +nelt): the sats' elements in order           */
+	uint32_t exr0, nexr;     /* exRange entries this round added: exr_out[exr0 .. +nexr)   */
+} bt2x_round_out;
+
+/* maxelt: -D ... maxIters (prioritizeSATups' maxelt, 400 by default).  Output arenas are
+ * caller-sized; BT2X_E_OVERFLOW reports the required sizes in used[0..2] (sats, elts,
+ * exr_out) and the call may be repeated. */
+int bt2x_seed_round(bt2x_ctx* ctx, const uint8_t* reads, uint64_t reads_bytes,
+                    const bt2x_seed_in* seeds, uint32_t nseeds,
+                    const bt2x_round_in* in, uint32_t nreads,
+                    const bt2x_exrange* exr, uint32_t nexr, uint32_t maxelt,
+                    bt2x_round_out* out,
+                    bt2x_sat* sats, uint32_t sat_cap,
+                    bt2x_resolve_out* elts, uint32_t elt_cap,
+                    bt2x_exrange* exr_out, uint32_t exr_cap,
+                    uint32_t used[3]);
+/* Device-pointer variant (inputs resident in HBM; used: 3 x u32 in HBM).  Events:
+ * BT2X_K_SEED brackets the seed kernel, BT2X_K_RESOLVE the ranking + resolution,
+ * BT2X_K_ROUND the whole round. */
+int bt2x_seed_round_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const bt2x_seed_in* d_seeds, uint32_t nseeds,
+                        const bt2x_round_in* d_in, uint32_t nreads, const bt2x_exrange* d_exr, uint32_t maxelt,
+                        bt2x_round_out* d_out, bt2x_sat* d_sats, uint32_t sat_cap,
+                        bt2x_resolve_out* d_elts, uint32_t elt_cap, bt2x_exrange* d_exr_out, uint32_t exr_cap,
+                        uint32_t* d_used, void* stream);
 
 const char* bt2x_version(void);
 /* sizeof of the ABI structs (seed_in, seed_out, dp_in, dp_out, aln_rec, scoring,

@@ -26,11 +26,21 @@ RESOLVE_IN = np.dtype([("row", "<u8"), ("qlen", "<u4"), ("pad", "<u4")], align=T
 RESOLVE_OUT = np.dtype([("joff", "<u8"), ("toff", "<u8"), ("tlen", "<u8"), ("tidx", "<u4"),
                         ("straddled", "<u4")], align=True)
 NO_TIDX = 0xFFFFFFFF
+ROUND_IN = np.dtype([("read_off", "<u8"), ("seed0", "<u8"), ("rnd_last", "<u4"), ("rnd_lastoff", "<i4"),
+                     ("exr0", "<u4"), ("nexr", "<u2"), ("nseeds", "<u2"), ("num_offs", "<u2"),
+                     ("rdlen", "<u2"), ("interval", "<u2"), ("offset", "<u2"), ("seedlen", "<u2"),
+                     ("pad", "<u2", 3)], align=True)
+EXRANGE = np.dtype([("sz", "<u8"), ("off", "<u4"), ("len", "<u2"), ("fw", "u1"), ("pad", "u1")], align=True)
+SAT = np.dtype([("rdoff", "<u4"), ("rand_n", "<u2"), ("fw", "u1"), ("seedlen", "u1")], align=True)
+ROUND_OUT = np.dtype([("rnd_last", "<u4"), ("rnd_lastoff", "<i4"), ("num_elts", "<u8"), ("nonz", "<u4"),
+                      ("status", "<u4"), ("sat0", "<u4"), ("nsat", "<u4"), ("elt0", "<u4"), ("nelt", "<u4"),
+                      ("exr0", "<u4"), ("nexr", "<u4")], align=True)
+ROUND_OK, ROUND_NO_HITS, ROUND_REDO = 0, 1, 2
 
 MAX_ROWS = 160
 MAX_COLS = 200
 E_OK, E_ARG, E_IO, E_NODEVICE, E_OVERFLOW, E_NOMEM = 0, -1, -2, -3, -4, -5
-K_SEED, K_DP, K_RESOLVE = 0, 1, 2
+K_SEED, K_DP, K_RESOLVE, K_ROUND = 0, 1, 2, 3
 
 EDIT_READ_GAP, EDIT_REF_GAP, EDIT_MM = 1, 2, 3
 

@@ -48,6 +48,16 @@ FUNCS = {
                                     ctypes.c_void_p]),
     "bt2x_resolve_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "bt2x_seed_round": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+    "bt2x_seed_round_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
     "bt2x_suffix_array": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
     "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
@@ -201,6 +211,15 @@ class Context:
     def resolve_dev(self, d_in: int, n: int, d_out: int, reject_straddle=False, stream=0):
         check(load().bt2x_resolve_dev(self.h, d_in, n, int(reject_straddle), d_out, stream),
               "bt2x_resolve_dev")
+
+    # ------------------------------------------------------------ seed round
+    def seed_round_dev(self, d_reads, d_seeds, nseeds, d_in, nreads, d_exr, maxelt, d_out, d_sats, sat_cap,
+                       d_elts, elt_cap, d_exr_out, exr_cap, d_used, stream=0):
+        """bt2x_seed_round_dev: seed search + ranking/prioritization + SA resolution of a
+        batch of reads, inputs resident in HBM."""
+        check(load().bt2x_seed_round_dev(self.h, d_reads, d_seeds, nseeds, d_in, nreads, d_exr, maxelt, d_out,
+                                         d_sats, sat_cap, d_elts, elt_cap, d_exr_out, exr_cap, d_used, stream),
+              "bt2x_seed_round_dev")
 
     def device_name(self) -> str:
         try:

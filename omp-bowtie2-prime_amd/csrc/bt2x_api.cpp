@@ -148,6 +148,10 @@ struct bt2x_ctx {
 	void* d_sa = nullptr; void* d_text = nullptr;
 	void* d_offs = nullptr; void* d_rstarts = nullptr; void* d_plen = nullptr;
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
+	// seed round: host-variant staging, and the round's own scratch (seed results, rows
+	// to resolve, per-lane workspace)
+	DevBuf b_rin, b_exr, b_rout, b_sats, b_elts, b_exro, b_used, b_sout, b_rows, b_ws;
+	const uint32_t* d_resolve_n = nullptr;     // element count of the last round's resolve (HBM)
 	DevBuf scratch;
 	int ncu = 0;
 	uint32_t chunk_groups = 16384;             // DP chunk: 1 Mi problems, ~34 GB of traceback bytes
@@ -160,7 +164,8 @@ struct bt2x_ctx {
 bt2x_ctx::~bt2x_ctx() {
 	(void)hipSetDevice(device);
 	if(stream) (void)hipStreamSynchronize(stream);
-	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch})
+	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch,
+	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws})
 		b->release();
 	for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen, (void*)d_stats,
 	               (void*)d_counters, (void*)d_queue})
@@ -321,11 +326,18 @@ extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) 
 	} else if(k == BT2X_K_RESOLVE) {
 		out->n_lf1 = st[9];
 		out->n_problems = c->n_resolve_last;
+		if(c->d_resolve_n) {
+			uint32_t nr = 0;
+			HIPCHK(hipMemcpy(&nr, c->d_resolve_n, sizeof nr, hipMemcpyDeviceToHost));
+			out->n_problems = nr;
+		}
 		// per element: 16 B in + 32 B out + one 4 B SA entry, or per LF step one 64 B
 		// block (128 B side) and one 8 B sample word at the end of the walk
 		const uint64_t step_b = c->ix.blk ? BT2X_BLK_BYTES : BT2X_SIDE_BYTES;
 		out->alg_bytes = out->n_problems * (16 + 32) +
 		                 (c->ix.sa ? 4 * out->n_problems : step_b * out->n_lf1 + 8 * out->n_problems);
+	} else if(k == BT2X_K_ROUND) {
+		return BT2X_E_ARG;                     // see BT2X_K_SEED and BT2X_K_RESOLVE
 	} else {
 		out->dp_cells = st[4]; out->dp_cols = st[5]; out->bt_cells = st[6];
 		out->n_problems = c->n_dp_last;
@@ -480,7 +492,9 @@ extern "C" int bt2x_abi_sizes(uint32_t* out, int n) {
 	                      (uint32_t)sizeof(bt2x_dp_in), (uint32_t)sizeof(bt2x_dp_out),
 	                      (uint32_t)sizeof(bt2x_aln_rec), (uint32_t)sizeof(bt2x_scoring),
 	                      (uint32_t)sizeof(bt2x_index_desc), (uint32_t)sizeof(bt2x_counters),
-	                      (uint32_t)sizeof(bt2x_resolve_in), (uint32_t)sizeof(bt2x_resolve_out)};
+	                      (uint32_t)sizeof(bt2x_resolve_in), (uint32_t)sizeof(bt2x_resolve_out),
+	                      (uint32_t)sizeof(bt2x_round_in), (uint32_t)sizeof(bt2x_round_out),
+	                      (uint32_t)sizeof(bt2x_sat), (uint32_t)sizeof(bt2x_exrange)};
 	const int m = (int)(sizeof s / sizeof s[0]);
 	for(int i = 0; i < n && i < m; i++) out[i] = s[i];
 	return m;
@@ -508,7 +522,106 @@ extern "C" int bt2x_resolve_dev(bt2x_ctx* c, const bt2x_resolve_in* d_in, uint32
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][1], s));
 	c->ev_valid[BT2X_K_RESOLVE] = true;
 	c->n_resolve_last = n;
+	c->d_resolve_n = nullptr;
 	return rc;
+}
+
+// ------------------------------------------------------------------- seed round
+extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt2x_seed_in* d_seeds, uint32_t nseeds,
+                                   const bt2x_round_in* d_in, uint32_t nreads, const bt2x_exrange* d_exr,
+                                   uint32_t maxelt, bt2x_round_out* d_out, bt2x_sat* d_sats, uint32_t sat_cap,
+                                   bt2x_resolve_out* d_elts, uint32_t elt_cap, bt2x_exrange* d_exr_out,
+                                   uint32_t exr_cap, uint32_t* d_used, void* stream) {
+	if(!c || !d_used) return BT2X_E_ARG;
+	if(!c->ix.sa && !c->ix.offs) return BT2X_E_ARG;        // index loaded without load_offs
+	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+	HIPCHK(hipSetDevice(c->device));
+	int rc;
+	const uint32_t lanes = bt2x_round_lanes(c->ncu);
+	if((rc = c->b_sout.ensure(sizeof(bt2x_seed_out) * (size_t)(nseeds ? nseeds : 1))) ||
+	   (rc = c->b_rows.ensure(sizeof(bt2x_resolve_in) * (size_t)(elt_cap ? elt_cap : 1))) ||
+	   (rc = c->b_ws.ensure(bt2x_round_ws_bytes() * lanes))) return rc;
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_ROUND][0], s));
+	// 1. seed search (searchAllSeedsDoAll)
+	HIPCHK(hipMemsetAsync(c->d_stats, 0, 3 * sizeof(unsigned long long), s));
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][0], s));
+	if((rc = bt2x_launch_seed(c->ix, d_reads, d_seeds, nseeds, 1, (bt2x_seed_out*)c->b_sout.p, c->d_stats, c->ncu, s)))
+		return rc;
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][1], s));
+	c->ev_valid[BT2X_K_SEED] = true;
+	c->n_seed_last = nseeds;
+	// 2. finalize + rank + prioritize per read, then 3. place every row
+	HIPCHK(hipMemsetAsync(d_used, 0, 3 * sizeof(uint32_t), s));
+	HIPCHK(hipMemsetAsync(c->d_stats + 8, 0, 3 * sizeof(unsigned long long), s));
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][0], s));
+	RoundLaunch a;
+	a.seeds = d_seeds; a.seed_out = (const bt2x_seed_out*)c->b_sout.p;
+	a.in = d_in; a.n = nreads; a.exr = d_exr; a.maxelt = maxelt;
+	a.out = d_out; a.sats = d_sats; a.sat_cap = sat_cap;
+	a.rows = (bt2x_resolve_in*)c->b_rows.p; a.row_cap = elt_cap;
+	a.exr_out = d_exr_out; a.exr_cap = exr_cap;
+	a.counters = d_used; a.ws = (uint8_t*)c->b_ws.p; a.nlanes = lanes;
+	if((rc = bt2x_launch_round(a, s))) return rc;
+	if((rc = bt2x_launch_resolve_dn(c->ix, a.rows, d_used + 1, elt_cap, 0, d_elts, c->d_stats + 8, c->ncu, s)))
+		return rc;
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][1], s));
+	HIPCHK(hipEventRecord(c->ev[BT2X_K_ROUND][1], s));
+	c->ev_valid[BT2X_K_RESOLVE] = c->ev_valid[BT2X_K_ROUND] = true;
+	c->d_resolve_n = d_used + 1;
+	return BT2X_OK;
+}
+
+extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads_bytes,
+                               const bt2x_seed_in* seeds, uint32_t nseeds,
+                               const bt2x_round_in* in, uint32_t nreads,
+                               const bt2x_exrange* exr, uint32_t nexr, uint32_t maxelt,
+                               bt2x_round_out* out,
+                               bt2x_sat* sats, uint32_t sat_cap,
+                               bt2x_resolve_out* elts, uint32_t elt_cap,
+                               bt2x_exrange* exr_out, uint32_t exr_cap,
+                               uint32_t used[3]) {
+	if(!c || !used || (nreads && (!in || !out)) || (nseeds && (!reads || !seeds))) return BT2X_E_ARG;
+	used[0] = used[1] = used[2] = 0;
+	if(nreads == 0) return BT2X_OK;
+	for(uint32_t i = 0; i < nseeds; i++)
+		if(seeds[i].seed_len < 1 || seeds[i].seed_len > 32 || seeds[i].read_off + seeds[i].seed_off + seeds[i].seed_len > reads_bytes)
+			return BT2X_E_ARG;
+	for(uint32_t r = 0; r < nreads; r++) {
+		const bt2x_round_in& q = in[r];
+		if(q.seed0 + q.nseeds > nseeds || (uint64_t)q.exr0 + q.nexr > nexr || q.interval == 0 || q.seedlen == 0 ||
+		   q.read_off + 2ull * q.rdlen > reads_bytes)
+			return BT2X_E_ARG;
+	}
+	HIPCHK(hipSetDevice(c->device));
+	int rc;
+	if((rc = c->b_reads.ensure(reads_bytes ? reads_bytes : 1)) ||
+	   (rc = c->b_in.ensure(sizeof(bt2x_seed_in) * (size_t)(nseeds ? nseeds : 1))) ||
+	   (rc = c->b_rin.ensure(sizeof(bt2x_round_in) * nreads)) ||
+	   (rc = c->b_exr.ensure(sizeof(bt2x_exrange) * (size_t)(nexr ? nexr : 1))) ||
+	   (rc = c->b_rout.ensure(sizeof(bt2x_round_out) * nreads)) ||
+	   (rc = c->b_sats.ensure(sizeof(bt2x_sat) * (size_t)(sat_cap ? sat_cap : 1))) ||
+	   (rc = c->b_elts.ensure(sizeof(bt2x_resolve_out) * (size_t)(elt_cap ? elt_cap : 1))) ||
+	   (rc = c->b_exro.ensure(sizeof(bt2x_exrange) * (size_t)(exr_cap ? exr_cap : 1))) ||
+	   (rc = c->b_used.ensure(4 * sizeof(uint32_t)))) return rc;
+	if(reads_bytes) HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
+	if(nseeds) HIPCHK(hipMemcpyAsync(c->b_in.p, seeds, sizeof(bt2x_seed_in) * nseeds, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->b_rin.p, in, sizeof(bt2x_round_in) * nreads, hipMemcpyHostToDevice, c->stream));
+	if(nexr) HIPCHK(hipMemcpyAsync(c->b_exr.p, exr, sizeof(bt2x_exrange) * nexr, hipMemcpyHostToDevice, c->stream));
+	rc = bt2x_seed_round_dev(c, (const uint8_t*)c->b_reads.p, (const bt2x_seed_in*)c->b_in.p, nseeds,
+	                         (const bt2x_round_in*)c->b_rin.p, nreads, (const bt2x_exrange*)c->b_exr.p, maxelt,
+	                         (bt2x_round_out*)c->b_rout.p, (bt2x_sat*)c->b_sats.p, sat_cap,
+	                         (bt2x_resolve_out*)c->b_elts.p, elt_cap, (bt2x_exrange*)c->b_exro.p, exr_cap,
+	                         (uint32_t*)c->b_used.p, c->stream);
+	if(rc) return rc;
+	HIPCHK(hipMemcpyAsync(used, c->b_used.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipMemcpyAsync(out, c->b_rout.p, sizeof(bt2x_round_out) * nreads, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	if(used[0] > sat_cap || used[1] > elt_cap || used[2] > exr_cap) return BT2X_E_OVERFLOW;
+	if(used[0]) HIPCHK(hipMemcpyAsync(sats, c->b_sats.p, sizeof(bt2x_sat) * used[0], hipMemcpyDeviceToHost, c->stream));
+	if(used[1]) HIPCHK(hipMemcpyAsync(elts, c->b_elts.p, sizeof(bt2x_resolve_out) * used[1], hipMemcpyDeviceToHost, c->stream));
+	if(used[2]) HIPCHK(hipMemcpyAsync(exr_out, c->b_exro.p, sizeof(bt2x_exrange) * used[2], hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return BT2X_OK;
 }
 
 extern "C" int bt2x_resolve(bt2x_ctx* c, const bt2x_resolve_in* in, uint32_t n, int reject_straddle,

@@ -48,6 +48,27 @@ int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed
 
 int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_t n, int reject,
                         bt2x_resolve_out* d_out, unsigned long long* d_ctr, void* stream);
+// element count in HBM (*d_n, at most cap): persistent grid-stride launch
+int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
+                           int reject, bt2x_resolve_out* d_out, unsigned long long* d_ctr, int ncu, void* stream);
+
+// Seed round (round_kernel.hip): per read, finalize + rank + prioritize after its seed
+// search; sats/rows/exr_out allocated by atomics on counters[0..2].
+struct RoundLaunch {
+	const bt2x_seed_in* seeds; const bt2x_seed_out* seed_out;
+	const bt2x_round_in* in; uint32_t n;
+	const bt2x_exrange* exr;
+	uint32_t maxelt;
+	bt2x_round_out* out;
+	bt2x_sat* sats; uint32_t sat_cap;
+	bt2x_resolve_in* rows; uint32_t row_cap;
+	bt2x_exrange* exr_out; uint32_t exr_cap;
+	uint32_t* counters;            // [0] sats, [1] rows, [2] exr_out (used, may exceed caps)
+	uint8_t* ws; uint32_t nlanes;  // per-lane workspace (bt2x_round_ws_bytes each)
+};
+size_t bt2x_round_ws_bytes();
+uint32_t bt2x_round_lanes(int ncu);
+int bt2x_launch_round(const RoundLaunch& a, void* stream);
 
 struct DpLaunch {
 	const uint8_t* reads; const uint8_t* quals; const uint8_t* refs;

@@ -1,0 +1,334 @@
+// round_core.h — one read's seed round after its seed search, as one GPU lane runs it
+// (bt2x_seed_round, include/bt2x.h): searchAllSeedsFinalize + SeedResults::add,
+// rankSeedHits, prioritizeSATups (with RowSampler and Random1toN), and the list of BW
+// rows extendSeeds may visit.  Integer/double code shared by the kernel (round_kernel.hip)
+// and, compiled as host code, by the CPU test that checks it against the host driver's
+// restatement (tests/cpp/test_round.cpp).
+//
+// Reference (file:line):
+//   searchAllSeedsFinalize / SeedResults::add   aligner_seed.cpp:508-540, aligner_seed.h:603-641
+//   AlignmentCache::addOnTheFly (nlex of the first add per BW range)   aligner_cache.h:558
+//   SeedResults::rankSeedHits                    aligner_seed.h:1000-1061
+//   SwDriver::prioritizeSATups                   aligner_sw_driver.cpp:61-260
+//   RowSampler                                   aligner_sw_driver.h:176-267
+//   Random1toN                                   random_util.h:32-230
+//   RandomSource (LCG)                           random_source.h:34-140
+// Floating point: RowSampler's masses and darts are IEEE double/float with no
+// contraction (the TU is built with -ffp-contract=off), as on the reference's x86-64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/bt2x.h"
+
+namespace bt2x_round {
+
+constexpr int kMaxOffs = 64;                  // seed offsets per strand
+constexpr int kMaxRanges = 2 * kMaxOffs;      // satpos2 entries
+constexpr int kMaxSat = 416;                  // satpos entries (<= maxelt + 4)
+constexpr int kArena = 6144;                  // uint16 list storage (swap lists)
+constexpr int kHash = 1024;                   // seen-set slots (range << 16 | element) + 1
+constexpr uint32_t kNsm = 5;                  // prioritizeSATups' nsm
+
+struct Rnd {                                  // RandomSource, LCG variant
+	uint32_t last;
+	int32_t lastOff;
+	__host__ __device__ uint32_t nextU32() {
+		last = 1664525u * last + 1013904223u;
+		uint32_t r = last >> 16;
+		last = 1664525u * last + 1013904223u;
+		r ^= last;
+		lastOff = 0;
+		return r;
+	}
+	__host__ __device__ bool nextBool() {
+		if(lastOff > 31) nextU32();
+		const uint32_t r = (last >> lastOff) & 1u;
+		lastOff++;
+		return r != 0;
+	}
+	__host__ __device__ float nextFloat() { return (float)nextU32() / (float)0xffffffffu; }
+};
+
+struct Range {                                // a satpos2 entry (SATupleAndPos)
+	uint64_t topf, size;
+	uint32_t rdoff;
+	uint16_t offidx;
+	uint8_t nlex, fw;
+};
+
+struct R1N {                                  // Random1toN state; lists live in the arena
+	uint16_t n, cur, thresh, list;            // list: arena offset of list_
+	uint8_t inited, swaplist, converted, pad;
+};
+
+// Per-lane workspace (global memory on the GPU).
+struct Ws {
+	uint64_t htopf[2][kMaxOffs], hn[2][kMaxOffs];
+	uint8_t hnlex[2][kMaxOffs], hvalid[2][kMaxOffs], hsorted[2][kMaxOffs];
+	uint16_t rankIdx[kMaxRanges];
+	uint8_t rankFw[kMaxRanges];
+	uint64_t cacheTop[kMaxRanges];
+	uint8_t cacheNlex[kMaxRanges];
+	Range r2[kMaxRanges];
+	bt2x_exrange exnew[kMaxRanges];
+	double masses[kMaxRanges], pre[kMaxRanges];
+	uint16_t live[kMaxRanges];
+	R1N r1n[kMaxRanges];
+	uint16_t arena[kArena];
+	uint32_t hash[kHash];
+	// the read's extension list: satpos[i] = (range, element offset, rand_n)
+	uint16_t satRange[kMaxSat], satN[kMaxSat];
+	uint32_t satElt[kMaxSat];
+};
+
+struct Result {
+	uint32_t status, nonz, nsat, nelt, nexnew;
+	uint64_t numElts;
+};
+
+// prioritizeSATups' "ranges" order (SATupleAndPos::operator<, aligner_sw_driver.h:140-171)
+__host__ __device__ inline bool range_less(const Range& a, const Range& b) {
+	if(a.size != b.size) return a.size < b.size;
+	if(a.topf != b.topf) return a.topf < b.topf;
+	if(a.offidx != b.offidx) return a.offidx < b.offidx;
+	if(a.rdoff != b.rdoff) return a.rdoff < b.rdoff;
+	return a.fw && !b.fw;                     // seedlen is the same for all seeds of a round
+}
+
+__host__ __device__ inline bool seen_test_set(Ws& w, uint32_t key) {      // key != 0
+	uint32_t h = (key * 2654435761u) >> 22;                                 // 10 bits
+	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1)) {
+		if(w.hash[h] == key) return true;
+		if(w.hash[h] == 0) { w.hash[h] = key; return false; }
+	}
+	return true;                                                             // full: cannot happen (<= 416 keys)
+}
+
+__host__ __device__ inline bool seen_has(const Ws& w, uint32_t key) {
+	uint32_t h = (key * 2654435761u) >> 22;
+	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1)) {
+		if(w.hash[h] == key) return true;
+		if(w.hash[h] == 0) return false;
+	}
+	return false;
+}
+
+// Random1toN::next over range ri; false on workspace overflow.
+__host__ __device__ inline bool r1n_next(Ws& w, int ri, Rnd& rnd, uint32_t& arenaTop, uint16_t& out) {
+	R1N& s = w.r1n[ri];
+	if(s.cur == 0 && !s.converted) {
+		if(s.n == 1) { s.cur = 1; out = 0; return true; }
+		if(s.swaplist) {
+			if(arenaTop + s.n > (uint32_t)kArena) return false;
+			s.list = (uint16_t)arenaTop;
+			arenaTop += s.n;
+			for(uint32_t i = 0; i < s.n; i++) w.arena[s.list + i] = (uint16_t)i;
+		}
+	}
+	if(s.swaplist) {
+		const uint32_t r = s.cur + rnd.nextU32() % (uint32_t)(s.n - s.cur);
+		if(r != s.cur) {
+			const uint16_t t = w.arena[s.list + s.cur];
+			w.arena[s.list + s.cur] = w.arena[s.list + r];
+			w.arena[s.list + r] = t;
+		}
+		out = w.arena[s.list + s.cur];
+		s.cur++;
+		return true;
+	}
+	// seen-list mode: redraw until unseen
+	uint16_t rn;
+	do {
+		rn = (uint16_t)(rnd.nextU32() % (uint32_t)s.n);
+	} while(seen_has(w, ((uint32_t)ri << 16 | rn) + 1u));
+	seen_test_set(w, ((uint32_t)ri << 16 | rn) + 1u);
+	s.cur++;
+	// s.cur draws so far = seen_.size()
+	if(s.cur >= s.thresh && s.cur < s.n) {
+		// convert to a swap list of the unseen elements, ascending
+		const uint32_t nl = (uint32_t)s.n - s.cur;
+		if(arenaTop + nl > (uint32_t)kArena) return false;
+		const uint16_t base = (uint16_t)arenaTop;
+		uint32_t k = 0;
+		for(uint32_t j = 0; j < s.n; j++)
+			if(!seen_has(w, ((uint32_t)ri << 16 | j) + 1u)) w.arena[base + k++] = (uint16_t)j;
+		arenaTop += nl;
+		s.list = base;
+		s.cur = 0;
+		s.n = (uint16_t)nl;
+		s.converted = 1;
+		s.swaplist = 1;
+	}
+	out = rn;
+	return true;
+}
+
+// The round for one read.  sin/sout: its seeds and their search results; exr: exRange
+// entries of earlier rounds.  Fills w.sat* (extension list) and w.exnew.
+__host__ __device__ inline Result run(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout,
+                                      const bt2x_exrange* exr, uint32_t maxelt, Rnd& rnd, Ws& w) {
+	Result res = {BT2X_ROUND_OK, 0, 0, 0, 0, 0};
+	const uint32_t numOffs = in.num_offs, L = in.seedlen, interval = in.interval, offset = in.offset;
+	if(numOffs > (uint32_t)kMaxOffs) { res.status = BT2X_ROUND_REDO; return res; }
+	for(int s = 0; s < 2; s++)
+		for(uint32_t i = 0; i < numOffs; i++) { w.hvalid[s][i] = 0; w.hsorted[s][i] = 0; }
+	// ---- searchAllSeedsFinalize: SeedResults::add + the per-read cache's first nlex
+	uint32_t ncache = 0;
+	for(uint32_t k = 0; k < in.nseeds; k++) {
+		const bt2x_seed_out d = sout[k];
+		if(!d.need_reporting) continue;
+		const bt2x_seed_in si = sin[k];
+		const bool fw = si.read_off == in.read_off;
+		const uint32_t depth = fw ? si.seed_off : (uint32_t)in.rdlen - si.seed_off - L;
+		const uint32_t idx = (depth - offset) / interval;
+		if(idx < numOffs) {                    // SeedResults::add ignores other offsets
+			const int s = fw ? 0 : 1;
+			w.htopf[s][idx] = d.topf; w.hn[s][idx] = d.botf - d.topf; w.hnlex[s][idx] = d.nlex; w.hvalid[s][idx] = 1;
+			res.numElts += d.botf - d.topf;
+			res.nonz++;
+		}
+		bool have = false;
+		for(uint32_t q = 0; q < ncache; q++) if(w.cacheTop[q] == d.topf) { have = true; break; }
+		if(!have) {
+			if(ncache >= (uint32_t)kMaxRanges) { res.status = BT2X_ROUND_REDO; return res; }
+			w.cacheTop[ncache] = d.topf; w.cacheNlex[ncache] = d.nlex; ncache++;
+		}
+	}
+	if(res.nonz == 0) { res.status = BT2X_ROUND_NO_HITS; return res; }
+	// ---- rankSeedHits (random strand order and start, smallest range first)
+	for(uint32_t r = 0; r < res.nonz; r++) {
+		uint64_t minsz = 0xffffffffu;
+		uint32_t minidx = 0;
+		int minfw = 1;
+		const bool rb = rnd.nextBool();
+		for(int fwi = 0; fwi <= 1; fwi++) {
+			const int fw = (fwi == (rb ? 1 : 0)) ? 1 : 0;
+			const int s = fw ? 0 : 1;
+			uint32_t i = rnd.nextU32() % numOffs;
+			for(uint32_t ii = 0; ii < numOffs; ii++) {
+				if(w.hvalid[s][i] && w.hn[s][i] > 0 && !w.hsorted[s][i] && w.hn[s][i] < minsz) {
+					minsz = w.hn[s][i]; minidx = i; minfw = fw;
+				}
+				if(++i == numOffs) i = 0;
+			}
+		}
+		if(minsz == 0xffffffffu) { res.status = BT2X_ROUND_REDO; return res; }
+		w.hsorted[minfw ? 0 : 1][minidx] = 1;
+		w.rankIdx[r] = (uint16_t)minidx;
+		w.rankFw[r] = (uint8_t)minfw;
+	}
+	// ---- prioritizeSATups: ranges by rank, minus those an extended range covers
+	uint32_t n2 = 0, nsmall = 0;
+	uint64_t nelt = 0;
+	for(uint32_t r = 0; r < res.nonz; r++) {
+		const uint32_t offidx = w.rankIdx[r];
+		const int fw = w.rankFw[r];
+		const int s = fw ? 0 : 1;
+		Range sp;
+		sp.topf = w.htopf[s][offidx];
+		sp.size = w.hn[s][offidx];
+		sp.rdoff = offidx * interval + offset;
+		sp.offidx = (uint16_t)offidx;
+		sp.fw = (uint8_t)fw;
+		sp.nlex = 0;
+		for(uint32_t q = 0; q < ncache; q++) if(w.cacheTop[q] == sp.topf) { sp.nlex = w.cacheNlex[q]; break; }
+		if(sp.size == 0) continue;
+		bool skip = false;
+		for(uint32_t q = 0; q < in.nexr && !skip; q++) {
+			const bt2x_exrange& er = exr[q];
+			if(er.fw == fw && er.off <= sp.rdoff && (uint64_t)er.off + er.len >= (uint64_t)sp.rdoff + L && sp.size <= er.sz)
+				skip = true;
+		}
+		for(uint32_t q = 0; q < res.nexnew && !skip; q++) {
+			const bt2x_exrange& er = w.exnew[q];
+			if(er.fw == fw && er.off <= sp.rdoff && (uint64_t)er.off + er.len >= (uint64_t)sp.rdoff + L && sp.size <= er.sz)
+				skip = true;
+		}
+		for(uint32_t q = 0; q < n2 && !skip; q++) skip = w.r2[q].topf == sp.topf;
+		if(skip) continue;
+		nelt += sp.size;
+		w.r2[n2++] = sp;
+		if(sp.size <= kNsm) nsmall++;
+		if(sp.nlex > 0) {
+			bt2x_exrange& e = w.exnew[res.nexnew++];
+			e.off = sp.rdoff - (fw ? sp.nlex : 0);
+			e.len = (uint16_t)(L + sp.nlex);
+			e.sz = sp.size;
+			e.fw = (uint8_t)fw;
+			e.pad = 0;
+		}
+	}
+	// stable insertion sort (std::stable_sort by SATupleAndPos order)
+	for(uint32_t i = 1; i < n2; i++) {
+		const Range x = w.r2[i];
+		uint32_t j = i;
+		while(j > 0 && range_less(x, w.r2[j - 1])) { w.r2[j] = w.r2[j - 1]; j--; }
+		w.r2[j] = x;
+	}
+	uint32_t nsat = 0;
+	uint64_t added = 0;
+	for(uint32_t j = 0; j < nsmall && added < maxelt; j++) {
+		if(nsat >= (uint32_t)kMaxSat) { res.status = BT2X_ROUND_REDO; return res; }
+		w.satRange[nsat] = (uint16_t)j; w.satElt[nsat] = 0; w.satN[nsat] = (uint16_t)w.r2[j].size; nsat++;
+		added += w.r2[j].size;
+	}
+	if(!(added >= maxelt || nsmall == n2)) {
+		// RowSampler over the larger ranges (lensq = szsq = true)
+		const uint32_t nb = n2 - nsmall;
+		double mass = 0.0f;
+		for(uint32_t i = 0; i < nb; i++) {
+			const Range& rg = w.r2[nsmall + i];
+			double num = (double)(rg.nlex + 1);
+			num *= num;
+			double den = (double)rg.size;
+			den *= den;
+			w.masses[i] = num / den;
+			mass += w.masses[i];
+			w.live[i] = (uint16_t)i;
+			R1N& s = w.r1n[i];
+			s.inited = 0; s.n = 0; s.cur = 0; s.converted = 0; s.swaplist = 0;
+		}
+		uint32_t nlive = nb;
+		auto rebuild = [&]() {
+			double sofar = 0.0f;
+			for(uint32_t k = 0; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
+		};
+		rebuild();
+		for(int k = 0; k < kHash; k++) w.hash[k] = 0;
+		uint32_t arenaTop = 0;
+		while(added < maxelt && added < nelt) {
+			const double rd = rnd.nextFloat() * mass;
+			// the dart: first live range whose running mass exceeds it (else the last live one)
+			uint32_t lo = 0, hi = nlive;
+			while(lo < hi) { const uint32_t mid = (lo + hi) >> 1; if(rd < w.pre[mid]) hi = mid; else lo = mid + 1; }
+			if(nlive == 0) { res.status = BT2X_ROUND_REDO; return res; }
+			const uint32_t bi = w.live[lo < nlive ? lo : nlive - 1];
+			R1N& s = w.r1n[bi];
+			if(!s.inited) {
+				const uint16_t n = (uint16_t)w.r2[nsmall + bi].size;          // uint16_t element type
+				if(n == 0) { res.status = BT2X_ROUND_REDO; return res; }
+				s.inited = 1; s.n = n; s.cur = 0; s.converted = 0; s.swaplist = n < 128 ? 1 : 0;
+				const uint16_t t = (uint16_t)(0.10f * (float)n);
+				s.thresh = t > 16 ? t : 16;
+			}
+			uint16_t rr;
+			if(!r1n_next(w, (int)bi, rnd, arenaTop, rr)) { res.status = BT2X_ROUND_REDO; return res; }
+			if(s.n > 0 && s.cur >= s.n) {                                       // done(): finishedRange
+				mass -= w.masses[bi];
+				uint32_t k = 0;
+				while(k < nlive && w.live[k] != bi) k++;
+				for(; k + 1 < nlive; k++) w.live[k] = w.live[k + 1];
+				nlive--;
+				rebuild();
+			}
+			if(nsat >= (uint32_t)kMaxSat) { res.status = BT2X_ROUND_REDO; return res; }
+			w.satRange[nsat] = (uint16_t)(nsmall + bi); w.satElt[nsat] = rr; w.satN[nsat] = 1; nsat++;
+			added++;
+		}
+	}
+	res.nsat = nsat;
+	res.nelt = (uint32_t)added;
+	return res;
+}
+
+} // namespace bt2x_round

@@ -626,13 +626,9 @@ __device__ __forceinline__ uint64_t sa_offset(const DevIndex& ix, uint64_t row, 
 	return OFF_MASK;
 }
 
-__global__ void __launch_bounds__(256)
-sa_resolve_kernel(DevIndex ix, const bt2x_resolve_in* __restrict__ in, uint32_t n, int reject,
-                  bt2x_resolve_out* __restrict__ out, unsigned long long* __restrict__ ctr) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	uint32_t steps = 0;
-	if(i < n) {
-		const bt2x_resolve_in e = in[i];
+// One element: Ebwt::getOffset + joinedToTextOff.
+__device__ __forceinline__ bt2x_resolve_out resolve_one(const DevIndex& ix, const bt2x_resolve_in e, int reject,
+                                                       uint32_t& steps) {
 		bt2x_resolve_out o;
 		o.joff = e.row <= ix.len ? sa_offset(ix, e.row, steps) : OFF_MASK;
 		o.toff = 0; o.tlen = 0; o.tidx = BT2X_NO_TIDX; o.straddled = 0;
@@ -660,10 +656,33 @@ sa_resolve_kernel(DevIndex ix, const bt2x_resolve_in* __restrict__ in, uint32_t 
 				bot = elt;
 			}
 		}
-		out[i] = o;
-	}
+		return o;
+}
+
+__global__ void __launch_bounds__(256)
+sa_resolve_kernel(DevIndex ix, const bt2x_resolve_in* __restrict__ in, uint32_t n, int reject,
+                  bt2x_resolve_out* __restrict__ out, unsigned long long* __restrict__ ctr) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	uint32_t steps = 0;
+	if(i < n) out[i] = resolve_one(ix, in[i], reject, steps);
 	if(ctr) {
 		// LF steps of this wave, one atomic per wave
+		uint64_t s = steps;
+		for(int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k);
+		if((threadIdx.x & 63) == 0 && s) atomicAdd(&ctr[1], (unsigned long long)s);
+	}
+}
+
+// The same over a count that lives in HBM (written by the kernel that produced the
+// elements), grid-stride; at most cap elements.
+__global__ void __launch_bounds__(256)
+sa_resolve_kernel_dn(DevIndex ix, const bt2x_resolve_in* __restrict__ in, const uint32_t* __restrict__ d_n,
+                     uint32_t cap, int reject, bt2x_resolve_out* __restrict__ out, unsigned long long* __restrict__ ctr) {
+	const uint32_t n = min(*d_n, cap);
+	uint32_t steps = 0;
+	for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+		out[i] = resolve_one(ix, in[i], reject, steps);
+	if(ctr) {
 		uint64_t s = steps;
 		for(int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k);
 		if((threadIdx.x & 63) == 0 && s) atomicAdd(&ctr[1], (unsigned long long)s);
@@ -723,6 +742,17 @@ int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed
 	else
 		hipLaunchKernelGGL(seed_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
 		                   ix, d_reads, d_in, n, do_extend, d_out, d_ctr);
+	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+}
+
+int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
+                           int reject, bt2x_resolve_out* d_out, unsigned long long* d_ctr, int ncu, void* stream) {
+	if(cap == 0) return 0;
+	if(!ix.sa && !ix.offs) return BT2X_E_ARG;
+	uint32_t blocks = (uint32_t)(ncu > 0 ? ncu : 256) * 8u;
+	if(blocks > (cap + 255) / 256) blocks = (cap + 255) / 256;
+	hipLaunchKernelGGL(sa_resolve_kernel_dn, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+	                   ix, d_in, d_n, cap, reject, d_out, d_ctr);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }
 

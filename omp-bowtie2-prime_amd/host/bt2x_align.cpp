@@ -546,6 +546,110 @@ int ExtendWalk::next(int64_t minsc, DpKey& k) {
 	}
 }
 
+void host_round(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout, const bt2x_exrange* exr,
+                uint32_t maxelt, Rng& rnd, RoundScratch& w, bt2x_round_out& out, std::vector<bt2x_sat>& sats,
+                std::vector<bt2x_resolve_in>& rows, std::vector<bt2x_exrange>& exr_out) {
+	std::memset(&out, 0, sizeof out);
+	const uint32_t numOffs = in.num_offs, interval = in.interval, offset = in.offset, L = in.seedlen;
+	const size_t exr0 = exr_out.size();
+	// searchAllSeedsFinalize + SeedResults::add (aligner_seed.cpp:508-540)
+	SeedHitsHip& hits = w.hits;
+	hits.reset(numOffs);
+	w.cacheNlex.clear();
+	for(uint32_t k = 0; k < in.nseeds; k++) {
+		const bt2x_seed_out& d = sout[k];
+		if(!d.need_reporting) continue;
+		const bool fw = sin[k].read_off == in.read_off;
+		const uint32_t depth = fw ? sin[k].seed_off : (uint32_t)(in.rdlen - sin[k].seed_off - L);
+		hits.add((depth - offset) / interval, fw, d);
+		bool have = false;
+		for(auto& e : w.cacheNlex) if(e.first == d.topf) { have = true; break; }
+		if(!have) w.cacheNlex.push_back({d.topf, d.nlex});
+	}
+	out.nonz = (uint32_t)hits.nonzeroOffsets();
+	out.num_elts = hits.numElts();
+	if(out.nonz == 0) {
+		out.status = BT2X_ROUND_NO_HITS;
+		out.rnd_last = rnd.last; out.rnd_lastoff = rnd.lastOff;
+		return;
+	}
+	hits.rankSeedHits(rnd, false);
+	// prioritizeSATups (aligner_sw_driver.cpp:61-260)
+	std::vector<SatPos>& satpos2 = w.satpos2;
+	satpos2.clear();
+	size_t nelt = 0, nsmall = 0;
+	const size_t nsm = 5;
+	auto covered = [&](const bt2x_exrange& er, bool fw, uint32_t rdoff, uint64_t size) {
+		return (er.fw != 0) == fw && er.off <= rdoff && (uint64_t)er.off + er.len >= (uint64_t)rdoff + L && size <= er.sz;
+	};
+	for(size_t r = 0; r < hits.nonzeroOffsets(); r++) {
+		uint32_t offidx = 0; bool fw = true;
+		const SeedHitsHip::Hit& h = hits.hitsByRank(r, offidx, fw);
+		const uint32_t rdoff = offidx * interval + offset;           // idx2off
+		SatPos sp;
+		sp.topf = h.topf; sp.size = h.numElts(); sp.key = h.topf;
+		for(auto& e : w.cacheNlex) if(e.first == h.topf) { sp.nlex = e.second; break; }
+		if(sp.size == 0) continue;
+		bool skip = false;
+		for(uint32_t q = 0; q < in.nexr && !skip; q++) skip = covered(exr[q], fw, rdoff, sp.size);
+		for(size_t q = exr0; q < exr_out.size() && !skip; q++) skip = covered(exr_out[q], fw, rdoff, sp.size);
+		if(!skip) for(const SatPos& o : satpos2) skip |= (o.key == sp.key);
+		if(skip) continue;
+		nelt += sp.size;
+		sp.origSz = sp.size;
+		sp.fw = fw; sp.offidx = offidx; sp.rdoff = rdoff; sp.seedlen = L;
+		satpos2.push_back(sp);
+		if(sp.size <= nsm) nsmall++;
+		if(sp.nlex > 0) {
+			bt2x_exrange er;
+			std::memset(&er, 0, sizeof er);
+			er.off = rdoff - (fw ? sp.nlex : 0);
+			er.len = (uint16_t)(L + sp.nlex);
+			er.sz = sp.size;
+			er.fw = fw ? 1 : 0;
+			exr_out.push_back(er);
+		}
+	}
+	std::stable_sort(satpos2.begin(), satpos2.end());
+	const size_t sat0 = sats.size();
+	auto emit = [&](const SatPos& sp, uint64_t first, uint32_t n) {
+		bt2x_sat st;
+		st.rdoff = sp.rdoff; st.rand_n = (uint16_t)n; st.fw = sp.fw ? 1 : 0; st.seedlen = (uint8_t)L;
+		sats.push_back(st);
+		for(uint32_t e = 0; e < n; e++) {
+			bt2x_resolve_in ri;
+			std::memset(&ri, 0, sizeof(ri));
+			ri.row = first + e;
+			ri.qlen = L;
+			rows.push_back(ri);
+		}
+	};
+	size_t added = 0;
+	for(size_t j = 0; j < nsmall && added < maxelt; j++) {
+		emit(satpos2[j], satpos2[j].topf, (uint32_t)satpos2[j].size);
+		added += satpos2[j].size;
+	}
+	if(!(added >= maxelt || nsmall == satpos2.size())) {
+		w.rows.init(satpos2, nsmall, satpos2.size());
+		std::vector<Random1toN>& rands = w.prioRands;
+		if(rands.size() < satpos2.size()) rands.resize(satpos2.size());
+		for(size_t q = 0; q < satpos2.size(); q++) rands[q].reset();
+		while(added < maxelt && added < nelt) {
+			const size_t ri = w.rows.next(rnd) + nsmall;
+			if(!rands[ri].inited()) rands[ri].init((uint16_t)satpos2[ri].size, false);
+			const size_t rr = rands[ri].next(rnd);
+			if(rands[ri].done()) w.rows.finishedRange(ri - nsmall);
+			emit(satpos2[ri], satpos2[ri].topf + rr, 1);
+			added++;
+		}
+	}
+	out.status = BT2X_ROUND_OK;
+	out.nsat = (uint32_t)(sats.size() - sat0);
+	out.nelt = (uint32_t)added;
+	out.nexr = (uint32_t)(exr_out.size() - exr0);
+	out.rnd_last = rnd.last; out.rnd_lastoff = rnd.lastOff;
+}
+
 // ---------------------------------------------------------------- SAM header
 
 std::string Aligner::header() const {
@@ -579,7 +683,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 	c->redAnchor.init(rdlen);
 	c->edbuf.clear();
 	c->memo.clear(); c->recs.clear(); c->edits.clear();
-	c->exRange[0].clear(); c->exRange[1].clear();
+	c->exRange.clear();
 	c->ndp_used = c->ntight = 0;
 	c->aligned = c->repetitive = false;
 	Prm prm;
@@ -594,7 +698,6 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		// instantiateSeeds (aligner_seed.cpp:411-447): fw seed i at depth, rc seed at rdlen-depth-L
 		const uint32_t nseeds = (rdlen - offset > L) ? 1 + (uint32_t)((rdlen - offset - L) / interval) : 1;
 		c->seed_in.clear();
-		c->seedIds.clear();
 		for(int fwi = 0; fwi < 2; fwi++) {
 			const bool fw = fwi == 0;
 			if((fw && P.nofw) || (!fw && P.norc)) continue;
@@ -611,110 +714,55 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 				si.seed_off = (uint8_t)st;
 				si.seed_len = (uint8_t)L;
 				c->seed_in.push_back(si);
-				c->seedIds.push_back({(uint8_t)fw, i});
 			}
 		}
 		PH(1);
-		if(!c->seed_in.empty()) co_await Awaiter{c, REQ_SEED};
-		PH_START();
-		// searchAllSeedsFinalize + SeedResults::add (aligner_seed.cpp:508-540)
-		SeedHitsHip& hits = c->hits;
-		hits.reset(nseeds);
-		c->cacheNlex.clear();
-		for(size_t k = 0; k < c->seedIds.size(); k++) {
-			const bt2x_seed_out& d = c->seed_out[k];
-			if(!d.need_reporting) continue;
-			hits.add(c->seedIds[k].second, c->seedIds[k].first != 0, d);
-			bool have = false;
-			for(auto& e : c->cacheNlex) if(e.first == d.topf) { have = true; break; }
-			if(!have) c->cacheNlex.push_back({d.topf, d.nlex});
+		if(c->seed_in.empty()) break;                                // no seed, no hit: done
+		// the rest of the round up to extendSeeds: on the GPU (bt2x_seed_round), or for a
+		// read it hands back, as seed search + host_round + SA resolution
+		bt2x_round_in& q = c->round_in;
+		std::memset(&q, 0, sizeof q);
+		q.rnd_last = rnd.last; q.rnd_lastoff = rnd.lastOff;
+		q.nseeds = (uint16_t)c->seed_in.size(); q.num_offs = (uint16_t)nseeds; q.rdlen = (uint16_t)rdlen;
+		q.interval = (uint16_t)interval; q.offset = (uint16_t)offset; q.seedlen = (uint16_t)L;
+		q.nexr = (uint16_t)c->exRange.size();
+		c->sats.clear(); c->exNew.clear();
+		bool redo = !gpu_round_;
+		if(!redo) {
+			co_await Awaiter{c, REQ_ROUND};                          // fills round_out, sats, res_out, exNew
+			PH_START();
+			redo = c->round_out.status == BT2X_ROUND_REDO;
+			if(redo) { c->sats.clear(); c->exNew.clear(); }
+			else { rnd.last = c->round_out.rnd_last; rnd.lastOff = c->round_out.rnd_lastoff; }
 		}
-		if(hits.nonzeroOffsets() == 0) break;                        // no seed hits: done
-		hits.rankSeedHits(rnd, false);
-		PH(2);
-
-		// ---------------------------------------------- prioritizeSATups (:61-260)
-		std::vector<SatPos>& satpos2 = c->satpos2;
+		if(redo) {
+			co_await Awaiter{c, REQ_SEED};
+			PH_START();
+			q.read_off = 0;                                          // seeds: patFw at 0, patRc at rdlen
+			c->res_in.clear();
+			host_round(q, c->seed_in.data(), c->seed_out.data(), c->exRange.data(), (uint32_t)P.mxIter, rnd, c->rs,
+			           c->round_out, c->sats, c->res_in, c->exNew);
+			if(!c->res_in.empty()) co_await Awaiter{c, REQ_RESOLVE};
+			PH_START();
+		}
+		const bt2x_round_out& ro = c->round_out;
+		if(ro.status == BT2X_ROUND_NO_HITS) break;                   // no seed hits: done
+		c->exRange.insert(c->exRange.end(), c->exNew.begin(), c->exNew.end());
+		// the extension list (SATupleAndPos) and each entry's first element
 		std::vector<SatPos>& satpos = c->satpos;
 		std::vector<uint32_t>& rand_ns = c->rand_ns;
-		satpos2.clear(); satpos.clear(); rand_ns.clear();
-		size_t nrange = 0, nelt = 0, nsmall = 0, nsmall_elts = 0;
-		const size_t nsm = 5, maxelt = P.mxIter;
-		for(size_t r = 0; r < hits.nonzeroOffsets(); r++) {
-			uint32_t offidx = 0; bool fw = true;
-			const SeedHitsHip::Hit& h = hits.hitsByRank(r, offidx, fw);
-			const uint32_t rdoff = offidx * interval + offset;           // idx2off
-			const uint32_t seedlen = L;
+		satpos.clear(); rand_ns.clear(); c->firstRow.clear();
+		uint32_t e0 = 0;
+		for(const bt2x_sat& st : c->sats) {
 			SatPos sp;
-			sp.topf = h.topf; sp.size = h.numElts(); sp.key = h.topf;
-			for(auto& e : c->cacheNlex) if(e.first == h.topf) { sp.nlex = e.second; break; }
-			if(sp.size == 0) continue;
-			nrange++; nelt += sp.size;
-			bool skip = false;
-			for(const ExtendRange& er : c->exRange[fw ? 0 : 1]) {
-				if(er.off <= rdoff && er.off + er.len >= rdoff + seedlen && sp.size <= er.sz) { skip = true; break; }
-			}
-			if(!skip) for(const SatPos& q : satpos2) skip |= (q.key == sp.key);
-			if(skip) { nrange--; nelt -= sp.size; continue; }
-			sp.origSz = sp.size;
-			sp.fw = fw; sp.offidx = offidx; sp.rdoff = rdoff; sp.seedlen = seedlen;
-			satpos2.push_back(sp);
-			if(sp.size <= nsm) { nsmall++; nsmall_elts += sp.size; }
-			if(sp.nlex > 0) {
-				const size_t p5 = rdoff - (fw ? sp.nlex : 0);
-				c->exRange[fw ? 0 : 1].push_back({p5, (size_t)seedlen + sp.nlex, sp.size});
-			}
+			sp.size = st.rand_n; sp.fw = st.fw != 0; sp.rdoff = st.rdoff; sp.seedlen = st.seedlen;
+			satpos.push_back(sp);
+			rand_ns.push_back(st.rand_n);
+			c->firstRow.push_back(e0);
+			e0 += st.rand_n;
 		}
-		PH(13);
-		std::stable_sort(satpos2.begin(), satpos2.end());
-		size_t nelt_added = 0;
-		for(size_t j = 0; j < nsmall && nelt_added < maxelt; j++) {
-			satpos.push_back(satpos2[j]);
-			rand_ns.push_back((uint32_t)satpos2[j].size);
-			nelt_added += satpos2[j].size;
-		}
-		PH(14);
-		if(!(nelt_added >= maxelt || nsmall == satpos2.size())) {
-			c->rows.init(satpos2, nsmall, satpos2.size());
-			std::vector<Random1toN>& rands = c->prioRands;
-			if(rands.size() < satpos2.size()) rands.resize(satpos2.size());
-			for(size_t q = 0; q < satpos2.size(); q++) rands[q].reset();
-			while(nelt_added < maxelt && nelt_added < nelt) {
-#ifdef BT2X_PHASE_PROF
-				t_ph.c[kPhases - 1]++;
-#endif
-				const size_t ri = c->rows.next(rnd) + nsmall;
-				if(!rands[ri].inited()) rands[ri].init((uint16_t)satpos2[ri].size, false);
-				const size_t rr = rands[ri].next(rnd);
-				if(rands[ri].done()) c->rows.finishedRange(ri - nsmall);
-				SatPos sp = satpos2[ri];
-				sp.topf = satpos2[ri].topf + rr;
-				sp.size = 1;
-				sp.nlex = 0;
-				satpos.push_back(sp);
-				rand_ns.push_back(1);
-				nelt_added++;
-			}
-		}
-		const size_t nelt_ = nelt_added;
-		PH(3);
-
-		// ----------------------- SA resolution of every element extendSeeds may visit
-		c->res_in.clear();
-		c->firstRow.resize(satpos.size());
-		for(size_t i = 0; i < satpos.size(); i++) {
-			c->firstRow[i] = (uint32_t)c->res_in.size();
-			for(uint32_t e = 0; e < rand_ns[i]; e++) {
-				bt2x_resolve_in ri;
-				std::memset(&ri, 0, sizeof(ri));
-				ri.row = satpos[i].topf + e;
-				ri.qlen = satpos[i].seedlen;
-				c->res_in.push_back(ri);
-			}
-		}
+		const size_t nelt_ = ro.nelt;
 		PH(4);
-		if(!c->res_in.empty()) co_await Awaiter{c, REQ_RESOLVE};
-		PH_START();
 
 		// -------------------------------------------------- extendSeeds (:278-631)
 		int ret;
@@ -817,7 +865,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			}
 		}
 		if(ret == EXTEND_EXHAUSTED_CANDIDATES || ret == EXTEND_EXCEEDED_SOFT_LIMIT || ret == EXTEND_POLICY_FULFILLED) {
-			if(hits.numElts() / hits.nonzeroOffsets() < P.seedBoostThresh) break;   // averageHitsPerSeed
+			if(c->round_out.num_elts / c->round_out.nonz < P.seedBoostThresh) break;   // averageHitsPerSeed
 			if(sink.done()) break;                                                  // doneWithMate
 		} else {
 			break;
@@ -854,8 +902,8 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 	PH_START();
 	pool().parallel_for(nch, 1, [&](long ch) {
 		Launch::Chunk& C = L.chunks[(size_t)ch];
-		C.ws.clear(); C.wr.clear(); C.wd.clear();
-		C.sbytes = C.nseed = C.nres = C.dbytes = C.nprob = C.rbytes = 0;
+		C.ws.clear(); C.wr.clear(); C.wd.clear(); C.wn.clear();
+		C.sbytes = C.nseed = C.nres = C.dbytes = C.nprob = C.rbytes = C.nbytes = C.nnseed = C.nexr = 0;
 		const long e = std::min(n, (ch + 1) * kChunk);
 		for(long i = ch * kChunk; i < e; i++) {
 			ReadCtx* c = cohort[(size_t)i];
@@ -866,20 +914,27 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			} else if(c->req == REQ_DP) {
 				C.wd.push_back(c); C.dbytes += 2 * c->rd.length(); C.nprob += c->dps.size();
 				for(const DpWork& d : c->dps) C.rbytes += d.key.ncol;
+			} else if(c->req == REQ_ROUND) {
+				C.wn.push_back(c); C.nbytes += 2 * c->rd.length(); C.nnseed += c->seed_in.size();
+				C.nexr += c->exRange.size();
 			}
 		}
 	});
 	PH(10);
 	// chunk bases
 	uint64_t nws = 0, nwr = 0, nwd = 0, sb = 0, sk = 0, rk = 0, db = 0, pk = 0, rb = 0;
+	uint64_t nwn = 0, nb = 0, nk = 0, ne = 0;
 	for(long ch = 0; ch < nch; ch++) {
 		Launch::Chunk& C = L.chunks[(size_t)ch];
 		C.ws0 = nws; C.sb0 = sb; C.sk0 = sk; C.wr0 = nwr; C.rk0 = rk; C.wd0 = nwd; C.db0 = db; C.pk0 = pk; C.rb0 = rb;
+		C.wn0 = nwn; C.nb0 = nb; C.nk0 = nk; C.ne0 = ne;
 		nws += C.ws.size(); sb += C.sbytes; sk += C.nseed;
 		nwr += C.wr.size(); rk += C.nres;
 		nwd += C.wd.size(); db += C.dbytes; pk += C.nprob; rb += C.rbytes;
+		nwn += C.wn.size(); nb += C.nbytes; nk += C.nnseed; ne += C.nexr;
 	}
-	L.ws.resize(nws); L.wr.resize(nwr); L.wd.resize(nwd);
+	L.ws.resize(nws); L.wr.resize(nwr); L.wd.resize(nwd); L.wn.resize(nwn);
+	L.round_reads.resize(nb); L.round_seeds.resize(nk); L.round_in.resize(nwn); L.round_exr.resize(ne);
 	L.sr.resize(nws + 1); L.sk.resize(nws + 1); L.rk.resize(nwr + 1);
 	L.qb.resize(nwd + 1); L.pb.resize(nwd + 1); L.fb.resize(pk + 1);
 	L.sr[nws] = sb; L.sk[nws] = sk; L.rk[nwr] = rk; L.qb[nwd] = db; L.pb[nwd] = pk; L.fb[pk] = rb;
@@ -934,6 +989,26 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			}
 			dbo += 2 * len;
 		}
+		// seed rounds: the read, its seeds rebased, its round header, its exRange entries
+		uint64_t nbo = C.nb0, nko = C.nk0, neo = C.ne0;
+		for(size_t k = 0; k < C.wn.size(); k++) {
+			ReadCtx* c = C.wn[k];
+			const size_t i = C.wn0 + k, len = c->rd.length();
+			L.wn[i] = c;
+			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.round_reads.begin() + (long)nbo);
+			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.round_reads.begin() + (long)(nbo + len));
+			bt2x_round_in q = c->round_in;
+			q.read_off = nbo; q.seed0 = nko; q.exr0 = (uint32_t)neo; q.nexr = (uint16_t)c->exRange.size();
+			L.round_in[i] = q;
+			for(const bt2x_seed_in& q0 : c->seed_in) {
+				bt2x_seed_in sq = q0;
+				sq.read_off += nbo;
+				L.round_seeds[nko++] = sq;
+			}
+			std::copy(c->exRange.begin(), c->exRange.end(), L.round_exr.begin() + (long)neo);
+			neo += c->exRange.size();
+			nbo += 2 * len;
+		}
 	});
 	PH(12);
 	L.t_gather = now_s() - tg;
@@ -941,7 +1016,13 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 
 // The launch's backend calls (on the GPU thread when pipelined).
 void Aligner::execute(Launch& L) {
-	L.t_seed = L.t_resolve = L.t_dp = 0;
+	L.t_seed = L.t_resolve = L.t_dp = L.t_round = 0;
+	if(!L.wn.empty()) {
+		const double t0 = now_s();
+		be_.seed_round(L.round_reads, L.round_seeds, L.round_in, L.round_exr, (uint32_t)p_.mxIter, L.round_out,
+		               L.round_sats, L.round_elts, L.round_exr_out);
+		L.t_round = now_s() - t0;
+	}
 	if(!L.ws.empty()) {
 		const double t0 = now_s();
 		be_.seed_search(L.seed_reads, L.seed_in, L.seed_out);
@@ -961,12 +1042,18 @@ void Aligner::execute(Launch& L) {
 
 // Hand every served read its results and resume it until it waits again or finishes.
 void Aligner::scatter_resume(Launch& L, RunStats& st) {
-	const long nws = (long)L.ws.size(), nwr = (long)L.wr.size(), nwd = (long)L.wd.size();
+	const long nws = (long)L.ws.size(), nwr = (long)L.wr.size(), nwd = (long)L.wd.size(), nwn = (long)L.wn.size();
+	if(nwn) {
+		st.round_launches++; st.rounds += (uint64_t)nwn; st.t_round += L.t_round;
+		st.seeds += L.round_seeds.size();
+		for(const bt2x_round_out& o : L.round_out) st.resolves += o.nelt;
+	}
 	if(nws) { st.seed_launches++; st.seeds += L.seed_in.size(); st.t_seed += L.t_seed; }
 	if(nwr) { st.resolve_launches++; st.resolves += L.res_in.size(); st.t_resolve += L.t_resolve; }
 	if(nwd) { st.dp_launches++; st.dps += L.dp_in.size(); st.t_dp += L.t_dp; }
-	st.t_backend += L.t_seed + L.t_resolve + L.t_dp;
+	st.t_backend += L.t_seed + L.t_resolve + L.t_dp + L.t_round;
 	L.run.clear();
+	L.run.insert(L.run.end(), L.wn.begin(), L.wn.end());
 	L.run.insert(L.run.end(), L.ws.begin(), L.ws.end());
 	L.run.insert(L.run.end(), L.wr.begin(), L.wr.end());
 	L.run.insert(L.run.end(), L.wd.begin(), L.wd.end());
@@ -975,6 +1062,19 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	st.t_gather += L.t_gather;
 	pool().parallel_for(nrun, 64, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
+		if(i < nwn) {
+			const bt2x_round_out& o = L.round_out[(size_t)i];
+			c->round_out = o;
+			if(o.status == BT2X_ROUND_OK) {
+				c->sats.assign(L.round_sats.begin() + o.sat0, L.round_sats.begin() + o.sat0 + o.nsat);
+				c->res_out.assign(L.round_elts.begin() + o.elt0, L.round_elts.begin() + o.elt0 + o.nelt);
+				c->exNew.assign(L.round_exr_out.begin() + o.exr0, L.round_exr_out.begin() + o.exr0 + o.nexr);
+			}
+			c->req = REQ_NONE;
+			c->task.h.resume();
+			return;
+		}
+		i -= nwn;
 		if(i < nws) {
 			c->seed_out.assign(L.seed_out.begin() + (long)L.sk[i], L.seed_out.begin() + (long)L.sk[i + 1]);
 		} else if(i < nws + nwr) {
@@ -1013,7 +1113,7 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 bool Aligner::step(std::vector<ReadCtx*>& act, RunStats& st) {
 	Launch& L = launch_[0];
 	gather(L, act);
-	if(L.ws.empty() && L.wr.empty() && L.wd.empty()) return false;
+	if(L.ws.empty() && L.wr.empty() && L.wd.empty() && L.wn.empty()) return false;
 	static const bool trace = std::getenv("BT2X_TRACE") != nullptr;
 	if(trace) std::fprintf(stderr, "BT2X_TRACE active=%zu seed=%zu resolve=%zu dp=%zu\n", act.size(), L.ws.size(),
 	                       L.wr.size(), L.wd.size());
@@ -1236,7 +1336,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		// retire and refill it, and gather its next launch.
 		std::vector<ReadCtx*> co[2];
 		const size_t cap = slots / 2;
-		auto empty = [](const Launch& L) { return L.ws.empty() && L.wr.empty() && L.wd.empty(); };
+		auto empty = [](const Launch& L) { return L.ws.empty() && L.wr.empty() && L.wd.empty() && L.wn.empty(); };
 		int a = 0;
 		refill(co[0], cap);
 		gather(launch_[0], co[0]);

@@ -574,7 +574,7 @@ struct DpWork {                     // one posed problem (its window is fetched 
 	bt2x_dp_in in;                  // read_off / qual_off / ref_off are set by the scheduler
 };
 
-enum ReqKind { REQ_NONE = 0, REQ_SEED = 1, REQ_RESOLVE = 2, REQ_DP = 3 };
+enum ReqKind { REQ_NONE = 0, REQ_SEED = 1, REQ_RESOLVE = 2, REQ_DP = 3, REQ_ROUND = 4 };
 
 struct ReadCtx;
 
@@ -625,8 +625,6 @@ struct SatPos {
 	}
 };
 
-struct ExtendRange { size_t off, len, sz; };
-
 // RowSampler (aligner_sw_driver.h:176-267), lensq = szsq = true.  next() is the
 // reference's linear dart walk over the non-eliminated ranges; here the running sums it
 // accumulates are kept (same order of double additions, so the same values) and the dart
@@ -670,6 +668,25 @@ private:
 		for(size_t k = 0; k < live.size(); k++) { sofar += masses[live[k]]; pre[k] = sofar; }
 	}
 };
+
+// The host restatement of a seed round after its seed search, with bt2x_seed_round's
+// contract (include/bt2x.h): searchAllSeedsFinalize + SeedResults::add
+// (aligner_seed.cpp:508-540), rankSeedHits (aligner_seed.h:1000-1061) and
+// prioritizeSATups (aligner_sw_driver.cpp:61-260).  Serves the reads the GPU round hands
+// back (BT2X_ROUND_REDO) and the CPU test backend; the SAM tests pin it to the reference.
+struct RoundScratch {
+	SeedHitsHip hits;
+	std::vector<std::pair<uint64_t, uint8_t>> cacheNlex;    // AlignmentCache: key -> nlex of the first add
+	std::vector<SatPos> satpos2;
+	RowSampler rows;
+	std::vector<Random1toN> prioRands;
+};
+// Appends the read's extension list to sats, its BW rows to rows (qlen = seed length) and
+// the exRange entries it adds to exr_out; returns status / nonz / numElts in `out` (the
+// offsets fields are left to the caller).
+void host_round(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout, const bt2x_exrange* exr,
+                uint32_t maxelt, Rng& rnd, RoundScratch& w, bt2x_round_out& out, std::vector<bt2x_sat>& sats,
+                std::vector<bt2x_resolve_in>& rows, std::vector<bt2x_exrange>& exr_out);
 
 // The candidate walk of extendSeeds (aligner_sw_driver.cpp:278-631) as a resumable
 // iterator: next() runs the loop up to its next DP problem (PROBLEM, the problem's key)
@@ -756,15 +773,14 @@ struct ReadCtx {
 	std::vector<DpMemo> memo;
 	std::vector<bt2x_aln_rec> recs;
 	std::vector<uint32_t> edits;
-	// seed round scratch
-	std::vector<std::pair<uint8_t, uint32_t>> seedIds;      // (fw, idx) of each searched seed
-	std::vector<std::pair<uint64_t, uint8_t>> cacheNlex;    // AlignmentCache: key -> nlex of the first add
-	SeedHitsHip hits;
-	std::vector<SatPos> satpos2, satpos;
+	// seed round: the GPU round's request and results (or, for a REDO read, the host's)
+	bt2x_round_in round_in;
+	bt2x_round_out round_out;
+	std::vector<bt2x_sat> sats;
+	std::vector<bt2x_exrange> exRange, exNew;           // extendSeeds' exRange (both strands)
+	RoundScratch rs;
+	std::vector<SatPos> satpos;
 	std::vector<uint32_t> rand_ns, firstRow;
-	std::vector<ExtendRange> exRange[2];
-	RowSampler rows;
-	std::vector<Random1toN> prioRands;
 	// extendSeeds state
 	SeenDiags seenDiags, seen2;
 	ExtendWalk walk, ahead;
@@ -807,6 +823,11 @@ public:
 	                      const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
 	                      std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
 	                      std::vector<uint32_t>& edits) = 0;
+	// bt2x_seed_round (include/bt2x.h)
+	virtual void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
+	                        const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr,
+	                        uint32_t maxelt, std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats,
+	                        std::vector<bt2x_resolve_out>& elts, std::vector<bt2x_exrange>& exr_out) = 0;
 };
 
 // -------------------------------------------------------------------- driver
@@ -815,7 +836,9 @@ struct RunStats {
 	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0;
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
 	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
-	double t_seed = 0, t_resolve = 0, t_dp = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0, t_wait = 0, t_gather = 0, t_retire = 0;
+	uint64_t round_launches = 0, rounds = 0, round_redo = 0;
+	double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0,
+	       t_wait = 0, t_gather = 0, t_retire = 0;
 };
 
 class Aligner {
@@ -824,6 +847,9 @@ public:
 	~Aligner();
 	// run(): overlap one cohort's GPU launches with the host work of another (default on)
 	void set_pipeline(bool on) { pipeline_ = on; }
+	// seed rounds through bt2x_seed_round (default on; off: seed search, host ranking and
+	// prioritization, SA resolution as three requests)
+	void set_gpu_round(bool on) { gpu_round_ = on; }
 	Aligner(const Aligner&) = delete;
 	Aligner& operator=(const Aligner&) = delete;
 	// SAM header (@HD, @SQ; sam.cpp:47-80)
@@ -836,8 +862,9 @@ public:
 private:
 	// one cohort's requests as one seed, one resolve and one DP launch
 	struct Launch {
-		std::vector<ReadCtx*> ws, wr, wd, run;          // reads waiting on each kind
+		std::vector<ReadCtx*> ws, wr, wd, wn, run;      // reads waiting on each kind (wn: rounds)
 		std::vector<uint64_t> sr, sk, rk, qb, pb, fb;  // per-read offsets into the buffers
+		std::vector<uint64_t> nr, nk, ne;               // rounds: read bytes, seeds, exRange entries
 		std::vector<uint8_t> seed_reads, dp_reads, dp_quals, dp_refs;
 		std::vector<bt2x_seed_in> seed_in;
 		std::vector<bt2x_seed_out> seed_out;
@@ -847,12 +874,20 @@ private:
 		std::vector<bt2x_dp_out> dp_out;
 		std::vector<bt2x_aln_rec> recs;
 		std::vector<uint32_t> edits;
-		double t_seed = 0, t_resolve = 0, t_dp = 0, t_gather = 0;
+		std::vector<uint8_t> round_reads;
+		std::vector<bt2x_seed_in> round_seeds;
+		std::vector<bt2x_round_in> round_in;
+		std::vector<bt2x_exrange> round_exr, round_exr_out;
+		std::vector<bt2x_round_out> round_out;
+		std::vector<bt2x_sat> round_sats;
+		std::vector<bt2x_resolve_out> round_elts;
+		double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_gather = 0;
 		// gather's per-chunk lists, sizes and bases
 		struct Chunk {
-			std::vector<ReadCtx*> ws, wr, wd;
-			uint64_t sbytes = 0, nseed = 0, nres = 0, dbytes = 0, nprob = 0, rbytes = 0;
+			std::vector<ReadCtx*> ws, wr, wd, wn;
+			uint64_t sbytes = 0, nseed = 0, nres = 0, dbytes = 0, nprob = 0, rbytes = 0, nbytes = 0, nnseed = 0, nexr = 0;
 			uint64_t ws0 = 0, sb0 = 0, sk0 = 0, wr0 = 0, rk0 = 0, wd0 = 0, db0 = 0, pk0 = 0, rb0 = 0;
+			uint64_t wn0 = 0, nb0 = 0, nk0 = 0, ne0 = 0;
 		};
 		std::vector<Chunk> chunks;
 	};
@@ -862,7 +897,7 @@ private:
 	void execute(Launch& L);
 	void scatter_resume(Launch& L, RunStats& st);
 	Launch launch_[2];
-	bool pipeline_ = true;
+	bool pipeline_ = true, gpu_round_ = true;
 	ReadCtx* take_ctx();
 	void retire(std::vector<ReadCtx*>& act, RunStats& st, void* ring);
 	// pooled read contexts (kept across runs; released by the destructor)

@@ -6,6 +6,7 @@
 //   bt2x-align -x <index base> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N]
 //              [-L N] [--mp MX,MN] [--np N] [--rdg O,E] [--rfg O,E] [--gbar N]
 //              [--seed N] [-p threads] [--slots N] [--device N] [--stats]
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -36,6 +37,33 @@ public:
 		out.resize(in.size());
 		bt2x::check(bt2x_resolve(ctx_, in.data(), (uint32_t)in.size(), 0, out.data()), "bt2x_resolve");
 	}
+	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
+	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
+	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
+	                std::vector<bt2x_exrange>& exr_out) override {
+		const uint32_t n = (uint32_t)in.size();
+		out.resize(n);
+		// arenas sized from the last launch's use per read (grown and retried on overflow)
+		uint32_t used[3] = {0, 0, 0};
+		uint32_t cap[3] = {(uint32_t)(sat_per_read_ * n) + 1024, (uint32_t)(elt_per_read_ * n) + 1024, 4 * n + 256};
+		for(int attempt = 0; attempt < 2; attempt++) {
+			sats.resize(cap[0]); elts.resize(cap[1]); exr_out.resize(cap[2]);
+			const int rc = bt2x_seed_round(ctx_, reads.data(), reads.size(), seeds.data(), (uint32_t)seeds.size(), in.data(),
+			                               n, exr.data(), (uint32_t)exr.size(), maxelt, out.data(), sats.data(), cap[0],
+			                               elts.data(), cap[1], exr_out.data(), cap[2], used);
+			if(rc == BT2X_E_OVERFLOW && attempt == 0) {
+				for(int k = 0; k < 3; k++) cap[k] = std::max(cap[k], used[k]);
+				continue;
+			}
+			bt2x::check(rc, "bt2x_seed_round");
+			break;
+		}
+		sats.resize(used[0]); elts.resize(used[1]); exr_out.resize(used[2]);
+		if(n) {
+			sat_per_read_ = std::max(8.0, 1.25 * used[0] / n);
+			elt_per_read_ = std::max(16.0, 1.25 * used[1] / n);
+		}
+	}
 	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
 	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
 	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
@@ -59,6 +87,7 @@ public:
 	}
 private:
 	bt2x_ctx* ctx_;
+	double sat_per_read_ = 16, elt_per_read_ = 64;
 };
 
 // --dump DIR: record every GPU launch's inputs (bench.py replays them from HBM).
@@ -74,6 +103,16 @@ public:
 	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
 		write("resolve", {{in.data(), in.size() * sizeof(bt2x_resolve_in)}});
 		in_.resolve(in, out);
+	}
+	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
+	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
+	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
+	                std::vector<bt2x_exrange>& exr_out) override {
+		in_.seed_round(reads, seeds, in, exr, maxelt, out, sats, elts, exr_out);
+		const uint64_t meta[4] = {maxelt, sats.size(), elts.size(), exr_out.size()};   // arena sizes the replay needs
+		write("round", {{reads.data(), reads.size()}, {seeds.data(), seeds.size() * sizeof(bt2x_seed_in)},
+		                {in.data(), in.size() * sizeof(bt2x_round_in)}, {exr.data(), exr.size() * sizeof(bt2x_exrange)},
+		                {meta, sizeof meta}});
 	}
 	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
 	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
@@ -114,7 +153,7 @@ int main(int argc, char** argv) {
 	Params p;
 	int threads = 16, device = 0;
 	size_t slots = 1 << 18;
-	bool stats = false, pipeline = true;
+	bool stats = false, pipeline = true, gpu_round = true;
 	std::string dump;
 	for(int i = 1; i < argc; i++) {
 		const std::string a = argv[i];
@@ -132,6 +171,7 @@ int main(int argc, char** argv) {
 		else if(a == "--stats") stats = true;
 		else if(a == "--dump") dump = val();
 		else if(a == "--no-pipeline") pipeline = false;
+		else if(a == "--no-gpu-round") gpu_round = false;
 		else if(a == "--end-to-end" || a == "--sensitive" || a == "--reorder" || a == "-q") {}
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); usage(); return 1; }
 	}
@@ -149,6 +189,7 @@ int main(int argc, char** argv) {
 		Backend& be = dumper ? static_cast<Backend&>(*dumper) : static_cast<Backend&>(hip);
 		Aligner al(p, ref, be);
 		al.set_pipeline(pipeline);
+		al.set_gpu_round(gpu_round);
 		FastqReader reader(fq.c_str());
 		struct rusage ru0;
 		getrusage(RUSAGE_SELF, &ru0);
@@ -185,11 +226,13 @@ int main(int argc, char** argv) {
 		if(stats)
 			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "
 			             "resolve_launches=%llu resolves=%llu t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f "
-			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu t_backend=%.4f t_step=%.4f t_wait=%.4f t_gather=%.4f t_retire=%.4f\n", (unsigned long long)st.reads, t_align,
+			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu t_backend=%.4f t_step=%.4f t_wait=%.4f t_gather=%.4f t_retire=%.4f "
+			             "round_launches=%llu rounds=%llu t_round=%.4f\n", (unsigned long long)st.reads, t_align,
 			             (unsigned long long)st.seed_launches, (unsigned long long)st.seeds, st.t_seed,
 			             (unsigned long long)st.resolve_launches, (unsigned long long)st.resolves, st.t_resolve,
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io, (unsigned long long)st.dps_used,
-			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait, st.t_gather, st.t_retire);
+			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait, st.t_gather, st.t_retire,
+			             (unsigned long long)st.round_launches, (unsigned long long)st.rounds, st.t_round);
 	} catch(const std::exception& e) {
 		std::fprintf(stderr, "bt2x-align: %s\n", e.what());
 		return 1;

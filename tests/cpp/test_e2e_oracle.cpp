@@ -53,6 +53,29 @@ public:
 			return;
 		}
 	}
+	// the oracle seed search, then the host restatement of the round (host_round), then
+	// the oracle SA resolution: the contract of bt2x_seed_round on the CPU
+	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
+	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
+	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
+	                std::vector<bt2x_exrange>& exr_out) override {
+		std::vector<bt2x_seed_out> so;
+		seed_search(reads, seeds, so);
+		out.resize(in.size());
+		sats.clear(); exr_out.clear();
+		std::vector<bt2x_resolve_in> rows;
+		RoundScratch w;
+		for(size_t r = 0; r < in.size(); r++) {
+			const bt2x_round_in& q = in[r];
+			Rng rnd;
+			rnd.last = q.rnd_last; rnd.lastOff = q.rnd_lastoff;
+			const uint32_t s0 = (uint32_t)sats.size(), e0 = (uint32_t)rows.size(), x0 = (uint32_t)exr_out.size();
+			host_round(q, seeds.data() + q.seed0, so.data() + q.seed0, exr.data() + q.exr0, maxelt, rnd, w, out[r],
+			           sats, rows, exr_out);
+			out[r].sat0 = s0; out[r].elt0 = e0; out[r].exr0 = x0;
+		}
+		resolve(rows, elts);
+	}
 private:
 	const bt2x_index_desc& idx_;
 	const bt2x_scoring& sc_;
@@ -63,7 +86,7 @@ private:
 class ReplayBackend : public Backend {
 public:
 	explicit ReplayBackend(Backend* rec) : rec_(rec) {}
-	void rewind() { rec_ = nullptr; k_ = kr_ = kd_ = 0; }
+	void rewind() { rec_ = nullptr; k_ = kr_ = kd_ = kn_ = 0; }
 	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
 	                 std::vector<bt2x_seed_out>& out) override {
 		if(rec_) { rec_->seed_search(reads, in, out); seeds_.push_back(out); } else out = seeds_[k_++];
@@ -78,7 +101,23 @@ public:
 		if(rec_) { rec_->dp_align(reads, quals, refs, in, out, recs, edits); dp_.push_back({out, recs, edits}); }
 		else { const auto& d = dp_[kd_++]; out = d.out; recs = d.recs; edits = d.edits; }
 	}
+	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
+	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
+	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
+	                std::vector<bt2x_exrange>& exr_out) override {
+		if(rec_) {
+			rec_->seed_round(reads, seeds, in, exr, maxelt, out, sats, elts, exr_out);
+			rounds_.push_back({out, sats, elts, exr_out});
+		} else {
+			const auto& d = rounds_[kn_++];
+			out = d.out; sats = d.sats; elts = d.elts; exr_out = d.exr;
+		}
+	}
 private:
+	struct Round { std::vector<bt2x_round_out> out; std::vector<bt2x_sat> sats; std::vector<bt2x_resolve_out> elts;
+	               std::vector<bt2x_exrange> exr; };
+	std::vector<Round> rounds_;
+	size_t kn_ = 0;
 	struct Dp { std::vector<bt2x_dp_out> out; std::vector<bt2x_aln_rec> recs; std::vector<uint32_t> edits; };
 	Backend* rec_;
 	size_t k_ = 0, kr_ = 0, kd_ = 0;
@@ -94,7 +133,7 @@ int main(int argc, char** argv) {
 	Params p;
 	size_t slots = 4096;
 	int threads = 4;
-	bool host_timing = false, pipeline = true;
+	bool host_timing = false, pipeline = true, gpu_round = true;
 	int reps = 1;
 	for(int i = 3; i < argc; i++) {
 		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
@@ -103,6 +142,7 @@ int main(int argc, char** argv) {
 		else if(a == "-p" && i + 1 < argc) threads = std::atoi(argv[++i]);
 		else if(a == "--host-timing") host_timing = true;
 		else if(a == "--no-pipeline") pipeline = false;
+		else if(a == "--no-gpu-round") gpu_round = false;
 		else if(a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); return 1; }
 	}
@@ -116,6 +156,7 @@ int main(int argc, char** argv) {
 		{
 			Aligner al0(p, ref, rb);
 			al0.set_pipeline(pipeline);
+			al0.set_gpu_round(gpu_round);
 			FastqReader fq(argv[2]);
 			std::FILE* nul = std::fopen("/dev/null", "wb");
 			al0.run(fq, nul, slots, threads);
@@ -126,6 +167,7 @@ int main(int argc, char** argv) {
 		// the timed run starts from an empty context pool, as bt2x-align does
 		Aligner al(p, ref, rb);
 		al.set_pipeline(pipeline);
+		al.set_gpu_round(gpu_round);
 		FastqReader fq(argv[2]);
 		struct rusage ru0, ru1;
 		getrusage(RUSAGE_SELF, &ru0);
@@ -148,6 +190,7 @@ int main(int argc, char** argv) {
 	}
 	Aligner al(p, ref, be);
 	al.set_pipeline(pipeline);
+	al.set_gpu_round(gpu_round);
 	FastqReader fq(argv[2]);
 	const RunStats st = al.run(fq, stdout, slots, threads);
 	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu "

@@ -84,6 +84,13 @@ def test_host_driver_vs_reference_sam(fixtures, name, idx, fq, opts):
         assert tight > 100, tight
 
 
+@pytest.mark.parametrize("name,idx,fq,opts", [SETS[1], SETS[4]], ids=[SETS[1][0], SETS[4][0]])
+def test_host_driver_vs_reference_sam_three_requests(fixtures, name, idx, fq, opts):
+    """The same with every seed round as seed search + host ranking/prioritization + SA
+    resolution (the path a read takes when the GPU round hands it back)."""
+    check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4", "--no-gpu-round"] + opts, name)
+
+
 def test_host_driver_slot_count_invariance(fixtures):
     """Results do not depend on how many reads are in flight."""
     outs = []
