@@ -63,10 +63,16 @@ struct RoundLaunch {
 	bt2x_sat* sats; uint32_t sat_cap;
 	bt2x_resolve_in* rows; uint32_t row_cap;
 	bt2x_exrange* exr_out; uint32_t exr_cap;
-	uint32_t* counters;            // [0] sats, [1] rows, [2] exr_out (used, may exceed caps)
-	uint8_t* ws; uint32_t nlanes;  // per-lane workspace (bt2x_round_ws_bytes each)
+	uint32_t* counters;            // [0] sats, [1] rows, [2] exr_out, [3] sampling jobs, [4] their ranges
+	                               // (used, may exceed caps)
+	uint8_t* jobs; uint32_t job_cap;
+	uint8_t* ranges; uint32_t range_cap;
+	uint8_t* ws; uint8_t* ws2; uint32_t nlanes;   // per-lane workspaces (prep, sample)
 };
 size_t bt2x_round_ws_bytes();
+size_t bt2x_round_ws2_bytes();
+size_t bt2x_round_job_bytes();
+size_t bt2x_round_range_bytes();
 uint32_t bt2x_round_lanes(int ncu);
 int bt2x_launch_round(const RoundLaunch& a, void* stream);
 

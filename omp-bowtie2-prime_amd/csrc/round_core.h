@@ -1,9 +1,12 @@
-// round_core.h — one read's seed round after its seed search, as one GPU lane runs it
+// round_core.h — one read's seed round after its seed search, as the GPU runs it
 // (bt2x_seed_round, include/bt2x.h): searchAllSeedsFinalize + SeedResults::add,
-// rankSeedHits, prioritizeSATups (with RowSampler and Random1toN), and the list of BW
-// rows extendSeeds may visit.  Integer/double code shared by the kernel (round_kernel.hip)
-// and, compiled as host code, by the CPU test that checks it against the host driver's
-// restatement (tests/cpp/test_round.cpp).
+// rankSeedHits and prioritizeSATups, in two parts:
+//   prep()    everything up to RowSampler's sampling, and how many elements it will draw;
+//   sample()  the sampling loop itself (RowSampler darts + Random1toN draws).
+// The kernel (round_kernel.hip) runs prep for every read and sample only for the reads
+// that need it, compacted, so the long RNG-sequential sampling loops of repetitive reads
+// do not hold whole waves of short reads.  Integer/double code shared with the CPU test
+// that checks it against the host driver's restatement (tests/cpp/test_round.cpp).
 //
 // Reference (file:line):
 //   searchAllSeedsFinalize / SeedResults::add   aligner_seed.cpp:508-540, aligner_seed.h:603-641
@@ -24,9 +27,8 @@ namespace bt2x_round {
 
 constexpr int kMaxOffs = 64;                  // seed offsets per strand
 constexpr int kMaxRanges = 2 * kMaxOffs;      // satpos2 entries
-constexpr int kMaxSat = 416;                  // satpos entries (<= maxelt + 4)
-constexpr int kArena = 6144;                  // uint16 list storage (swap lists)
-constexpr int kHash = 1024;                   // seen-set slots (range << 16 | element) + 1
+constexpr int kArena = 4096;                  // uint16 list storage (swap lists)
+constexpr int kHash = 1024;                   // seen-set slots: (range << 16 | element) + 1
 constexpr uint32_t kNsm = 5;                  // prioritizeSATups' nsm
 
 struct Rnd {                                  // RandomSource, LCG variant
@@ -61,28 +63,34 @@ struct R1N {                                  // Random1toN state; lists live in
 	uint8_t inited, swaplist, converted, pad;
 };
 
-// Per-lane workspace (global memory on the GPU).
-struct Ws {
+// prep()'s per-lane workspace
+struct PrepWs {
 	uint64_t htopf[2][kMaxOffs], hn[2][kMaxOffs];
 	uint8_t hnlex[2][kMaxOffs], hvalid[2][kMaxOffs], hsorted[2][kMaxOffs];
 	uint16_t rankIdx[kMaxRanges];
 	uint8_t rankFw[kMaxRanges];
 	uint64_t cacheTop[kMaxRanges];
 	uint8_t cacheNlex[kMaxRanges];
-	Range r2[kMaxRanges];
+	Range r2[kMaxRanges];                     // prioritizeSATups' ranges, sorted
 	bt2x_exrange exnew[kMaxRanges];
+};
+
+// sample()'s per-lane workspace
+struct SampleWs {
 	double masses[kMaxRanges], pre[kMaxRanges];
 	uint16_t live[kMaxRanges];
 	R1N r1n[kMaxRanges];
 	uint16_t arena[kArena];
 	uint32_t hash[kHash];
-	// the read's extension list: satpos[i] = (range, element offset, rand_n)
-	uint16_t satRange[kMaxSat], satN[kMaxSat];
-	uint32_t satElt[kMaxSat];
 };
 
-struct Result {
-	uint32_t status, nonz, nsat, nelt, nexnew;
+struct Prep {
+	uint32_t status, nonz, nexnew;
+	uint32_t n2;                              // ranges in r2
+	uint32_t nsmall;                          // ranges of <= nsm elements (r2[0 .. nsmall))
+	uint32_t nsmallSat;                       // of those, taken whole (maxelt may stop early)
+	uint64_t smallElts;                       // their elements
+	uint64_t nsamples;                        // elements sample() draws from r2[nsmall .. n2)
 	uint64_t numElts;
 };
 
@@ -95,79 +103,15 @@ __host__ __device__ inline bool range_less(const Range& a, const Range& b) {
 	return a.fw && !b.fw;                     // seedlen is the same for all seeds of a round
 }
 
-__host__ __device__ inline bool seen_test_set(Ws& w, uint32_t key) {      // key != 0
-	uint32_t h = (key * 2654435761u) >> 22;                                 // 10 bits
-	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1)) {
-		if(w.hash[h] == key) return true;
-		if(w.hash[h] == 0) { w.hash[h] = key; return false; }
-	}
-	return true;                                                             // full: cannot happen (<= 416 keys)
+__host__ __device__ inline bool exr_covers(const bt2x_exrange& er, int fw, uint32_t rdoff, uint32_t L, uint64_t size) {
+	return er.fw == fw && er.off <= rdoff && (uint64_t)er.off + er.len >= (uint64_t)rdoff + L && size <= er.sz;
 }
 
-__host__ __device__ inline bool seen_has(const Ws& w, uint32_t key) {
-	uint32_t h = (key * 2654435761u) >> 22;
-	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1)) {
-		if(w.hash[h] == key) return true;
-		if(w.hash[h] == 0) return false;
-	}
-	return false;
-}
-
-// Random1toN::next over range ri; false on workspace overflow.
-__host__ __device__ inline bool r1n_next(Ws& w, int ri, Rnd& rnd, uint32_t& arenaTop, uint16_t& out) {
-	R1N& s = w.r1n[ri];
-	if(s.cur == 0 && !s.converted) {
-		if(s.n == 1) { s.cur = 1; out = 0; return true; }
-		if(s.swaplist) {
-			if(arenaTop + s.n > (uint32_t)kArena) return false;
-			s.list = (uint16_t)arenaTop;
-			arenaTop += s.n;
-			for(uint32_t i = 0; i < s.n; i++) w.arena[s.list + i] = (uint16_t)i;
-		}
-	}
-	if(s.swaplist) {
-		const uint32_t r = s.cur + rnd.nextU32() % (uint32_t)(s.n - s.cur);
-		if(r != s.cur) {
-			const uint16_t t = w.arena[s.list + s.cur];
-			w.arena[s.list + s.cur] = w.arena[s.list + r];
-			w.arena[s.list + r] = t;
-		}
-		out = w.arena[s.list + s.cur];
-		s.cur++;
-		return true;
-	}
-	// seen-list mode: redraw until unseen
-	uint16_t rn;
-	do {
-		rn = (uint16_t)(rnd.nextU32() % (uint32_t)s.n);
-	} while(seen_has(w, ((uint32_t)ri << 16 | rn) + 1u));
-	seen_test_set(w, ((uint32_t)ri << 16 | rn) + 1u);
-	s.cur++;
-	// s.cur draws so far = seen_.size()
-	if(s.cur >= s.thresh && s.cur < s.n) {
-		// convert to a swap list of the unseen elements, ascending
-		const uint32_t nl = (uint32_t)s.n - s.cur;
-		if(arenaTop + nl > (uint32_t)kArena) return false;
-		const uint16_t base = (uint16_t)arenaTop;
-		uint32_t k = 0;
-		for(uint32_t j = 0; j < s.n; j++)
-			if(!seen_has(w, ((uint32_t)ri << 16 | j) + 1u)) w.arena[base + k++] = (uint16_t)j;
-		arenaTop += nl;
-		s.list = base;
-		s.cur = 0;
-		s.n = (uint16_t)nl;
-		s.converted = 1;
-		s.swaplist = 1;
-	}
-	out = rn;
-	return true;
-}
-
-// The round for one read.  sin/sout: its seeds and their search results; exr: exRange
-// entries of earlier rounds.  Fills w.sat* (extension list) and w.exnew.
-__host__ __device__ inline Result run(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout,
-                                      const bt2x_exrange* exr, uint32_t maxelt, Rnd& rnd, Ws& w) {
-	Result res = {BT2X_ROUND_OK, 0, 0, 0, 0, 0};
+// Finalize, rank and prioritize up to the sampling decision.
+__host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout,
+                                     const bt2x_exrange* exr, uint32_t maxelt, Rnd& rnd, PrepWs& w) {
+	Prep res = {};
+	res.status = BT2X_ROUND_OK;
 	const uint32_t numOffs = in.num_offs, L = in.seedlen, interval = in.interval, offset = in.offset;
 	if(numOffs > (uint32_t)kMaxOffs) { res.status = BT2X_ROUND_REDO; return res; }
 	for(int s = 0; s < 2; s++)
@@ -234,16 +178,8 @@ __host__ __device__ inline Result run(const bt2x_round_in& in, const bt2x_seed_i
 		for(uint32_t q = 0; q < ncache; q++) if(w.cacheTop[q] == sp.topf) { sp.nlex = w.cacheNlex[q]; break; }
 		if(sp.size == 0) continue;
 		bool skip = false;
-		for(uint32_t q = 0; q < in.nexr && !skip; q++) {
-			const bt2x_exrange& er = exr[q];
-			if(er.fw == fw && er.off <= sp.rdoff && (uint64_t)er.off + er.len >= (uint64_t)sp.rdoff + L && sp.size <= er.sz)
-				skip = true;
-		}
-		for(uint32_t q = 0; q < res.nexnew && !skip; q++) {
-			const bt2x_exrange& er = w.exnew[q];
-			if(er.fw == fw && er.off <= sp.rdoff && (uint64_t)er.off + er.len >= (uint64_t)sp.rdoff + L && sp.size <= er.sz)
-				skip = true;
-		}
+		for(uint32_t q = 0; q < in.nexr && !skip; q++) skip = exr_covers(exr[q], fw, sp.rdoff, L, sp.size);
+		for(uint32_t q = 0; q < res.nexnew && !skip; q++) skip = exr_covers(w.exnew[q], fw, sp.rdoff, L, sp.size);
 		for(uint32_t q = 0; q < n2 && !skip; q++) skip = w.r2[q].topf == sp.topf;
 		if(skip) continue;
 		nelt += sp.size;
@@ -265,70 +201,137 @@ __host__ __device__ inline Result run(const bt2x_round_in& in, const bt2x_seed_i
 		while(j > 0 && range_less(x, w.r2[j - 1])) { w.r2[j] = w.r2[j - 1]; j--; }
 		w.r2[j] = x;
 	}
-	uint32_t nsat = 0;
+	// small ranges whole, then (if needed) one draw per element up to maxelt
 	uint64_t added = 0;
-	for(uint32_t j = 0; j < nsmall && added < maxelt; j++) {
-		if(nsat >= (uint32_t)kMaxSat) { res.status = BT2X_ROUND_REDO; return res; }
-		w.satRange[nsat] = (uint16_t)j; w.satElt[nsat] = 0; w.satN[nsat] = (uint16_t)w.r2[j].size; nsat++;
-		added += w.r2[j].size;
-	}
+	uint32_t nsat = 0;
+	for(uint32_t j = 0; j < nsmall && added < maxelt; j++) { nsat++; added += w.r2[j].size; }
+	res.n2 = n2; res.nsmall = nsmall; res.nsmallSat = nsat; res.smallElts = added;
+	res.nsamples = 0;
 	if(!(added >= maxelt || nsmall == n2)) {
-		// RowSampler over the larger ranges (lensq = szsq = true)
-		const uint32_t nb = n2 - nsmall;
-		double mass = 0.0f;
-		for(uint32_t i = 0; i < nb; i++) {
-			const Range& rg = w.r2[nsmall + i];
-			double num = (double)(rg.nlex + 1);
-			num *= num;
-			double den = (double)rg.size;
-			den *= den;
-			w.masses[i] = num / den;
-			mass += w.masses[i];
-			w.live[i] = (uint16_t)i;
-			R1N& s = w.r1n[i];
-			s.inited = 0; s.n = 0; s.cur = 0; s.converted = 0; s.swaplist = 0;
-		}
-		uint32_t nlive = nb;
-		auto rebuild = [&]() {
-			double sofar = 0.0f;
-			for(uint32_t k = 0; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
-		};
-		rebuild();
-		for(int k = 0; k < kHash; k++) w.hash[k] = 0;
-		uint32_t arenaTop = 0;
-		while(added < maxelt && added < nelt) {
-			const double rd = rnd.nextFloat() * mass;
-			// the dart: first live range whose running mass exceeds it (else the last live one)
-			uint32_t lo = 0, hi = nlive;
-			while(lo < hi) { const uint32_t mid = (lo + hi) >> 1; if(rd < w.pre[mid]) hi = mid; else lo = mid + 1; }
-			if(nlive == 0) { res.status = BT2X_ROUND_REDO; return res; }
-			const uint32_t bi = w.live[lo < nlive ? lo : nlive - 1];
-			R1N& s = w.r1n[bi];
-			if(!s.inited) {
-				const uint16_t n = (uint16_t)w.r2[nsmall + bi].size;          // uint16_t element type
-				if(n == 0) { res.status = BT2X_ROUND_REDO; return res; }
-				s.inited = 1; s.n = n; s.cur = 0; s.converted = 0; s.swaplist = n < 128 ? 1 : 0;
-				const uint16_t t = (uint16_t)(0.10f * (float)n);
-				s.thresh = t > 16 ? t : 16;
-			}
-			uint16_t rr;
-			if(!r1n_next(w, (int)bi, rnd, arenaTop, rr)) { res.status = BT2X_ROUND_REDO; return res; }
-			if(s.n > 0 && s.cur >= s.n) {                                       // done(): finishedRange
-				mass -= w.masses[bi];
-				uint32_t k = 0;
-				while(k < nlive && w.live[k] != bi) k++;
-				for(; k + 1 < nlive; k++) w.live[k] = w.live[k + 1];
-				nlive--;
-				rebuild();
-			}
-			if(nsat >= (uint32_t)kMaxSat) { res.status = BT2X_ROUND_REDO; return res; }
-			w.satRange[nsat] = (uint16_t)(nsmall + bi); w.satElt[nsat] = rr; w.satN[nsat] = 1; nsat++;
-			added++;
+		const uint64_t top = (uint64_t)maxelt < nelt ? (uint64_t)maxelt : nelt;
+		res.nsamples = top > added ? top - added : 0;
+	}
+	return res;
+}
+
+__host__ __device__ inline bool seen_has(const SampleWs& w, uint32_t key) {       // key != 0
+	uint32_t h = (key * 2654435761u) >> 22;                                      // 10 bits
+	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1)) {
+		if(w.hash[h] == key) return true;
+		if(w.hash[h] == 0) return false;
+	}
+	return false;
+}
+
+__host__ __device__ inline void seen_add(SampleWs& w, uint32_t key) {
+	uint32_t h = (key * 2654435761u) >> 22;
+	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1))
+		if(w.hash[h] == 0 || w.hash[h] == key) { w.hash[h] = key; return; }
+}
+
+// Random1toN::next over range ri; false on workspace overflow.
+__host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t& arenaTop, uint16_t& out) {
+	R1N& s = w.r1n[ri];
+	if(s.cur == 0 && !s.converted) {
+		if(s.n == 1) { s.cur = 1; out = 0; return true; }
+		if(s.swaplist) {
+			if(arenaTop + s.n > (uint32_t)kArena) return false;
+			s.list = (uint16_t)arenaTop;
+			arenaTop += s.n;
+			for(uint32_t i = 0; i < s.n; i++) w.arena[s.list + i] = (uint16_t)i;
 		}
 	}
-	res.nsat = nsat;
-	res.nelt = (uint32_t)added;
-	return res;
+	if(s.swaplist) {
+		const uint32_t r = s.cur + rnd.nextU32() % (uint32_t)(s.n - s.cur);
+		if(r != s.cur) {
+			const uint16_t t = w.arena[s.list + s.cur];
+			w.arena[s.list + s.cur] = w.arena[s.list + r];
+			w.arena[s.list + r] = t;
+		}
+		out = w.arena[s.list + s.cur];
+		s.cur++;
+		return true;
+	}
+	// seen-list mode: redraw until unseen
+	uint16_t rn;
+	do {
+		rn = (uint16_t)(rnd.nextU32() % (uint32_t)s.n);
+	} while(seen_has(w, ((uint32_t)ri << 16 | rn) + 1u));
+	seen_add(w, ((uint32_t)ri << 16 | rn) + 1u);
+	s.cur++;                                  // = seen_.size()
+	if(s.cur >= s.thresh && s.cur < s.n) {
+		// convert to a swap list of the unseen elements, ascending
+		const uint32_t nl = (uint32_t)s.n - s.cur;
+		if(arenaTop + nl > (uint32_t)kArena) return false;
+		const uint16_t base = (uint16_t)arenaTop;
+		uint32_t k = 0;
+		for(uint32_t j = 0; j < s.n; j++)
+			if(!seen_has(w, ((uint32_t)ri << 16 | j) + 1u)) w.arena[base + k++] = (uint16_t)j;
+		arenaTop += nl;
+		s.list = base;
+		s.cur = 0;
+		s.n = (uint16_t)nl;
+		s.converted = 1;
+		s.swaplist = 1;
+	}
+	out = rn;
+	return true;
+}
+
+// RowSampler over big[0 .. nb) (lensq = szsq = true) and one Random1toN per range:
+// emit(k, bi, element) for each of the nsamples draws.  False on workspace overflow.
+template<class Emit>
+__host__ __device__ inline bool sample(const Range* big, uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w,
+                                       Emit&& emit) {
+	if(nb > (uint32_t)kMaxRanges) return false;
+	double mass = 0.0f;
+	for(uint32_t i = 0; i < nb; i++) {
+		double num = (double)(big[i].nlex + 1);
+		num *= num;
+		double den = (double)big[i].size;
+		den *= den;
+		w.masses[i] = num / den;
+		mass += w.masses[i];
+		w.live[i] = (uint16_t)i;
+		R1N& s = w.r1n[i];
+		s.inited = 0; s.n = 0; s.cur = 0; s.converted = 0; s.swaplist = 0;
+	}
+	uint32_t nlive = nb;
+	auto rebuild = [&]() {
+		double sofar = 0.0f;
+		for(uint32_t k = 0; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
+	};
+	rebuild();
+	for(int k = 0; k < kHash; k++) w.hash[k] = 0;
+	uint32_t arenaTop = 0;
+	for(uint64_t k = 0; k < nsamples; k++) {
+		const double rd = rnd.nextFloat() * mass;
+		// the dart: first live range whose running mass exceeds it (else the last live one)
+		if(nlive == 0) return false;
+		uint32_t lo = 0, hi = nlive;
+		while(lo < hi) { const uint32_t mid = (lo + hi) >> 1; if(rd < w.pre[mid]) hi = mid; else lo = mid + 1; }
+		const uint32_t bi = w.live[lo < nlive ? lo : nlive - 1];
+		R1N& s = w.r1n[bi];
+		if(!s.inited) {
+			const uint16_t n = (uint16_t)big[bi].size;                         // uint16_t element type
+			if(n == 0) return false;
+			s.inited = 1; s.n = n; s.cur = 0; s.converted = 0; s.swaplist = n < 128 ? 1 : 0;
+			const uint16_t t = (uint16_t)(0.10f * (float)n);
+			s.thresh = t > 16 ? t : 16;
+		}
+		uint16_t rr;
+		if(!r1n_next(w, (int)bi, rnd, arenaTop, rr)) return false;
+		if(s.n > 0 && s.cur >= s.n) {                                          // done(): finishedRange
+			mass -= w.masses[bi];
+			uint32_t q = 0;
+			while(q < nlive && w.live[q] != bi) q++;
+			for(; q + 1 < nlive; q++) w.live[q] = w.live[q + 1];
+			nlive--;
+			rebuild();
+		}
+		emit(k, bi, rr);
+	}
+	return true;
 }
 
 } // namespace bt2x_round

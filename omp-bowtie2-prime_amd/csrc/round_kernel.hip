@@ -1,13 +1,19 @@
 // round_kernel.hip — the per-read part of a seed round on gfx950 (bt2x_seed_round):
-// after the seed kernel, one lane per read runs searchAllSeedsFinalize, rankSeedHits and
-// prioritizeSATups (round_core.h) and appends the read's extension list and the BW rows
-// to resolve to arenas allocated with atomics; sa_resolve_kernel_dn then places the rows.
+// after the seed kernel,
+//   round_prep_kernel    one lane per read: searchAllSeedsFinalize, rankSeedHits and
+//                        prioritizeSATups up to the sampling decision (round_core.h
+//                        prep()).  It reserves the read's whole extension list and row
+//                        range with atomics, writes the ranges it keeps whole, and queues
+//                        a sampling job (the larger ranges + RNG state) for reads that
+//                        draw elements;
+//   round_sample_kernel  one lane per queued job: RowSampler + Random1toN draws
+//                        (sample()), written into the reserved slots;
+// then sa_resolve_kernel_dn places every row.
 //
-// This is RNG-sequential, branchy integer work with a few hundred operations per read
-// (a few thousand for repetitive reads that sample up to maxelt elements): latency, not
-// bandwidth.  A persistent grid of lanes, each with a private workspace in HBM, walks the
-// reads; the kernel's value is that the host never touches these phases and the rows
-// never cross PCIe.
+// RNG-sequential, branchy integer work of a few hundred operations per read, latency
+// bound.  Splitting the sampling off matters: in one kernel, the ~10 % of reads that draw
+// up to maxelt elements held their whole wave for every read the wave processed; queued,
+// the sampling lanes of a wave carry similar loads.
 #include <hip/hip_runtime.h>
 #include "bt2x_device.h"
 #include "round_core.h"
@@ -16,58 +22,133 @@ namespace {
 
 using namespace bt2x_round;
 
+struct Job {                 // one read's sampling work
+	uint32_t read;           // index into in/out
+	uint32_t nb;             // larger ranges, ranges[range0 .. +nb)
+	uint32_t range0;
+	uint32_t sat_base, elt_base;
+	uint32_t rnd_last;
+	int32_t rnd_lastoff;
+	uint32_t nsamples;
+	uint32_t seedlen;
+	uint32_t pad;
+};
+
 __global__ void __launch_bounds__(64)
-round_kernel(RoundLaunch a) {
+round_prep_kernel(RoundLaunch a) {
 	const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-	Ws& w = *reinterpret_cast<Ws*>(a.ws + (size_t)lane * sizeof(Ws));
+	PrepWs& w = *reinterpret_cast<PrepWs*>(a.ws + (size_t)lane * sizeof(PrepWs));
+	Job* jobs = reinterpret_cast<Job*>(a.jobs);
+	Range* ranges = reinterpret_cast<Range*>(a.ranges);
 	for(uint32_t r = lane; r < a.n; r += gridDim.x * blockDim.x) {
 		const bt2x_round_in in = a.in[r];
 		Rnd rnd{in.rnd_last, in.rnd_lastoff};
-		const Result res = run(in, a.seeds + in.seed0, a.seed_out + in.seed0, a.exr + in.exr0, a.maxelt, rnd, w);
+		Prep p = prep(in, a.seeds + in.seed0, a.seed_out + in.seed0, a.exr + in.exr0, a.maxelt, rnd, w);
 		bt2x_round_out o;
 		o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
-		o.num_elts = res.numElts; o.nonz = res.nonz; o.status = res.status;
+		o.num_elts = p.numElts; o.nonz = p.nonz; o.status = p.status;
 		o.sat0 = o.nsat = o.elt0 = o.nelt = o.exr0 = o.nexr = 0;
-		if(res.status == BT2X_ROUND_OK) {
-			o.nsat = res.nsat; o.nelt = res.nelt; o.nexr = res.nexnew;
-			o.sat0 = atomicAdd(&a.counters[0], res.nsat);
-			o.elt0 = atomicAdd(&a.counters[1], res.nelt);
-			o.exr0 = res.nexnew ? atomicAdd(&a.counters[2], res.nexnew) : 0;
+		if(p.status == BT2X_ROUND_OK) {
 			const uint32_t L = in.seedlen;
-			if(o.sat0 + res.nsat <= a.sat_cap && o.elt0 + res.nelt <= a.row_cap) {
-				uint32_t e = o.elt0;
-				for(uint32_t i = 0; i < res.nsat; i++) {
-					const Range& rg = w.r2[w.satRange[i]];
-					bt2x_sat s;
-					s.rdoff = rg.rdoff; s.rand_n = w.satN[i]; s.fw = rg.fw; s.seedlen = (uint8_t)L;
-					a.sats[o.sat0 + i] = s;
-					for(uint32_t k = 0; k < w.satN[i]; k++) {
-						bt2x_resolve_in ri;
-						ri.row = rg.topf + w.satElt[i] + k;
-						ri.qlen = L;
-						ri.pad = 0;
-						a.rows[e++] = ri;
+			const uint32_t nsat = p.nsmallSat + (uint32_t)p.nsamples, nelt = (uint32_t)(p.smallElts + p.nsamples);
+			uint32_t job = 0xffffffffu, range0 = 0;
+			const uint32_t nb = p.n2 - p.nsmall;
+			if(p.nsamples) {
+				job = atomicAdd(&a.counters[3], 1u);
+				range0 = atomicAdd(&a.counters[4], nb);
+				if(job >= a.job_cap || range0 + nb > a.range_cap) {
+					p.status = BT2X_ROUND_REDO;                  // hand the read back to the host
+					if(job < a.job_cap) {                         // an empty job keeps the queue dense
+						Job j = {};
+						j.read = r; j.rnd_last = rnd.last; j.rnd_lastoff = rnd.lastOff;
+						jobs[job] = j;
 					}
 				}
 			}
-			if(o.exr0 + res.nexnew <= a.exr_cap)
-				for(uint32_t i = 0; i < res.nexnew; i++) a.exr_out[o.exr0 + i] = w.exnew[i];
+			if(p.status == BT2X_ROUND_OK) {
+				o.nsat = nsat; o.nelt = nelt; o.nexr = p.nexnew;
+				o.sat0 = atomicAdd(&a.counters[0], nsat);
+				o.elt0 = atomicAdd(&a.counters[1], nelt);
+				o.exr0 = p.nexnew ? atomicAdd(&a.counters[2], p.nexnew) : 0;
+				if(o.sat0 + nsat <= a.sat_cap && o.elt0 + nelt <= a.row_cap) {
+					uint32_t e = o.elt0;
+					for(uint32_t i = 0; i < p.nsmallSat; i++) {
+						const Range& rg = w.r2[i];
+						bt2x_sat s;
+						s.rdoff = rg.rdoff; s.rand_n = (uint16_t)rg.size; s.fw = rg.fw; s.seedlen = (uint8_t)L;
+						a.sats[o.sat0 + i] = s;
+						for(uint32_t k = 0; k < (uint32_t)rg.size; k++) {
+							bt2x_resolve_in ri;
+							ri.row = rg.topf + k; ri.qlen = L; ri.pad = 0;
+							a.rows[e++] = ri;
+						}
+					}
+				}
+				if(o.exr0 + p.nexnew <= a.exr_cap)
+					for(uint32_t i = 0; i < p.nexnew; i++) a.exr_out[o.exr0 + i] = w.exnew[i];
+				if(p.nsamples) {
+					for(uint32_t i = 0; i < nb; i++) ranges[range0 + i] = w.r2[p.nsmall + i];
+					Job j;
+					j.read = r; j.nb = nb; j.range0 = range0;
+					j.sat_base = o.sat0 + p.nsmallSat; j.elt_base = (uint32_t)(o.elt0 + p.smallElts);
+					j.rnd_last = rnd.last; j.rnd_lastoff = rnd.lastOff;
+					j.nsamples = (uint32_t)p.nsamples; j.seedlen = L; j.pad = 0;
+					jobs[job] = j;
+				}
+			} else {
+				o.status = p.status;
+			}
 		}
 		a.out[r] = o;
 	}
 }
 
+__global__ void __launch_bounds__(64)
+round_sample_kernel(RoundLaunch a) {
+	const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+	SampleWs& w = *reinterpret_cast<SampleWs*>(a.ws2 + (size_t)lane * sizeof(SampleWs));
+	const Job* jobs = reinterpret_cast<const Job*>(a.jobs);
+	const Range* ranges = reinterpret_cast<const Range*>(a.ranges);
+	const uint32_t njobs = min(a.counters[3], a.job_cap);
+	const bool fits = a.counters[0] <= a.sat_cap && a.counters[1] <= a.row_cap;
+	for(uint32_t q = lane; q < njobs; q += gridDim.x * blockDim.x) {
+		const Job j = jobs[q];
+		const Range* big = ranges + j.range0;
+		Rnd rnd{j.rnd_last, j.rnd_lastoff};
+		const bool ok = sample(big, j.nb, j.nsamples, rnd, w, [&](uint64_t k, uint32_t bi, uint16_t elt) {
+			if(!fits) return;
+			const Range& rg = big[bi];
+			bt2x_sat s;
+			s.rdoff = rg.rdoff; s.rand_n = 1; s.fw = rg.fw; s.seedlen = (uint8_t)j.seedlen;
+			a.sats[j.sat_base + k] = s;
+			bt2x_resolve_in ri;
+			ri.row = rg.topf + elt; ri.qlen = j.seedlen; ri.pad = 0;
+			a.rows[j.elt_base + k] = ri;
+		});
+		bt2x_round_out& o = a.out[j.read];
+		o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
+		if(!ok) o.status = BT2X_ROUND_REDO;
+	}
+}
+
 } // namespace
 
-size_t bt2x_round_ws_bytes() { return sizeof(Ws); }
+size_t bt2x_round_ws_bytes() { return sizeof(PrepWs); }
+size_t bt2x_round_ws2_bytes() { return sizeof(SampleWs); }
+size_t bt2x_round_job_bytes() { return sizeof(Job); }
+size_t bt2x_round_range_bytes() { return sizeof(Range); }
 
-// 2 one-wave workgroups per CU: the work per read is small, the workspace is not
-uint32_t bt2x_round_lanes(int ncu) { return (uint32_t)(ncu > 0 ? ncu : 256) * 2u * 64u; }
+// 4 one-wave workgroups per CU: small work per read, workspaces in HBM
+uint32_t bt2x_round_lanes(int ncu) { return (uint32_t)(ncu > 0 ? ncu : 256) * 4u * 64u; }
 
 int bt2x_launch_round(const RoundLaunch& a, void* stream) {
 	if(a.n == 0) return 0;
 	uint32_t blocks = a.nlanes / 64;
 	if(blocks > (a.n + 63) / 64) blocks = (a.n + 63) / 64;
-	hipLaunchKernelGGL(round_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+	hipLaunchKernelGGL(round_prep_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
+	uint32_t sblocks = a.nlanes / 64;
+	if(sblocks > (a.job_cap + 63) / 64) sblocks = (a.job_cap + 63) / 64;
+	if(sblocks < 1) sblocks = 1;
+	hipLaunchKernelGGL(round_sample_kernel, dim3(sblocks), dim3(64), 0, (hipStream_t)stream, a);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }

@@ -65,27 +65,44 @@ Got run_host(const Case& c, uint32_t maxelt) {
 	return g;
 }
 
-Got run_core(const Case& c, uint32_t maxelt, bt2x_round::Ws& w) {
+struct CoreWs { bt2x_round::PrepWs p; bt2x_round::SampleWs s; };
+
+// prep() then sample(), composed the way round_kernel.hip lays the read's output out
+Got run_core(const Case& c, uint32_t maxelt, CoreWs& w) {
 	Got g;
 	bt2x_round::Rnd rnd{c.in.rnd_last, c.in.rnd_lastoff};
-	const bt2x_round::Result res = bt2x_round::run(c.in, c.seeds.data(), c.so.data(), c.exr.data(), maxelt, rnd, w);
+	const bt2x_round::Prep p = bt2x_round::prep(c.in, c.seeds.data(), c.so.data(), c.exr.data(), maxelt, rnd, w.p);
 	std::memset(&g.out, 0, sizeof g.out);
-	g.out.status = res.status; g.out.nonz = res.nonz; g.out.num_elts = res.numElts;
-	g.out.rnd_last = rnd.last; g.out.rnd_lastoff = rnd.lastOff;
-	if(res.status == BT2X_ROUND_OK) {
-		for(uint32_t i = 0; i < bt2x_round::kMaxRanges && i + 1 < res.nsat; i++) {
-			if(w.r1n[i].inited && w.r1n[i].converted) g_converted++;
-			if(w.r1n[i].inited && (!w.r1n[i].swaplist || w.r1n[i].converted)) g_seenmode++;
-		}
-		for(uint32_t i = 0; i < res.nsat; i++) {
-			const bt2x_round::Range& rg = w.r2[w.satRange[i]];
+	g.out.status = p.status; g.out.nonz = p.nonz; g.out.num_elts = p.numElts;
+	if(p.status == BT2X_ROUND_OK) {
+		for(uint32_t i = 0; i < p.nsmallSat; i++) {
+			const bt2x_round::Range& rg = w.p.r2[i];
 			bt2x_sat s;
-			s.rdoff = rg.rdoff; s.rand_n = w.satN[i]; s.fw = rg.fw; s.seedlen = (uint8_t)c.in.seedlen;
+			s.rdoff = rg.rdoff; s.rand_n = (uint16_t)rg.size; s.fw = rg.fw; s.seedlen = (uint8_t)c.in.seedlen;
 			g.sats.push_back(s);
-			for(uint32_t k = 0; k < w.satN[i]; k++) g.rows.push_back(rg.topf + w.satElt[i] + k);
+			for(uint32_t k = 0; k < (uint32_t)rg.size; k++) g.rows.push_back(rg.topf + k);
 		}
-		g.exr.assign(w.exnew, w.exnew + res.nexnew);
+		if(p.nsamples) {
+			const bt2x_round::Range* big = w.p.r2 + p.nsmall;
+			const uint32_t nb = p.n2 - p.nsmall;
+			const size_t s0 = g.sats.size(), e0 = g.rows.size();
+			g.sats.resize(s0 + p.nsamples);
+			g.rows.resize(e0 + p.nsamples);
+			const bool ok = bt2x_round::sample(big, nb, p.nsamples, rnd, w.s, [&](uint64_t k, uint32_t bi, uint16_t elt) {
+				bt2x_sat s;
+				s.rdoff = big[bi].rdoff; s.rand_n = 1; s.fw = big[bi].fw; s.seedlen = (uint8_t)c.in.seedlen;
+				g.sats[s0 + k] = s;
+				g.rows[e0 + k] = big[bi].topf + elt;
+			});
+			if(!ok) g.out.status = BT2X_ROUND_REDO;
+			for(uint32_t i = 0; i < nb; i++) {
+				if(w.s.r1n[i].inited && w.s.r1n[i].converted) g_converted++;
+				if(w.s.r1n[i].inited && (!w.s.r1n[i].swaplist || w.s.r1n[i].converted)) g_seenmode++;
+			}
+		}
+		g.exr.assign(w.p.exnew, w.p.exnew + p.nexnew);
 	}
+	g.out.rnd_last = rnd.last; g.out.rnd_lastoff = rnd.lastOff;
 	return g;
 }
 
@@ -157,7 +174,7 @@ int main(int argc, char** argv) {
 	const uint32_t maxelts[] = {400, 1, 3, 7, 20, 60};
 	size_t bad = 0, n = 0, nsampled = 0;
 	if(!gpu) {
-		std::vector<bt2x_round::Ws> ws(1);
+		std::vector<CoreWs> ws(1);
 		for(uint32_t me : maxelts)
 			for(const Case& c : cases) {
 				const Got a = run_host(c, me), b = run_core(c, me, ws[0]);
