@@ -199,6 +199,9 @@ def run_aligner(args, base, fq, sam, gpu, dump=None):
     ru = [ln for ln in err.splitlines() if ln.startswith("BT2X_RUSAGE_ALIGN")]
     if ru:
         st["rusage_align"] = {k: float(v) for k, v in (t.split("=") for t in ru[-1].split()[1:])}
+    gl = [ln for ln in err.splitlines() if ln.startswith("BT2X_GPU")]
+    if gl:
+        st["gpu"] = {k: float(v) for k, v in (t.split("=") for t in gl[-1].split()[1:])}
     st["wall_incl_index_load"] = wall
     st["peak_rss_mib"] = peak
     st["summary"] = [ln.strip() for ln in err.splitlines() if "aligned" in ln or "overall" in ln]

@@ -150,7 +150,7 @@ struct bt2x_ctx {
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
 	// seed round: host-variant staging, and the round's own scratch (seed results, rows
 	// to resolve, per-lane workspace)
-	DevBuf b_rin, b_exr, b_rout, b_sats, b_elts, b_exro, b_used, b_sout, b_rows, b_ws, b_ws2, b_jobs, b_ranges, b_rcnt;
+	DevBuf b_rin, b_exr, b_rout, b_sats, b_elts, b_exro, b_used, b_sout, b_rows, b_ws, b_jobs, b_ranges, b_rcnt;
 	const uint32_t* d_resolve_n = nullptr;     // element count of the last round's resolve (HBM)
 	DevBuf scratch;
 	int ncu = 0;
@@ -165,7 +165,7 @@ bt2x_ctx::~bt2x_ctx() {
 	(void)hipSetDevice(device);
 	if(stream) (void)hipStreamSynchronize(stream);
 	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch,
-	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws, &b_ws2,
+	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws,
 	                 &b_jobs, &b_ranges, &b_rcnt})
 		b->release();
 	for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen, (void*)d_stats,
@@ -544,7 +544,7 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	const uint32_t job_cap = nreads ? nreads : 1, range_cap = 24 * job_cap;
 	if((rc = c->b_sout.ensure(sizeof(bt2x_seed_out) * (size_t)(nseeds ? nseeds : 1))) ||
 	   (rc = c->b_rows.ensure(sizeof(bt2x_resolve_in) * (size_t)(elt_cap ? elt_cap : 1))) ||
-	   (rc = c->b_ws.ensure(bt2x_round_ws_bytes() * lanes)) || (rc = c->b_ws2.ensure(bt2x_round_ws2_bytes() * lanes)) ||
+	   (rc = c->b_ws.ensure(bt2x_round_ws_bytes() * lanes)) ||
 	   (rc = c->b_jobs.ensure(bt2x_round_job_bytes() * job_cap)) ||
 	   (rc = c->b_ranges.ensure(bt2x_round_range_bytes() * range_cap)) ||
 	   (rc = c->b_rcnt.ensure(8 * sizeof(uint32_t)))) return rc;
@@ -568,7 +568,7 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	a.out = d_out; a.sats = d_sats; a.sat_cap = sat_cap;
 	a.rows = (bt2x_resolve_in*)c->b_rows.p; a.row_cap = elt_cap;
 	a.exr_out = d_exr_out; a.exr_cap = exr_cap;
-	a.counters = cnt; a.ws = (uint8_t*)c->b_ws.p; a.ws2 = (uint8_t*)c->b_ws2.p; a.nlanes = lanes;
+	a.counters = cnt; a.ws = (uint8_t*)c->b_ws.p; a.nlanes = lanes;
 	a.jobs = (uint8_t*)c->b_jobs.p; a.job_cap = job_cap; a.ranges = (uint8_t*)c->b_ranges.p; a.range_cap = range_cap;
 	if((rc = bt2x_launch_round(a, s))) return rc;
 	if((rc = bt2x_launch_resolve_dn(c->ix, a.rows, cnt + 1, elt_cap, 0, d_elts, c->d_stats + 8, c->ncu, s)))

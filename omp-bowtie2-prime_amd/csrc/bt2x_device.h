@@ -67,10 +67,9 @@ struct RoundLaunch {
 	                               // (used, may exceed caps)
 	uint8_t* jobs; uint32_t job_cap;
 	uint8_t* ranges; uint32_t range_cap;
-	uint8_t* ws; uint8_t* ws2; uint32_t nlanes;   // per-lane workspaces (prep, sample)
+	uint8_t* ws; uint32_t nlanes;  // per-lane workspace of the prep kernel
 };
 size_t bt2x_round_ws_bytes();
-size_t bt2x_round_ws2_bytes();
 size_t bt2x_round_job_bytes();
 size_t bt2x_round_range_bytes();
 uint32_t bt2x_round_lanes(int ncu);

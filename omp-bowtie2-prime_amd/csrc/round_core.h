@@ -75,13 +75,25 @@ struct PrepWs {
 	bt2x_exrange exnew[kMaxRanges];
 };
 
-// sample()'s per-lane workspace
+// sample()'s workspace (one per job; the kernel keeps it in LDS)
 struct SampleWs {
+	Range big[kMaxRanges];                    // the job's ranges
 	double masses[kMaxRanges], pre[kMaxRanges];
 	uint16_t live[kMaxRanges];
 	R1N r1n[kMaxRanges];
 	uint16_t arena[kArena];
 	uint32_t hash[kHash];
+};
+
+// How sample() spreads its list work over the lanes that run one job together.  All
+// lanes run the RNG-sequential loop in lockstep on the same values (wave-uniform); the
+// list fills, seen-set clears and the seen-to-swap conversion scan are lane-strided.
+struct SerialCoop {                           // one thread (host test, host builds)
+	__host__ __device__ uint32_t lane() const { return 0; }
+	__host__ __device__ uint32_t width() const { return 1; }
+	__host__ __device__ void sync() const {}
+	__host__ __device__ uint64_t ballot(bool p) const { return p ? 1u : 0u; }
+	__host__ __device__ bool leader() const { return true; }
 };
 
 struct Prep {
@@ -217,38 +229,51 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 __host__ __device__ inline bool seen_has(const SampleWs& w, uint32_t key) {       // key != 0
 	uint32_t h = (key * 2654435761u) >> 22;                                      // 10 bits
 	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1)) {
-		if(w.hash[h] == key) return true;
-		if(w.hash[h] == 0) return false;
+		const uint32_t v = w.hash[h];
+		if(v == key) return true;
+		if(v == 0) return false;
 	}
 	return false;
 }
 
-__host__ __device__ inline void seen_add(SampleWs& w, uint32_t key) {
+// false when the set is full
+__host__ __device__ inline bool seen_add(SampleWs& w, uint32_t key) {
 	uint32_t h = (key * 2654435761u) >> 22;
 	for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1))
-		if(w.hash[h] == 0 || w.hash[h] == key) { w.hash[h] = key; return; }
+		if(w.hash[h] == 0 || w.hash[h] == key) { w.hash[h] = key; return true; }
+	return false;
+}
+
+__host__ __device__ inline uint32_t popc64(uint64_t m) {
+#ifdef __HIP_DEVICE_COMPILE__
+	return (uint32_t)__popcll(m);
+#else
+	return (uint32_t)__builtin_popcountll(m);
+#endif
 }
 
 // Random1toN::next over range ri; false on workspace overflow.
-__host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t& arenaTop, uint16_t& out) {
+template<class C>
+__host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t& arenaTop, uint16_t& out,
+                                         const C& co) {
 	R1N& s = w.r1n[ri];
 	if(s.cur == 0 && !s.converted) {
 		if(s.n == 1) { s.cur = 1; out = 0; return true; }
 		if(s.swaplist) {
 			if(arenaTop + s.n > (uint32_t)kArena) return false;
-			s.list = (uint16_t)arenaTop;
+			const uint32_t list = arenaTop;
+			for(uint32_t i = co.lane(); i < s.n; i += co.width()) w.arena[list + i] = (uint16_t)i;
+			co.sync();
+			s.list = (uint16_t)list;
 			arenaTop += s.n;
-			for(uint32_t i = 0; i < s.n; i++) w.arena[s.list + i] = (uint16_t)i;
 		}
 	}
 	if(s.swaplist) {
 		const uint32_t r = s.cur + rnd.nextU32() % (uint32_t)(s.n - s.cur);
-		if(r != s.cur) {
-			const uint16_t t = w.arena[s.list + s.cur];
-			w.arena[s.list + s.cur] = w.arena[s.list + r];
-			w.arena[s.list + r] = t;
-		}
-		out = w.arena[s.list + s.cur];
+		const uint16_t a = w.arena[s.list + s.cur], b = w.arena[s.list + r];
+		w.arena[s.list + r] = a;                  // r == cur leaves it as it was
+		w.arena[s.list + s.cur] = b;
+		out = b;
 		s.cur++;
 		return true;
 	}
@@ -257,18 +282,24 @@ __host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t
 	do {
 		rn = (uint16_t)(rnd.nextU32() % (uint32_t)s.n);
 	} while(seen_has(w, ((uint32_t)ri << 16 | rn) + 1u));
-	seen_add(w, ((uint32_t)ri << 16 | rn) + 1u);
+	if(!seen_add(w, ((uint32_t)ri << 16 | rn) + 1u)) return false;
 	s.cur++;                                  // = seen_.size()
 	if(s.cur >= s.thresh && s.cur < s.n) {
 		// convert to a swap list of the unseen elements, ascending
 		const uint32_t nl = (uint32_t)s.n - s.cur;
 		if(arenaTop + nl > (uint32_t)kArena) return false;
-		const uint16_t base = (uint16_t)arenaTop;
+		const uint32_t base = arenaTop;
 		uint32_t k = 0;
-		for(uint32_t j = 0; j < s.n; j++)
-			if(!seen_has(w, ((uint32_t)ri << 16 | j) + 1u)) w.arena[base + k++] = (uint16_t)j;
+		for(uint32_t j0 = 0; j0 < s.n; j0 += co.width()) {
+			const uint32_t j = j0 + co.lane();
+			const bool un = j < s.n && !seen_has(w, ((uint32_t)ri << 16 | j) + 1u);
+			const uint64_t m = co.ballot(un);
+			if(un) w.arena[base + k + popc64(m & ((1ull << co.lane()) - 1ull))] = (uint16_t)j;
+			k += popc64(m);
+		}
+		co.sync();
 		arenaTop += nl;
-		s.list = base;
+		s.list = (uint16_t)base;
 		s.cur = 0;
 		s.n = (uint16_t)nl;
 		s.converted = 1;
@@ -278,31 +309,33 @@ __host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t
 	return true;
 }
 
-// RowSampler over big[0 .. nb) (lensq = szsq = true) and one Random1toN per range:
-// emit(k, bi, element) for each of the nsamples draws.  False on workspace overflow.
-template<class Emit>
-__host__ __device__ inline bool sample(const Range* big, uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w,
+// RowSampler over w.big[0 .. nb) (lensq = szsq = true) and one Random1toN per range:
+// emit(k, bi, element) for each of the nsamples draws (on the leader lane).  The caller
+// fills w.big; false on workspace overflow.
+template<class C, class Emit>
+__host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, const C& co,
                                        Emit&& emit) {
 	if(nb > (uint32_t)kMaxRanges) return false;
-	double mass = 0.0f;
-	for(uint32_t i = 0; i < nb; i++) {
-		double num = (double)(big[i].nlex + 1);
+	for(uint32_t k = co.lane(); k < (uint32_t)kHash; k += co.width()) w.hash[k] = 0;
+	for(uint32_t i = co.lane(); i < nb; i += co.width()) {
+		double num = (double)(w.big[i].nlex + 1);
 		num *= num;
-		double den = (double)big[i].size;
+		double den = (double)w.big[i].size;
 		den *= den;
 		w.masses[i] = num / den;
-		mass += w.masses[i];
 		w.live[i] = (uint16_t)i;
 		R1N& s = w.r1n[i];
 		s.inited = 0; s.n = 0; s.cur = 0; s.converted = 0; s.swaplist = 0;
 	}
+	co.sync();
+	double mass = 0.0f;
+	for(uint32_t i = 0; i < nb; i++) mass += w.masses[i];
 	uint32_t nlive = nb;
 	auto rebuild = [&]() {
 		double sofar = 0.0f;
 		for(uint32_t k = 0; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
 	};
 	rebuild();
-	for(int k = 0; k < kHash; k++) w.hash[k] = 0;
 	uint32_t arenaTop = 0;
 	for(uint64_t k = 0; k < nsamples; k++) {
 		const double rd = rnd.nextFloat() * mass;
@@ -313,14 +346,14 @@ __host__ __device__ inline bool sample(const Range* big, uint32_t nb, uint64_t n
 		const uint32_t bi = w.live[lo < nlive ? lo : nlive - 1];
 		R1N& s = w.r1n[bi];
 		if(!s.inited) {
-			const uint16_t n = (uint16_t)big[bi].size;                         // uint16_t element type
+			const uint16_t n = (uint16_t)w.big[bi].size;                       // uint16_t element type
 			if(n == 0) return false;
 			s.inited = 1; s.n = n; s.cur = 0; s.converted = 0; s.swaplist = n < 128 ? 1 : 0;
 			const uint16_t t = (uint16_t)(0.10f * (float)n);
 			s.thresh = t > 16 ? t : 16;
 		}
 		uint16_t rr;
-		if(!r1n_next(w, (int)bi, rnd, arenaTop, rr)) return false;
+		if(!r1n_next(w, (int)bi, rnd, arenaTop, rr, co)) return false;
 		if(s.n > 0 && s.cur >= s.n) {                                          // done(): finishedRange
 			mass -= w.masses[bi];
 			uint32_t q = 0;
@@ -329,7 +362,7 @@ __host__ __device__ inline bool sample(const Range* big, uint32_t nb, uint64_t n
 			nlive--;
 			rebuild();
 		}
-		emit(k, bi, rr);
+		if(co.leader()) emit(k, bi, rr);
 	}
 	return true;
 }

@@ -6,8 +6,8 @@
 //                        range with atomics, writes the ranges it keeps whole, and queues
 //                        a sampling job (the larger ranges + RNG state) for reads that
 //                        draw elements;
-//   round_sample_kernel  one lane per queued job: RowSampler + Random1toN draws
-//                        (sample()), written into the reserved slots;
+//   round_sample_kernel  one wave per queued job, workspace in LDS: RowSampler +
+//                        Random1toN draws (sample()), written into the reserved slots;
 // then sa_resolve_kernel_dn places every row.
 //
 // RNG-sequential, branchy integer work of a few hundred operations per read, latency
@@ -103,21 +103,39 @@ round_prep_kernel(RoundLaunch a) {
 	}
 }
 
+struct WaveCoop {                            // a one-wave workgroup runs one job
+	__device__ uint32_t lane() const { return threadIdx.x; }
+	__device__ uint32_t width() const { return 64; }
+	__device__ void sync() const { __syncthreads(); }
+	__device__ uint64_t ballot(bool p) const { return __ballot(p); }
+	__device__ bool leader() const { return threadIdx.x == 0; }
+};
+
+// One wave per job, its workspace in LDS: the sampling loop is a chain of dependent
+// list/mass lookups, so it runs at LDS latency instead of HBM latency.  Jobs are taken
+// from a queue counter (counters[5]) so long and short jobs balance over the grid.
 __global__ void __launch_bounds__(64)
 round_sample_kernel(RoundLaunch a) {
-	const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-	SampleWs& w = *reinterpret_cast<SampleWs*>(a.ws2 + (size_t)lane * sizeof(SampleWs));
+	__shared__ SampleWs w;
+	__shared__ uint32_t qsh;
+	const WaveCoop co;
 	const Job* jobs = reinterpret_cast<const Job*>(a.jobs);
 	const Range* ranges = reinterpret_cast<const Range*>(a.ranges);
 	const uint32_t njobs = min(a.counters[3], a.job_cap);
 	const bool fits = a.counters[0] <= a.sat_cap && a.counters[1] <= a.row_cap;
-	for(uint32_t q = lane; q < njobs; q += gridDim.x * blockDim.x) {
+	for(;;) {
+		if(threadIdx.x == 0) qsh = atomicAdd(&a.counters[5], 1u);
+		__syncthreads();
+		const uint32_t q = qsh;
+		__syncthreads();
+		if(q >= njobs) break;
 		const Job j = jobs[q];
-		const Range* big = ranges + j.range0;
+		for(uint32_t i = threadIdx.x; i < j.nb && i < (uint32_t)kMaxRanges; i += 64) w.big[i] = ranges[j.range0 + i];
+		__syncthreads();
 		Rnd rnd{j.rnd_last, j.rnd_lastoff};
-		const bool ok = sample(big, j.nb, j.nsamples, rnd, w, [&](uint64_t k, uint32_t bi, uint16_t elt) {
+		const bool ok = sample(j.nb, j.nsamples, rnd, w, co, [&](uint64_t k, uint32_t bi, uint16_t elt) {
 			if(!fits) return;
-			const Range& rg = big[bi];
+			const Range& rg = w.big[bi];
 			bt2x_sat s;
 			s.rdoff = rg.rdoff; s.rand_n = 1; s.fw = rg.fw; s.seedlen = (uint8_t)j.seedlen;
 			a.sats[j.sat_base + k] = s;
@@ -125,16 +143,18 @@ round_sample_kernel(RoundLaunch a) {
 			ri.row = rg.topf + elt; ri.qlen = j.seedlen; ri.pad = 0;
 			a.rows[j.elt_base + k] = ri;
 		});
-		bt2x_round_out& o = a.out[j.read];
-		o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
-		if(!ok) o.status = BT2X_ROUND_REDO;
+		if(threadIdx.x == 0) {
+			bt2x_round_out& o = a.out[j.read];
+			o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
+			if(!ok) o.status = BT2X_ROUND_REDO;
+		}
+		__syncthreads();
 	}
 }
 
 } // namespace
 
 size_t bt2x_round_ws_bytes() { return sizeof(PrepWs); }
-size_t bt2x_round_ws2_bytes() { return sizeof(SampleWs); }
 size_t bt2x_round_job_bytes() { return sizeof(Job); }
 size_t bt2x_round_range_bytes() { return sizeof(Range); }
 
@@ -146,8 +166,9 @@ int bt2x_launch_round(const RoundLaunch& a, void* stream) {
 	uint32_t blocks = a.nlanes / 64;
 	if(blocks > (a.n + 63) / 64) blocks = (a.n + 63) / 64;
 	hipLaunchKernelGGL(round_prep_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, a);
-	uint32_t sblocks = a.nlanes / 64;
-	if(sblocks > (a.job_cap + 63) / 64) sblocks = (a.job_cap + 63) / 64;
+	// persistent: 6 one-wave groups per CU (LDS: ~20 KiB each), jobs from the queue
+	uint32_t sblocks = a.nlanes / 64 / 4 * 6;
+	if(sblocks > a.job_cap) sblocks = a.job_cap;
 	if(sblocks < 1) sblocks = 1;
 	hipLaunchKernelGGL(round_sample_kernel, dim3(sblocks), dim3(64), 0, (hipStream_t)stream, a);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;

@@ -41,6 +41,7 @@ public:
 	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
 	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
 	                std::vector<bt2x_exrange>& exr_out) override {
+		const auto t0 = std::chrono::steady_clock::now();
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
 		// arenas sized from the last launch's use per read (grown and retried on overflow)
@@ -63,11 +64,18 @@ public:
 			sat_per_read_ = std::max(8.0, 1.25 * used[0] / n);
 			elt_per_read_ = std::max(16.0, 1.25 * used[1] / n);
 		}
+		gs.k_round_ms += std::max(0.0, bt2x_last_kernel_ms(ctx_, BT2X_K_ROUND));
+		gs.round_h2d += reads.size() + seeds.size() * sizeof(bt2x_seed_in) + n * sizeof(bt2x_round_in) +
+		                exr.size() * sizeof(bt2x_exrange);
+		gs.round_d2h += n * sizeof(bt2x_round_out) + sats.size() * sizeof(bt2x_sat) +
+		                elts.size() * sizeof(bt2x_resolve_out) + exr_out.size() * sizeof(bt2x_exrange);
+		gs.t_round_call += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 	}
 	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
 	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
 	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
 	              std::vector<uint32_t>& edits) override {
+		const auto t0 = std::chrono::steady_clock::now();
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
 		uint32_t rec_cap = 4 * n + 64, edit_cap = 48 * n + 256;
@@ -82,9 +90,17 @@ public:
 			bt2x::check(rc, "bt2x_dp_align");
 			recs.resize(nrec);
 			edits.resize(ned);
+			gs.k_dp_ms += std::max(0.0, bt2x_last_kernel_ms(ctx_, BT2X_K_DP));
+			gs.dp_h2d += reads.size() + quals.size() + refs.size() + n * sizeof(bt2x_dp_in);
+			gs.dp_d2h += n * sizeof(bt2x_dp_out) + nrec * sizeof(bt2x_aln_rec) + ned * sizeof(uint32_t);
+			gs.t_dp_call += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 			return;
 		}
 	}
+	struct GpuStats {                      // kernel time and bytes over PCIe, per request kind
+		double k_round_ms = 0, k_dp_ms = 0, t_round_call = 0, t_dp_call = 0;
+		uint64_t round_h2d = 0, round_d2h = 0, dp_h2d = 0, dp_d2h = 0;
+	} gs;
 private:
 	bt2x_ctx* ctx_;
 	double sat_per_read_ = 16, elt_per_read_ = 64;
@@ -233,6 +249,13 @@ int main(int argc, char** argv) {
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io, (unsigned long long)st.dps_used,
 			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait, st.t_gather, st.t_retire,
 			             (unsigned long long)st.round_launches, (unsigned long long)st.rounds, st.t_round);
+		if(stats) {
+			const HipBackend::GpuStats& g = hip.gs;
+			std::fprintf(stderr, "BT2X_GPU k_round=%.4f t_round_call=%.4f round_h2d_mib=%.1f round_d2h_mib=%.1f "
+			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f\n", g.k_round_ms * 1e-3, g.t_round_call,
+			             g.round_h2d / 1048576.0, g.round_d2h / 1048576.0, g.k_dp_ms * 1e-3, g.t_dp_call,
+			             g.dp_h2d / 1048576.0, g.dp_d2h / 1048576.0);
+		}
 	} catch(const std::exception& e) {
 		std::fprintf(stderr, "bt2x-align: %s\n", e.what());
 		return 1;
