@@ -395,6 +395,13 @@ int bt2x_seed_round_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const bt2x_seed_i
                         bt2x_resolve_out* d_elts, uint32_t elt_cap, bt2x_exrange* d_exr_out, uint32_t exr_cap,
                         uint32_t* d_used, void* stream);
 
+/* Page-locked host memory for the buffers a caller hands to the host-pointer entry points
+ * (their copies then run as DMA at the link's rate instead of staging through pageable
+ * memory).  NULL on failure; bt2x_host_free(NULL) is a no-op.  Not needed for
+ * correctness: every entry point accepts ordinary memory. */
+void* bt2x_host_alloc(size_t bytes);
+void  bt2x_host_free(void* p);
+
 const char* bt2x_version(void);
 /* sizeof of the ABI structs (seed_in, seed_out, dp_in, dp_out, aln_rec, scoring,
  * index_desc, counters), for binding self-checks; returns the count. */

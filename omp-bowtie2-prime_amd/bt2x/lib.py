@@ -59,6 +59,8 @@ FUNCS = {
                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                            ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
+    "bt2x_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
+    "bt2x_host_free": (None, [ctypes.c_void_p]),
     "bt2x_suffix_array": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
     "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
     "bt2x_build_index_sa": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,

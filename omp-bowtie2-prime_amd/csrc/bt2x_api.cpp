@@ -117,6 +117,16 @@ extern "C" void bt2x_scoring_default(bt2x_scoring* sc) {
 	bt2x_scoring_init(sc);
 }
 
+extern "C" void* bt2x_host_alloc(size_t bytes) {
+	void* p = nullptr;
+	if(hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+	return p;
+}
+
+extern "C" void bt2x_host_free(void* p) {
+	if(p) (void)hipHostFree(p);
+}
+
 extern "C" const char* bt2x_version(void) { return "bt2x 0.1 (gfx950; abi 1)"; }
 
 // -------------------------------------------------------------------- context

@@ -5,6 +5,7 @@
 // that must round exactly like the reference's x86-64 build.
 #include "bt2x_align.hpp"
 
+#include <atomic>
 #include <cctype>
 #include <charconv>
 #include <chrono>
@@ -62,6 +63,35 @@ void tune_malloc() {
 	mallopt(M_TRIM_THRESHOLD, INT_MAX);
 	mallopt(M_TOP_PAD, 64 << 20);
 	mallopt(M_MMAP_THRESHOLD, 32 << 20);
+}
+
+namespace {
+struct HostHooks { void* (*alloc)(size_t); void (*release)(void*); };
+void* plain_alloc(size_t n) { return std::malloc(n); }
+void plain_free(void* p) { std::free(p); }
+std::atomic<const HostHooks*> g_hooks{nullptr};
+const HostHooks kPlain{plain_alloc, plain_free};
+constexpr size_t kHostHdr = 64;               // keeps the payload 64-byte aligned
+}
+
+void set_host_allocator(void* (*alloc)(size_t), void (*release)(void*)) {
+	// hooks live for the process; a block is freed by the hook that allocated it
+	g_hooks.store(alloc ? new HostHooks{alloc, release} : &kPlain);
+}
+
+void* host_alloc(size_t bytes) {
+	const HostHooks* h = g_hooks.load();
+	if(!h) h = &kPlain;
+	uint8_t* p = static_cast<uint8_t*>(h->alloc(bytes + kHostHdr));
+	if(!p) throw std::bad_alloc();
+	*reinterpret_cast<const HostHooks**>(p) = h;
+	return p + kHostHdr;
+}
+
+void host_free(void* q) noexcept {
+	if(!q) return;
+	uint8_t* p = static_cast<uint8_t*>(q) - kHostHdr;
+	(*reinterpret_cast<const HostHooks**>(p))->release(p);
 }
 
 const uint8_t kAsc2Dna[256] = {   // alphabet.cpp:142 (A/C/G/T, either case; all else N)

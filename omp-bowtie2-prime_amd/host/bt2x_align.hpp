@@ -58,6 +58,32 @@
 #include "bt2x_shims.hpp"
 #include "work_pool.hpp"
 
+namespace bt2x { namespace host {
+
+// Host buffers that cross PCIe (the launch buffers handed to a Backend) come from a
+// hook, so the GPU backend can supply page-locked memory that the DMA engines read and
+// write directly (pageable copies stage through the driver at a fraction of the link's
+// rate).  Resizing such a buffer default-initialises, so a launch does not zero what
+// the gather or the GPU overwrites anyway.
+void set_host_allocator(void* (*alloc)(size_t), void (*release)(void*));
+void* host_alloc(size_t bytes);               // remembers which hook allocated it
+void host_free(void* p) noexcept;
+
+template<class T> struct HostAlloc {
+	using value_type = T;
+	HostAlloc() = default;
+	template<class U> HostAlloc(const HostAlloc<U>&) noexcept {}
+	T* allocate(size_t n) { return static_cast<T*>(host_alloc(n * sizeof(T))); }
+	void deallocate(T* p, size_t) noexcept { host_free(p); }
+	template<class U> void construct(U* p) noexcept { ::new((void*)p) U; }
+	template<class U, class... A> void construct(U* p, A&&... a) { ::new((void*)p) U(std::forward<A>(a)...); }
+	template<class U> bool operator==(const HostAlloc<U>&) const noexcept { return true; }
+	template<class U> bool operator!=(const HostAlloc<U>&) const noexcept { return false; }
+};
+template<class T> using HostVec = std::vector<T, HostAlloc<T>>;
+
+}} // namespace bt2x::host
+
 namespace bt2x {
 namespace host {
 
@@ -816,18 +842,18 @@ class Backend {
 public:
 	virtual ~Backend() {}
 	// reads: concatenated oriented reads; in[i].read_off indexes it
-	virtual void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
-	                         std::vector<bt2x_seed_out>& out) = 0;
-	virtual void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) = 0;
-	virtual void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
-	                      const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
-	                      std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
-	                      std::vector<uint32_t>& edits) = 0;
+	virtual void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
+	                         HostVec<bt2x_seed_out>& out) = 0;
+	virtual void resolve(const HostVec<bt2x_resolve_in>& in, HostVec<bt2x_resolve_out>& out) = 0;
+	virtual void dp_align(const HostVec<uint8_t>& reads, const HostVec<uint8_t>& quals,
+	                      const HostVec<uint8_t>& refs, const HostVec<bt2x_dp_in>& in,
+	                      HostVec<bt2x_dp_out>& out, HostVec<bt2x_aln_rec>& recs,
+	                      HostVec<uint32_t>& edits) = 0;
 	// bt2x_seed_round (include/bt2x.h)
-	virtual void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
-	                        const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr,
-	                        uint32_t maxelt, std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats,
-	                        std::vector<bt2x_resolve_out>& elts, std::vector<bt2x_exrange>& exr_out) = 0;
+	virtual void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
+	                        const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr,
+	                        uint32_t maxelt, HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats,
+	                        HostVec<bt2x_resolve_out>& elts, HostVec<bt2x_exrange>& exr_out) = 0;
 };
 
 // -------------------------------------------------------------------- driver
@@ -865,22 +891,22 @@ private:
 		std::vector<ReadCtx*> ws, wr, wd, wn, run;      // reads waiting on each kind (wn: rounds)
 		std::vector<uint64_t> sr, sk, rk, qb, pb, fb;  // per-read offsets into the buffers
 		std::vector<uint64_t> nr, nk, ne;               // rounds: read bytes, seeds, exRange entries
-		std::vector<uint8_t> seed_reads, dp_reads, dp_quals, dp_refs;
-		std::vector<bt2x_seed_in> seed_in;
-		std::vector<bt2x_seed_out> seed_out;
-		std::vector<bt2x_resolve_in> res_in;
-		std::vector<bt2x_resolve_out> res_out;
-		std::vector<bt2x_dp_in> dp_in;
-		std::vector<bt2x_dp_out> dp_out;
-		std::vector<bt2x_aln_rec> recs;
-		std::vector<uint32_t> edits;
-		std::vector<uint8_t> round_reads;
-		std::vector<bt2x_seed_in> round_seeds;
-		std::vector<bt2x_round_in> round_in;
-		std::vector<bt2x_exrange> round_exr, round_exr_out;
-		std::vector<bt2x_round_out> round_out;
-		std::vector<bt2x_sat> round_sats;
-		std::vector<bt2x_resolve_out> round_elts;
+		HostVec<uint8_t> seed_reads, dp_reads, dp_quals, dp_refs;
+		HostVec<bt2x_seed_in> seed_in;
+		HostVec<bt2x_seed_out> seed_out;
+		HostVec<bt2x_resolve_in> res_in;
+		HostVec<bt2x_resolve_out> res_out;
+		HostVec<bt2x_dp_in> dp_in;
+		HostVec<bt2x_dp_out> dp_out;
+		HostVec<bt2x_aln_rec> recs;
+		HostVec<uint32_t> edits;
+		HostVec<uint8_t> round_reads;
+		HostVec<bt2x_seed_in> round_seeds;
+		HostVec<bt2x_round_in> round_in;
+		HostVec<bt2x_exrange> round_exr, round_exr_out;
+		HostVec<bt2x_round_out> round_out;
+		HostVec<bt2x_sat> round_sats;
+		HostVec<bt2x_resolve_out> round_elts;
 		double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_gather = 0;
 		// gather's per-chunk lists, sizes and bases
 		struct Chunk {

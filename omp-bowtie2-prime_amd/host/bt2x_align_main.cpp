@@ -27,20 +27,20 @@ namespace {
 class HipBackend : public Backend {
 public:
 	explicit HipBackend(bt2x_ctx* ctx) : ctx_(ctx) {}
-	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
-	                 std::vector<bt2x_seed_out>& out) override {
+	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
+	                 HostVec<bt2x_seed_out>& out) override {
 		out.resize(in.size());
 		bt2x::check(bt2x_seed_search(ctx_, reads.data(), reads.size(), in.data(), (uint32_t)in.size(), 1,
 		                             out.data()), "bt2x_seed_search");
 	}
-	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+	void resolve(const HostVec<bt2x_resolve_in>& in, HostVec<bt2x_resolve_out>& out) override {
 		out.resize(in.size());
 		bt2x::check(bt2x_resolve(ctx_, in.data(), (uint32_t)in.size(), 0, out.data()), "bt2x_resolve");
 	}
-	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
-	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
-	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
-	                std::vector<bt2x_exrange>& exr_out) override {
+	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
+	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_exrange>& exr_out) override {
 		const auto t0 = std::chrono::steady_clock::now();
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
@@ -71,10 +71,10 @@ public:
 		                elts.size() * sizeof(bt2x_resolve_out) + exr_out.size() * sizeof(bt2x_exrange);
 		gs.t_round_call += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 	}
-	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
-	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
-	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
-	              std::vector<uint32_t>& edits) override {
+	void dp_align(const HostVec<uint8_t>& reads, const HostVec<uint8_t>& quals,
+	              const HostVec<uint8_t>& refs, const HostVec<bt2x_dp_in>& in,
+	              HostVec<bt2x_dp_out>& out, HostVec<bt2x_aln_rec>& recs,
+	              HostVec<uint32_t>& edits) override {
 		const auto t0 = std::chrono::steady_clock::now();
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
@@ -111,29 +111,29 @@ private:
 class DumpBackend : public Backend {
 public:
 	DumpBackend(Backend& inner, const std::string& dir) : in_(inner), dir_(dir) {}
-	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
-	                 std::vector<bt2x_seed_out>& out) override {
+	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
+	                 HostVec<bt2x_seed_out>& out) override {
 		write("seed", {{reads.data(), reads.size()}, {in.data(), in.size() * sizeof(bt2x_seed_in)}});
 		in_.seed_search(reads, in, out);
 	}
-	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+	void resolve(const HostVec<bt2x_resolve_in>& in, HostVec<bt2x_resolve_out>& out) override {
 		write("resolve", {{in.data(), in.size() * sizeof(bt2x_resolve_in)}});
 		in_.resolve(in, out);
 	}
-	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
-	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
-	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
-	                std::vector<bt2x_exrange>& exr_out) override {
+	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
+	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_exrange>& exr_out) override {
 		in_.seed_round(reads, seeds, in, exr, maxelt, out, sats, elts, exr_out);
 		const uint64_t meta[4] = {maxelt, sats.size(), elts.size(), exr_out.size()};   // arena sizes the replay needs
 		write("round", {{reads.data(), reads.size()}, {seeds.data(), seeds.size() * sizeof(bt2x_seed_in)},
 		                {in.data(), in.size() * sizeof(bt2x_round_in)}, {exr.data(), exr.size() * sizeof(bt2x_exrange)},
 		                {meta, sizeof meta}});
 	}
-	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
-	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
-	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
-	              std::vector<uint32_t>& edits) override {
+	void dp_align(const HostVec<uint8_t>& reads, const HostVec<uint8_t>& quals,
+	              const HostVec<uint8_t>& refs, const HostVec<bt2x_dp_in>& in,
+	              HostVec<bt2x_dp_out>& out, HostVec<bt2x_aln_rec>& recs,
+	              HostVec<uint32_t>& edits) override {
 		in_.dp_align(reads, quals, refs, in, out, recs, edits);
 		const uint64_t used[2] = {recs.size(), edits.size()};      // arena sizes the replay needs
 		write("dp", {{reads.data(), reads.size()}, {quals.data(), quals.size()}, {refs.data(), refs.size()},
@@ -200,6 +200,7 @@ int main(int argc, char** argv) {
 		ref.init(index.desc(), idx);
 		bt2x::Device dev(device, index, p.sc);
 		HipBackend hip(dev.ctx());
+		set_host_allocator(bt2x_host_alloc, bt2x_host_free);     // launch buffers page-locked
 		std::unique_ptr<DumpBackend> dumper;
 		if(!dump.empty()) dumper.reset(new DumpBackend(hip, dump));
 		Backend& be = dumper ? static_cast<Backend&>(*dumper) : static_cast<Backend&>(hip);

@@ -24,21 +24,21 @@ namespace {
 class OracleBackend : public Backend {
 public:
 	OracleBackend(const bt2x_index_desc& idx, const bt2x_scoring& sc) : idx_(idx), sc_(sc) {}
-	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
-	                 std::vector<bt2x_seed_out>& out) override {
+	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
+	                 HostVec<bt2x_seed_out>& out) override {
 		out.resize(in.size());
 		if(bt2o_seed_search(&idx_, reads.data(), in.data(), (uint32_t)in.size(), 1, out.data(), nullptr) != 0)
 			throw std::runtime_error("oracle seed search");
 	}
-	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+	void resolve(const HostVec<bt2x_resolve_in>& in, HostVec<bt2x_resolve_out>& out) override {
 		out.resize(in.size());
 		if(bt2o_resolve(&idx_, in.data(), (uint32_t)in.size(), 0, out.data(), nullptr) != 0)
 			throw std::runtime_error("oracle resolve");
 	}
-	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
-	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
-	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
-	              std::vector<uint32_t>& edits) override {
+	void dp_align(const HostVec<uint8_t>& reads, const HostVec<uint8_t>& quals,
+	              const HostVec<uint8_t>& refs, const HostVec<bt2x_dp_in>& in,
+	              HostVec<bt2x_dp_out>& out, HostVec<bt2x_aln_rec>& recs,
+	              HostVec<uint32_t>& edits) override {
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
 		uint32_t rec_cap = 4 * n + 64, edit_cap = 48 * n + 256;
@@ -55,26 +55,29 @@ public:
 	}
 	// the oracle seed search, then the host restatement of the round (host_round), then
 	// the oracle SA resolution: the contract of bt2x_seed_round on the CPU
-	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
-	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
-	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
-	                std::vector<bt2x_exrange>& exr_out) override {
-		std::vector<bt2x_seed_out> so;
+	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
+	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_exrange>& exr_out) override {
+		HostVec<bt2x_seed_out> so;
 		seed_search(reads, seeds, so);
 		out.resize(in.size());
-		sats.clear(); exr_out.clear();
+		std::vector<bt2x_sat> sv;
+		std::vector<bt2x_exrange> xv;
 		std::vector<bt2x_resolve_in> rows;
 		RoundScratch w;
 		for(size_t r = 0; r < in.size(); r++) {
 			const bt2x_round_in& q = in[r];
 			Rng rnd;
 			rnd.last = q.rnd_last; rnd.lastOff = q.rnd_lastoff;
-			const uint32_t s0 = (uint32_t)sats.size(), e0 = (uint32_t)rows.size(), x0 = (uint32_t)exr_out.size();
+			const uint32_t s0 = (uint32_t)sv.size(), e0 = (uint32_t)rows.size(), x0 = (uint32_t)xv.size();
 			host_round(q, seeds.data() + q.seed0, so.data() + q.seed0, exr.data() + q.exr0, maxelt, rnd, w, out[r],
-			           sats, rows, exr_out);
+			           sv, rows, xv);
 			out[r].sat0 = s0; out[r].elt0 = e0; out[r].exr0 = x0;
 		}
-		resolve(rows, elts);
+		sats.assign(sv.begin(), sv.end());
+		exr_out.assign(xv.begin(), xv.end());
+		resolve(HostVec<bt2x_resolve_in>(rows.begin(), rows.end()), elts);
 	}
 private:
 	const bt2x_index_desc& idx_;
@@ -87,24 +90,24 @@ class ReplayBackend : public Backend {
 public:
 	explicit ReplayBackend(Backend* rec) : rec_(rec) {}
 	void rewind() { rec_ = nullptr; k_ = kr_ = kd_ = kn_ = 0; }
-	void seed_search(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& in,
-	                 std::vector<bt2x_seed_out>& out) override {
+	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
+	                 HostVec<bt2x_seed_out>& out) override {
 		if(rec_) { rec_->seed_search(reads, in, out); seeds_.push_back(out); } else out = seeds_[k_++];
 	}
-	void resolve(const std::vector<bt2x_resolve_in>& in, std::vector<bt2x_resolve_out>& out) override {
+	void resolve(const HostVec<bt2x_resolve_in>& in, HostVec<bt2x_resolve_out>& out) override {
 		if(rec_) { rec_->resolve(in, out); res_.push_back(out); } else out = res_[kr_++];
 	}
-	void dp_align(const std::vector<uint8_t>& reads, const std::vector<uint8_t>& quals,
-	              const std::vector<uint8_t>& refs, const std::vector<bt2x_dp_in>& in,
-	              std::vector<bt2x_dp_out>& out, std::vector<bt2x_aln_rec>& recs,
-	              std::vector<uint32_t>& edits) override {
+	void dp_align(const HostVec<uint8_t>& reads, const HostVec<uint8_t>& quals,
+	              const HostVec<uint8_t>& refs, const HostVec<bt2x_dp_in>& in,
+	              HostVec<bt2x_dp_out>& out, HostVec<bt2x_aln_rec>& recs,
+	              HostVec<uint32_t>& edits) override {
 		if(rec_) { rec_->dp_align(reads, quals, refs, in, out, recs, edits); dp_.push_back({out, recs, edits}); }
 		else { const auto& d = dp_[kd_++]; out = d.out; recs = d.recs; edits = d.edits; }
 	}
-	void seed_round(const std::vector<uint8_t>& reads, const std::vector<bt2x_seed_in>& seeds,
-	                const std::vector<bt2x_round_in>& in, const std::vector<bt2x_exrange>& exr, uint32_t maxelt,
-	                std::vector<bt2x_round_out>& out, std::vector<bt2x_sat>& sats, std::vector<bt2x_resolve_out>& elts,
-	                std::vector<bt2x_exrange>& exr_out) override {
+	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
+	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_exrange>& exr_out) override {
 		if(rec_) {
 			rec_->seed_round(reads, seeds, in, exr, maxelt, out, sats, elts, exr_out);
 			rounds_.push_back({out, sats, elts, exr_out});
@@ -114,15 +117,15 @@ public:
 		}
 	}
 private:
-	struct Round { std::vector<bt2x_round_out> out; std::vector<bt2x_sat> sats; std::vector<bt2x_resolve_out> elts;
-	               std::vector<bt2x_exrange> exr; };
+	struct Round { HostVec<bt2x_round_out> out; HostVec<bt2x_sat> sats; HostVec<bt2x_resolve_out> elts;
+	               HostVec<bt2x_exrange> exr; };
 	std::vector<Round> rounds_;
 	size_t kn_ = 0;
-	struct Dp { std::vector<bt2x_dp_out> out; std::vector<bt2x_aln_rec> recs; std::vector<uint32_t> edits; };
+	struct Dp { HostVec<bt2x_dp_out> out; HostVec<bt2x_aln_rec> recs; HostVec<uint32_t> edits; };
 	Backend* rec_;
 	size_t k_ = 0, kr_ = 0, kd_ = 0;
-	std::vector<std::vector<bt2x_seed_out>> seeds_;
-	std::vector<std::vector<bt2x_resolve_out>> res_;
+	std::vector<HostVec<bt2x_seed_out>> seeds_;
+	std::vector<HostVec<bt2x_resolve_out>> res_;
 	std::vector<Dp> dp_;
 };
 }
