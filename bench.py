@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
                     help="OpenMP threads of the reference CPU baseline (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prep-only", action="store_true",
+                    help="write the genome index and reads, print their paths, exit (profiling the aligner)")
     ap.add_argument("--lookahead", type=int, default=16, help="bt2x-align --lookahead (DP problems posed per request)")
     ap.add_argument("--slots", type=int, default=1 << 17,
                     help="bt2x-align --slots (reads in flight) of the end-to-end run; the launch-recording run "
@@ -311,6 +313,9 @@ def main():
     write_fastq(fq, reads, quals)
     del reads, quals
     mark(f"{n} reads written to {fq}")
+    if args.prep_only:
+        print(f"BT2X_DATA {base} {fq}", flush=True)
+        return
 
     # ---- 1. the aligner: launch recording run, then the end-to-end timing run
     ddir = os.path.join(rdir, "dump")

@@ -302,6 +302,260 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 	}
 }
 
+// ------------------------------------------------------- wave-per-problem mode
+// The aligner's DP rounds end in a tail of small launches (the few reads that need many
+// rounds): there one lane per problem leaves the chip idle and a launch still costs the
+// R x C serial cell updates of one lane, ~1.5-6 ms.  This mode gives each problem a whole
+// wave.  Lane l owns rows 4l .. 4l+3 and the wave sweeps anti-diagonals: at time t lane l
+// computes column t - l, taking the H and F of the row above from lane l-1 (one DPP
+// wave_shr), so a problem takes C + R/4 steps.  Values and flags are the lane kernel's
+// (same recurrence and traceback byte); the traceback bytes stay in LDS, column-major with
+// a lane's 4 rows in one dword, and the walk (lane 0) reads and marks them at LDS latency.
+constexpr int kWaveTbWords = kCols * kRows / 4;              // 8000 dwords = 31.25 KiB
+constexpr size_t kWaveRecStageBytes = (size_t)kRecStage * sizeof(bt2x_aln_rec);
+
+__device__ __forceinline__ uint32_t subs(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
+
+__global__ void __launch_bounds__(64)
+dp_wave_kernel(DevScoring sc, DpLaunch a) {
+	__shared__ uint32_t tbw[kWaveTbWords];
+	__shared__ uint8_t refw[kCols], lastrow[kCols], cands[kCols];
+	__shared__ uint32_t stage_ed[kEditStage];
+	uint8_t* tbb = reinterpret_cast<uint8_t*>(tbw);
+	const int lane = threadIdx.x;
+	bt2x_aln_rec* stage_rec = reinterpret_cast<bt2x_aln_rec*>(a.scratch + (size_t)blockIdx.x * kWaveRecStageBytes);
+	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0;
+	const uint32_t rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
+	for(uint32_t pi = blockIdx.x; pi < a.n; pi += gridDim.x) {
+		const bt2x_dp_in p = a.in[pi];
+		const int R = p.rdlen, C = p.ncol;
+		const uint8_t* rd = a.reads + p.read_off;
+		const uint8_t* qu = a.quals + p.qual_off;
+		const uint8_t* rf = a.refs + p.ref_off;
+		const int L = (R + 3) >> 2;                 // lanes holding rows
+		const int S = 4 * L;                        // bytes per traceback column
+		for(int j = lane; j < C; j += 64) refw[j] = rf[j];
+		// this lane's rows: read code (7 = N), mismatch penalty, gap-barred open/extend
+		uint32_t rc[4], mm[4], rdoe[4], rfoe[4], rfee[4];
+#pragma unroll
+		for(int r = 0; r < 4; r++) {
+			const int i = 4 * lane + r;
+			uint32_t c = 7, m = npen;
+			bool gbar = true;
+			if(i < R) {
+				int q = (int)qu[i] - 33;
+				q = q < 0 ? 0 : (q > 255 ? 255 : q);
+				gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
+				const int b = rd[i];
+				if(b <= 3) { c = (uint32_t)b; m = (uint32_t)sc.mmpen[q]; }
+			}
+			rc[r] = c; mm[r] = m;
+			const uint32_t bar = gbar ? 256u : 0u, r0 = (i == 0) ? 256u : 0u;   // row 0 has no F
+			rdoe[r] = rdo + bar; rfoe[r] = rfo + bar + r0; rfee[r] = rfe + bar + r0;
+		}
+		__syncthreads();
+		// ---- fill: H/E of the previous column for my rows; H[i][-1] = E = 0, H[-1][*] = 0xff
+		uint32_t Hp0 = 0, Hp1 = 0, Hp2 = 0, Hp3 = 0, Ep0 = 0, Ep1 = 0, Ep2 = 0, Ep3 = 0;
+		uint32_t hupPrev = lane == 0 ? 0xffu : 0u;  // H[4l-1][j-1]
+		uint32_t bot = 0;                           // my bottom row's H | F << 16, last column
+		const int lastLane = (R - 1) >> 2, lastR = (R - 1) & 3;
+		const int T = C + L - 1;
+		for(int t = 0; t < T; t++) {
+			const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bot, 0x138, 0xf, 0xf, false);
+			const int j = t - lane;
+			if(lane < L && j >= 0 && j < C) {
+				uint32_t hu = lane == 0 ? 0xffu : (up & 0xffffu);
+				uint32_t fu = lane == 0 ? 0u : (up >> 16);
+				uint32_t hdiag = hupPrev;
+				hupPrev = hu;
+				const uint32_t refc = refw[j];
+				const bool refN = refc > 3;
+				uint32_t tbv = 0;
+#define BT2X_WAVE_CELL(r, HP, EP)                                                               \
+				{                                                                               \
+					const uint32_t x = rc[r] ^ refc;                                            \
+					const uint32_t pen = refN ? npen : (x ? mm[r] : 0u);                        \
+					const uint32_t d = subs(hdiag, pen);                                        \
+					const uint32_t hl_o = subs(HP, rdoe[r]), e = max(hl_o, subs(EP, rde));      \
+					const uint32_t hu_o = subs(hu, rfoe[r]), f = max(hu_o, subs(fu, rfee[r]));  \
+					const uint32_t h = max(max(d, e), f);                                       \
+					const uint32_t tb = (x ? (uint32_t)TB_MM : 0u) | (hl_o != e ? (uint32_t)TB_EONE : 0u) | \
+					                    (hu_o != f ? (uint32_t)TB_FONE : 0u) | (f != h ? (uint32_t)TB_FNE : 0u) | \
+					                    (d != h ? (uint32_t)TB_DNE : 0u);                           \
+					tbv |= tb << (8 * r);                                                       \
+					hdiag = HP; HP = h; EP = e; hu = h; fu = f;                                 \
+				}
+				BT2X_WAVE_CELL(0, Hp0, Ep0)
+				BT2X_WAVE_CELL(1, Hp1, Ep1)
+				BT2X_WAVE_CELL(2, Hp2, Ep2)
+				BT2X_WAVE_CELL(3, Hp3, Ep3)
+#undef BT2X_WAVE_CELL
+				tbw[j * L + lane] = tbv;
+				bot = hu | (fu << 16);
+				if(lane == lastLane)
+					lastrow[j] = (uint8_t)(lastR == 0 ? Hp0 : lastR == 1 ? Hp1 : lastR == 2 ? Hp2 : Hp3);
+			}
+		}
+		__syncthreads();
+		// ---- best score, candidates in DpBtCandidate order (score desc, col desc)
+		const int thr = (int)p.minsc + 0xff;
+		int lrmax = 0, nc = 0;
+		for(int j = lane; j < C; j += 64) { const int v = lastrow[j]; lrmax = imax(lrmax, v); nc += v >= thr; }
+		lrmax = wave_max(lrmax);
+		for(int d = 32; d > 0; d >>= 1) nc += __shfl_xor(nc, d);
+		st_cells += (unsigned long long)R * C;
+		st_cols += C;
+		bt2x_dp_out o;
+		o.nrec = 0; o.rec_off = 0;
+		const int score = lrmax - 0xff;
+		if(score < p.minsc) {
+			o.status = 0; o.best = score; o.ncand = 0;
+			if(lane == 0) a.out[pi] = o;
+			__syncthreads();
+			continue;
+		}
+		o.status = nc > 0 ? 1 : 0; o.best = score; o.ncand = (uint16_t)nc;
+		for(int j = lane; j < C; j += 64) {
+			const int v = lastrow[j];
+			if(v < thr) continue;
+			const int key = (v << 8) | j;
+			int rank = 0;
+			for(int k = 0; k < C; k++) { const int w = lastrow[k]; rank += ((w << 8) | k) > key; }
+			cands[rank] = (uint8_t)j;
+		}
+		__syncthreads();
+		// ---- SwAligner::nextAlignment until done(), on lane 0 (see walk_problem)
+		if(lane == 0) {
+			if(o.status != 0 && o.ncand > 0 && a.ablate != 1) {
+				const int rdo_ = sc.rdo, rde_ = sc.rde, rfo_ = sc.rfo, rfe_ = sc.rfe;
+				const int ncand = o.ncand, row0 = R - 1;
+				int ndone = 0, nrec = 0;
+				while(ndone < ncand) {
+					int ntries = 0, hi = 0;
+					bool found = false;
+					while(ndone < ncand) {
+						const int col0 = cands[ndone];
+						ndone++;
+						if(tbb[col0 * S + row0] & TB_MARK) continue;
+						ntries++;
+						if(a.ablate == 2) continue;
+						int row = row0, col = col0, ct = 2, bscore = 0, ns = 0, gaps = 0, ne = 0;
+						bool over_core = false, ok = true;
+						uint32_t tb_end = 0;
+						int bo = col * S + row;
+						uint32_t tb = tbb[bo];
+						while(true) {
+							st_bt++;
+							if(tb & TB_MARK) { ok = false; break; }
+							const int diag = col - row + (int)p.triml;
+							over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);
+							if(row == 0) { tbb[bo] = (uint8_t)TB_MARK; tb_end = tb; break; }
+							const uint32_t dne = tb & TB_DNE, fne = (tb >> 1) & 1u;
+							const uint32_t fext = (tb >> 2) & 1u, eext = (tb >> 3) & 1u;
+							const bool inH = ct == 2;
+							const bool isD = inH && !dne;
+							const bool isF = (ct == 1) || (inH && dne && !fne);
+							const int nct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);
+							const int cbo = bo;
+							bo += isD ? -(S + 1) : isF ? -1 : -S;
+							const int crow = row, ccol = col;
+							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;
+							const uint32_t ctb = tb;
+							tb = tbb[bo];
+							tbb[cbo] = (uint8_t)TB_MARK;               // setReportedThrough
+							if(isD) {
+								if(ctb & TB_MM) {
+									const int rdc = rd[crow], refc = refw[ccol];
+									const bool amb = rdc > 3 || refc > 3;
+									const int q0 = (int)qu[crow] - 33;
+									const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
+									stage_ed[ne++] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(refc), acgtn(rdc));
+									bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
+									if(amb) ns++;
+								}
+							} else {
+								const bool open = nct == 2;
+								stage_ed[ne++] = isF ? pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rd[crow]))
+								                     : pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(refw[ccol]), '-');
+								bscore -= isF ? (open ? rfo_ : rfe_) : (open ? rdo_ : rde_);
+								gaps++;
+							}
+						}
+						if(!ok || !over_core) { hi = max(hi, ne); continue; }
+						if(tb_end & TB_MM) {
+							const int rdc = rd[row], refc = refw[col];
+							const bool amb = rdc > 3 || refc > 3;
+							const int q0 = (int)qu[row] - 33;
+							const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
+							stage_ed[ne++] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
+							bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
+							if(amb) ns++;
+						}
+						if(ns > p.nceil) { hi = max(hi, ne); continue; }
+						int refns = 0;
+						for(int k = col; k <= col0; k++) refns += (refw[k] > 3);
+						const int extent = R - (R - row0 - 1);
+						if(p.fw) {
+							for(int k = 0; k < ne / 2; k++) {
+								const uint32_t x = stage_ed[k];
+								stage_ed[k] = stage_ed[ne - 1 - k];
+								stage_ed[ne - 1 - k] = x;
+							}
+						} else {
+							for(int k = 0; k < ne; k++) {
+								const uint32_t e = stage_ed[k];
+								const uint32_t pos = (uint32_t)extent - (e & 0x3ffu) - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
+								stage_ed[k] = (e & ~0x3ffu) | (pos & 0x3ffu);
+							}
+						}
+						hi = max(hi, ne);
+						found = true;
+						bt2x_aln_rec r;
+						r.ntries = (uint16_t)ntries; r.ok = 1; r.pad0 = 0;
+						r.score = (int16_t)bscore; r.ns = (uint16_t)ns; r.gaps = (uint16_t)gaps;
+						r.nedit = (uint16_t)ne; r.bases_aligned = (uint16_t)(extent - ne);
+						r.refns = (uint16_t)refns; r.refoff = (int64_t)col + p.refl;
+						uint32_t eo = 0;
+						if(hi > 0) {
+							eo = atomicAdd(&a.counters[1], (uint32_t)hi);
+							if(eo + (uint32_t)hi <= a.edit_cap) for(int k = 0; k < hi; k++) a.edits[eo + k] = stage_ed[k];
+						}
+						r.edit_off = eo; r.nbuf = (uint32_t)hi;
+						stage_rec[nrec] = r;
+						break;
+					}
+					if(!found) {
+						bt2x_aln_rec r;
+						r.ntries = (uint16_t)ntries; r.ok = 0; r.pad0 = 0; r.score = 0; r.ns = 0; r.gaps = 0;
+						r.nedit = 0; r.bases_aligned = 0; r.refns = 0; r.refoff = 0;
+						uint32_t eo = 0;
+						if(hi > 0) {
+							eo = atomicAdd(&a.counters[1], (uint32_t)hi);
+							if(eo + (uint32_t)hi <= a.edit_cap) for(int k = 0; k < hi; k++) a.edits[eo + k] = stage_ed[k];
+						}
+						r.edit_off = eo; r.nbuf = (uint32_t)hi;
+						stage_rec[nrec] = r;
+						nrec++;
+						break;
+					}
+					nrec++;
+				}
+				const uint32_t ro = atomicAdd(&a.counters[0], (uint32_t)nrec);
+				if(ro + (uint32_t)nrec <= a.rec_cap)
+					for(int k = 0; k < nrec; k++) a.recs[ro + k] = stage_rec[k];
+				o.nrec = (uint16_t)nrec; o.rec_off = ro;
+			}
+			a.out[pi] = o;
+		}
+		__syncthreads();
+	}
+	if(a.stats && lane == 0) {
+		atomicAdd(&a.stats[0], st_cells);
+		atomicAdd(&a.stats[1], st_cols);
+		atomicAdd(&a.stats[2], st_bt);
+	}
+}
+
 // kFused: the same wave walks its 64 problems right after their fill, while the
 // traceback bytes are still in the Infinity Cache; slots are per resident wave.
 template<bool kDebug, bool kFused>
@@ -604,6 +858,15 @@ static bool dp_split_mode() {
 	return m == 1;
 }
 
+// Largest launch run one wave per problem (BT2X_DP_WAVE=0: never, =1: always; else
+// BT2X_DP_WAVE_MAX problems, default 32768: below that a lane-per-problem launch does not
+// fill the chip and costs its serial R x C fill anyway).
+static uint32_t dp_wave_max() {                 // read per launch (tests switch modes)
+	const char* w = getenv("BT2X_DP_WAVE");
+	const char* x = getenv("BT2X_DP_WAVE_MAX");
+	return (w && w[0] == '0') ? 0u : (w && w[0] == '1') ? 0xffffffffu : (x ? (uint32_t)atoll(x) : 32768u);
+}
+
 // Scratch: split = `chunk_groups` fill group regions + one staging slot per resident walk
 // wave; fused = one group region + staging slot per resident fill wave.
 size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups) {
@@ -632,6 +895,15 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 	const bool dbg = a0.digests || a0.cands;
 	DpLaunch a = a0;
 	const uint32_t groups_all = (a0.n + 63) / 64;
+	if(!dbg && a0.n <= dp_wave_max()) {
+		// small launch: one wave per problem (persistent, 4 waves per CU by LDS)
+		uint32_t wb = (uint32_t)a0.ncu * 4u;
+		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
+		if(wb > slots) wb = (uint32_t)slots;
+		if(wb > a0.n) wb = a0.n;
+		hipLaunchKernelGGL(dp_wave_kernel, dim3(wb), dim3(64), 0, s, sc, a);
+		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+	}
 	if(!dp_split_mode()) {
 		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)(dbg ? fused_bpc_dbg : fused_bpc);
 		if(fb > groups_all) fb = groups_all;

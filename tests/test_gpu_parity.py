@@ -120,6 +120,25 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     assert (out["status"] == 1).sum() > 20000
     assert (recs["nbuf"] > recs["nedit"]).sum() > 1000      # failed attempts' leftovers are exercised
 
+    # the production kernels without debug outputs: lane-per-problem and wave-per-problem
+    # (the small-launch mode), every record and the whole edit-buffer image
+    sel = np.arange(len(dp)) < 12000
+    fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff", "nbuf"]
+    for wave in ("0", "1"):
+        os.environ["BT2X_DP_WAVE"] = wave
+        try:
+            out, recs, edits = ctx.dp_align(rd, qu, rf, dp, debug=False)[:3]
+        finally:
+            del os.environ["BT2X_DP_WAVE"]
+        np.testing.assert_array_equal(out[["status", "best", "ncand", "nrec"]], eo[["status", "best", "ncand", "nrec"]])
+        for i in np.nonzero(out["nrec"] * sel)[0]:
+            a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
+            b = erecs[eo["rec_off"][i]: eo["rec_off"][i] + eo["nrec"][i]]
+            assert (a[fields] == b[fields]).all(), (wave, i)
+            for ra, rb in zip(a, b):
+                np.testing.assert_array_equal(edits[ra["edit_off"]: ra["edit_off"] + ra["nbuf"]],
+                                              eedits[rb["edit_off"]: rb["edit_off"] + rb["nbuf"]])
+
 
 def test_dp_rejects_shapes_outside_reference_limits(ctxs):
     ctx = ctxs["rep"][0]
@@ -283,10 +302,12 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits):
                                           eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
 
 
-@pytest.mark.parametrize("debug", [False, True])
-def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug):
-    """Production (debug=False) and debug kernels on random shapes/penalty thresholds at the
-    ABI limits vs the oracle: statuses, candidates, every nextAlignment record and edit."""
+@pytest.mark.parametrize("debug,wave", [(False, "0"), (False, "1"), (True, "0")])
+def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, monkeypatch):
+    """Production (debug=False; lane-per-problem and wave-per-problem modes) and debug
+    kernels on random shapes/penalty thresholds at the ABI limits vs the oracle: statuses,
+    candidates, every nextAlignment record and edit."""
+    monkeypatch.setenv("BT2X_DP_WAVE", wave)
     rd, qu, rf, inp = _random_dp_problems(6000, seed=77 + int(debug))
     ctx = ctxs["rep"][0]
     res = ctx.dp_align(rd, qu, rf, inp, debug=debug)
@@ -299,8 +320,11 @@ def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug):
     assert (out["status"] == 1).sum() > 1000 and (out["status"] == 0).sum() > 100
 
 
-def test_dp_production_kernel_on_golden(ctxs):
-    """The production (non-debug) kernel reproduces the reference records of the golden set."""
+@pytest.mark.parametrize("wave", ["0", "1"])
+def test_dp_production_kernel_on_golden(ctxs, wave, monkeypatch):
+    """The production (non-debug) kernel, in both modes, reproduces the reference records of
+    the golden set."""
+    monkeypatch.setenv("BT2X_DP_WAVE", wave)
     case = g.DpCase(os.path.join(g.GOLDEN, "dp_rep_dpad12.txt.xz"))
     ctx = ctxs["rep"][0]
     out, recs, edits = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
