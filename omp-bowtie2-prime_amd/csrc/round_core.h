@@ -88,12 +88,33 @@ struct SampleWs {
 // How sample() spreads its list work over the lanes that run one job together.  All
 // lanes run the RNG-sequential loop in lockstep on the same values (wave-uniform); the
 // list fills, seen-set clears and the seen-to-swap conversion scan are lane-strided.
+// The RowSampler's live list and running sums are behind rs_* so the wave version can keep
+// them in registers (lane l holds entries l and l+64) and find the dart with two ballots.
 struct SerialCoop {                           // one thread (host test, host builds)
 	__host__ __device__ uint32_t lane() const { return 0; }
 	__host__ __device__ uint32_t width() const { return 1; }
 	__host__ __device__ void sync() const {}
 	__host__ __device__ uint64_t ballot(bool p) const { return p ? 1u : 0u; }
 	__host__ __device__ bool leader() const { return true; }
+	// live = 0 .. nb-1 (w.masses filled)
+	__host__ __device__ void rs_init(SampleWs& w, uint32_t nb) { for(uint32_t i = 0; i < nb; i++) w.live[i] = (uint16_t)i; }
+	// pre[k] = masses[live[0]] + ... + masses[live[k]], summed in that order
+	__host__ __device__ void rs_rebuild(SampleWs& w, uint32_t nlive) {
+		double sofar = 0.0f;
+		for(uint32_t k = 0; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
+	}
+	// the first live range whose running mass exceeds rd (else the last live one)
+	__host__ __device__ uint32_t rs_dart(const SampleWs& w, double rd, uint32_t nlive) const {
+		uint32_t lo = 0, hi = nlive;
+		while(lo < hi) { const uint32_t mid = (lo + hi) >> 1; if(rd < w.pre[mid]) hi = mid; else lo = mid + 1; }
+		return w.live[lo < nlive ? lo : nlive - 1];
+	}
+	// drop range bi from the live list (order kept)
+	__host__ __device__ void rs_remove(SampleWs& w, uint32_t bi, uint32_t nlive) {
+		uint32_t q = 0;
+		while(q < nlive && w.live[q] != bi) q++;
+		for(; q + 1 < nlive; q++) w.live[q] = w.live[q + 1];
+	}
 };
 
 struct Prep {
@@ -313,7 +334,7 @@ __host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t
 // emit(k, bi, element) for each of the nsamples draws (on the leader lane).  The caller
 // fills w.big; false on workspace overflow.
 template<class C, class Emit>
-__host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, const C& co,
+__host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, C& co,
                                        Emit&& emit) {
 	if(nb > (uint32_t)kMaxRanges) return false;
 	for(uint32_t k = co.lane(); k < (uint32_t)kHash; k += co.width()) w.hash[k] = 0;
@@ -323,7 +344,6 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 		double den = (double)w.big[i].size;
 		den *= den;
 		w.masses[i] = num / den;
-		w.live[i] = (uint16_t)i;
 		R1N& s = w.r1n[i];
 		s.inited = 0; s.n = 0; s.cur = 0; s.converted = 0; s.swaplist = 0;
 	}
@@ -331,19 +351,14 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 	double mass = 0.0f;
 	for(uint32_t i = 0; i < nb; i++) mass += w.masses[i];
 	uint32_t nlive = nb;
-	auto rebuild = [&]() {
-		double sofar = 0.0f;
-		for(uint32_t k = 0; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
-	};
-	rebuild();
+	co.rs_init(w, nb);
+	co.rs_rebuild(w, nlive);
 	uint32_t arenaTop = 0;
 	for(uint64_t k = 0; k < nsamples; k++) {
 		const double rd = rnd.nextFloat() * mass;
 		// the dart: first live range whose running mass exceeds it (else the last live one)
 		if(nlive == 0) return false;
-		uint32_t lo = 0, hi = nlive;
-		while(lo < hi) { const uint32_t mid = (lo + hi) >> 1; if(rd < w.pre[mid]) hi = mid; else lo = mid + 1; }
-		const uint32_t bi = w.live[lo < nlive ? lo : nlive - 1];
+		const uint32_t bi = co.rs_dart(w, rd, nlive);
 		R1N& s = w.r1n[bi];
 		if(!s.inited) {
 			const uint16_t n = (uint16_t)w.big[bi].size;                       // uint16_t element type
@@ -356,11 +371,9 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 		if(!r1n_next(w, (int)bi, rnd, arenaTop, rr, co)) return false;
 		if(s.n > 0 && s.cur >= s.n) {                                          // done(): finishedRange
 			mass -= w.masses[bi];
-			uint32_t q = 0;
-			while(q < nlive && w.live[q] != bi) q++;
-			for(; q + 1 < nlive; q++) w.live[q] = w.live[q + 1];
+			co.rs_remove(w, bi, nlive);
 			nlive--;
-			rebuild();
+			co.rs_rebuild(w, nlive);
 		}
 		if(co.leader()) emit(k, bi, rr);
 	}

@@ -103,12 +103,56 @@ round_prep_kernel(RoundLaunch a) {
 	}
 }
 
+__device__ __forceinline__ double readlane_f64(double v, uint32_t k) {
+	const uint64_t u = __builtin_bit_cast(uint64_t, v);
+	const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, (int)k);
+	const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), (int)k);
+	return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 struct WaveCoop {                            // a one-wave workgroup runs one job
+	// RowSampler state in registers: live range ids, their masses and running sums of
+	// list positions l and l + 64
+	uint32_t lv0, lv1;
+	double m0, m1, p0, p1;
 	__device__ uint32_t lane() const { return threadIdx.x; }
 	__device__ uint32_t width() const { return 64; }
 	__device__ void sync() const { __syncthreads(); }
 	__device__ uint64_t ballot(bool p) const { return __ballot(p); }
 	__device__ bool leader() const { return threadIdx.x == 0; }
+	__device__ void rs_init(const SampleWs& w, uint32_t nb) {
+		const uint32_t l = threadIdx.x;
+		lv0 = l; lv1 = l + 64;
+		m0 = l < nb ? w.masses[l] : 0.0; m1 = l + 64 < nb ? w.masses[l + 64] : 0.0;
+	}
+	// the running sums in list order, one uniform addition per position (as SerialCoop)
+	__device__ void rs_rebuild(const SampleWs&, uint32_t nlive) {
+		const uint32_t l = threadIdx.x;
+		double sofar = 0.0f;
+		const uint32_t n0 = nlive < 64 ? nlive : 64;
+		for(uint32_t k = 0; k < n0; k++) { sofar += readlane_f64(m0, k); if(l == k) p0 = sofar; }
+		for(uint32_t k = 64; k < nlive; k++) { sofar += readlane_f64(m1, k - 64); if(l == k - 64) p1 = sofar; }
+	}
+	// the count of running sums <= rd is the bisection's upper bound
+	__device__ uint32_t rs_dart(const SampleWs&, double rd, uint32_t nlive) const {
+		const uint32_t l = threadIdx.x;
+		const uint32_t lo = (uint32_t)__popcll(__ballot(l < nlive && p0 <= rd)) +
+		                    (uint32_t)__popcll(__ballot(l + 64 < nlive && p1 <= rd));
+		const uint32_t idx = lo < nlive ? lo : nlive - 1;
+		return (uint32_t)__builtin_amdgcn_readlane((int)(idx < 64 ? lv0 : lv1), (int)(idx & 63));
+	}
+	__device__ void rs_remove(const SampleWs&, uint32_t bi, uint32_t nlive) {
+		const uint32_t l = threadIdx.x;
+		const uint64_t b0 = __ballot(l < nlive && lv0 == bi), b1 = __ballot(l + 64 < nlive && lv1 == bi);
+		const uint32_t q = b0 ? (uint32_t)__ffsll((unsigned long long)b0) - 1 : 64 + (uint32_t)__ffsll((unsigned long long)b1) - 1;
+		// positions >= q take their successor's entry
+		const uint32_t nl0 = __shfl(lv0, (int)((l + 1) & 63)), nl1 = __shfl(lv1, (int)((l + 1) & 63));
+		const double nm0 = __shfl(m0, (int)((l + 1) & 63)), nm1 = __shfl(m1, (int)((l + 1) & 63));
+		const uint32_t h0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)lv1);     // lv1 of lane 0
+		const double hm = readlane_f64(m1, 0);
+		if(l >= q) { lv0 = l == 63 ? h0 : nl0; m0 = l == 63 ? hm : nm0; }
+		if(l + 64 >= q) { lv1 = nl1; m1 = nm1; }
+	}
 };
 
 // One wave per job, its workspace in LDS: the sampling loop is a chain of dependent
@@ -118,7 +162,7 @@ __global__ void __launch_bounds__(64)
 round_sample_kernel(RoundLaunch a) {
 	__shared__ SampleWs w;
 	__shared__ uint32_t qsh;
-	const WaveCoop co;
+	WaveCoop co;
 	const Job* jobs = reinterpret_cast<const Job*>(a.jobs);
 	const Range* ranges = reinterpret_cast<const Range*>(a.ranges);
 	const uint32_t njobs = min(a.counters[3], a.job_cap);

@@ -86,10 +86,11 @@ Got run_core(const Case& c, uint32_t maxelt, CoreWs& w) {
 			const bt2x_round::Range* big = w.p.r2 + p.nsmall;
 			const uint32_t nb = p.n2 - p.nsmall;
 			for(uint32_t i = 0; i < nb && i < (uint32_t)bt2x_round::kMaxRanges; i++) w.s.big[i] = big[i];
+			bt2x_round::SerialCoop co;
 			const size_t s0 = g.sats.size(), e0 = g.rows.size();
 			g.sats.resize(s0 + p.nsamples);
 			g.rows.resize(e0 + p.nsamples);
-			const bool ok = bt2x_round::sample(nb, p.nsamples, rnd, w.s, bt2x_round::SerialCoop(), [&](uint64_t k, uint32_t bi, uint16_t elt) {
+			const bool ok = bt2x_round::sample(nb, p.nsamples, rnd, w.s, co, [&](uint64_t k, uint32_t bi, uint16_t elt) {
 				bt2x_sat s;
 				s.rdoff = big[bi].rdoff; s.rand_n = 1; s.fw = big[bi].fw; s.seedlen = (uint8_t)c.in.seedlen;
 				g.sats[s0 + k] = s;

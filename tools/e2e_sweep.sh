@@ -11,5 +11,5 @@ for opts in "$@"; do
   envs=()
   while [[ "$opts" =~ ^([A-Z_]+=[^ ]*)\ (.*)$ ]]; do envs+=("${BASH_REMATCH[1]}"); opts="${BASH_REMATCH[2]}"; done
   timeout -k 10 300 env "${envs[@]}" "$ALIGN" -x "$W/syn1000000000_s2024" -U "$W/rank0/reads.fq" -S "$W/sweep.sam" --dpad 12 \
-      -p "${OMP_NUM_THREADS:-16}" --stats $opts 2>&1 | grep -E "BT2X_STATS|BT2X_RUSAGE|overall" || exit 1
+      -p "${OMP_NUM_THREADS:-16}" --stats $opts 2>&1 | grep -E "BT2X_STATS|BT2X_RUSAGE|BT2X_GPU|overall" || exit 1
 done
