@@ -402,6 +402,11 @@ def main():
                 for kk in (("seed", "resolve") if kind == "round" else (kind,)):
                     for k, v in ctx.last_counters(kid[kk]).items():
                         counters[kk][k] = counters[kk].get(k, 0) + v
+                if kind == "round":
+                    rs = ctx.last_round_stats()
+                    for k in ("reads", "jobs", "samples"):
+                        counters["round"][k] = counters["round"].get(k, 0) + rs[k]
+                    counters["round"]["max_samples"] = max(counters["round"].get("max_samples", 0), rs["max_samples"])
 
     ctr = {k: {} for k in kid}          # algorithmic-work counters (deterministic per step)
     for w in range(max(args.warmup, 1)):
@@ -481,7 +486,8 @@ def main():
         "kernels": {"seed_ms": round(kms["seed"], 3), "resolve_ms": round(kms["resolve"], 3),
                     "dp_ms": round(kms["dp"], 3), "seed_alg_bytes": fm_bytes, "resolve_alg_bytes": res_bytes,
                     "dp_alg_bytes": dp_bytes, "launches": nl, "units": units,
-                    "counters_seed": cs, "counters_resolve": cr, "counters_dp": cd},
+                    "counters_seed": cs, "counters_resolve": cr, "counters_dp": cd,
+                    "round_sampling": ctr["round"]},
         "end_to_end": {"value": round(n * world / e2e_t / 1e6, 4), "unit": "M reads/s",
                        "what": "bt2x-align FASTQ->SAM wall time (host driver, PCIe, SAM formatting; "
                                f"index load excluded; --slots {args.slots}, launches overlapped with host "

@@ -135,6 +135,9 @@ typedef struct {
 	uint64_t alg_bytes;   /* algorithmic HBM bytes of the launch */
 } bt2x_counters;
 int bt2x_last_counters(const bt2x_ctx* ctx, int kernel, bt2x_counters* out);
+/* The last seed round's sampling work (bt2x_seed_round[_dev]): out[0] reads, out[1] reads
+ * that sampled (RowSampler jobs), out[2] elements drawn, out[3] most elements one read drew. */
+int bt2x_last_round_stats(const bt2x_ctx* ctx, uint32_t out[4]);
 
 /* ------------------------------------------------------------ seed search */
 

@@ -60,6 +60,7 @@ FUNCS = {
                                            ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
     "bt2x_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
+    "bt2x_last_round_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "bt2x_host_free": (None, [ctypes.c_void_p]),
     "bt2x_suffix_array": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
     "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
@@ -246,6 +247,12 @@ class Context:
         c = abi.Counters()
         check(load().bt2x_last_counters(self.h, kernel, ctypes.byref(c)), "bt2x_last_counters")
         return c.as_dict()
+
+    def last_round_stats(self) -> dict:
+        """The last seed round's sampling work (bt2x_last_round_stats)."""
+        o = (ctypes.c_uint32 * 4)()
+        check(load().bt2x_last_round_stats(self.h, o), "bt2x_last_round_stats")
+        return {"reads": o[0], "jobs": o[1], "samples": o[2], "max_samples": o[3]}
 
 
 def build_index(fasta: str, outbase: str, off_rate: int = 4, ftab_chars: int = 10) -> str:

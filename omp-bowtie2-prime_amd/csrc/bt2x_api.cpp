@@ -169,6 +169,7 @@ struct bt2x_ctx {
 	unsigned long long* d_stats = nullptr;     // [0..2] seed, [4..6] dp, [8..10] resolve
 	uint32_t* d_counters = nullptr;
 	uint64_t n_seed_last = 0, n_dp_last = 0, n_resolve_last = 0;
+	uint32_t n_round_last = 0;
 };
 
 bt2x_ctx::~bt2x_ctx() {
@@ -355,6 +356,18 @@ extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) 
 		// traceback byte per cell written + reference window + read codes/quals
 		out->alg_bytes = out->dp_cells + out->dp_cols;
 	}
+	return BT2X_OK;
+}
+
+extern "C" int bt2x_last_round_stats(const bt2x_ctx* c, uint32_t out[4]) {
+	if(!c || !out) return BT2X_E_ARG;
+	out[0] = out[1] = out[2] = out[3] = 0;
+	if(!c->b_rcnt.p) return BT2X_OK;
+	uint32_t cnt[8];
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(hipMemcpy(cnt, c->b_rcnt.p, sizeof cnt, hipMemcpyDeviceToHost));
+	out[0] = c->n_round_last; out[1] = cnt[3]; out[2] = cnt[6]; out[3] = cnt[7];
 	return BT2X_OK;
 }
 
@@ -568,6 +581,7 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][1], s));
 	c->ev_valid[BT2X_K_SEED] = true;
 	c->n_seed_last = nseeds;
+	c->n_round_last = nreads;
 	// 2. finalize + rank + prioritize per read, then 3. place every row
 	HIPCHK(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), s));
 	HIPCHK(hipMemsetAsync(c->d_stats + 8, 0, 3 * sizeof(unsigned long long), s));

@@ -115,6 +115,16 @@ struct SerialCoop {                           // one thread (host test, host bui
 		while(q < nlive && w.live[q] != bi) q++;
 		for(; q + 1 < nlive; q++) w.live[q] = w.live[q + 1];
 	}
+	// per-range Random1toN state and range fields (the wave keeps them in registers)
+	__host__ __device__ void r1n_reset(SampleWs& w, uint32_t nb) {
+		for(uint32_t i = 0; i < nb; i++) { R1N& r = w.r1n[i]; r.inited = 0; r.n = 0; r.cur = 0; r.converted = 0; r.swaplist = 0; }
+	}
+	__host__ __device__ R1N r1n_get(const SampleWs& w, uint32_t bi) const { return w.r1n[bi]; }
+	__host__ __device__ void r1n_set(SampleWs& w, uint32_t bi, const R1N& r) { w.r1n[bi] = r; }
+	__host__ __device__ void big_load(const SampleWs&, uint32_t) {}
+	__host__ __device__ Range big_get(const SampleWs& w, uint32_t bi) const { return w.big[bi]; }
+	// seen-set membership of key, adding it when absent; full: the set had no room
+	__host__ __device__ bool seen_test_add(SampleWs& w, uint32_t key, bool& full) const;
 };
 
 struct Prep {
@@ -265,6 +275,12 @@ __host__ __device__ inline bool seen_add(SampleWs& w, uint32_t key) {
 	return false;
 }
 
+__host__ __device__ inline bool SerialCoop::seen_test_add(SampleWs& w, uint32_t key, bool& full) const {
+	if(seen_has(w, key)) return true;
+	if(!seen_add(w, key)) full = true;
+	return false;
+}
+
 __host__ __device__ inline uint32_t popc64(uint64_t m) {
 #ifdef __HIP_DEVICE_COMPILE__
 	return (uint32_t)__popcll(m);
@@ -275,9 +291,8 @@ __host__ __device__ inline uint32_t popc64(uint64_t m) {
 
 // Random1toN::next over range ri; false on workspace overflow.
 template<class C>
-__host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t& arenaTop, uint16_t& out,
+__host__ __device__ inline bool r1n_next(SampleWs& w, R1N& s, int ri, Rnd& rnd, uint32_t& arenaTop, uint16_t& out,
                                          const C& co) {
-	R1N& s = w.r1n[ri];
 	if(s.cur == 0 && !s.converted) {
 		if(s.n == 1) { s.cur = 1; out = 0; return true; }
 		if(s.swaplist) {
@@ -298,12 +313,13 @@ __host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t
 		s.cur++;
 		return true;
 	}
-	// seen-list mode: redraw until unseen
+	// seen-list mode: redraw until unseen (the unseen draw joins the set)
 	uint16_t rn;
+	bool full = false;
 	do {
 		rn = (uint16_t)(rnd.nextU32() % (uint32_t)s.n);
-	} while(seen_has(w, ((uint32_t)ri << 16 | rn) + 1u));
-	if(!seen_add(w, ((uint32_t)ri << 16 | rn) + 1u)) return false;
+	} while(co.seen_test_add(w, ((uint32_t)ri << 16 | rn) + 1u, full));
+	if(full) return false;
 	s.cur++;                                  // = seen_.size()
 	if(s.cur >= s.thresh && s.cur < s.n) {
 		// convert to a swap list of the unseen elements, ascending
@@ -331,7 +347,7 @@ __host__ __device__ inline bool r1n_next(SampleWs& w, int ri, Rnd& rnd, uint32_t
 }
 
 // RowSampler over w.big[0 .. nb) (lensq = szsq = true) and one Random1toN per range:
-// emit(k, bi, element) for each of the nsamples draws (on the leader lane).  The caller
+// emit(k, range, element) for each of the nsamples draws (on the leader lane).  The caller
 // fills w.big; false on workspace overflow.
 template<class C, class Emit>
 __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, C& co,
@@ -344,10 +360,10 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 		double den = (double)w.big[i].size;
 		den *= den;
 		w.masses[i] = num / den;
-		R1N& s = w.r1n[i];
-		s.inited = 0; s.n = 0; s.cur = 0; s.converted = 0; s.swaplist = 0;
 	}
 	co.sync();
+	co.r1n_reset(w, nb);
+	co.big_load(w, nb);
 	double mass = 0.0f;
 	for(uint32_t i = 0; i < nb; i++) mass += w.masses[i];
 	uint32_t nlive = nb;
@@ -359,23 +375,25 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 		// the dart: first live range whose running mass exceeds it (else the last live one)
 		if(nlive == 0) return false;
 		const uint32_t bi = co.rs_dart(w, rd, nlive);
-		R1N& s = w.r1n[bi];
+		R1N s = co.r1n_get(w, bi);
+		const Range rg = co.big_get(w, bi);
 		if(!s.inited) {
-			const uint16_t n = (uint16_t)w.big[bi].size;                       // uint16_t element type
+			const uint16_t n = (uint16_t)rg.size;                              // uint16_t element type
 			if(n == 0) return false;
 			s.inited = 1; s.n = n; s.cur = 0; s.converted = 0; s.swaplist = n < 128 ? 1 : 0;
 			const uint16_t t = (uint16_t)(0.10f * (float)n);
 			s.thresh = t > 16 ? t : 16;
 		}
 		uint16_t rr;
-		if(!r1n_next(w, (int)bi, rnd, arenaTop, rr, co)) return false;
+		if(!r1n_next(w, s, (int)bi, rnd, arenaTop, rr, co)) return false;
+		co.r1n_set(w, bi, s);
 		if(s.n > 0 && s.cur >= s.n) {                                          // done(): finishedRange
 			mass -= w.masses[bi];
 			co.rs_remove(w, bi, nlive);
 			nlive--;
 			co.rs_rebuild(w, nlive);
 		}
-		if(co.leader()) emit(k, bi, rr);
+		if(co.leader()) emit(k, rg, rr);
 	}
 	return true;
 }

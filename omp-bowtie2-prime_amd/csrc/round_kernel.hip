@@ -115,6 +115,74 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 	// list positions l and l + 64
 	uint32_t lv0, lv1;
 	double m0, m1, p0, p1;
+	// Random1toN state of ranges l and l + 64 (n | cur << 16, thresh | list << 16, flags)
+	// and their fields (topf, size, rdoff | fw << 24)
+	uint32_t ra[3], rb[3];
+	uint32_t ga[4], gb[4];
+	__device__ void r1n_reset(const SampleWs&, uint32_t) {
+		for(int i = 0; i < 3; i++) { ra[i] = 0; rb[i] = 0; }
+	}
+	__device__ R1N r1n_get(const SampleWs&, uint32_t bi) const {
+		const uint32_t l = bi & 63;
+		const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ra[0] : rb[0]), (int)l);
+		const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ra[1] : rb[1]), (int)l);
+		const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ra[2] : rb[2]), (int)l);
+		R1N r;
+		r.n = (uint16_t)w0; r.cur = (uint16_t)(w0 >> 16); r.thresh = (uint16_t)w1; r.list = (uint16_t)(w1 >> 16);
+		r.inited = (uint8_t)w2; r.swaplist = (uint8_t)(w2 >> 8); r.converted = (uint8_t)(w2 >> 16); r.pad = 0;
+		return r;
+	}
+	__device__ void r1n_set(const SampleWs&, uint32_t bi, const R1N& r) {
+		const uint32_t w0 = (uint32_t)r.n | ((uint32_t)r.cur << 16), w1 = (uint32_t)r.thresh | ((uint32_t)r.list << 16);
+		const uint32_t w2 = (uint32_t)r.inited | ((uint32_t)r.swaplist << 8) | ((uint32_t)r.converted << 16);
+		if(threadIdx.x == (bi & 63)) {
+			if(bi < 64) { ra[0] = w0; ra[1] = w1; ra[2] = w2; } else { rb[0] = w0; rb[1] = w1; rb[2] = w2; }
+		}
+	}
+	__device__ void big_load(const SampleWs& w, uint32_t nb) {
+		const uint32_t l = threadIdx.x;
+		for(int h = 0; h < 2; h++) {
+			uint32_t* g = h ? gb : ga;
+			const uint32_t i = l + 64 * h;
+			if(i < nb) {
+				const Range& r = w.big[i];
+				g[0] = (uint32_t)r.topf; g[1] = (uint32_t)(r.topf >> 32); g[2] = (uint32_t)r.size;
+				g[3] = r.rdoff | ((uint32_t)r.fw << 24);
+			} else {
+				g[0] = g[1] = g[2] = g[3] = 0;
+			}
+		}
+	}
+	__device__ Range big_get(const SampleWs&, uint32_t bi) const {
+		const uint32_t l = bi & 63;
+		const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ga[0] : gb[0]), (int)l);
+		const uint32_t g1 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ga[1] : gb[1]), (int)l);
+		const uint32_t g2 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ga[2] : gb[2]), (int)l);
+		const uint32_t g3 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ga[3] : gb[3]), (int)l);
+		Range r;
+		r.topf = ((uint64_t)g1 << 32) | g0; r.size = g2; r.rdoff = g3 & 0xffffffu; r.fw = (uint8_t)(g3 >> 24);
+		r.offidx = 0; r.nlex = 0;
+		return r;
+	}
+	// 64 probes of the linear-probing set at once: the first slot holding the key or
+	// empty is where the serial probe would stop
+	__device__ bool seen_test_add(SampleWs& w, uint32_t key, bool& full) const {
+		uint32_t h = (key * 2654435761u) >> 22;
+		for(int base = 0; base < kHash; base += 64) {
+			const uint32_t slot = (h + (uint32_t)base + threadIdx.x) & (kHash - 1);
+			const uint32_t v = w.hash[slot];
+			const uint64_t mk = __ballot(v == key), me = __ballot(v == 0);
+			const uint64_t m = mk | me;
+			if(m) {
+				const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
+				if((mk >> f) & 1) return true;
+				if(threadIdx.x == f) w.hash[slot] = key;
+				return false;
+			}
+		}
+		full = true;
+		return false;
+	}
 	__device__ uint32_t lane() const { return threadIdx.x; }
 	__device__ uint32_t width() const { return 64; }
 	__device__ void sync() const { __syncthreads(); }
@@ -174,12 +242,12 @@ round_sample_kernel(RoundLaunch a) {
 		__syncthreads();
 		if(q >= njobs) break;
 		const Job j = jobs[q];
+		if(threadIdx.x == 0) { atomicAdd(&a.counters[6], j.nsamples); atomicMax(&a.counters[7], j.nsamples); }
 		for(uint32_t i = threadIdx.x; i < j.nb && i < (uint32_t)kMaxRanges; i += 64) w.big[i] = ranges[j.range0 + i];
 		__syncthreads();
 		Rnd rnd{j.rnd_last, j.rnd_lastoff};
-		const bool ok = sample(j.nb, j.nsamples, rnd, w, co, [&](uint64_t k, uint32_t bi, uint16_t elt) {
+		const bool ok = sample(j.nb, j.nsamples, rnd, w, co, [&](uint64_t k, const Range& rg, uint16_t elt) {
 			if(!fits) return;
-			const Range& rg = w.big[bi];
 			bt2x_sat s;
 			s.rdoff = rg.rdoff; s.rand_n = 1; s.fw = rg.fw; s.seedlen = (uint8_t)j.seedlen;
 			a.sats[j.sat_base + k] = s;

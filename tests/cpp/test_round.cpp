@@ -90,11 +90,11 @@ Got run_core(const Case& c, uint32_t maxelt, CoreWs& w) {
 			const size_t s0 = g.sats.size(), e0 = g.rows.size();
 			g.sats.resize(s0 + p.nsamples);
 			g.rows.resize(e0 + p.nsamples);
-			const bool ok = bt2x_round::sample(nb, p.nsamples, rnd, w.s, co, [&](uint64_t k, uint32_t bi, uint16_t elt) {
+			const bool ok = bt2x_round::sample(nb, p.nsamples, rnd, w.s, co, [&](uint64_t k, const bt2x_round::Range& rg, uint16_t elt) {
 				bt2x_sat s;
-				s.rdoff = big[bi].rdoff; s.rand_n = 1; s.fw = big[bi].fw; s.seedlen = (uint8_t)c.in.seedlen;
+				s.rdoff = rg.rdoff; s.rand_n = 1; s.fw = rg.fw; s.seedlen = (uint8_t)c.in.seedlen;
 				g.sats[s0 + k] = s;
-				g.rows[e0 + k] = big[bi].topf + elt;
+				g.rows[e0 + k] = rg.topf + elt;
 			});
 			if(!ok) g.out.status = BT2X_ROUND_REDO;
 			for(uint32_t i = 0; i < nb; i++) {
