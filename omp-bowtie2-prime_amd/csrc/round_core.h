@@ -78,7 +78,7 @@ struct PrepWs {
 // sample()'s workspace (one per job; the kernel keeps it in LDS)
 struct SampleWs {
 	Range big[kMaxRanges];                    // the job's ranges
-	double masses[kMaxRanges], pre[kMaxRanges];
+	double masses[kMaxRanges], pre[kMaxRanges], mlive[kMaxRanges];   // mlive: masses in live order
 	uint16_t live[kMaxRanges];
 	R1N r1n[kMaxRanges];
 	uint16_t arena[kArena];
@@ -98,10 +98,11 @@ struct SerialCoop {                           // one thread (host test, host bui
 	__host__ __device__ bool leader() const { return true; }
 	// live = 0 .. nb-1 (w.masses filled)
 	__host__ __device__ void rs_init(SampleWs& w, uint32_t nb) { for(uint32_t i = 0; i < nb; i++) w.live[i] = (uint16_t)i; }
-	// pre[k] = masses[live[0]] + ... + masses[live[k]], summed in that order
-	__host__ __device__ void rs_rebuild(SampleWs& w, uint32_t nlive) {
-		double sofar = 0.0f;
-		for(uint32_t k = 0; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
+	// pre[k] = masses[live[0]] + ... + masses[live[k]], summed in that order; entries
+	// below `from` are unchanged since the last rebuild
+	__host__ __device__ void rs_rebuild(SampleWs& w, uint32_t nlive, uint32_t from) {
+		double sofar = from ? w.pre[from - 1] : 0.0f;
+		for(uint32_t k = from; k < nlive; k++) { sofar += w.masses[w.live[k]]; w.pre[k] = sofar; }
 	}
 	// the first live range whose running mass exceeds rd (else the last live one)
 	__host__ __device__ uint32_t rs_dart(const SampleWs& w, double rd, uint32_t nlive) const {
@@ -109,11 +110,13 @@ struct SerialCoop {                           // one thread (host test, host bui
 		while(lo < hi) { const uint32_t mid = (lo + hi) >> 1; if(rd < w.pre[mid]) hi = mid; else lo = mid + 1; }
 		return w.live[lo < nlive ? lo : nlive - 1];
 	}
-	// drop range bi from the live list (order kept)
-	__host__ __device__ void rs_remove(SampleWs& w, uint32_t bi, uint32_t nlive) {
+	// drop range bi from the live list (order kept); returns its position
+	__host__ __device__ uint32_t rs_remove(SampleWs& w, uint32_t bi, uint32_t nlive) {
 		uint32_t q = 0;
 		while(q < nlive && w.live[q] != bi) q++;
+		const uint32_t pos = q;
 		for(; q + 1 < nlive; q++) w.live[q] = w.live[q + 1];
+		return pos;
 	}
 	// per-range Random1toN state and range fields (the wave keeps them in registers)
 	__host__ __device__ void r1n_reset(SampleWs& w, uint32_t nb) {
@@ -368,7 +371,7 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 	for(uint32_t i = 0; i < nb; i++) mass += w.masses[i];
 	uint32_t nlive = nb;
 	co.rs_init(w, nb);
-	co.rs_rebuild(w, nlive);
+	co.rs_rebuild(w, nlive, 0);
 	uint32_t arenaTop = 0;
 	for(uint64_t k = 0; k < nsamples; k++) {
 		const double rd = rnd.nextFloat() * mass;
@@ -389,9 +392,9 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 		co.r1n_set(w, bi, s);
 		if(s.n > 0 && s.cur >= s.n) {                                          // done(): finishedRange
 			mass -= w.masses[bi];
-			co.rs_remove(w, bi, nlive);
+			const uint32_t q = co.rs_remove(w, bi, nlive);
 			nlive--;
-			co.rs_rebuild(w, nlive);
+			co.rs_rebuild(w, nlive, q);
 		}
 		if(co.leader()) emit(k, rg, rr);
 	}

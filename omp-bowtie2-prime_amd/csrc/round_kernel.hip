@@ -188,18 +188,31 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 	__device__ void sync() const { __syncthreads(); }
 	__device__ uint64_t ballot(bool p) const { return __ballot(p); }
 	__device__ bool leader() const { return threadIdx.x == 0; }
-	__device__ void rs_init(const SampleWs& w, uint32_t nb) {
+	__device__ void rs_init(SampleWs& w, uint32_t nb) {
 		const uint32_t l = threadIdx.x;
 		lv0 = l; lv1 = l + 64;
 		m0 = l < nb ? w.masses[l] : 0.0; m1 = l + 64 < nb ? w.masses[l + 64] : 0.0;
+		w.mlive[l] = m0; w.mlive[l + 64] = m1;
+		__syncthreads();
 	}
-	// the running sums in list order, one uniform addition per position (as SerialCoop)
-	__device__ void rs_rebuild(const SampleWs&, uint32_t nlive) {
+	// the running sums in list order from position `from` (lane 0, the order SerialCoop
+	// sums in), then every lane takes its two
+	__device__ void rs_rebuild(SampleWs& w, uint32_t nlive, uint32_t from) {
 		const uint32_t l = threadIdx.x;
-		double sofar = 0.0f;
-		const uint32_t n0 = nlive < 64 ? nlive : 64;
-		for(uint32_t k = 0; k < n0; k++) { sofar += readlane_f64(m0, k); if(l == k) p0 = sofar; }
-		for(uint32_t k = 64; k < nlive; k++) { sofar += readlane_f64(m1, k - 64); if(l == k - 64) p1 = sofar; }
+		if(l == 0) {
+			double sofar = from ? w.pre[from - 1] : 0.0f;
+			uint32_t k = from;
+			for(; k + 4 <= nlive; k += 4) {
+				const double a0 = w.mlive[k], a1 = w.mlive[k + 1], a2 = w.mlive[k + 2], a3 = w.mlive[k + 3];
+				sofar += a0; w.pre[k] = sofar;
+				sofar += a1; w.pre[k + 1] = sofar;
+				sofar += a2; w.pre[k + 2] = sofar;
+				sofar += a3; w.pre[k + 3] = sofar;
+			}
+			for(; k < nlive; k++) { sofar += w.mlive[k]; w.pre[k] = sofar; }
+		}
+		__syncthreads();
+		p0 = w.pre[l]; p1 = w.pre[l + 64];
 	}
 	// the count of running sums <= rd is the bisection's upper bound
 	__device__ uint32_t rs_dart(const SampleWs&, double rd, uint32_t nlive) const {
@@ -209,7 +222,7 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 		const uint32_t idx = lo < nlive ? lo : nlive - 1;
 		return (uint32_t)__builtin_amdgcn_readlane((int)(idx < 64 ? lv0 : lv1), (int)(idx & 63));
 	}
-	__device__ void rs_remove(const SampleWs&, uint32_t bi, uint32_t nlive) {
+	__device__ uint32_t rs_remove(SampleWs& w, uint32_t bi, uint32_t nlive) {
 		const uint32_t l = threadIdx.x;
 		const uint64_t b0 = __ballot(l < nlive && lv0 == bi), b1 = __ballot(l + 64 < nlive && lv1 == bi);
 		const uint32_t q = b0 ? (uint32_t)__ffsll((unsigned long long)b0) - 1 : 64 + (uint32_t)__ffsll((unsigned long long)b1) - 1;
@@ -220,6 +233,9 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 		const double hm = readlane_f64(m1, 0);
 		if(l >= q) { lv0 = l == 63 ? h0 : nl0; m0 = l == 63 ? hm : nm0; }
 		if(l + 64 >= q) { lv1 = nl1; m1 = nm1; }
+		w.mlive[l] = m0; w.mlive[l + 64] = m1;
+		__syncthreads();
+		return q;
 	}
 };
 
