@@ -559,7 +559,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 // kFused: the same wave walks its 64 problems right after their fill, while the
 // traceback bytes are still in the Infinity Cache; slots are per resident wave.
 template<bool kDebug, bool kFused>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 	// LDS: the last DP row (4 columns per dword) for candidate ordering.  12.8 KiB per wave.
 	__shared__ uint32_t lds[(kCols / 4) * 64];
@@ -588,9 +588,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const uint8_t* rf = a.refs + p.ref_off;
 		const int thr = (int)p.minsc + 0xff;
 		// ------------- row info (rows >= R: N, barred) ------------------------------
-		// 4 rows per dword, held in VGPRs for the whole fill (constant per problem)
+		// 4 rows per dword, in LDS for the whole fill (constant per problem; the region
+		// holds the last row after the fill)
 		const uint32_t kNone = row_info(7, true, npen);
-		uint32_t Info[kRowWords];
 #pragma unroll
 		for(int blk = 0; blk < kRowWords; blk++) {
 			uint32_t w = kNone * 0x01010101u;
@@ -610,7 +610,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 					w |= b << (8 * r);
 				}
 			}
-			Info[blk] = w;
+			lds[blk * 64 + lane] = w;
 		}
 		// ------------- fill: two columns per sweep, per-row state in VGPRs ------------
 		// H and E of the previous column, 4 rows per dword (40 dwords each for 160 rows).
@@ -633,10 +633,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			// hoisted out of the pair loop as 2 x 161 precomputed lane masks (SGPR spills)
 			int rmax = Rmax, rmin = Rmin, rl = R;
 			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl));
-			// opaque row info per pair: the per-step info pairs built from it would
-			// otherwise be hoisted out of the pair loop for all 161 steps (VGPR blow-up)
-#pragma unroll
-			for(int k = 0; k < kRowWords; k++) asm volatile("" : "+v"(Info[k]));
+			// row-info loads stay inside the pair (hoisted out of it they would hold all 40
+			// words in VGPRs)
+			asm volatile("" ::: "memory");
 			const int ca = refa, cb = refb;
 			refa = (j0 + 2 < C) ? rf[j0 + 2] : 4;      // prefetch the next pair's bases
 			refb = (j0 + 3 < C) ? rf[j0 + 3] : 4;
@@ -654,8 +653,8 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				if(st <= rmax) {                             // wave-uniform
 				const int blk = st >> 2, r = st & 3;
 				// --- operands: low half = (row st, col j0), high half = (row st-1, col j0+1)
-				const uint32_t iw = Info[blk < kRowWords ? blk : kRowWords - 1];
-				const uint32_t iv = Info[blk > 0 ? blk - 1 : 0];
+				const uint32_t iw = lds[(blk < kRowWords ? blk : kRowWords - 1) * 64 + lane];
+				const uint32_t iv = lds[(blk > 0 ? blk - 1 : 0) * 64 + lane];
 				uint32_t info = (st == 0) ? perm(0, iw, 0x0c0c0c00u)
 				              : (st == kRows) ? (perm(iw, 0, 0x0c070c0cu) | (kNone & 0xffu))
 				              : (r == 0) ? perm(iv, iw, 0x0c070c00u)
