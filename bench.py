@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--prep-only", action="store_true",
                     help="write the genome index and reads, print their paths, exit (profiling the aligner)")
-    ap.add_argument("--lookahead", type=int, default=16, help="bt2x-align --lookahead (DP problems posed per request)")
+    ap.add_argument("--lookahead", type=int, default=8, help="bt2x-align --lookahead (DP problems posed per request)")
     ap.add_argument("--slots", type=int, default=1 << 17,
                     help="bt2x-align --slots (reads in flight) of the end-to-end run; the launch-recording run "
                          "batches the whole --reads batch (--slots = --reads, --no-pipeline)")

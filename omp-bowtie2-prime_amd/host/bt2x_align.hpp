@@ -413,7 +413,7 @@ struct Params {
 	int tighten = 3;
 	uint32_t randSeed = 0;          // --seed
 	bool nofw = false, norc = false;
-	size_t lookahead = 16;          // DP problems posed per request (not a reference option;
+	size_t lookahead = 8;           // DP problems posed per request (not a reference option;
 	                                // results do not depend on it)
 	Params() {
 		bt2x_scoring_default(&sc);
