@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -22,6 +23,39 @@
 using namespace bt2x::host;
 
 namespace {
+
+// Page-locked blocks by power-of-two class, kept for reuse: pinning and unpinning cost
+// milliseconds per call (0.6 s of a 1 M-read run when the launch buffers grew through
+// hipHostMalloc/hipHostFree directly), so a freed block waits for the next request of
+// its class instead of going back to the driver.
+class PinnedCache {
+public:
+	static void* alloc(size_t n) { return inst().get(n); }
+	static void release(void* p) { inst().put(p); }
+private:
+	static constexpr size_t kHdr = 64;
+	static PinnedCache& inst() { static PinnedCache c; return c; }
+	void* get(size_t n) {
+		int cls = 12;
+		while(((size_t)1 << cls) < n + kHdr) cls++;
+		{
+			std::lock_guard<std::mutex> g(mu_);
+			if(!free_[cls].empty()) { void* p = free_[cls].back(); free_[cls].pop_back(); return p; }
+		}
+		uint8_t* b = static_cast<uint8_t*>(bt2x_host_alloc((size_t)1 << cls));
+		if(!b) return nullptr;
+		*reinterpret_cast<int*>(b) = cls;
+		return b + kHdr;
+	}
+	void put(void* p) {
+		uint8_t* b = static_cast<uint8_t*>(p) - kHdr;
+		const int cls = *reinterpret_cast<int*>(b);
+		std::lock_guard<std::mutex> g(mu_);
+		free_[cls].push_back(p);
+	}
+	std::mutex mu_;
+	std::vector<void*> free_[64];
+};
 
 // Product backend: every request kind is one bt2x C-ABI call on the context's GPU.
 class HipBackend : public Backend {
@@ -200,7 +234,7 @@ int main(int argc, char** argv) {
 		ref.init(index.desc(), idx);
 		bt2x::Device dev(device, index, p.sc);
 		HipBackend hip(dev.ctx());
-		set_host_allocator(bt2x_host_alloc, bt2x_host_free);     // launch buffers page-locked
+		set_host_allocator(PinnedCache::alloc, PinnedCache::release);   // launch buffers page-locked
 		std::unique_ptr<DumpBackend> dumper;
 		if(!dump.empty()) dumper.reset(new DumpBackend(hip, dump));
 		Backend& be = dumper ? static_cast<Backend&>(*dumper) : static_cast<Backend&>(hip);
