@@ -119,7 +119,7 @@ extern "C" void bt2x_scoring_default(bt2x_scoring* sc) {
 
 extern "C" void* bt2x_host_alloc(size_t bytes) {
 	void* p = nullptr;
-	if(hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+	if(hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
 	return p;
 }
 

@@ -1302,6 +1302,36 @@ void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, void* ringp) {
 	act.resize(w);
 }
 
+namespace {
+// Element counts of reserve_launch_buffers for a cohort of `reads`, generous for 150 bp
+// reads: half of them in a seed round (fw + rc, ~20 seeds, up to 64 elements each), all
+// of them in a DP request (3 problems of ~200 columns on average).
+struct LaunchSizes {
+	size_t nr, nd, np;
+	LaunchSizes(const Params& p, size_t reads)
+		: nr(reads / 2), nd(reads), np(reads * 3) {}
+};
+}
+
+std::vector<size_t> Aligner::launch_buffer_bytes(const Params& p, size_t reads) {
+	const LaunchSizes z(p, reads);
+	return {z.nr * 320, z.nr * 24 * sizeof(bt2x_seed_in), z.nr * sizeof(bt2x_round_in), z.nr * 4 * sizeof(bt2x_exrange),
+	        z.nr * sizeof(bt2x_round_out), z.nr * 64 * sizeof(bt2x_sat), z.nr * 64 * sizeof(bt2x_resolve_out),
+	        z.nr * 4 * sizeof(bt2x_exrange), z.nd * 320, z.nd * 320, z.np * 210, z.np * sizeof(bt2x_dp_in),
+	        z.np * sizeof(bt2x_dp_out), (z.np * 4 + 64) * sizeof(bt2x_aln_rec), (z.np * 48 + 256) * sizeof(uint32_t)};
+}
+
+void Aligner::reserve_launch_buffers(size_t reads) {
+	const LaunchSizes z(p_, reads);
+	for(Launch& L : launch_) {
+		L.round_reads.reserve(z.nr * 320); L.round_seeds.reserve(z.nr * 24); L.round_in.reserve(z.nr);
+		L.round_exr.reserve(z.nr * 4); L.round_out.reserve(z.nr); L.round_sats.reserve(z.nr * 64);
+		L.round_elts.reserve(z.nr * 64); L.round_exr_out.reserve(z.nr * 4);
+		L.dp_reads.reserve(z.nd * 320); L.dp_quals.reserve(z.nd * 320); L.dp_refs.reserve(z.np * 210);
+		L.dp_in.reserve(z.np); L.dp_out.reserve(z.np); L.recs.reserve(z.np * 4 + 64); L.edits.reserve(z.np * 48 + 256);
+	}
+}
+
 RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads, double* t_run) {
 	RunStats st;
 	use_threads(threads);
@@ -1315,6 +1345,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	OutRing ring;
 	SamWriter writer(out);
 	if(slots < 2) slots = 2;
+	reserve_launch_buffers(pipeline_ ? slots / 2 : slots);
 	// New reads join cohort `co` (up to `cap` reads in it): decoded and run up to their
 	// first request, in parallel.
 	auto refill = [&](std::vector<ReadCtx*>& co, size_t cap) {

@@ -876,6 +876,11 @@ public:
 	// seed rounds through bt2x_seed_round (default on; off: seed search, host ranking and
 	// prioritization, SA resolution as three requests)
 	void set_gpu_round(bool on) { gpu_round_ = on; }
+	// Size both launches' buffers for `reads` reads per launch up front: page-locked
+	// buffers cost milliseconds per allocation, so growing them launch by launch is slow.
+	void reserve_launch_buffers(size_t reads);
+	// The byte sizes reserve_launch_buffers asks for, per launch (to pre-allocate them).
+	static std::vector<size_t> launch_buffer_bytes(const Params& p, size_t reads);
 	Aligner(const Aligner&) = delete;
 	Aligner& operator=(const Aligner&) = delete;
 	// SAM header (@HD, @SQ; sam.cpp:47-80)
