@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 output of tools/profile_r01.sh into committed profile summaries.
+"""Turn rocprofv3 output of tools/profile_e2e.sh into committed profile summaries.
 
 Inputs (a gpurun_out/ tree): prof_kt/run_kernel_stats.csv (+ run_kernel_trace.csv),
 prof_fetch/run_counter_collection.csv (--pmc FETCH_SIZE), prof_write/... (WRITE_SIZE).
@@ -21,7 +21,8 @@ from collections import defaultdict
 
 # logical op -> the kernels one call launches (per-launch figures are summed over them)
 KERNELS = {"seed": ("seed_init_kernel", "seed_kernel"), "resolve": ("sa_resolve_kernel",),
-           "dp": ("dp_fill_kernel", "dp_walk_kernel", "dp_kernel")}
+           "round": ("round_prep_kernel", "round_sample_kernel"),
+           "dp": ("dp_fill_kernel", "dp_walk_kernel", "dp_wave_kernel", "dp_kernel")}
 
 
 def short(name: str) -> str | None:
