@@ -74,26 +74,19 @@ __device__ __forceinline__ u16x2 as2(uint32_t v) { return __builtin_bit_cast(u16
 __device__ __forceinline__ uint32_t as1(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ uint32_t psubs(uint32_t a, uint32_t b) { return as1(__builtin_elementwise_sub_sat(as2(a), as2(b))); }
 __device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) { return as1(__builtin_elementwise_max(as2(a), as2(b))); }
-__device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) {
-	uint32_t r;   // v_pk_min_u16 (the generic min of a 0/1 bound is lowered to compares)
-	asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-	return r;
-}
+// v_pk_min_u16.  A constant 0x00010001 bound would be lowered to compares, so callers
+// pass it in a register the optimizer cannot see through (`one2`, made opaque once).
+// No inline asm here: asm blocks get conservative hazard padding (an s_nop after each).
+__device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) { return as1(__builtin_elementwise_min(as2(a), as2(b))); }
 __device__ __forceinline__ uint32_t pmul(uint32_t a, uint32_t b) { return as1(as2(a) * as2(b)); }
 __device__ __forceinline__ uint32_t pmul_lo(uint32_t a, uint32_t b) {
 	uint32_t r; asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
 }
 __device__ __forceinline__ uint32_t pshr(uint32_t a, uint32_t sh) { return as1(as2(a) >> (u16x2){(unsigned short)sh, (unsigned short)sh}); }
-// per-half "not equal" flag, 0 or 1
-__device__ __forceinline__ uint32_t pne(uint32_t a, uint32_t b) { return pmin(a ^ b, 0x00010001u); }
+// per-half "not equal" flag, 0 or 1 (one2 = 0x00010001 in a register)
+__device__ __forceinline__ uint32_t pne(uint32_t a, uint32_t b, uint32_t one2) { return pmin(a ^ b, one2); }
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
-// (a << 1) | b and (a << 5) + b as single VOP3 ops (the generic forms get re-associated)
-__device__ __forceinline__ uint32_t shl1_or(uint32_t a, uint32_t b) {
-	uint32_t r; asm("v_lshl_or_b32 %0, %1, 1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
-}
-__device__ __forceinline__ uint32_t shl5_add(uint32_t a, uint32_t b) {
-	uint32_t r; asm("v_lshl_add_u32 %0, %1, 5, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
-}
+__device__ __forceinline__ uint32_t opaque(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
 
 enum { H_NONE = 0, H_DIAG = 1, H_REF_OPEN = 2, H_RFGAP_EXT = 3, H_READ_OPEN = 4, H_RDGAP_EXT = 5 };
 enum { EDIT_READ_GAP = 1, EDIT_REF_GAP = 2, EDIT_MM = 3 };
@@ -566,6 +559,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 	const int lane = threadIdx.x;
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0;
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
+	const uint32_t one2 = opaque(0x00010001u);
 
 	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
 		uint8_t* gslot = kFused ? a.scratch + (size_t)blockIdx.x * (kGroupBytes + kWalkSlotBytes)
@@ -676,7 +670,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				// row 0 has no F (low half at st 0, high half at st 1)
 				const uint32_t gbm = info & 0x00080008u;
 				const uint32_t r0 = (st == 0) ? 0x00000100u : (st == 1) ? 0x01000000u : 0u;
-				const uint32_t rdoe = shl5_add(gbm, rdo2), rfoe = shl5_add(gbm, rfo2 + r0), rfee = shl5_add(gbm, rfe2 + r0);
+				const uint32_t rdoe = (gbm << 5) + rdo2, rfoe = (gbm << 5) + (rfo2 + r0), rfee = (gbm << 5) + (rfe2 + r0);
 				const uint32_t d = psubs(hdiag, pen);
 				const uint32_t hl_o = psubs(hl, rdoe), el_e = psubs(el, rde2);
 				const uint32_t e = pmax(hl_o, el_e);
@@ -684,11 +678,11 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				const uint32_t f = pmax(hu_o, fu_e);
 				const uint32_t h = pmax(pmax(d, e), f);
 				// traceback flags
-				uint32_t tb = pmin(xrc, 0x00010001u);                 // TB_MM
-				tb = shl1_or(tb, pne(hl_o, e));                        // TB_EONE
-				tb = shl1_or(tb, pne(hu_o, f));                        // TB_FONE
-				tb = shl1_or(tb, pne(f, h));                           // TB_FNE
-				tb = shl1_or(tb, pne(d, h));                           // TB_DNE
+				uint32_t tb = pmin(xrc, one2);                        // TB_MM
+				tb = (tb << 1) | pne(hl_o, e, one2);                   // TB_EONE
+				tb = (tb << 1) | pne(hu_o, f, one2);                   // TB_FONE
+				tb = (tb << 1) | pne(f, h, one2);                      // TB_FNE
+				tb = (tb << 1) | pne(d, h, one2);                      // TB_DNE
 				if(kDebug && a.digests) {
 					if(st < R && j0 < C) {
 						dg0 += cell_digest(st, j0, 0, e & 0xffffu);
@@ -784,8 +778,8 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				const uint32_t cq = (uint32_t)q * 0x40004u + 0x10000u;     // cols 4q, 4q+1
 				const uint32_t ka = perm(cq, w4, 0x01060004u);             // [4q, s0, 4q+1, s1]
 				const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);  // [4q+2, s2, 4q+3, s3]
-				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), 0x00010001u), ka));
-				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), 0x00010001u), kb));
+				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
+				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
 			}
 			const int best = (int)max(best2 & 0xffffu, best2 >> 16);
 			cur_key = best;
