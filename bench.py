@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
                     help="OpenMP threads of the reference CPU baseline (the box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--replay-ablate", type=int, default=0,
+                    help="profiling only: BT2X_DP_ABLATE for the replay (1: DP fill without the walk); outputs invalid")
     ap.add_argument("--prep-only", action="store_true",
                     help="write the genome index and reads, print their paths, exit (profiling the aligner)")
     ap.add_argument("--lookahead", type=int, default=8, help="bt2x-align --lookahead (DP problems posed per request)")
@@ -329,6 +331,8 @@ def main():
     mark(f"{len(launches)} launches loaded")
 
     # ---- 2. replay the launch sequence from HBM
+    if args.replay_ablate:
+        os.environ["BT2X_DP_ABLATE"] = str(args.replay_ablate)
     if world == 1 or backend != "nccl":
         torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)

@@ -142,7 +142,6 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
                                              bt2x_aln_rec* stage_rec, unsigned long long& st_bt) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 	const uint32_t gl = (uint32_t)lane;
-	const uint8_t* dir8 = gslot + kDirOff;
 	const __amdgpu_buffer_rsrc_t dirsrc =
 		__builtin_amdgcn_make_buffer_rsrc(gslot + kDirOff, 0, (int)(kDirBytesLane * 64u), 0x00020000);
 	const uint8_t* cands = gslot + kCandOff;
@@ -156,6 +155,14 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 		const int ncand = o.ncand;
 		const int row0 = R - 1;
 		int ndone = 0, nrec = 0;
+		// Candidate starts are fetched ahead: the next candidate's column two attempts early
+		// and its start byte one attempt early.  A byte fetched before the attempt in
+		// between reflects every earlier attempt's marks; that attempt's own marks in the
+		// start row are the columns [mlo, mhi] it left behind (start-row moves go left only).
+		int c_next = cands[gl];
+		uint32_t b_next = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)tb_addr(row0, c_next, gl), 0, 0);
+		int c_next2 = ncand > 1 ? cands[64 + gl] : 0;
+		int mlo = 1, mhi = 0;                                  // last attempt's start-row marks
 		// stage_ed doubles as the reference's per-read edit buffer (SwResult::alres.ned_,
 		// bt2x.h "edit-buffer image"): attempts write it from index 0, a success leaves its
 		// final list there; hi = entries written during the current call.
@@ -163,23 +170,31 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 			int ntries = 0, hi = 0;
 			bool found = false;
 			while(ndone < ncand) {
-				const int col0 = cands[(size_t)ndone * 64 + gl];
+				const int col0 = c_next;
+				uint32_t tb = b_next;
+				if(col0 >= mlo && col0 <= mhi) tb = TB_MARK;
 				ndone++;
+				if(ndone < ncand) {
+					c_next = c_next2;
+					b_next = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)tb_addr(row0, c_next, gl), 0, 0);
+					if(ndone + 1 < ncand) c_next2 = cands[(size_t)(ndone + 1) * 64 + gl];
+				}
+				mlo = 1; mhi = 0;
 				// candidate start cell already traversed -> skipped, no RNG draw
-				if(dir8[tb_addr(row0, col0, gl)] & TB_MARK) continue;
+				if(tb & TB_MARK) continue;
 				ntries++;
 				if(a.ablate == 2) continue;          // profiling: no backtrace walks
 				// ------------- backtraceNucleotidesEnd2EndSseU8 -------------
 				int row = row0, col = col0, ct = 2 /*H*/, bscore = 0, ns = 0, gaps = 0, ne = 0;
 				bool over_core = false, ok = true;
 				uint32_t tb_end = 0;
+				mlo = col0; mhi = col0;
 				// One dependent load per step: the next cell's byte is issued before this
 				// cell's mark store, so the in-order vmcnt never waits on a store.  Moves are
 				// decided branch-free and the byte offset is updated incrementally (32-bit,
 				// buffer addressing); read/reference/quality bytes only where TB_MM says an
 				// edit is recorded.
 				uint32_t bo = (uint32_t)tb_addr(row, col, gl);
-				uint32_t tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)bo, 0, 0);
 				while(true) {
 					st_bt++;
 					if(tb & TB_MARK) { ok = false; break; }         // reportedThrough
@@ -211,6 +226,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 					const uint32_t ctb = tb;
 					tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)bo, 0, 0);
 					__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)cbo, 0, 0);   // setReportedThrough
+					if(crow == row0) mlo = ccol;
 					if(isD) {
 						if(ctb & TB_MM) {
 							const int rdc = rd[crow], refc = rf[ccol];
