@@ -87,7 +87,10 @@ public:
 		out.resize(n);
 		// arenas sized from the last launch's use per read (grown and retried on overflow)
 		uint32_t used[3] = {0, 0, 0};
-		uint32_t cap[3] = {(uint32_t)(sat_per_read_ * n) + 1024, (uint32_t)(elt_per_read_ * n) + 1024, 4 * n + 256};
+		// (at least the buffers' reserved capacity: a retry re-runs the whole round)
+		uint32_t cap[3] = {(uint32_t)std::max<size_t>((size_t)(sat_per_read_ * n) + 1024, sats.capacity()),
+		                   (uint32_t)std::max<size_t>((size_t)(elt_per_read_ * n) + 1024, elts.capacity()),
+		                   (uint32_t)std::max<size_t>(4 * (size_t)n + 256, exr_out.capacity())};
 		for(int attempt = 0; attempt < 2; attempt++) {
 			sats.resize(cap[0]); elts.resize(cap[1]); exr_out.resize(cap[2]);
 			const int rc = bt2x_seed_round(ctx_, reads.data(), reads.size(), seeds.data(), (uint32_t)seeds.size(), in.data(),
@@ -95,6 +98,7 @@ public:
 			                               elts.data(), cap[1], exr_out.data(), cap[2], used);
 			if(rc == BT2X_E_OVERFLOW && attempt == 0) {
 				for(int k = 0; k < 3; k++) cap[k] = std::max(cap[k], used[k]);
+				gs.retries++;
 				continue;
 			}
 			bt2x::check(rc, "bt2x_seed_round");
@@ -119,7 +123,8 @@ public:
 		const auto t0 = std::chrono::steady_clock::now();
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
-		uint32_t rec_cap = 4 * n + 64, edit_cap = 48 * n + 256;
+		uint32_t rec_cap = (uint32_t)std::max<size_t>(4 * (size_t)n + 64, recs.capacity()),
+		         edit_cap = (uint32_t)std::max<size_t>(48 * (size_t)n + 256, edits.capacity());
 		for(int attempt = 0; attempt < 2; attempt++) {
 			recs.resize(rec_cap);
 			edits.resize(edit_cap);
@@ -127,7 +132,7 @@ public:
 			const int rc = bt2x_dp_align(ctx_, reads.data(), reads.size(), quals.data(), quals.size(),
 			                             refs.data(), refs.size(), in.data(), n, out.data(), recs.data(), rec_cap,
 			                             &nrec, edits.data(), edit_cap, &ned, nullptr);
-			if(rc == BT2X_E_OVERFLOW && attempt == 0) { rec_cap = nrec; edit_cap = ned; continue; }
+			if(rc == BT2X_E_OVERFLOW && attempt == 0) { rec_cap = nrec; edit_cap = ned; gs.retries++; continue; }
 			bt2x::check(rc, "bt2x_dp_align");
 			recs.resize(nrec);
 			edits.resize(ned);
@@ -140,7 +145,7 @@ public:
 	}
 	struct GpuStats {                      // kernel time and bytes over PCIe, per request kind
 		double k_round_ms = 0, k_dp_ms = 0, t_round_call = 0, t_dp_call = 0;
-		uint64_t round_h2d = 0, round_d2h = 0, dp_h2d = 0, dp_d2h = 0;
+		uint64_t round_h2d = 0, round_d2h = 0, dp_h2d = 0, dp_d2h = 0, retries = 0;
 	} gs;
 private:
 	bt2x_ctx* ctx_;
@@ -305,9 +310,9 @@ int main(int argc, char** argv) {
 		if(stats) {
 			const HipBackend::GpuStats& g = hip.gs;
 			std::fprintf(stderr, "BT2X_GPU k_round=%.4f t_round_call=%.4f round_h2d_mib=%.1f round_d2h_mib=%.1f "
-			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f\n", g.k_round_ms * 1e-3, g.t_round_call,
+			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f retries=%llu\n", g.k_round_ms * 1e-3, g.t_round_call,
 			             g.round_h2d / 1048576.0, g.round_d2h / 1048576.0, g.k_dp_ms * 1e-3, g.t_dp_call,
-			             g.dp_h2d / 1048576.0, g.dp_d2h / 1048576.0);
+			             g.dp_h2d / 1048576.0, g.dp_d2h / 1048576.0, (unsigned long long)g.retries);
 		}
 	} catch(const std::exception& e) {
 		std::fprintf(stderr, "bt2x-align: %s\n", e.what());
