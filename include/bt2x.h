@@ -188,7 +188,13 @@ typedef struct {
  * recs[rec_off .. rec_off + nrec). */
 typedef struct {
 	int32_t  status;         /* align() return value                            */
-	int32_t  best;           /* best score out of align(); INT32_MIN if saturated */
+	int32_t  best;           /* best score out of align(); INT32_MIN if saturated.
+	                          * Exact whenever status != 0.  With the banded fill
+	                          * (default; BT2X_DP_BAND=0 turns it off) a failed
+	                          * problem's best is <= the reference's and < minsc:
+	                          * cells no path scoring >= minsc can use are not
+	                          * computed.  The reference reads it only into the
+	                          * off-by-default Xs:i tag (aligner_sw_driver.cpp:515). */
 	uint16_t ncand;          /* btncand_.size()                                  */
 	uint16_t nrec;
 	uint32_t rec_off;

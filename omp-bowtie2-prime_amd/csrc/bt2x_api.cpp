@@ -441,6 +441,7 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	a.cands = d_debug ? d_debug->cands : nullptr;
 	a.scratch = (uint8_t*)c->scratch.p; a.chunk_groups = groups; a.ncu = c->ncu; a.queue = c->d_queue;
 	{ const char* ab = getenv("BT2X_DP_ABLATE"); a.ablate = (ab && *ab >= '1' && *ab <= '2') ? (uint32_t)(*ab - '0') : 0u; }
+	{ const char* bd = getenv("BT2X_DP_BAND"); a.band = (bd && bd[0] == '0') ? 0u : 1u; }
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));

@@ -91,6 +91,7 @@ struct DpLaunch {
 	int ncu;                       // compute units (persistent grid sizing)
 	uint32_t* queue;               // walk-kernel problem queue counter (device)
 	uint32_t ablate;               // profiling only: 1 = stop after the fill, 2 = no backtrace walks (outputs invalid)
+	uint32_t band;                 // 1: lane-kernel fill restricted to the exact diagonal band (dp_kernel.hip)
 };
 size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups);
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream);

@@ -633,6 +633,34 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const uint32_t rdo2 = (uint32_t)rdo * 0x10001u, rde2 = (uint32_t)rde * 0x10001u;
 		const uint32_t rfo2 = (uint32_t)rfo * 0x10001u, rfe2 = (uint32_t)rfe * 0x10001u;
 		const uint32_t npen2 = (uint32_t)npen * 0x10001u;
+		// Diagonal band (exact).  A path from row 0 to row R-1 scoring >= minsc
+		// pays for at most G gap positions (every gap position costs >= the cheapest extension,
+		// the first of a run >= the cheapest open), so it stays inside diagonals [-G, C-R+G]:
+		// it starts on a diagonal >= 0 (row 0, col >= 0), ends on one <= C-R, and each gap
+		// moves it by one.  Only cells of such paths reach a candidate's score, flags and
+		// backtrace (a cell whose every optimal prefix leaves the band is on no candidate's
+		// path), so the fill computes each column's rows [j-(C-R+G)-M, j+G+M] (M = 2 extra
+		// diagonals); cells outside hold "dead" zeros (<= their true values, so no computed
+		// value exceeds the reference's).  The wave sweeps the union of its lanes' windows:
+		// per column pair, steps [j0 - wdhi, j0 + wdlo], clipped to [0, Rmax]; both ends move
+		// down monotonically, so state rows entering at the bottom were never written (zero)
+		// and rows above the top are never read again.  Cells below minsc in the last row may
+		// then report a lower `best` (status 0 only); candidates, records and edits are the
+		// full fill's.  kDebug (E/F/H digests) and band = 0 fill the whole rectangle.
+		int wdhi = 1 << 20, wdlo = 1 << 20;
+		if(!kDebug && a.band) {
+			const int mo = imax(1, rdo < rfo ? rdo : rfo);
+			int me = rde < rfe ? rde : rfe;
+			me = me < mo ? me : mo;
+			const int budget = -(int)p.minsc;                     // cost a candidate may pay
+			int G = (me <= 0) ? (1 << 16) : (budget < mo ? 0 : 1 + (budget - mo) / me);
+			G = G > (1 << 16) ? (1 << 16) : G;
+			constexpr int kBandMargin = 2;
+			const int dh = active ? (C - R) + G + kBandMargin : -(1 << 20);
+			const int dl = active ? G + kBandMargin + 2 : -(1 << 20);
+			wdhi = __builtin_amdgcn_readfirstlane(wave_max(dh));
+			wdlo = __builtin_amdgcn_readfirstlane(wave_max(dl));
+		}
 		const int npairs = (Cmax + 1) >> 1;
 		const __amdgpu_buffer_rsrc_t dirsrc =
 			__builtin_amdgcn_make_buffer_rsrc(dir, 0, (int)(kDirBytesLane * 64u), 0x00020000);
@@ -642,7 +670,10 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			// opaque per pair: keeps the per-step guards and last-row compares from being
 			// hoisted out of the pair loop as 2 x 161 precomputed lane masks (SGPR spills)
 			int rmax = Rmax, rmin = Rmin, rl = R;
-			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl));
+			int slo = j0 - wdhi, shi = j0 + wdlo;           // this pair's step window (band)
+			slo = slo < 0 ? 0 : slo;
+			shi = shi > rmax ? rmax : shi;
+			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl), "+s"(slo), "+s"(shi));
 			// row-info loads stay inside the pair (hoisted out of it they would hold all 40
 			// words in VGPRs)
 			asm volatile("" ::: "memory");
@@ -660,7 +691,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			int lra = 0, lrb = 0;                           // H[R-1][j0], H[R-1][j0+1]
 #pragma unroll
 			for(int st = 0; st < kSteps; st++) {
-				if(st <= rmax) {                             // wave-uniform
+				if(st >= slo && st <= shi) {                             // wave-uniform
 				const int blk = st >> 2, r = st & 3;
 				// --- operands: low half = (row st, col j0), high half = (row st-1, col j0+1)
 				const uint32_t iw = lds[(blk < kRowWords ? blk : kRowWords - 1) * 64 + lane];
@@ -729,7 +760,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 					                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
 				} else {
 					tbacc = tb;
-					if(st == rmax)
+					if(st == shi)
 						__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, lane * 4,
 						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
 				}

@@ -130,7 +130,7 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
             out, recs, edits = ctx.dp_align(rd, qu, rf, dp, debug=False)[:3]
         finally:
             del os.environ["BT2X_DP_WAVE"]
-        np.testing.assert_array_equal(out[["status", "best", "ncand", "nrec"]], eo[["status", "best", "ncand", "nrec"]])
+        _compare_out(out, eo, dp, banded=(wave == "0"))
         for i in np.nonzero(out["nrec"] * sel)[0]:
             a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
             b = erecs[eo["rec_off"][i]: eo["rec_off"][i] + eo["nrec"][i]]
@@ -210,7 +210,11 @@ def test_cpp_host_shims_match_golden(golden_dir, tmp_path, gold, mode, limit):
     for i, (_, a, ns) in enumerate(recs):
         ga, gn = got[i]
         k = 4 if mode == "batch" else 3
-        assert ga[:k] == a[:k], (i, ga, a)
+        if a[1] == "1":
+            assert ga[:k] == a[:k], (i, ga, a)
+        else:
+            # a failed align(): the banded fill's best may be lower (dp_kernel.hip, _compare_out)
+            assert ga[1] == a[1] and ga[3:k] == a[3:k] and int(ga[2]) <= int(a[2]), (i, ga, a)
         assert gn == ns, (i, gn, ns)
         ncalls += len(ns)
     assert ncalls > 0
@@ -290,8 +294,23 @@ def _random_dp_problems(n, seed):
     return np.concatenate(rd), np.concatenate(qu), np.concatenate(rf), inp
 
 
-def _compare_dp(out, recs, edits, eo, erecs, eedits):
-    np.testing.assert_array_equal(out[["status", "best", "ncand", "nrec"]], eo[["status", "best", "ncand", "nrec"]])
+def _compare_out(out, eo, inp, banded):
+    """align() verdicts.  The banded production fill (dp_kernel.hip, BT2X_DP_BAND) computes
+    only cells a path scoring >= minsc can use, so `best` of a failed problem (status 0)
+    may come out lower than the reference's, and stays below minsc; everything else is
+    exact."""
+    np.testing.assert_array_equal(out[["status", "ncand", "nrec"]], eo[["status", "ncand", "nrec"]])
+    if not banded:
+        np.testing.assert_array_equal(out["best"], eo["best"])
+        return
+    ok = eo["status"] == 1
+    np.testing.assert_array_equal(out["best"][ok], eo["best"][ok])
+    assert (out["best"][~ok] <= eo["best"][~ok]).all()
+    assert (out["best"][~ok] < inp["minsc"][~ok].astype(np.int32)).all()
+
+
+def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, banded):
+    _compare_out(out, eo, inp, banded)
     fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff"]
     for i in np.nonzero(out["nrec"])[0]:
         a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
@@ -302,18 +321,20 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits):
                                           eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
 
 
-@pytest.mark.parametrize("debug,wave", [(False, "0"), (False, "1"), (True, "0")])
-def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, monkeypatch):
-    """Production (debug=False; lane-per-problem and wave-per-problem modes) and debug
-    kernels on random shapes/penalty thresholds at the ABI limits vs the oracle: statuses,
-    candidates, every nextAlignment record and edit."""
+@pytest.mark.parametrize("debug,wave,band", [(False, "0", "1"), (False, "0", "0"), (False, "1", "1"),
+                                             (True, "0", "1")])
+def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, monkeypatch):
+    """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
+    wave-per-problem mode) and debug kernels on random shapes/penalty thresholds at the ABI
+    limits vs the oracle: statuses, candidates, every nextAlignment record and edit."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
+    monkeypatch.setenv("BT2X_DP_BAND", band)
     rd, qu, rf, inp = _random_dp_problems(6000, seed=77 + int(debug))
     ctx = ctxs["rep"][0]
     res = ctx.dp_align(rd, qu, rf, inp, debug=debug)
     eo, erecs, eedits, edig, ecands, _ = ol.dp_align(ol.default_scoring(), rd, qu, rf, inp)
     out, recs, edits = res[0], res[1], res[2]
-    _compare_dp(out, recs, edits, eo, erecs, eedits)
+    _compare_dp(out, recs, edits, eo, erecs, eedits, inp, banded=(not debug and wave == "0" and band == "1"))
     if debug:
         np.testing.assert_array_equal(res[3], edig)
         np.testing.assert_array_equal(res[4], ecands)
@@ -329,7 +350,7 @@ def test_dp_production_kernel_on_golden(ctxs, wave, monkeypatch):
     ctx = ctxs["rep"][0]
     out, recs, edits = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
     eo, erecs, eedits, _, _, _ = ol.dp_align(ol.default_scoring(), case.reads, case.quals, case.refs, case.inp)
-    _compare_dp(out, recs, edits, eo, erecs, eedits)
+    _compare_dp(out, recs, edits, eo, erecs, eedits, case.inp, banded=(wave == "0"))
 
 
 def test_empty_batches(ctxs):
