@@ -671,7 +671,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			// hoisted out of the pair loop as 2 x 161 precomputed lane masks (SGPR spills)
 			int rmax = Rmax, rmin = Rmin, rl = R;
 			int slo = j0 - wdhi, shi = j0 + wdlo;           // this pair's step window (band)
-			slo = slo < 0 ? 0 : slo;
+			slo = slo < 0 ? 0 : (slo & ~3);
 			shi = shi > rmax ? rmax : shi;
 			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl), "+s"(slo), "+s"(shi));
 			// row-info loads stay inside the pair (hoisted out of it they would hold all 40
@@ -690,8 +690,13 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			uint32_t tbacc = 0;
 			int lra = 0, lrb = 0;                           // H[R-1][j0], H[R-1][j0+1]
 #pragma unroll
-			for(int st = 0; st < kSteps; st++) {
-				if(st >= slo && st <= shi) {                             // wave-uniform
+			// the window is widened to whole 4-step blocks at its top: a skipped block costs one
+			// scalar branch (the extra rows are outside every lane's band: any values do)
+			for(int b4 = 0; b4 < kSteps; b4 += 4) {
+			if(b4 >= slo && b4 <= shi) {                                 // wave-uniform
+#pragma unroll
+			for(int st = b4; st < b4 + 4 && st < kSteps; st++) {
+				if(st <= shi) {                                          // wave-uniform
 				const int blk = st >> 2, r = st & 3;
 				// --- operands: low half = (row st, col j0), high half = (row st-1, col j0+1)
 				const uint32_t iw = lds[(blk < kRowWords ? blk : kRowWords - 1) * 64 + lane];
@@ -766,6 +771,8 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				}
 				hlp = hl; hp = h; fp = f; ep = e;
 				}
+			}
+			}
 			}
 			if(j0 < C) {
 				lastrow[(size_t)j0 * 64 + lane] = (uint8_t)lra;
