@@ -672,7 +672,8 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			int rmax = Rmax, rmin = Rmin, rl = R;
 			int slo = j0 - wdhi, shi = j0 + wdlo;           // this pair's step window (band)
 			slo = slo < 0 ? 0 : (slo & ~3);
-			shi = shi > rmax ? rmax : shi;
+			shi = (shi > rmax ? rmax : shi) | 3;            // whole blocks (steps past Rmax: unused rows)
+			shi = shi > kSteps - 1 ? kSteps - 1 : shi;
 			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl), "+s"(slo), "+s"(shi));
 			// row-info loads stay inside the pair (hoisted out of it they would hold all 40
 			// words in VGPRs)
@@ -690,13 +691,14 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			uint32_t tbacc = 0;
 			int lra = 0, lrb = 0;                           // H[R-1][j0], H[R-1][j0+1]
 #pragma unroll
-			// the window is widened to whole 4-step blocks at its top: a skipped block costs one
-			// scalar branch (the extra rows are outside every lane's band: any values do)
+			// the window is widened to whole 4-step blocks: a skipped block costs one scalar
+			// branch and a computed one none (the extra rows are outside every lane's band, or
+			// past its read: any values do)
 			for(int b4 = 0; b4 < kSteps; b4 += 4) {
 			if(b4 >= slo && b4 <= shi) {                                 // wave-uniform
 #pragma unroll
 			for(int st = b4; st < b4 + 4 && st < kSteps; st++) {
-				if(st <= shi) {                                          // wave-uniform
+				{
 				const int blk = st >> 2, r = st & 3;
 				// --- operands: low half = (row st, col j0), high half = (row st-1, col j0+1)
 				const uint32_t iw = lds[(blk < kRowWords ? blk : kRowWords - 1) * 64 + lane];
