@@ -194,6 +194,34 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				// decided branch-free and the byte offset is updated incrementally (32-bit,
 				// buffer addressing); read/reference/quality bytes only where TB_MM says an
 				// edit is recorded.
+				// The bottom gap-barrier rows (R-gapbar .. R-1) hold no E or F (open and extend
+				// are barred there, E[i][0] = 0), so every cell there has h == d and the walk
+				// moves diagonally; and no earlier attempt has marked these cells (an attempt
+				// enters them only from its own start cell, and each start column is tried
+				// once).  Those moves need no traceback byte: only their mismatch edits, from
+				// independent loads of read and reference bytes.  Their marks are never read,
+				// so they are not written.
+				const int kb = min(min(sc.gapbar, row0), col0);
+				if(kb > 0) {
+					const int diag = col0 - row0 + (int)p.triml;
+					over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);
+					for(int t = 0; t < kb; t++) {
+						const int crow = row0 - t, ccol = col0 - t;
+						const int rdc = rd[crow], refc = rf[ccol];
+						if(rdc != refc || rdc > 3 || refc > 3) {
+							const bool amb = rdc > 3 || refc > 3;
+							const int q0 = (int)qu[crow] - 33;
+							const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
+							stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(refc), acgtn(rdc));
+							ne++;
+							bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
+							if(amb) ns++;
+						}
+					}
+					st_bt += (unsigned long long)kb;
+					row -= kb; col -= kb;
+					tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)tb_addr(row, col, gl), 0, 0);
+				}
 				uint32_t bo = (uint32_t)tb_addr(row, col, gl);
 				while(true) {
 					st_bt++;
