@@ -929,11 +929,16 @@ static int blocks_per_cu(const void* fn) {
 
 // DP modes: fused (default): one persistent kernel fills and walks each group (the walk
 // reads bytes written moments ago); split: fill kernel over a chunk, then a walk kernel.
-static bool dp_split_mode() {
+static int dp_mode() {                          // 0 fused, 1 split, 2 concurrent split
 	static int m = -1;
-	if(m < 0) { const char* e = getenv("BT2X_DP_MODE"); m = (e && e[0] == 's') ? 1 : 0; }
-	return m == 1;
+	if(m < 0) { const char* e = getenv("BT2X_DP_MODE"); m = (e && e[0] == 's') ? 1 : (e && e[0] == 'c') ? 2 : 0; }
+	return m;
 }
+static bool dp_split_mode() { return dp_mode() != 0; }
+// Concurrent split mode: chunks of kConcGroups groups, double-buffered; the fill of chunk
+// i+1 (2 waves/SIMD) runs beside the walk of chunk i (second stream, low-VGPR kernel), so
+// the walks' load latency no longer holds fill issue slots.
+constexpr uint32_t kConcGroups = 1024;
 
 // Largest launch run one wave per problem (BT2X_DP_WAVE=0: never, =1: always; else
 // BT2X_DP_WAVE_MAX problems, default 32768: below that a lane-per-problem launch does not
@@ -953,6 +958,10 @@ size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups) {
 		return (size_t)ncu * nb * (kGroupBytes + kWalkSlotBytes);
 	}
 	const size_t walk_slots = (size_t)ncu * blocks_per_cu((const void*)dp_walk_kernel);
+	if(dp_mode() == 2) {
+		const uint32_t cg = chunk_groups < kConcGroups ? chunk_groups : kConcGroups;
+		return 2 * (size_t)cg * kGroupBytes + walk_slots * kWalkSlotBytes;
+	}
 	return (size_t)chunk_groups * kGroupBytes + walk_slots * kWalkSlotBytes;
 }
 
@@ -986,6 +995,48 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		if(fb > groups_all) fb = groups_all;
 		if(dbg) hipLaunchKernelGGL((dp_fill_kernel<true, true>), dim3(fb), dim3(64), 0, s, sc, a, 0u, a0.n);
 		else hipLaunchKernelGGL((dp_fill_kernel<false, true>), dim3(fb), dim3(64), 0, s, sc, a, 0u, a0.n);
+		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+	}
+	if(dp_mode() == 2) {
+		static hipStream_t s2[64];
+		static hipEvent_t evf[64][2], evw[64][2], evj[64];
+		int dev = 0;
+		if(hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BT2X_E_NODEVICE;
+		if(!s2[dev]) {
+			if(hipStreamCreateWithFlags(&s2[dev], hipStreamNonBlocking) != hipSuccess) return BT2X_E_NODEVICE;
+			for(int b = 0; b < 2; b++) {
+				hipEventCreateWithFlags(&evf[dev][b], hipEventDisableTiming);
+				hipEventCreateWithFlags(&evw[dev][b], hipEventDisableTiming);
+			}
+			hipEventCreateWithFlags(&evj[dev], hipEventDisableTiming);
+		}
+		const uint32_t cg = a0.chunk_groups < kConcGroups ? a0.chunk_groups : kConcGroups;
+		a.walk_scratch = a0.scratch + 2 * (size_t)cg * kGroupBytes;
+		const uint32_t chunk = cg * 64;
+		hipEventRecord(evj[dev], s);                       // the walk stream starts after prior work
+		hipStreamWaitEvent(s2[dev], evj[dev], 0);
+		uint32_t i = 0;
+		for(uint32_t base = 0; base < a0.n; base += chunk, i++) {
+			const uint32_t np = (a0.n - base < chunk) ? a0.n - base : chunk;
+			const uint32_t groups = (np + 63) / 64;
+			const int b = (int)(i & 1);
+			DpLaunch ai = a;
+			ai.scratch = a0.scratch + (size_t)b * cg * kGroupBytes;
+			if(i >= 2) hipStreamWaitEvent(s, evw[dev][b], 0);   // chunk i-2's walk left the buffer
+			uint32_t fb = (uint32_t)a0.ncu * 8u;               // 2 waves per SIMD
+			if(fb > groups) fb = groups;
+			if(dbg) hipLaunchKernelGGL((dp_fill_kernel<true, false>), dim3(fb), dim3(64), 0, s, sc, ai, base, np);
+			else hipLaunchKernelGGL((dp_fill_kernel<false, false>), dim3(fb), dim3(64), 0, s, sc, ai, base, np);
+			hipEventRecord(evf[dev][b], s);
+			if(a0.ablate == 1) continue;
+			hipStreamWaitEvent(s2[dev], evf[dev][b], 0);
+			uint32_t wb = (uint32_t)a0.ncu * 8u;
+			if(wb > groups) wb = groups;
+			hipLaunchKernelGGL(dp_walk_kernel, dim3(wb), dim3(64), 0, s2[dev], sc, ai, base, np);
+			hipEventRecord(evw[dev][b], s2[dev]);
+		}
+		hipEventRecord(evj[dev], s2[dev]);
+		hipStreamWaitEvent(s, evj[dev], 0);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
 	a.walk_scratch = a0.scratch + (size_t)a0.chunk_groups * kGroupBytes;
