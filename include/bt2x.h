@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define BT2X_ABI_VERSION 1
+#define BT2X_ABI_VERSION 2
 
 enum {
 	BT2X_OK = 0,
@@ -132,7 +132,12 @@ typedef struct {
 	uint64_t dp_cols;     /* C summed                         */
 	uint64_t bt_cells;    /* backtrace cells visited          */
 	uint64_t n_problems;
-	uint64_t alg_bytes;   /* algorithmic HBM bytes of the launch */
+	uint64_t alg_bytes;   /* algorithmic HBM bytes of the launch: for the DP, the
+	                         traceback bytes the kernel writes (dp_cells_computed) plus
+	                         the reference windows; SURVEY §8(d)'s reference-equivalent
+	                         figure is 3*dp_cells + dp_cols + profile bytes */
+	uint64_t dp_cells_computed; /* DP cells the fill computed (the diagonal band, or the
+	                         whole rectangle when unbanded), <= dp_cells */
 } bt2x_counters;
 int bt2x_last_counters(const bt2x_ctx* ctx, int kernel, bt2x_counters* out);
 /* The last seed round's sampling work (bt2x_seed_round[_dev]): out[0] reads, out[1] reads
@@ -169,7 +174,16 @@ int bt2x_seed_search_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const bt2x_seed_
 
 /* One end-to-end DP problem, i.e. SwAligner state after initRead + initRef
  * (aligner_sw.cpp:35-229): oriented read codes/qualities (rd_/qu_), reference window
- * codes (0-4; rf_ before the 1<<c mask step) of ncol columns, DPRect fields. */
+ * codes (0-4; rf_ before the 1<<c mask step) of ncol columns, DPRect fields.
+ *
+ * flags & BT2X_DP_I16 selects the signed 16-bit kernel, i.e. SwAligner::initRef's
+ * enable8_ == false in a -DENABLE_I16 build (aligner_sw.cpp:77-83: enable8 && minsc >=
+ * -254): alignEnd2EndSseI16 (aligner_swsse_ee_i16.cpp:548-676) instead of the u8 one.
+ * Scores then live in [0x8000, 0x7fff] (0x7fff = score 0, no saturation before -65535),
+ * minsc is not clamped (it must be >= -32767, the field's range), align()'s best is the
+ * reference's lrmax - 0xff of the i16 value (aligner_swsse_ee_i16.cpp:645), and every
+ * attempted candidate consumes {reseed = rnd.nextU32()+1; rnd.init(reseed);} instead of
+ * the u8 path's rnd.init(reseed+1) (aligner_sw.cpp:336-348; bt2x_aln_rec.ntries). */
 typedef struct {
 	uint64_t read_off;       /* reads[read_off .. +rdlen): codes 0-4            */
 	uint64_t qual_off;       /* quals[qual_off .. +rdlen): Phred+33 characters  */
@@ -181,20 +195,25 @@ typedef struct {
 	int16_t  nceil;          /* max Ns in the reference portion                 */
 	uint16_t triml, corel, corer;
 	uint8_t  fw;             /* orientation: rc results get invertEdits()       */
-	uint8_t  pad;
+	uint8_t  flags;          /* BT2X_DP_I16                                      */
 } bt2x_dp_in;
+#define BT2X_DP_I16 1u
 
 /* Result of align() for one problem.  Its nextAlignment() call sequence is
  * recs[rec_off .. rec_off + nrec). */
 typedef struct {
 	int32_t  status;         /* align() return value                            */
-	int32_t  best;           /* best score out of align(); INT32_MIN if saturated.
-	                          * Exact whenever status != 0.  With the banded fill
-	                          * (default; BT2X_DP_BAND=0 turns it off) a failed
-	                          * problem's best is <= the reference's and < minsc:
-	                          * cells no path scoring >= minsc can use are not
-	                          * computed.  The reference reads it only into the
-	                          * off-by-default Xs:i tag (aligner_sw_driver.cpp:515). */
+	int32_t  best;           /* best score out of align() (u8: lrmax - 0xff; i16: the
+	                          * reference's lrmax - 0xff of the int16 value);
+	                          * INT32_MIN if saturated.  Exact whenever status != 0,
+	                          * and for failed problems too with BT2X_OPT_EXACT_BEST
+	                          * (the default).  Without it a failed problem of a
+	                          * launch the banded lane kernel runs may report a lower
+	                          * best (still < minsc): the fill skips cells no path
+	                          * scoring >= minsc can use.  The reference copies a failed
+	                          * problem's best into prm.bestLtMinscMate1
+	                          * (aligner_sw_driver.cpp:515-517), printed by ZT:Z under
+	                          * --mapq-extra (sam.cpp:519-544). */
 	uint16_t ncand;          /* btncand_.size()                                  */
 	uint16_t nrec;
 	uint32_t rec_off;
@@ -237,10 +256,14 @@ typedef struct {
 #define BT2X_EDIT_QCHR(e) ((char)(((uint32_t)(e) >> 24) & 0xffu))
 
 /* Optional debug outputs (may be NULL): per-problem order-independent digests of the
- * filled E, F, H matrices (bt2x_cell_digest) and the sorted candidate list
- * (DpBtCandidate order, aligner_sw_nuc.h:149), BT2X_MAX_COLS entries per problem,
- * each (col << 16) | (row << 8)... see bt2x_cand_pack. */
+ * filled E, F, H matrices (bt2x_cell_digest of each cell's value as the reference
+ * stores it: the u8 byte, or the int16 bit pattern) and the sorted candidate list
+ * (DpBtCandidate order, aligner_sw_nuc.h:149), BT2X_MAX_COLS entries per problem
+ * (0xffffffff past ncand).  u8 entries are BT2X_CAND_PACK(row, col, score); i16
+ * entries BT2X_CAND_PACK16(col, score) (the row is always rdlen - 1,
+ * aligner_swsse_ee_i16.cpp:529); score = DpBtCandidate::score, the raw cell value. */
 #define BT2X_CAND_PACK(row, col, score) (((uint32_t)(col) << 16) | ((uint32_t)(row) << 8) | (uint32_t)(score))
+#define BT2X_CAND_PACK16(col, score) (((uint32_t)(col) << 16) | ((uint32_t)(score) & 0xffffu))
 typedef struct {
 	uint64_t* digests;       /* 3 per problem: E, F, H                       */
 	uint32_t* cands;         /* BT2X_MAX_COLS per problem                    */
@@ -258,12 +281,25 @@ int bt2x_dp_align(bt2x_ctx* ctx,
                   uint32_t* edits, uint32_t edit_cap, uint32_t* nedit_used,
                   bt2x_dp_debug* debug);
 
-/* Device-pointer variant: all buffers in HBM; counters (2 x u32: recs, edits) in HBM. */
+/* Device-pointer variant: all buffers in HBM; counters (4 x u32: recs used, edits used,
+ * then kernel scratch) in HBM.  launch_flags: BT2X_DPL_I16 when any problem carries
+ * BT2X_DP_I16 (the 16-bit kernels run the launch; an i16 problem in a launch without
+ * it is reported BT2X_E_ARG by the host variant, and comes back with status -1 here),
+ * BT2X_DPL_EXACT_BEST for exact best of failed problems (bt2x_dp_out.best).  The host
+ * variant derives both (the second from BT2X_OPT_EXACT_BEST). */
+#define BT2X_DPL_I16 1u
+#define BT2X_DPL_EXACT_BEST 2u
 int bt2x_dp_align_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const uint8_t* d_quals,
                       const uint8_t* d_refs, const bt2x_dp_in* d_in, uint32_t n,
                       bt2x_dp_out* d_out, bt2x_aln_rec* d_recs, uint32_t rec_cap,
                       uint32_t* d_edits, uint32_t edit_cap, uint32_t* d_counters,
-                      bt2x_dp_debug* d_debug, void* stream);
+                      bt2x_dp_debug* d_debug, uint32_t launch_flags, void* stream);
+
+/* Context options.  BT2X_OPT_EXACT_BEST (default 1): bt2x_dp_align reports the exact
+ * best of failed problems (one extra unbanded pass over them); 0 when the caller never
+ * reads it (bowtie2 prints it only under --mapq-extra). */
+enum { BT2X_OPT_EXACT_BEST = 1 };
+int bt2x_set_option(bt2x_ctx* ctx, int option, int64_t value);
 
 /* Order-independent digest of one matrix cell (shared by oracle, kernel and harness). */
 static inline uint64_t bt2x_cell_digest(uint32_t row, uint32_t col, uint32_t mat, uint32_t val) {

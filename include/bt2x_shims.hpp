@@ -39,16 +39,28 @@ struct Error : std::runtime_error {
 
 inline void check(int rc, const char* what) { if(rc != BT2X_OK) throw Error(rc, what); }
 
-// SwAligner::nextAlignment's per-candidate RNG use for the u8 kernel
-// (aligner_sw.cpp:324-336): reseed = nextU32()+1; init(reseed); backtrace; init(reseed+1).
+// SwAligner::nextAlignment's per-candidate RNG use: u8 kernel (aligner_sw.cpp:324-336)
+// reseed = nextU32()+1; init(reseed); backtrace; init(reseed+1); i16 kernel (:338-348)
+// reseed = nextU32()+1; backtrace; init(reseed).  The backtraces draw nothing.
 template<class Rnd>
-inline void replay_backtrace_draws(Rnd& rnd, unsigned ntries) {
+inline void replay_backtrace_draws(Rnd& rnd, unsigned ntries, bool i16 = false) {
 	for(unsigned t = 0; t < ntries; t++) {
 		const uint32_t reseed = rnd.nextU32() + 1;
 		rnd.init(reseed);
-		rnd.init(reseed + 1);
+		if(!i16) rnd.init(reseed + 1);
 	}
 }
+
+// SwAligner::initRef's kernel choice (aligner_sw.cpp:77-83): a -DENABLE_I16 build runs
+// the i16 kernel unless enable8 && minsc >= -254 and leaves minsc as is; the stock build
+// always runs u8 with minsc clamped to -254.  The shims follow the build they are
+// compiled into (the reference's own ENABLE_I16 macro).
+#ifdef ENABLE_I16
+constexpr bool kI16Build = true;
+#else
+constexpr bool kI16Build = false;
+#endif
+inline bool dp_uses_i16(bool i16build, bool enable8, int64_t minsc) { return i16build && !(enable8 && minsc >= -254); }
 
 // -------------------------------------------------------------- index / device
 
@@ -278,12 +290,15 @@ public:
 	// characters.  nsUpto counts Ns among the first `upto` window characters.
 	template<class Rect, class Refs>
 	bool initRef(int slot, bool fw, size_t refidx, const Rect& rect, const Refs& refs,
-	             int64_t reflen, int64_t minsc, size_t upto, size_t& nsUpto, int& prob) {
+	             int64_t reflen, int64_t minsc, size_t upto, size_t& nsUpto, int& prob,
+	             bool enable8 = true) {
 		const int64_t rfi = rect.refl, rff = rect.refr + 2;
 		const size_t rflen = (size_t)(rff - rfi);
 		if(rflen > BT2X_MAX_COLS) return false;
 		const ReadSlot& r = rslots_.at((size_t)slot);
-		if(minsc < -254) minsc = -254;               // aligner_sw.cpp:77-83
+		const bool i16 = dp_uses_i16(kI16Build, enable8, minsc);
+		if(!i16 && minsc < -254) minsc = -254;       // aligner_sw.cpp:77-83
+		if(minsc < -32767) throw Error(BT2X_E_ARG, "SwBatch::initRef: minsc below the int16 range");
 		bt2x_dp_in p;
 		std::memset(&p, 0, sizeof(p));
 		p.read_off = fw ? r.fw_off : r.rc_off;
@@ -296,6 +311,7 @@ public:
 		p.nceil = (int16_t)r.nceil;
 		p.triml = (uint16_t)rect.triml; p.corel = (uint16_t)rect.corel; p.corer = (uint16_t)rect.corer;
 		p.fw = fw ? 1 : 0;
+		p.flags = i16 ? BT2X_DP_I16 : 0;
 		nsUpto = 0;
 		for(size_t i = 0; i < rflen; i++) {
 			const int64_t off = rfi + (int64_t)i;
@@ -353,7 +369,7 @@ public:
 		uint32_t& k = cursor_[(size_t)prob];
 		if(o.status == 0 || k >= o.nrec) return false;
 		const bt2x_aln_rec& r = recs_[o.rec_off + k++];
-		replay_backtrace_draws(rnd, r.ntries);
+		replay_backtrace_draws(rnd, r.ntries, (in_[(size_t)prob].flags & BT2X_DP_I16) != 0);
 		res.image.assign(edits_.begin() + r.edit_off, edits_.begin() + r.edit_off + r.nbuf);
 		if(!r.ok) { cursor_[(size_t)prob] = o.nrec; return false; }
 		res.score = r.score; res.ns = r.ns; res.gaps = r.gaps; res.bases_aligned = r.bases_aligned;
@@ -403,11 +419,11 @@ public:
 	}
 	template<class Rect, class Refs>
 	bool initRef(bool fw, size_t refidx, const Rect& rect, const Refs& refs, int64_t reflen,
-	             int64_t minsc, bool /*enable8*/, bool /*extend*/, size_t upto, size_t& nsUpto) {
+	             int64_t minsc, bool enable8, bool /*extend*/, size_t upto, size_t& nsUpto) {
 		prob_ = -1;
 		if(slot_ < 0) return false;
 		b_.clear_problems();
-		return b_.initRef(slot_, fw, refidx, rect, refs, reflen, minsc, upto, nsUpto, prob_);
+		return b_.initRef(slot_, fw, refidx, rect, refs, reflen, minsc, upto, nsUpto, prob_, enable8);
 	}
 	bool align(int64_t& best) {
 		if(prob_ < 0) return false;

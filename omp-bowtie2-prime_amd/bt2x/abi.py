@@ -15,7 +15,10 @@ SEED_OUT = np.dtype([("topf", "<u8"), ("botf", "<u8"), ("nlex", "u1"),
 DP_IN = np.dtype([("read_off", "<u8"), ("qual_off", "<u8"), ("ref_off", "<u8"),
                   ("refl", "<i8"), ("rdlen", "<u2"), ("ncol", "<u2"), ("minsc", "<i2"),
                   ("nceil", "<i2"), ("triml", "<u2"), ("corel", "<u2"), ("corer", "<u2"),
-                  ("fw", "u1"), ("pad", "u1")], align=True)
+                  ("fw", "u1"), ("flags", "u1")], align=True)
+DP_I16 = 1                  # bt2x_dp_in.flags: the reference's signed 16-bit DP (--no-sse8)
+DPL_I16, DPL_EXACT_BEST = 1, 2
+OPT_EXACT_BEST = 1
 DP_OUT = np.dtype([("status", "<i4"), ("best", "<i4"), ("ncand", "<u2"), ("nrec", "<u2"),
                    ("rec_off", "<u4")], align=True)
 ALN_REC = np.dtype([("ntries", "<u2"), ("ok", "u1"), ("pad0", "u1"), ("score", "<i2"),
@@ -51,8 +54,13 @@ def edit_fields(e: int) -> tuple[int, int, str, str]:
     return e & 0x3FF, (e >> 12) & 7, chr((e >> 16) & 0xFF), chr((e >> 24) & 0xFF)
 
 
-def cand_fields(c: int) -> tuple[int, int, int]:
+def cand_fields(c: int, i16: bool = False) -> tuple[int | None, int, int]:
+    """Unpack a debug candidate -> (row, col, DpBtCandidate::score).  i16 entries
+    (BT2X_CAND_PACK16) carry no row (always rdlen - 1) and an int16 score."""
     c = int(c)
+    if i16:
+        sc = c & 0xFFFF
+        return None, c >> 16, sc - 0x10000 if sc >= 0x8000 else sc
     return (c >> 8) & 0xFF, c >> 16, c & 0xFF
 
 
@@ -90,7 +98,7 @@ class Scoring(ctypes.Structure):
 class Counters(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("n_bilf", "n_lf1", "n_ftab", "dp_cells", "dp_cols", "bt_cells",
-                 "n_problems", "alg_bytes")]
+                 "n_problems", "alg_bytes", "dp_cells_computed")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

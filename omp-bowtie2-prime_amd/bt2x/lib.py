@@ -43,7 +43,8 @@ FUNCS = {
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
-                                         ctypes.POINTER(abi.DpDebug), ctypes.c_void_p]),
+                                         ctypes.POINTER(abi.DpDebug), ctypes.c_uint32, ctypes.c_void_p]),
+    "bt2x_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
     "bt2x_resolve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
                                     ctypes.c_void_p]),
     "bt2x_resolve_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
@@ -193,10 +194,15 @@ class Context:
         return out, recs[: nrec.value], edits[: nedit.value], dig, cands
 
     def dp_align_dev(self, d_reads, d_quals, d_refs, d_in, n, d_out, d_recs, rec_cap, d_edits,
-                     edit_cap, d_counters, stream=0):
+                     edit_cap, d_counters, stream=0, launch_flags=0):
+        """bt2x_dp_align_dev; launch_flags: abi.DPL_I16 (some problem is BT2X_DP_I16),
+        abi.DPL_EXACT_BEST (exact best of failed problems).  d_counters: 4 x u32."""
         check(load().bt2x_dp_align_dev(self.h, d_reads, d_quals, d_refs, d_in, n, d_out, d_recs,
-                                       rec_cap, d_edits, edit_cap, d_counters, None, stream),
+                                       rec_cap, d_edits, edit_cap, d_counters, None, launch_flags, stream),
               "bt2x_dp_align_dev")
+
+    def set_option(self, option: int, value: int) -> None:
+        check(load().bt2x_set_option(self.h, option, int(value)), "bt2x_set_option")
 
     # ------------------------------------------------------- SA resolution
     def resolve(self, rows, qlen, reject_straddle: bool = False) -> np.ndarray:

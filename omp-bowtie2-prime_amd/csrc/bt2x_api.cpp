@@ -162,7 +162,8 @@ struct bt2x_ctx {
 	// to resolve, per-lane workspace)
 	DevBuf b_rin, b_exr, b_rout, b_sats, b_elts, b_exro, b_used, b_sout, b_rows, b_ws, b_jobs, b_ranges, b_rcnt;
 	const uint32_t* d_resolve_n = nullptr;     // element count of the last round's resolve (HBM)
-	DevBuf scratch;
+	DevBuf scratch, b_fail;
+	bool exact_best = true;                    // BT2X_OPT_EXACT_BEST
 	int ncu = 0;
 	uint32_t chunk_groups = 16384;             // DP chunk: 1 Mi problems, ~34 GB of traceback bytes
 	uint32_t* d_queue = nullptr;
@@ -175,7 +176,7 @@ struct bt2x_ctx {
 bt2x_ctx::~bt2x_ctx() {
 	(void)hipSetDevice(device);
 	if(stream) (void)hipStreamSynchronize(stream);
-	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch,
+	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch, &b_fail,
 	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws,
 	                 &b_jobs, &b_ranges, &b_rcnt})
 		b->release();
@@ -316,6 +317,12 @@ extern "C" void bt2x_close(bt2x_ctx* c) {
 	delete c;        // ~bt2x_ctx releases everything
 }
 
+extern "C" int bt2x_set_option(bt2x_ctx* c, int option, int64_t value) {
+	if(!c) return BT2X_E_ARG;
+	if(option == BT2X_OPT_EXACT_BEST) { c->exact_best = value != 0; return BT2X_OK; }
+	return BT2X_E_ARG;
+}
+
 extern "C" double bt2x_last_kernel_ms(const bt2x_ctx* c, int k) {
 	if(!c || k < 0 || k >= BT2X_K_COUNT || !c->ev_valid[k]) return -1.0;
 	float ms = -1.0f;
@@ -339,6 +346,8 @@ extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) 
 		out->n_lf1 = st[9];
 		out->n_problems = c->n_resolve_last;
 		if(c->d_resolve_n) {
+			// the count is written by the round's kernels on the caller's stream
+			if(c->ev_valid[BT2X_K_RESOLVE]) HIPCHK(hipEventSynchronize(c->ev[BT2X_K_RESOLVE][1]));
 			uint32_t nr = 0;
 			HIPCHK(hipMemcpy(&nr, c->d_resolve_n, sizeof nr, hipMemcpyDeviceToHost));
 			out->n_problems = nr;
@@ -351,10 +360,12 @@ extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) 
 	} else if(k == BT2X_K_ROUND) {
 		return BT2X_E_ARG;                     // see BT2X_K_SEED and BT2X_K_RESOLVE
 	} else {
-		out->dp_cells = st[4]; out->dp_cols = st[5]; out->bt_cells = st[6];
+		if(c->ev_valid[BT2X_K_DP]) HIPCHK(hipEventSynchronize(c->ev[BT2X_K_DP][1]));
+		HIPCHK(hipMemcpy(st, c->d_stats, sizeof st, hipMemcpyDeviceToHost));
+		out->dp_cells = st[4]; out->dp_cols = st[5]; out->bt_cells = st[6]; out->dp_cells_computed = st[7];
 		out->n_problems = c->n_dp_last;
-		// traceback byte per cell written + reference window + read codes/quals
-		out->alg_bytes = out->dp_cells + out->dp_cols;
+		// traceback byte per cell the fill computes and writes + reference window
+		out->alg_bytes = out->dp_cells_computed + out->dp_cols;
 	}
 	return BT2X_OK;
 }
@@ -424,15 +435,17 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
                                  const uint8_t* d_refs, const bt2x_dp_in* d_in, uint32_t n,
                                  bt2x_dp_out* d_out, bt2x_aln_rec* d_recs, uint32_t rec_cap,
                                  uint32_t* d_edits, uint32_t edit_cap, uint32_t* d_counters,
-                                 bt2x_dp_debug* d_debug, void* stream) {
+                                 bt2x_dp_debug* d_debug, uint32_t launch_flags, void* stream) {
 	if(!c || !d_counters) return BT2X_E_ARG;
 	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
 	HIPCHK(hipSetDevice(c->device));
 	uint32_t groups = 0;
 	int rc = ensure_scratch(c, n, &groups);
 	if(rc) return rc;
-	HIPCHK(hipMemsetAsync(d_counters, 0, 2 * sizeof(uint32_t), s));
-	HIPCHK(hipMemsetAsync(c->d_stats + 4, 0, 3 * sizeof(unsigned long long), s));
+	const bool exact = (launch_flags & BT2X_DPL_EXACT_BEST) != 0;
+	if(exact && (rc = c->b_fail.ensure(sizeof(uint32_t) * (size_t)(n ? n : 1)))) return rc;
+	HIPCHK(hipMemsetAsync(d_counters, 0, 4 * sizeof(uint32_t), s));
+	HIPCHK(hipMemsetAsync(c->d_stats + 4, 0, 4 * sizeof(unsigned long long), s));
 	DpLaunch a{};
 	a.reads = d_reads; a.quals = d_quals; a.refs = d_refs; a.in = d_in; a.n = n; a.out = d_out;
 	a.recs = d_recs; a.rec_cap = rec_cap; a.edits = d_edits; a.edit_cap = edit_cap;
@@ -442,6 +455,8 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	a.scratch = (uint8_t*)c->scratch.p; a.chunk_groups = groups; a.ncu = c->ncu; a.queue = c->d_queue;
 	{ const char* ab = getenv("BT2X_DP_ABLATE"); a.ablate = (ab && *ab >= '1' && *ab <= '2') ? (uint32_t)(*ab - '0') : 0u; }
 	{ const char* bd = getenv("BT2X_DP_BAND"); a.band = (bd && bd[0] == '0') ? 0u : 1u; }
+	a.wide = (launch_flags & BT2X_DPL_I16) ? 1u : 0u;
+	a.fail_list = exact ? (uint32_t*)c->b_fail.p : nullptr;
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));
@@ -463,13 +478,18 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
 	if(nrec_used) *nrec_used = 0;
 	if(nedit_used) *nedit_used = 0;
 	if(n == 0) return BT2X_OK;
-	// shape checks: the kernel trusts these (reference limits)
+	// shape checks: the kernel trusts these (reference limits; the u8 kernel's
+	// minsc floor, aligner_sw.cpp:77-83)
+	uint32_t launch_flags = c->exact_best ? BT2X_DPL_EXACT_BEST : 0u;
 	for(uint32_t i = 0; i < n; i++) {
 		const bt2x_dp_in& p = in[i];
+		const bool i16 = (p.flags & BT2X_DP_I16) != 0;
 		if(p.rdlen < 1 || p.rdlen > BT2X_MAX_ROWS || p.ncol < 1 || p.ncol + 1 > BT2X_MAX_COLS ||
 		   p.read_off + p.rdlen > reads_bytes || p.qual_off + p.rdlen > quals_bytes ||
-		   p.ref_off + p.ncol > refs_bytes || p.minsc < -254 || p.minsc > 0)
+		   p.ref_off + p.ncol > refs_bytes || p.minsc < (i16 ? -32767 : -254) || p.minsc > 0 ||
+		   (p.flags & ~BT2X_DP_I16) != 0)
 			return BT2X_E_ARG;
+		if(i16) launch_flags |= BT2X_DPL_I16;
 	}
 	HIPCHK(hipSetDevice(c->device));
 	int rc;
@@ -495,14 +515,15 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
 	                       (const uint8_t*)c->b_refs.p, (const bt2x_dp_in*)c->b_in.p, n,
 	                       (bt2x_dp_out*)c->b_out.p, (bt2x_aln_rec*)c->b_recs.p, rec_cap,
 	                       (uint32_t*)c->b_edits.p, edit_cap, c->d_counters,
-	                       (dd.digests || dd.cands) ? &dd : nullptr, c->stream);
+	                       (dd.digests || dd.cands) ? &dd : nullptr, launch_flags, c->stream);
 	if(rc) return rc;
-	uint32_t used[2] = {0, 0};
+	uint32_t used[4] = {0, 0, 0, 0};
 	HIPCHK(hipMemcpyAsync(used, c->d_counters, sizeof used, hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(hipMemcpyAsync(out, c->b_out.p, sizeof(bt2x_dp_out) * n, hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(hipStreamSynchronize(c->stream));
 	if(nrec_used) *nrec_used = used[0];
 	if(nedit_used) *nedit_used = used[1];
+	if(used[3]) return BT2X_E_ARG;                            // cannot happen: launch_flags cover in[]
 	if(used[0] > rec_cap || used[1] > edit_cap) return BT2X_E_OVERFLOW;
 	if(used[0]) HIPCHK(hipMemcpy(recs, c->b_recs.p, sizeof(bt2x_aln_rec) * used[0], hipMemcpyDeviceToHost));
 	if(used[1]) HIPCHK(hipMemcpy(edits, c->b_edits.p, sizeof(uint32_t) * used[1], hipMemcpyDeviceToHost));

@@ -81,8 +81,9 @@ struct DpLaunch {
 	bt2x_dp_out* out;
 	bt2x_aln_rec* recs; uint32_t rec_cap;
 	uint32_t* edits; uint32_t edit_cap;
-	uint32_t* counters;            // [0] recs used, [1] edits used, [2..] stats (u32 pairs)
-	unsigned long long* stats;     // dp_cells, dp_cols, bt_cells
+	uint32_t* counters;            // [0] recs used, [1] edits used, [2] fail_list entries, [3] refused
+	                               // (i16 problems in a u8 launch)
+	unsigned long long* stats;     // dp_cells, dp_cols, bt_cells, dp_cells_computed
 	uint64_t* digests;             // optional, 3 per problem
 	uint32_t* cands;               // optional, BT2X_MAX_COLS per problem
 	uint8_t* scratch;              // chunk_groups fill regions, then the walk staging slots
@@ -92,6 +93,9 @@ struct DpLaunch {
 	uint32_t* queue;               // walk-kernel problem queue counter (device)
 	uint32_t ablate;               // profiling only: 1 = stop after the fill, 2 = no backtrace walks (outputs invalid)
 	uint32_t band;                 // 1: lane-kernel fill restricted to the exact diagonal band (dp_kernel.hip)
+	uint32_t wide;                 // 1: the 16-bit lane kernels (some problem is BT2X_DP_I16)
+	uint32_t* fail_list;           // n entries, or NULL: queue the banded fill's failed problems for
+	                               // the exact-best pass (BT2X_DPL_EXACT_BEST)
 };
 size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups);
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream);

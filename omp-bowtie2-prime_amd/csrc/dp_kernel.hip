@@ -40,7 +40,7 @@ constexpr int kCols = BT2X_MAX_COLS;          // 200
 constexpr int kSteps = kRows + 1;             // steps per column pair (rows 0..R-1, skew 1)
 constexpr int kPairWords = (kSteps + 1) / 2;  // traceback dwords per column pair (2 steps each)
 constexpr uint32_t kDirBytesLane = (kCols / 2) * kPairWords * 4;   // 32400
-constexpr uint32_t kLastRowBytesLane = 256;
+constexpr uint32_t kLastRowBytesLane = 512;                        // u16 per column (i16 kernel)
 constexpr uint32_t kCandBytesLane = kCols;                         // sorted candidate columns
 constexpr uint32_t kEditStage = 400;                               // >= R + C + 2
 constexpr uint32_t kRecStage = kCols + 8;                          // >= ncand + 1
@@ -146,7 +146,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 		__builtin_amdgcn_make_buffer_rsrc(gslot + kDirOff, 0, (int)(kDirBytesLane * 64u), 0x00020000);
 	const uint8_t* cands = gslot + kCandOff;
 	bt2x_dp_out o = a.out[pi];
-	if(o.status != 0 && o.ncand > 0 && a.ablate != 1) {
+	if(o.status > 0 && o.ncand > 0 && a.ablate != 1) {
 		const bt2x_dp_in p = a.in[pi];
 		const int R = p.rdlen;
 		const uint8_t* rd = a.reads + p.read_off;
@@ -348,24 +348,46 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 // wave_shr), so a problem takes C + R/4 steps.  Values and flags are the lane kernel's
 // (same recurrence and traceback byte); the traceback bytes stay in LDS, column-major with
 // a lane's 4 rows in one dword, and the walk (lane 0) reads and marks them at LDS latency.
+// Cells are plain u32 here, so one body serves both value domains: u8 (top 0xff) and
+// i16 (the int16 range shifted to [0, 0xffff]: top 0xffff = score 0, floor 0 = -65535);
+// barred gap terms subtract 0x10000, which floors either domain.
 constexpr int kWaveTbWords = kCols * kRows / 4;              // 8000 dwords = 31.25 KiB
 constexpr size_t kWaveRecStageBytes = (size_t)kRecStage * sizeof(bt2x_aln_rec);
 
 __device__ __forceinline__ uint32_t subs(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
 
+// align()'s verdict from the last row's maximum lrmax (top-relative value) and the
+// number of candidates: alignEnd2EndSseU8 (aligner_swsse_ee_u8.cpp:637-668) and
+// alignEnd2EndSseI16 (aligner_swsse_ee_i16.cpp:642-673; its "score" subtracts 0xff from
+// the int16 value, so it is lrmax - 0x8000 - 0xff here).
+__device__ __forceinline__ void dp_verdict(bool i16, int lrmax, int minsc, int ncand, int& status, int& best) {
+	const int score = lrmax - (i16 ? 0x80ff : 0xff);
+	if(score < minsc) { status = 0; best = score; }
+	else if(lrmax == 0) { status = 0; best = INT32_MIN; }       // saturated (MIN_U8 / MIN_I16)
+	else { status = ncand > 0 ? 1 : 0; best = score; }
+}
+
+// kBestOnly: the exact `best` of the problems the banded lane kernel failed
+// (a.fail_list[0 .. a.counters[2])): the whole rectangle's last-row maximum, nothing else.
+template<bool kBestOnly>
 __global__ void __launch_bounds__(64)
 dp_wave_kernel(DevScoring sc, DpLaunch a) {
-	__shared__ uint32_t tbw[kWaveTbWords];
-	__shared__ uint8_t refw[kCols], lastrow[kCols], cands[kCols];
-	__shared__ uint32_t stage_ed[kEditStage];
+	__shared__ uint32_t tbw[kBestOnly ? 1 : kWaveTbWords];
+	__shared__ uint8_t refw[kCols], cands[kCols];
+	__shared__ uint16_t lastrow[kCols];
+	__shared__ uint32_t stage_ed[kBestOnly ? 1 : kEditStage];
 	uint8_t* tbb = reinterpret_cast<uint8_t*>(tbw);
 	const int lane = threadIdx.x;
-	bt2x_aln_rec* stage_rec = reinterpret_cast<bt2x_aln_rec*>(a.scratch + (size_t)blockIdx.x * kWaveRecStageBytes);
+	bt2x_aln_rec* stage_rec = kBestOnly ? nullptr : reinterpret_cast<bt2x_aln_rec*>(a.scratch + (size_t)blockIdx.x * kWaveRecStageBytes);
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0;
 	const uint32_t rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
-	for(uint32_t pi = blockIdx.x; pi < a.n; pi += gridDim.x) {
+	const uint32_t nwork = kBestOnly ? min(a.counters[2], a.n) : a.n;
+	for(uint32_t k = blockIdx.x; k < nwork; k += gridDim.x) {
+		const uint32_t pi = kBestOnly ? a.fail_list[k] : k;
 		const bt2x_dp_in p = a.in[pi];
 		const int R = p.rdlen, C = p.ncol;
+		const bool i16 = (p.flags & BT2X_DP_I16) != 0;
+		const uint32_t top = i16 ? 0xffffu : 0xffu;
 		const uint8_t* rd = a.reads + p.read_off;
 		const uint8_t* qu = a.quals + p.qual_off;
 		const uint8_t* rf = a.refs + p.ref_off;
@@ -387,13 +409,13 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 				if(b <= 3) { c = (uint32_t)b; m = (uint32_t)sc.mmpen[q]; }
 			}
 			rc[r] = c; mm[r] = m;
-			const uint32_t bar = gbar ? 256u : 0u, r0 = (i == 0) ? 256u : 0u;   // row 0 has no F
+			const uint32_t bar = gbar ? 0x10000u : 0u, r0 = (i == 0) ? 0x10000u : 0u;   // row 0 has no F
 			rdoe[r] = rdo + bar; rfoe[r] = rfo + bar + r0; rfee[r] = rfe + bar + r0;
 		}
 		__syncthreads();
-		// ---- fill: H/E of the previous column for my rows; H[i][-1] = E = 0, H[-1][*] = 0xff
+		// ---- fill: H/E of the previous column for my rows; H[i][-1] = E = floor, H[-1][*] = top
 		uint32_t Hp0 = 0, Hp1 = 0, Hp2 = 0, Hp3 = 0, Ep0 = 0, Ep1 = 0, Ep2 = 0, Ep3 = 0;
-		uint32_t hupPrev = lane == 0 ? 0xffu : 0u;  // H[4l-1][j-1]
+		uint32_t hupPrev = lane == 0 ? top : 0u;    // H[4l-1][j-1]
 		uint32_t bot = 0;                           // my bottom row's H | F << 16, last column
 		const int lastLane = (R - 1) >> 2, lastR = (R - 1) & 3;
 		const int T = C + L - 1;
@@ -401,7 +423,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bot, 0x138, 0xf, 0xf, false);
 			const int j = t - lane;
 			if(lane < L && j >= 0 && j < C) {
-				uint32_t hu = lane == 0 ? 0xffu : (up & 0xffffu);
+				uint32_t hu = lane == 0 ? top : (up & 0xffffu);
 				uint32_t fu = lane == 0 ? 0u : (up >> 16);
 				uint32_t hdiag = hupPrev;
 				hupPrev = hu;
@@ -416,10 +438,12 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 					const uint32_t hl_o = subs(HP, rdoe[r]), e = max(hl_o, subs(EP, rde));      \
 					const uint32_t hu_o = subs(hu, rfoe[r]), f = max(hu_o, subs(fu, rfee[r]));  \
 					const uint32_t h = max(max(d, e), f);                                       \
-					const uint32_t tb = (x ? (uint32_t)TB_MM : 0u) | (hl_o != e ? (uint32_t)TB_EONE : 0u) | \
-					                    (hu_o != f ? (uint32_t)TB_FONE : 0u) | (f != h ? (uint32_t)TB_FNE : 0u) | \
-					                    (d != h ? (uint32_t)TB_DNE : 0u);                           \
-					tbv |= tb << (8 * r);                                                       \
+					if(!kBestOnly) {                                                            \
+						const uint32_t tb = (x ? (uint32_t)TB_MM : 0u) | (hl_o != e ? (uint32_t)TB_EONE : 0u) | \
+						                    (hu_o != f ? (uint32_t)TB_FONE : 0u) | (f != h ? (uint32_t)TB_FNE : 0u) | \
+						                    (d != h ? (uint32_t)TB_DNE : 0u);                       \
+						tbv |= tb << (8 * r);                                                   \
+					}                                                                           \
 					hdiag = HP; HP = h; EP = e; hu = h; fu = f;                                 \
 				}
 				BT2X_WAVE_CELL(0, Hp0, Ep0)
@@ -427,37 +451,42 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 				BT2X_WAVE_CELL(2, Hp2, Ep2)
 				BT2X_WAVE_CELL(3, Hp3, Ep3)
 #undef BT2X_WAVE_CELL
-				tbw[j * L + lane] = tbv;
+				if(!kBestOnly) tbw[j * L + lane] = tbv;
 				bot = hu | (fu << 16);
 				if(lane == lastLane)
-					lastrow[j] = (uint8_t)(lastR == 0 ? Hp0 : lastR == 1 ? Hp1 : lastR == 2 ? Hp2 : Hp3);
+					lastrow[j] = (uint16_t)(lastR == 0 ? Hp0 : lastR == 1 ? Hp1 : lastR == 2 ? Hp2 : Hp3);
 			}
 		}
 		__syncthreads();
 		// ---- best score, candidates in DpBtCandidate order (score desc, col desc)
-		const int thr = (int)p.minsc + 0xff;
+		const int thr = (int)p.minsc + (int)top;
 		int lrmax = 0, nc = 0;
 		for(int j = lane; j < C; j += 64) { const int v = lastrow[j]; lrmax = imax(lrmax, v); nc += v >= thr; }
 		lrmax = wave_max(lrmax);
 		for(int d = 32; d > 0; d >>= 1) nc += __shfl_xor(nc, d);
+		int status = 0, best = 0;
+		dp_verdict(i16, lrmax, p.minsc, nc, status, best);
+		if(kBestOnly) {
+			if(lane == 0) a.out[pi].best = best;
+			__syncthreads();
+			continue;
+		}
 		st_cells += (unsigned long long)R * C;
 		st_cols += C;
 		bt2x_dp_out o;
 		o.nrec = 0; o.rec_off = 0;
-		const int score = lrmax - 0xff;
-		if(score < p.minsc) {
-			o.status = 0; o.best = score; o.ncand = 0;
+		o.status = status; o.best = best; o.ncand = status ? (uint16_t)nc : (uint16_t)0;
+		if(!status) {
 			if(lane == 0) a.out[pi] = o;
 			__syncthreads();
 			continue;
 		}
-		o.status = nc > 0 ? 1 : 0; o.best = score; o.ncand = (uint16_t)nc;
 		for(int j = lane; j < C; j += 64) {
 			const int v = lastrow[j];
 			if(v < thr) continue;
 			const int key = (v << 8) | j;
 			int rank = 0;
-			for(int k = 0; k < C; k++) { const int w = lastrow[k]; rank += ((w << 8) | k) > key; }
+			for(int k2 = 0; k2 < C; k2++) { const int w = lastrow[k2]; rank += ((w << 8) | k2) > key; }
 			cands[rank] = (uint8_t)j;
 		}
 		__syncthreads();
@@ -530,19 +559,19 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 						}
 						if(ns > p.nceil) { hi = max(hi, ne); continue; }
 						int refns = 0;
-						for(int k = col; k <= col0; k++) refns += (refw[k] > 3);
+						for(int k2 = col; k2 <= col0; k2++) refns += (refw[k2] > 3);
 						const int extent = R - (R - row0 - 1);
 						if(p.fw) {
-							for(int k = 0; k < ne / 2; k++) {
-								const uint32_t x = stage_ed[k];
-								stage_ed[k] = stage_ed[ne - 1 - k];
-								stage_ed[ne - 1 - k] = x;
+							for(int k2 = 0; k2 < ne / 2; k2++) {
+								const uint32_t x = stage_ed[k2];
+								stage_ed[k2] = stage_ed[ne - 1 - k2];
+								stage_ed[ne - 1 - k2] = x;
 							}
 						} else {
-							for(int k = 0; k < ne; k++) {
-								const uint32_t e = stage_ed[k];
+							for(int k2 = 0; k2 < ne; k2++) {
+								const uint32_t e = stage_ed[k2];
 								const uint32_t pos = (uint32_t)extent - (e & 0x3ffu) - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
-								stage_ed[k] = (e & ~0x3ffu) | (pos & 0x3ffu);
+								stage_ed[k2] = (e & ~0x3ffu) | (pos & 0x3ffu);
 							}
 						}
 						hi = max(hi, ne);
@@ -555,7 +584,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 						uint32_t eo = 0;
 						if(hi > 0) {
 							eo = atomicAdd(&a.counters[1], (uint32_t)hi);
-							if(eo + (uint32_t)hi <= a.edit_cap) for(int k = 0; k < hi; k++) a.edits[eo + k] = stage_ed[k];
+							if(eo + (uint32_t)hi <= a.edit_cap) for(int k2 = 0; k2 < hi; k2++) a.edits[eo + k2] = stage_ed[k2];
 						}
 						r.edit_off = eo; r.nbuf = (uint32_t)hi;
 						stage_rec[nrec] = r;
@@ -568,7 +597,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 						uint32_t eo = 0;
 						if(hi > 0) {
 							eo = atomicAdd(&a.counters[1], (uint32_t)hi);
-							if(eo + (uint32_t)hi <= a.edit_cap) for(int k = 0; k < hi; k++) a.edits[eo + k] = stage_ed[k];
+							if(eo + (uint32_t)hi <= a.edit_cap) for(int k2 = 0; k2 < hi; k2++) a.edits[eo + k2] = stage_ed[k2];
 						}
 						r.edit_off = eo; r.nbuf = (uint32_t)hi;
 						stage_rec[nrec] = r;
@@ -579,29 +608,40 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 				}
 				const uint32_t ro = atomicAdd(&a.counters[0], (uint32_t)nrec);
 				if(ro + (uint32_t)nrec <= a.rec_cap)
-					for(int k = 0; k < nrec; k++) a.recs[ro + k] = stage_rec[k];
+					for(int k2 = 0; k2 < nrec; k2++) a.recs[ro + k2] = stage_rec[k2];
 				o.nrec = (uint16_t)nrec; o.rec_off = ro;
 			}
 			a.out[pi] = o;
 		}
 		__syncthreads();
 	}
-	if(a.stats && lane == 0) {
+	if(!kBestOnly && a.stats && lane == 0) {
 		atomicAdd(&a.stats[0], st_cells);
 		atomicAdd(&a.stats[1], st_cols);
 		atomicAdd(&a.stats[2], st_bt);
+		atomicAdd(&a.stats[3], st_cells);              // whole rectangles
 	}
 }
 
 // kFused: the same wave walks its 64 problems right after their fill, while the
 // traceback bytes are still in the Infinity Cache; slots are per resident wave.
-template<bool kDebug, bool kFused>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+// kWide: the 16-bit value domain (launches holding BT2X_DP_I16 problems, the reference's
+// alignEnd2EndSseI16): the same sweep with 16-bit row state (2 rows per dword, 80 + 80
+// VGPRs, so 2 waves/SIMD instead of 3), a per-lane top value (0xff for u8 problems,
+// 0xffff for i16 ones: the int16 range shifted by 0x8000), barred gap terms masked to
+// the floor, and 16-bit last rows.  Flags, candidates and the walk are unchanged: every
+// traceback test is an equality between a cell on a path scoring >= minsc and a
+// neighbour term, identical in both domains (aligner_swsse_ee_i16.cpp:746-1352 is the
+// u8 backtrace over int16 cells).
+template<bool kDebug, bool kFused, bool kWide>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWide ? 2 : 3)))
 dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
-	// LDS: the last DP row (4 columns per dword) for candidate ordering.  12.8 KiB per wave.
+	// LDS: the row info during the fill, then the last DP row (4 column keys per dword)
+	// for candidate ordering.  12.8 KiB per wave.
 	__shared__ uint32_t lds[(kCols / 4) * 64];
+	constexpr int kStateWords = kWide ? kRows / 2 : kRowWords;   // H/E state dwords per lane
 	const int lane = threadIdx.x;
-	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0;
+	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0, st_comp = 0;
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 	const uint32_t one2 = opaque(0x00010001u);
 
@@ -610,21 +650,26 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		                        : a.scratch + (size_t)grp * kGroupBytes;
 		uint32_t* dir = reinterpret_cast<uint32_t*>(gslot + kDirOff);
 		uint8_t* lastrow = gslot + kLastRowOff;
+		uint16_t* lastrow16 = reinterpret_cast<uint16_t*>(gslot + kLastRowOff);
 		uint8_t* cands = gslot + kCandOff;
 		const uint32_t pi = base + grp * 64 + lane;
 		const bool active = grp * 64 + lane < nprob;
 		bt2x_dp_in p;
 		if(active) p = a.in[pi];
 		else { p.read_off = p.qual_off = p.ref_off = 0; p.refl = 0; p.rdlen = 0; p.ncol = 0;
-		       p.minsc = 0; p.nceil = 0; p.triml = p.corel = p.corer = 0; p.fw = 1; p.pad = 0; }
+		       p.minsc = 0; p.nceil = 0; p.triml = p.corel = p.corer = 0; p.fw = 1; p.flags = 0; }
+		const bool i16 = kWide && (p.flags & BT2X_DP_I16);
+		// an i16 problem in a u8 launch (bt2x_dp_align_dev without BT2X_DPL_I16): refused
+		const bool refused = !kWide && active && (p.flags & BT2X_DP_I16);
 		const int R = p.rdlen, C = p.ncol;
+		const int top = i16 ? 0xffff : 0xff;            // score 0 (H of row -1)
 		// wave-uniform bounds in SGPRs: every per-step guard below is a scalar branch
 		const int Rmax = __builtin_amdgcn_readfirstlane(wave_max(R));
 		const int Cmax = __builtin_amdgcn_readfirstlane(wave_max(C));
 		const uint8_t* rd = a.reads + p.read_off;
 		const uint8_t* qu = a.quals + p.qual_off;
 		const uint8_t* rf = a.refs + p.ref_off;
-		const int thr = (int)p.minsc + 0xff;
+		const int thr = (int)p.minsc + top;
 		// ------------- row info (rows >= R: N, barred) ------------------------------
 		// 4 rows per dword, in LDS for the whole fill (constant per problem; the region
 		// holds the last row after the fill)
@@ -651,16 +696,20 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			lds[blk * 64 + lane] = w;
 		}
 		// ------------- fill: two columns per sweep, per-row state in VGPRs ------------
-		// H and E of the previous column, 4 rows per dword (40 dwords each for 160 rows).
-		uint32_t Hs[kRowWords], Es[kRowWords];
+		// H and E of the previous column: u8 4 rows per dword (40 + 40 dwords for 160
+		// rows), wide 2 rows per dword (80 + 80).
+		uint32_t Hs[kStateWords], Es[kStateWords];
 #pragma unroll
-		for(int b = 0; b < kRowWords; b++) { Hs[b] = 0; Es[b] = 0; }
+		for(int b = 0; b < kStateWords; b++) { Hs[b] = 0; Es[b] = 0; }
 		uint64_t dg0 = 0, dg1 = 0, dg2 = 0;
 		int lrmax = 0, ncand = 0;
 		const int Rmin = __builtin_amdgcn_readfirstlane(-wave_max(-R));
 		const uint32_t rdo2 = (uint32_t)rdo * 0x10001u, rde2 = (uint32_t)rde * 0x10001u;
 		const uint32_t rfo2 = (uint32_t)rfo * 0x10001u, rfe2 = (uint32_t)rfe * 0x10001u;
 		const uint32_t npen2 = (uint32_t)npen * 0x10001u;
+		const uint32_t topLo = (uint32_t)top, topHi = (uint32_t)top << 16;
+		// digests hash the reference's stored value: the u8 byte, or the int16 bit pattern
+		const uint32_t dgx = i16 ? 0x8000u : 0u;
 		// Diagonal band (exact).  A path from row 0 to row R-1 scoring >= minsc
 		// pays for at most G gap positions (every gap position costs >= the cheapest extension,
 		// the first of a run >= the cheapest open), so it stays inside diagonals [-G, C-R+G]:
@@ -673,8 +722,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		// per column pair, steps [j0 - wdhi, j0 + wdlo], clipped to [0, Rmax]; both ends move
 		// down monotonically, so state rows entering at the bottom were never written (zero)
 		// and rows above the top are never read again.  Cells below minsc in the last row may
-		// then report a lower `best` (status 0 only); candidates, records and edits are the
-		// full fill's.  kDebug (E/F/H digests) and band = 0 fill the whole rectangle.
+		// then report a lower `best` (status 0 only; BT2X_DPL_EXACT_BEST recomputes those);
+		// candidates, records and edits are the full fill's.  kDebug (E/F/H digests) and
+		// band = 0 fill the whole rectangle.
 		int wdhi = 1 << 20, wdlo = 1 << 20;
 		if(!kDebug && a.band) {
 			const int mo = imax(1, rdo < rfo ? rdo : rfo);
@@ -702,6 +752,8 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			slo = slo < 0 ? 0 : (slo & ~3);
 			shi = (shi > rmax ? rmax : shi) | 3;            // whole blocks (steps past Rmax: unused rows)
 			shi = shi > kSteps - 1 ? kSteps - 1 : shi;
+			// cells this lane's sweep computes for the pair (two per step)
+			if(active && shi >= slo) st_comp += 2u * (unsigned)(shi - slo + 1);
 			asm volatile("" : "+s"(rmax), "+s"(rmin), "+v"(rl), "+s"(slo), "+s"(shi));
 			// row-info loads stay inside the pair (hoisted out of it they would hold all 40
 			// words in VGPRs)
@@ -735,28 +787,50 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				              : (st == kRows) ? (perm(iw, 0, 0x0c070c0cu) | (kNone & 0xffu))
 				              : (r == 0) ? perm(iv, iw, 0x0c070c00u)
 				                         : perm(0, iw, 0x0c000c00u | ((uint32_t)(r - 1) << 16) | (uint32_t)r);
-				const uint32_t hsw = st < kRows ? Hs[blk] : 0u, esw = st < kRows ? Es[blk] : 0u;
-				// hl: H[st][j0-1] | H[st-1][j0] (row -1 of any column is 0xff: start anywhere)
-				const uint32_t hl = (st == 0) ? perm(0, hsw, 0x0c0c0c00u) | 0x00ff0000u
-				                              : perm(hp, hsw, 0x0c040c00u | (uint32_t)r);
-				const uint32_t el = (st == 0) ? perm(0, esw, 0x0c0c0c00u)
-				                              : perm(ep, esw, 0x0c040c00u | (uint32_t)r);
-				const uint32_t hdiag = (st == 0) ? 0x000000ffu : hlp;
+				uint32_t hl, el, hdiag;
+				if(!kWide) {
+					const uint32_t hsw = st < kRows ? Hs[blk] : 0u, esw = st < kRows ? Es[blk] : 0u;
+					// hl: H[st][j0-1] | H[st-1][j0] (row -1 of any column is 0xff: start anywhere)
+					hl = (st == 0) ? perm(0, hsw, 0x0c0c0c00u) | 0x00ff0000u
+					               : perm(hp, hsw, 0x0c040c00u | (uint32_t)r);
+					el = (st == 0) ? perm(0, esw, 0x0c0c0c00u)
+					               : perm(ep, esw, 0x0c040c00u | (uint32_t)r);
+					hdiag = (st == 0) ? 0x000000ffu : hlp;
+				} else {
+					const int hw = st >> 1, hr = st & 1;
+					const uint32_t hsw = st < kRows ? Hs[hw < kStateWords ? hw : kStateWords - 1] : 0u;
+					const uint32_t esw = st < kRows ? Es[hw < kStateWords ? hw : kStateWords - 1] : 0u;
+					const uint32_t hsel = hr ? 0x05040302u : 0x05040100u;
+					hl = (st == 0) ? ((hsw & 0xffffu) | topHi) : perm(hp, hsw, hsel);
+					el = (st == 0) ? (esw & 0xffffu) : perm(ep, esw, hsel);
+					hdiag = (st == 0) ? topLo : hlp;
+				}
 				// penalty: 0 on a match, mm on a mismatch, npen if either base is N
 				// (x & 7) << 8 is >= 256 in a half whose codes differ: min(mm, that) = mm or 0
 				// (x != 0 also for N bases: a read N is 7 and a reference N is 4)
 				const uint32_t xrc = (info ^ refc2) & 0x00070007u;
 				uint32_t pen = pmin(pshr(info, 4), xrc << 8);
 				pen = (pen & ~coln) | (npen2 & coln);
-				// gap barrier rows: open/extend penalties >= 256 saturate the term to 0;
-				// row 0 has no F (low half at st 0, high half at st 1)
 				const uint32_t gbm = info & 0x00080008u;
-				const uint32_t r0 = (st == 0) ? 0x00000100u : (st == 1) ? 0x01000000u : 0u;
-				const uint32_t rdoe = (gbm << 5) + rdo2, rfoe = (gbm << 5) + (rfo2 + r0), rfee = (gbm << 5) + (rfe2 + r0);
 				const uint32_t d = psubs(hdiag, pen);
-				const uint32_t hl_o = psubs(hl, rdoe), el_e = psubs(el, rde2);
+				uint32_t hl_o, el_e, hu_o, fu_e;
+				if(!kWide) {
+					// gap barrier rows: open/extend penalties >= 256 saturate the term to 0;
+					// row 0 has no F (low half at st 0, high half at st 1)
+					const uint32_t r0 = (st == 0) ? 0x00000100u : (st == 1) ? 0x01000000u : 0u;
+					const uint32_t rdoe = (gbm << 5) + rdo2, rfoe = (gbm << 5) + (rfo2 + r0), rfee = (gbm << 5) + (rfe2 + r0);
+					hl_o = psubs(hl, rdoe); el_e = psubs(el, rde2);
+					hu_o = psubs(hp, rfoe); fu_e = psubs(fp, rfee);
+				} else {
+					// 16-bit halves: barred terms are masked to the floor (0x8000 added twice in
+					// the reference, aligner_swsse_ee_i16.cpp:112 and :400-420)
+					const uint32_t r0 = (st == 0) ? 0x0000ffffu : (st == 1) ? 0xffff0000u : 0u;
+					const uint32_t bm = (gbm >> 3) * 0xffffu;
+					const uint32_t fm = ~(bm | r0);
+					hl_o = psubs(hl, rdo2) & ~bm; el_e = psubs(el, rde2);
+					hu_o = psubs(hp, rfo2) & fm; fu_e = psubs(fp, rfe2) & fm;
+				}
 				const uint32_t e = pmax(hl_o, el_e);
-				const uint32_t hu_o = psubs(hp, rfoe), fu_e = psubs(fp, rfee);
 				const uint32_t f = pmax(hu_o, fu_e);
 				const uint32_t h = pmax(pmax(d, e), f);
 				// traceback flags
@@ -767,27 +841,36 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				tb = (tb << 1) | pne(d, h, one2);                      // TB_DNE
 				if(kDebug && a.digests) {
 					if(st < R && j0 < C) {
-						dg0 += cell_digest(st, j0, 0, e & 0xffffu);
-						dg1 += cell_digest(st, j0, 1, f & 0xffffu);
-						dg2 += cell_digest(st, j0, 2, h & 0xffffu);
+						dg0 += cell_digest(st, j0, 0, (e & 0xffffu) ^ dgx);
+						dg1 += cell_digest(st, j0, 1, (f & 0xffffu) ^ dgx);
+						dg2 += cell_digest(st, j0, 2, (h & 0xffffu) ^ dgx);
 					}
 					if(st >= 1 && st - 1 < R && j0 + 1 < C) {
-						dg0 += cell_digest(st - 1, j0 + 1, 0, e >> 16);
-						dg1 += cell_digest(st - 1, j0 + 1, 1, f >> 16);
-						dg2 += cell_digest(st - 1, j0 + 1, 2, h >> 16);
+						dg0 += cell_digest(st - 1, j0 + 1, 0, (e >> 16) ^ dgx);
+						dg1 += cell_digest(st - 1, j0 + 1, 1, (f >> 16) ^ dgx);
+						dg2 += cell_digest(st - 1, j0 + 1, 2, (h >> 16) ^ dgx);
 					}
 				}
 				// last row of each column (per-lane R; only in the wave's R range)
 				if(st + 1 >= rmin) {                         // wave-uniform
-					lra = (st == rl - 1) ? (int)(h & 0xffu) : lra;
-					lrb = (st == rl) ? (int)((h >> 16) & 0xffu) : lrb;
+					lra = (st == rl - 1) ? (int)(h & (kWide ? 0xffffu : 0xffu)) : lra;
+					lrb = (st == rl) ? (int)((h >> 16) & (kWide ? 0xffffu : 0xffu)) : lrb;
 				}
 				// the high half's outputs (row st-1 of column j0+1) replace row st-1 state
 				if(st >= 1) {
-					const int pb = (st - 1) >> 2, pr = (st - 1) & 3;
-					const uint32_t selh = (0x03020100u & ~(0xffu << (8 * pr))) | (6u << (8 * pr));
-					Hs[pb] = perm(h, Hs[pb], selh);
-					Es[pb] = perm(e, Es[pb], selh);
+					if(!kWide) {
+						const int pb = (st - 1) >> 2, pr = (st - 1) & 3;
+						const uint32_t selh = (0x03020100u & ~(0xffu << (8 * pr))) | (6u << (8 * pr));
+						Hs[pb] = perm(h, Hs[pb], selh);
+						Es[pb] = perm(e, Es[pb], selh);
+					} else {
+						const int pb = (st - 1) >> 1;
+						const uint32_t selh = ((st - 1) & 1) ? 0x07060100u : 0x03020706u;
+						if(pb < kStateWords) {
+							Hs[pb] = perm(h, Hs[pb], selh);
+							Es[pb] = perm(e, Es[pb], selh);
+						}
+					}
 				}
 				// two steps' flags of both columns per traceback dword
 				if(st & 1) {
@@ -805,12 +888,14 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			}
 			}
 			if(j0 < C) {
-				lastrow[(size_t)j0 * 64 + lane] = (uint8_t)lra;
+				if(kWide) lastrow16[(size_t)j0 * 64 + lane] = (uint16_t)lra;
+				else lastrow[(size_t)j0 * 64 + lane] = (uint8_t)lra;
 				lrmax = imax(lrmax, lra);
 				ncand += (lra >= thr);
 			}
 			if(j0 + 1 < C) {
-				lastrow[(size_t)(j0 + 1) * 64 + lane] = (uint8_t)lrb;
+				if(kWide) lastrow16[(size_t)(j0 + 1) * 64 + lane] = (uint16_t)lrb;
+				else lastrow[(size_t)(j0 + 1) * 64 + lane] = (uint8_t)lrb;
 				lrmax = imax(lrmax, lrb);
 				ncand += (lrb >= thr);
 			}
@@ -825,51 +910,86 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		}
 		bt2x_dp_out o;
 		o.nrec = 0; o.rec_off = 0;
-		const int score = lrmax - 0xff;
-		if(score < p.minsc) {
-			o.status = 0; o.best = score; o.ncand = 0;
+		int status = 0, best = 0;
+		dp_verdict(i16, lrmax, p.minsc, ncand, status, best);
+		if(refused) { status = -1; best = 0; atomicAdd(&a.counters[3], 1u); }
+		o.status = status; o.best = best; o.ncand = status > 0 ? (uint16_t)ncand : (uint16_t)0;
+		if(status <= 0) {
 			a.out[pi] = o;
+			// the banded fill's best of a failed problem is a lower bound: queue it for the
+			// exact pass (dp_wave_kernel<true>)
+			if(status == 0 && a.fail_list && a.band && !kDebug) a.fail_list[atomicAdd(&a.counters[2], 1u)] = pi;
 			if(kDebug && a.cands)
 				for(int k = 0; k < kCols; k++) a.cands[(size_t)pi * kCols + k] = 0xffffffffu;
 			continue;
 		}
-		o.status = ncand > 0 ? 1 : 0; o.best = score; o.ncand = (uint16_t)ncand;
 		// ------------- candidate order (DpBtCandidate: score desc, col desc) --------
-		// the last row moves into LDS; repeated max-below-key scans emit the sorted
-		// candidate columns for the walk kernel
-		// (up to the wave's widest problem: columns >= C read as score 0)
+		// the last row moves into LDS as one key byte per column (u8: the cell value, 0
+		// below the threshold never being reached; wide: value - threshold + 1 when it
+		// qualifies, else 0 -- a byte when -minsc <= 254, which holds for every u8
+		// problem and every i16 problem of default scoring); repeated max-below-key scans
+		// emit the sorted candidate columns for the walk (up to the wave's widest problem:
+		// columns >= C read as key 0)
 		const int nw = (Cmax + 3) >> 2;                  // wave-uniform (Cmax: all lanes)
-		for(int q = 0; q < nw; q++) {
-			uint32_t w4 = 0;
-			for(int r = 0; r < 4; r++) {
-				const int j = q * 4 + r;
-				if(j < C) w4 |= (uint32_t)lastrow[(size_t)j * 64 + lane] << (8 * r);
-			}
-			lds[q * 64 + lane] = w4;
-		}
 		a.out[pi] = o;
-		int cur_key = 0xffff;
 		const int row0 = R - 1;
-		// Two columns per packed op: key = score << 8 | col in each 16-bit half; the max
-		// key below the previous one is the next candidate (keys of scores below the
-		// threshold are smaller than every qualifying key and are never reached).
-		for(int k = 0; k < ncand; k++) {
-			const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
-			uint32_t best2 = 0;
-#pragma unroll 2
+		const bool byteKeys = !kWide || __builtin_amdgcn_readfirstlane(wave_max(-(int)p.minsc)) <= 254;
+		if(byteKeys) {
 			for(int q = 0; q < nw; q++) {
-				const uint32_t w4 = lds[q * 64 + lane];
-				const uint32_t cq = (uint32_t)q * 0x40004u + 0x10000u;     // cols 4q, 4q+1
-				const uint32_t ka = perm(cq, w4, 0x01060004u);             // [4q, s0, 4q+1, s1]
-				const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);  // [4q+2, s2, 4q+3, s3]
-				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
-				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
+				uint32_t w4 = 0;
+				for(int r = 0; r < 4; r++) {
+					const int j = q * 4 + r;
+					if(j < C) {
+						uint32_t kv;
+						if(!kWide) kv = lastrow[(size_t)j * 64 + lane];
+						else { const int v = lastrow16[(size_t)j * 64 + lane]; kv = v >= thr ? (uint32_t)(v - thr + 1) : 0u; }
+						w4 |= kv << (8 * r);
+					}
+				}
+				lds[q * 64 + lane] = w4;
 			}
-			const int best = (int)max(best2 & 0xffffu, best2 >> 16);
-			cur_key = best;
-			cands[(size_t)k * 64 + lane] = (uint8_t)(best & 0xff);
-			if(kDebug && a.cands)
-				a.cands[(size_t)pi * kCols + k] = BT2X_CAND_PACK(row0, best & 0xff, best >> 8);
+			int cur_key = 0xffff;
+			// Two columns per packed op: key = score << 8 | col in each 16-bit half; the max
+			// key below the previous one is the next candidate (keys of scores below the
+			// threshold are smaller than every qualifying key and are never reached).
+			for(int k = 0; k < ncand; k++) {
+				const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
+				uint32_t best2 = 0;
+#pragma unroll 2
+				for(int q = 0; q < nw; q++) {
+					const uint32_t w4 = lds[q * 64 + lane];
+					const uint32_t cq = (uint32_t)q * 0x40004u + 0x10000u;     // cols 4q, 4q+1
+					const uint32_t ka = perm(cq, w4, 0x01060004u);             // [4q, s0, 4q+1, s1]
+					const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);  // [4q+2, s2, 4q+3, s3]
+					best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
+					best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
+				}
+				const int bk = (int)max(best2 & 0xffffu, best2 >> 16);
+				cur_key = bk;
+				cands[(size_t)k * 64 + lane] = (uint8_t)(bk & 0xff);
+				if(kDebug && a.cands) {
+					const int score = kWide ? (bk >> 8) - 1 + thr : (bk >> 8);
+					a.cands[(size_t)pi * kCols + k] = i16 ? BT2X_CAND_PACK16(bk & 0xff, score - 0x8000)
+					                                      : BT2X_CAND_PACK(row0, bk & 0xff, score);
+				}
+			}
+		} else {
+			// an i16 problem with minsc < -254 in the wave: 32-bit keys (value << 8 | col)
+			// straight from the last row (rare: non-default --score-min)
+			int cur_key = 0x7fffffff;
+			for(int k = 0; k < ncand; k++) {
+				int bk = -1;
+				for(int j = 0; j < Cmax; j++) {
+					const int v = j < C ? (int)lastrow16[(size_t)j * 64 + lane] : -1;
+					const int key = v >= thr ? ((v << 8) | j) : -1;
+					bk = (key < cur_key && key > bk) ? key : bk;
+				}
+				cur_key = bk;
+				cands[(size_t)k * 64 + lane] = (uint8_t)(bk & 0xff);
+				if(kDebug && a.cands)
+					a.cands[(size_t)pi * kCols + k] = i16 ? BT2X_CAND_PACK16(bk & 0xff, (bk >> 8) - 0x8000)
+					                                      : BT2X_CAND_PACK(row0, bk & 0xff, bk >> 8);
+			}
 		}
 		if(kDebug && a.cands)
 			for(int k = ncand; k < kCols; k++) a.cands[(size_t)pi * kCols + k] = 0xffffffffu;
@@ -884,11 +1004,13 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			st_cells += __shfl_xor(st_cells, d);
 			st_cols += __shfl_xor(st_cols, d);
 			st_bt += __shfl_xor(st_bt, d);
+			st_comp += __shfl_xor(st_comp, d);
 		}
 		if(lane == 0) {
 			atomicAdd(&a.stats[0], st_cells);
 			atomicAdd(&a.stats[1], st_cols);
 			if(kFused) atomicAdd(&a.stats[2], st_bt);
+			atomicAdd(&a.stats[3], st_comp);
 		}
 	}
 }
@@ -927,131 +1049,109 @@ static int blocks_per_cu(const void* fn) {
 	return nb;
 }
 
+// Resident workgroups per CU of every DP kernel variant, measured once (thread-safe
+// static initialisation).
+namespace {
+struct DpOccupancy {
+	int fused[2][2];                // [debug][wide]
+	int fill[2][2];                 // split-mode fill kernels
+	int walk, wave;
+	DpOccupancy() {
+		fused[0][0] = blocks_per_cu((const void*)dp_fill_kernel<false, true, false>);
+		fused[1][0] = blocks_per_cu((const void*)dp_fill_kernel<true, true, false>);
+		fused[0][1] = blocks_per_cu((const void*)dp_fill_kernel<false, true, true>);
+		fused[1][1] = blocks_per_cu((const void*)dp_fill_kernel<true, true, true>);
+		fill[0][0] = blocks_per_cu((const void*)dp_fill_kernel<false, false, false>);
+		fill[1][0] = blocks_per_cu((const void*)dp_fill_kernel<true, false, false>);
+		fill[0][1] = blocks_per_cu((const void*)dp_fill_kernel<false, false, true>);
+		fill[1][1] = blocks_per_cu((const void*)dp_fill_kernel<true, false, true>);
+		walk = blocks_per_cu((const void*)dp_walk_kernel);
+		wave = blocks_per_cu((const void*)dp_wave_kernel<true>);
+	}
+};
+const DpOccupancy& occupancy() { static const DpOccupancy o; return o; }
+
 // DP modes: fused (default): one persistent kernel fills and walks each group (the walk
-// reads bytes written moments ago); split: fill kernel over a chunk, then a walk kernel.
-static int dp_mode() {                          // 0 fused, 1 split, 2 concurrent split
-	static int m = -1;
-	if(m < 0) { const char* e = getenv("BT2X_DP_MODE"); m = (e && e[0] == 's') ? 1 : (e && e[0] == 'c') ? 2 : 0; }
-	return m;
+// reads bytes written moments ago); split (BT2X_DP_MODE=split, experiments): fill
+// kernel over a chunk, then a walk kernel.  Read per launch.
+bool dp_split_mode() {
+	const char* e = getenv("BT2X_DP_MODE");
+	return e && e[0] == 's';
 }
-static bool dp_split_mode() { return dp_mode() != 0; }
-// Concurrent split mode: chunks of kConcGroups groups, double-buffered; the fill of chunk
-// i+1 (2 waves/SIMD) runs beside the walk of chunk i (second stream, low-VGPR kernel), so
-// the walks' load latency no longer holds fill issue slots.
-constexpr uint32_t kConcGroups = 1024;
 
 // Largest launch run one wave per problem (BT2X_DP_WAVE=0: never, =1: always; else
 // BT2X_DP_WAVE_MAX problems, default 32768: below that a lane-per-problem launch does not
 // fill the chip and costs its serial R x C fill anyway).
-static uint32_t dp_wave_max() {                 // read per launch (tests switch modes)
+uint32_t dp_wave_max() {                        // read per launch (tests switch modes)
 	const char* w = getenv("BT2X_DP_WAVE");
 	const char* x = getenv("BT2X_DP_WAVE_MAX");
 	return (w && w[0] == '0') ? 0u : (w && w[0] == '1') ? 0xffffffffu : (x ? (uint32_t)atoll(x) : 32768u);
 }
 
+template<bool kDebug, bool kFused>
+void launch_fill(bool wide, uint32_t grid, hipStream_t s, const DevScoring& sc, const DpLaunch& a, uint32_t base,
+                 uint32_t np) {
+	if(wide) hipLaunchKernelGGL((dp_fill_kernel<kDebug, kFused, true>), dim3(grid), dim3(64), 0, s, sc, a, base, np);
+	else hipLaunchKernelGGL((dp_fill_kernel<kDebug, kFused, false>), dim3(grid), dim3(64), 0, s, sc, a, base, np);
+}
+} // namespace
+
 // Scratch: split = `chunk_groups` fill group regions + one staging slot per resident walk
-// wave; fused = one group region + staging slot per resident fill wave.
+// wave; fused = one group region + staging slot per resident fill wave (the wave-per-
+// problem mode uses the same region as per-wave record staging).
 size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups) {
+	const DpOccupancy& o = occupancy();
 	if(!dp_split_mode()) {
-		const int nb = max(blocks_per_cu((const void*)dp_fill_kernel<false, true>),
-		                   blocks_per_cu((const void*)dp_fill_kernel<true, true>));
+		int nb = 0;
+		for(int d = 0; d < 2; d++) for(int w = 0; w < 2; w++) nb = max(nb, o.fused[d][w]);
 		return (size_t)ncu * nb * (kGroupBytes + kWalkSlotBytes);
 	}
-	const size_t walk_slots = (size_t)ncu * blocks_per_cu((const void*)dp_walk_kernel);
-	if(dp_mode() == 2) {
-		const uint32_t cg = chunk_groups < kConcGroups ? chunk_groups : kConcGroups;
-		return 2 * (size_t)cg * kGroupBytes + walk_slots * kWalkSlotBytes;
-	}
-	return (size_t)chunk_groups * kGroupBytes + walk_slots * kWalkSlotBytes;
+	return (size_t)chunk_groups * kGroupBytes + (size_t)ncu * o.walk * kWalkSlotBytes;
 }
 
-// Split mode runs the batch in chunks of chunk_groups x 64 problems: fill (persistent grid
-// sized by occupancy, VGPR-bound) then walk per chunk, on one stream.
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 	if(a0.n == 0) return 0;
 	hipStream_t s = (hipStream_t)stream;
-	static int fill_bpc_dbg = 0, fill_bpc = 0, fused_bpc_dbg = 0, fused_bpc = 0, walk_bpc = 0;
-	if(!fill_bpc) {
-		fill_bpc = blocks_per_cu((const void*)dp_fill_kernel<false, false>);
-		fill_bpc_dbg = blocks_per_cu((const void*)dp_fill_kernel<true, false>);
-		fused_bpc = blocks_per_cu((const void*)dp_fill_kernel<false, true>);
-		fused_bpc_dbg = blocks_per_cu((const void*)dp_fill_kernel<true, true>);
-		walk_bpc = blocks_per_cu((const void*)dp_walk_kernel);
-	}
+	const DpOccupancy& occ = occupancy();
 	const bool dbg = a0.digests || a0.cands;
+	const bool wide = a0.wide != 0;
 	DpLaunch a = a0;
 	const uint32_t groups_all = (a0.n + 63) / 64;
 	if(!dbg && a0.n <= dp_wave_max()) {
-		// small launch: one wave per problem (persistent, 4 waves per CU by LDS)
+		// small launch: one wave per problem (persistent, 4 waves per CU by LDS); it fills
+		// whole rectangles, so every best is exact
 		uint32_t wb = (uint32_t)a0.ncu * 4u;
 		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
 		if(wb > slots) wb = (uint32_t)slots;
 		if(wb > a0.n) wb = a0.n;
-		hipLaunchKernelGGL(dp_wave_kernel, dim3(wb), dim3(64), 0, s, sc, a);
+		hipLaunchKernelGGL(dp_wave_kernel<false>, dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
 	if(!dp_split_mode()) {
-		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)(dbg ? fused_bpc_dbg : fused_bpc);
+		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.fused[dbg ? 1 : 0][wide ? 1 : 0];
 		if(fb > groups_all) fb = groups_all;
-		if(dbg) hipLaunchKernelGGL((dp_fill_kernel<true, true>), dim3(fb), dim3(64), 0, s, sc, a, 0u, a0.n);
-		else hipLaunchKernelGGL((dp_fill_kernel<false, true>), dim3(fb), dim3(64), 0, s, sc, a, 0u, a0.n);
-		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
-	}
-	if(dp_mode() == 2) {
-		static hipStream_t s2[64];
-		static hipEvent_t evf[64][2], evw[64][2], evj[64];
-		int dev = 0;
-		if(hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BT2X_E_NODEVICE;
-		if(!s2[dev]) {
-			if(hipStreamCreateWithFlags(&s2[dev], hipStreamNonBlocking) != hipSuccess) return BT2X_E_NODEVICE;
-			for(int b = 0; b < 2; b++) {
-				hipEventCreateWithFlags(&evf[dev][b], hipEventDisableTiming);
-				hipEventCreateWithFlags(&evw[dev][b], hipEventDisableTiming);
-			}
-			hipEventCreateWithFlags(&evj[dev], hipEventDisableTiming);
-		}
-		const uint32_t cg = a0.chunk_groups < kConcGroups ? a0.chunk_groups : kConcGroups;
-		a.walk_scratch = a0.scratch + 2 * (size_t)cg * kGroupBytes;
-		const uint32_t chunk = cg * 64;
-		hipEventRecord(evj[dev], s);                       // the walk stream starts after prior work
-		hipStreamWaitEvent(s2[dev], evj[dev], 0);
-		uint32_t i = 0;
-		for(uint32_t base = 0; base < a0.n; base += chunk, i++) {
+		if(dbg) launch_fill<true, true>(wide, fb, s, sc, a, 0u, a0.n);
+		else launch_fill<false, true>(wide, fb, s, sc, a, 0u, a0.n);
+	} else {
+		a.walk_scratch = a0.scratch + (size_t)a0.chunk_groups * kGroupBytes;
+		const uint32_t chunk = a0.chunk_groups * 64;
+		for(uint32_t base = 0; base < a0.n; base += chunk) {
 			const uint32_t np = (a0.n - base < chunk) ? a0.n - base : chunk;
 			const uint32_t groups = (np + 63) / 64;
-			const int b = (int)(i & 1);
-			DpLaunch ai = a;
-			ai.scratch = a0.scratch + (size_t)b * cg * kGroupBytes;
-			if(i >= 2) hipStreamWaitEvent(s, evw[dev][b], 0);   // chunk i-2's walk left the buffer
-			uint32_t fb = (uint32_t)a0.ncu * 8u;               // 2 waves per SIMD
+			uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.fill[dbg ? 1 : 0][wide ? 1 : 0];
 			if(fb > groups) fb = groups;
-			if(dbg) hipLaunchKernelGGL((dp_fill_kernel<true, false>), dim3(fb), dim3(64), 0, s, sc, ai, base, np);
-			else hipLaunchKernelGGL((dp_fill_kernel<false, false>), dim3(fb), dim3(64), 0, s, sc, ai, base, np);
-			hipEventRecord(evf[dev][b], s);
+			if(dbg) launch_fill<true, false>(wide, fb, s, sc, a, base, np);
+			else launch_fill<false, false>(wide, fb, s, sc, a, base, np);
 			if(a0.ablate == 1) continue;
-			hipStreamWaitEvent(s2[dev], evf[dev][b], 0);
-			uint32_t wb = (uint32_t)a0.ncu * 8u;
+			uint32_t wb = (uint32_t)a0.ncu * (uint32_t)occ.walk;
 			if(wb > groups) wb = groups;
-			hipLaunchKernelGGL(dp_walk_kernel, dim3(wb), dim3(64), 0, s2[dev], sc, ai, base, np);
-			hipEventRecord(evw[dev][b], s2[dev]);
+			hipLaunchKernelGGL(dp_walk_kernel, dim3(wb), dim3(64), 0, s, sc, a, base, np);
 		}
-		hipEventRecord(evj[dev], s2[dev]);
-		hipStreamWaitEvent(s, evj[dev], 0);
-		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
-	a.walk_scratch = a0.scratch + (size_t)a0.chunk_groups * kGroupBytes;
-	const uint32_t chunk = a0.chunk_groups * 64;
-	for(uint32_t base = 0; base < a0.n; base += chunk) {
-		const uint32_t np = (a0.n - base < chunk) ? a0.n - base : chunk;
-		const uint32_t groups = (np + 63) / 64;
-		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)(dbg ? fill_bpc_dbg : fill_bpc);
-		if(fb > groups) fb = groups;
-		if(dbg) hipLaunchKernelGGL((dp_fill_kernel<true, false>), dim3(fb), dim3(64), 0, s, sc, a, base, np);
-		else hipLaunchKernelGGL((dp_fill_kernel<false, false>), dim3(fb), dim3(64), 0, s, sc, a, base, np);
-		if(a0.ablate == 1) continue;
-		uint32_t wb = (uint32_t)a0.ncu * (uint32_t)walk_bpc;
-		if(wb > groups) wb = groups;
-		hipLaunchKernelGGL(dp_walk_kernel, dim3(wb), dim3(64), 0, s, sc, a, base, np);
+	// exact best of the problems the banded fill failed (queued in a.fail_list)
+	if(a0.fail_list && a0.band && !dbg) {
+		const uint32_t wb = (uint32_t)a0.ncu * (uint32_t)occ.wave;
+		hipLaunchKernelGGL(dp_wave_kernel<true>, dim3(wb), dim3(64), 0, s, sc, a);
 	}
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -496,7 +497,7 @@ void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, 
 
 // SwAligner::initRef's problem for key k (the window, BitPairReference::getStretch, is
 // fetched when the scheduler gathers the launch).
-void pose_dp(std::vector<DpWork>& dps, const DpKey& k, size_t rdlen, int nceil) {
+void pose_dp(const Params& P, std::vector<DpWork>& dps, const DpKey& k, size_t rdlen, int nceil) {
 	dps.emplace_back();
 	DpWork& d = dps.back();
 	d.key = k;
@@ -504,7 +505,10 @@ void pose_dp(std::vector<DpWork>& dps, const DpKey& k, size_t rdlen, int nceil) 
 	d.in.refl = k.refl;
 	d.in.rdlen = (uint16_t)rdlen;
 	d.in.ncol = (uint16_t)k.ncol;
-	d.in.minsc = (int16_t)std::max<int64_t>(k.minsc, -254);
+	const bool i16 = P.dpI16(k.minsc);
+	if(i16 && k.minsc < -32767) throw std::runtime_error("minimum score below the i16 kernel's range");
+	d.in.minsc = (int16_t)std::max<int64_t>(k.minsc, i16 ? -32767 : -254);
+	d.in.flags = i16 ? BT2X_DP_I16 : 0;
 	d.in.nceil = (int16_t)nceil;
 	d.in.triml = (uint16_t)k.triml; d.in.corel = (uint16_t)k.corel; d.in.corer = (uint16_t)k.corer;
 	d.in.fw = k.fw ? 1 : 0;
@@ -701,7 +705,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 	// P0, bt2_search.cpp:2467-2553
 	int64_t minsc = P.scoreMin.f<int64_t>((double)rdlen);
 	if(minsc > 0) minsc = 0;
-	else if(minsc < -254) minsc = -254;
+	else if(minsc < -254 && !P.i16build) minsc = -254;        // stock build only
 	PH_START();
 	Rng rnd;
 	rnd.init(rd.seed);
@@ -811,7 +815,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 					// pose this problem and the ones the walk reaches next if each of them
 					// fails (a copy of the walk over copies of the state it advances)
 					c->dps.clear();
-					pose_dp(c->dps, key, rdlen, swNceil);
+					pose_dp(P, c->dps, key, rdlen, swNceil);
 					if(P.lookahead > 1) {
 						Rng rnd2 = rnd;
 						Prm prm2 = prm;
@@ -828,7 +832,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 							}
 							bool dup = false;
 							for(const DpWork& d : c->dps) dup = dup || d.key == k2;
-							if(!dup) pose_dp(c->dps, k2, rdlen, swNceil);
+							if(!dup) pose_dp(P, c->dps, k2, rdlen, swNceil);
 						}
 					}
 					PH(6);
@@ -853,12 +857,12 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 					const bt2x_aln_rec& rec = c->recs[d.rec0 + k];
 					// -M tightening below raises minsc between the calls of this problem, but the
 					// record sequence needs no re-filtering: nextAlignment's score filter compares
-					// the candidate's raw u8 cell value (DpBtCandidate::score = lr in 0..255,
-					// aligner_swsse_ee_u8.cpp:519) with minsc <= 0 (aligner_sw.cpp:274), so it
-					// never fires and the calls proceed exactly as posed (tests/test_e2e.py,
-					// tandem-repeat fixture).
+					// the candidate's raw cell value (DpBtCandidate::score = lr: 0..255 for u8,
+					// aligner_swsse_ee_u8.cpp:519; >= 0 for every i16 candidate, i16.cpp:527)
+					// with minsc <= 0 (aligner_sw.cpp:274), so it never fires and the calls
+					// proceed exactly as posed (tests/test_e2e.py, tandem-repeat fixture).
 					if(minsc != minsc_posed) c->ntight++;
-					replay_backtrace_draws(rnd, rec.ntries);
+					replay_backtrace_draws(rnd, rec.ntries, P.dpI16(key.minsc));
 					// the call's writes to the read's edit buffer (bt2x.h)
 					if(c->edbuf.size() < rec.nbuf) c->edbuf.resize(rec.nbuf);
 					std::copy(c->edits.begin() + rec.edit_off, c->edits.begin() + rec.edit_off + rec.nbuf, c->edbuf.begin());
@@ -1080,7 +1084,10 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	}
 	if(nws) { st.seed_launches++; st.seeds += L.seed_in.size(); st.t_seed += L.t_seed; }
 	if(nwr) { st.resolve_launches++; st.resolves += L.res_in.size(); st.t_resolve += L.t_resolve; }
-	if(nwd) { st.dp_launches++; st.dps += L.dp_in.size(); st.t_dp += L.t_dp; }
+	if(nwd) {
+		st.dp_launches++; st.dps += L.dp_in.size(); st.t_dp += L.t_dp;
+		st.dp_max_launch = std::max<uint64_t>(st.dp_max_launch, L.dp_in.size());
+	}
 	st.t_backend += L.t_seed + L.t_resolve + L.t_dp + L.t_round;
 	L.run.clear();
 	L.run.insert(L.run.end(), L.wn.begin(), L.wn.end());
@@ -1309,7 +1316,7 @@ namespace {
 struct LaunchSizes {
 	size_t nr, nd, np;
 	LaunchSizes(const Params& p, size_t reads)
-		: nr(reads / 2), nd(reads), np(reads * 3) {}
+		: nr(reads / 2), nd(reads), np(reads * 3) { (void)p; }
 };
 }
 
@@ -1398,20 +1405,35 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		std::vector<ReadCtx*> co[2];
 		const size_t cap = slots / 2;
 		auto empty = [](const Launch& L) { return L.ws.empty() && L.wr.empty() && L.wd.empty() && L.wn.empty(); };
+		// A backend error on the GPU thread is carried over to this one and rethrown after
+		// the join; unwinding on either side joins the thread first (a joinable std::thread
+		// must not be destroyed).
+		std::exception_ptr gpu_err;
+		auto start = [&](int k) {
+			return std::thread([this, k, &gpu_err] {
+				try { execute(launch_[k]); } catch(...) { gpu_err = std::current_exception(); }
+			});
+		};
+		std::thread gpu;
+		struct Joiner { std::thread& t; ~Joiner() { if(t.joinable()) t.join(); } } joiner{gpu};
+		auto join = [&] {
+			gpu.join();
+			if(gpu_err) std::rethrow_exception(gpu_err);
+		};
 		int a = 0;
 		refill(co[0], cap);
 		gather(launch_[0], co[0]);
-		std::thread gpu([this] { execute(launch_[0]); });
+		gpu = start(0);
 		refill(co[1], cap);
 		gather(launch_[1], co[1]);
 		while(true) {
 			// invariant: the GPU thread runs launch a (cohort a waits on it); launch b is
 			// gathered from cohort b
 			const double t0 = now_s();
-			gpu.join();
+			join();
 			st.t_wait += now_s() - t0;
 			const int b = 1 - a;
-			gpu = std::thread([this, b] { execute(launch_[b]); });
+			gpu = start(b);
 			const double t1 = now_s();
 			scatter_resume(launch_[a], st);
 			retire_write(co[a]);
@@ -1421,7 +1443,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			if(eof && co[a].empty() && co[b].empty() && empty(launch_[a]) && empty(launch_[b])) break;
 			a = b;
 		}
-		if(gpu.joinable()) gpu.join();
+		join();
 	}
 	writer.finish();
 	if(t_run) *t_run = now_s() - t_start;

@@ -413,6 +413,11 @@ struct Params {
 	int tighten = 3;
 	uint32_t randSeed = 0;          // --seed
 	bool nofw = false, norc = false;
+	// DP kernel choice (aligner_sw.cpp:77-83, bt2_search.cpp:1350-1356, 2484-2492): the stock
+	// build runs u8 only, minsc clamped to -254; a -DENABLE_I16 build (i16build) keeps minsc
+	// and runs the i16 kernel unless enable8 && minsc >= -254.  --no-sse8 implies i16build
+	// (the stock build ignores it with a warning).
+	bool enable8 = true, i16build = false;
 	size_t lookahead = 8;           // DP problems posed per request (not a reference option;
 	                                // results do not depend on it)
 	Params() {
@@ -436,7 +441,36 @@ struct Params {
 		while(s >= minsc) { s -= first ? refGapOpen() : refGapExtend(); first = false; num++; }
 		return num - 1;
 	}
+	// SwAligner::initRef's enable8_ (aligner_sw.cpp:77-83)
+	bool dpI16(int64_t minsc) const { return dp_uses_i16(i16build, enable8, minsc); }
 };
+
+// SeedAlignmentPolicy's PARSE_FUNC (aligner_seed_policy.cpp:47-75) over an existing
+// function: type, constant, coefficient, minimum -- and a fifth token sets the minimum
+// too, as there.  false on a bad type letter.
+inline bool parse_func_tokens(SimpleFunc& f, const std::string& s) {
+	std::vector<std::string> t;
+	size_t b = 0;
+	for(;;) {
+		const size_t e = s.find(',', b);
+		t.push_back(s.substr(b, e == std::string::npos ? std::string::npos : e - b));
+		if(e == std::string::npos) break;
+		b = e + 1;
+	}
+	if(t.size() >= 1) {
+		const std::string& y = t[0];
+		if(y == "C" || y == "Constant") f.type = 1;
+		else if(y == "L" || y == "Linear") f.type = 2;
+		else if(y == "S" || y == "Sqrt") f.type = 3;
+		else if(y == "G" || y == "Log") f.type = 4;
+		else return false;
+	}
+	if(t.size() >= 2) f.C = std::strtod(t[1].c_str(), nullptr);
+	if(t.size() >= 3) f.L = std::strtod(t[2].c_str(), nullptr);
+	if(t.size() >= 4) f.I = std::strtod(t[3].c_str(), nullptr);
+	if(t.size() >= 5) f.I = std::strtod(t[4].c_str(), nullptr);
+	return true;
+}
 
 // The bowtie2-align-l options that change the hot path's results (bt2_search.cpp:446-643;
 // presets expand to -D/-R/-L/-i, SeedAlignmentPolicy).  Returns the number of argv
@@ -445,7 +479,19 @@ inline int parse_align_option(Params& p, int argc, char** argv, int i) {
 	const std::string a = argv[i];
 	const bool has = i + 1 < argc;
 	auto pair = [&](int& x, int& y) { std::sscanf(argv[i + 1], "%d,%d", &x, &y); };
+	if(a == "--sse8") { p.enable8 = true; return 1; }
+	if(a == "--no-sse8") { p.enable8 = false; p.i16build = true; return 1; }
+	if(a == "--i16-build") { p.i16build = true; return 1; }    // (not a reference option)
 	if(!has) return 0;
+	// --score-min / --n-ceil / -i: the policy strings of bt2_search.cpp:1436-1541, parsed
+	// by PARSE_FUNC; a malformed function is reported as an unconsumed option
+	if(a == "--score-min" || a == "--min-score") return parse_func_tokens(p.scoreMin, argv[i + 1]) ? 2 : 0;
+	if(a == "-i") return parse_func_tokens(p.msIval, argv[i + 1]) ? 2 : 0;
+	if(a == "--n-ceil") {
+		const std::string v = argv[i + 1];
+		const size_t ncomma = (size_t)std::count(v.begin(), v.end(), ',');
+		return parse_func_tokens(p.nCeil, ncomma == 2 ? v : "L," + v) ? 2 : 0;
+	}
 	if(a == "--dpad") { p.maxhalf = (size_t)std::atol(argv[i + 1]); return 2; }
 	if(a == "-D") { p.streak = (size_t)std::atol(argv[i + 1]); return 2; }
 	if(a == "-R") { p.nSeedRounds = std::atoi(argv[i + 1]); return 2; }
@@ -863,6 +909,7 @@ struct RunStats {
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
 	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
 	uint64_t round_launches = 0, rounds = 0, round_redo = 0;
+	uint64_t dp_max_launch = 0;     // problems in the largest DP launch
 	double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0,
 	       t_wait = 0, t_gather = 0, t_retire = 0;
 };

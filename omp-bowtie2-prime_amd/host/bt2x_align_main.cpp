@@ -4,8 +4,12 @@
 // there is no CPU fallback.
 //
 //   bt2x-align -x <index base> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N]
-//              [-L N] [--mp MX,MN] [--np N] [--rdg O,E] [--rfg O,E] [--gbar N]
-//              [--seed N] [-p threads] [--slots N] [--device N] [--stats]
+//              [-L N] [-i FUNC] [--score-min FUNC] [--n-ceil FUNC] [--mp MX,MN] [--np N]
+//              [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N] [--no-sse8] [--i16-build]
+//              [-p threads] [--slots N] [--device N] [--stats]
+// --no-sse8 runs the signed 16-bit DP as the reference's -DENABLE_I16 build does
+// (aligner_swsse_ee_i16.cpp); --i16-build emulates that build's default (u8 unless the
+// minimum score is below -254).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -203,7 +207,8 @@ private:
 void usage() {
 	std::fprintf(stderr,
 	             "usage: bt2x-align -x <index> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N] [-L N]\n"
-	             "                  [--mp MX,MN] [--np N] [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N]\n"
+	             "                  [-i FUNC] [--score-min FUNC] [--n-ceil FUNC] [--mp MX,MN] [--np N]\n"
+	             "                  [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N] [--no-sse8] [--i16-build]\n"
 	             "                  [-p threads] [--slots N] [--device N] [--stats]\n");
 }
 
@@ -255,6 +260,9 @@ int main(int argc, char** argv) {
 		RefInfo ref;
 		ref.init(index.desc(), idx);
 		bt2x::Device dev(device, index, p.sc);
+		// align()'s best of a failed DP feeds only --mapq-extra's ZT:Z, which this driver does
+		// not print: skip the kernels' exact-best pass (bt2x.h BT2X_OPT_EXACT_BEST)
+		bt2x::check(bt2x_set_option(dev.ctx(), BT2X_OPT_EXACT_BEST, 0), "bt2x_set_option");
 		HipBackend hip(dev.ctx());
 		set_host_allocator(PinnedCache::alloc, PinnedCache::release);   // launch buffers page-locked
 		std::unique_ptr<DumpBackend> dumper;
@@ -301,12 +309,13 @@ int main(int argc, char** argv) {
 			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "
 			             "resolve_launches=%llu resolves=%llu t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f "
 			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu t_backend=%.4f t_step=%.4f t_wait=%.4f t_gather=%.4f t_retire=%.4f "
-			             "round_launches=%llu rounds=%llu t_round=%.4f\n", (unsigned long long)st.reads, t_align,
+			             "round_launches=%llu rounds=%llu t_round=%.4f dp_max_launch=%llu\n", (unsigned long long)st.reads, t_align,
 			             (unsigned long long)st.seed_launches, (unsigned long long)st.seeds, st.t_seed,
 			             (unsigned long long)st.resolve_launches, (unsigned long long)st.resolves, st.t_resolve,
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io, (unsigned long long)st.dps_used,
 			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait, st.t_gather, st.t_retire,
-			             (unsigned long long)st.round_launches, (unsigned long long)st.rounds, st.t_round);
+			             (unsigned long long)st.round_launches, (unsigned long long)st.rounds, st.t_round,
+			             (unsigned long long)st.dp_max_launch);
 		if(stats) {
 			const HipBackend::GpuStats& g = hip.gs;
 			std::fprintf(stderr, "BT2X_GPU k_round=%.4f t_round_call=%.4f round_h2d_mib=%.1f round_d2h_mib=%.1f "

@@ -346,11 +346,15 @@ static inline int matches_ex(int i, int j) {           /* mask.h:37-43 */
 	return ((1 << i) & j) != 0 ? 1 : 0;
 }
 
+/* Cell values: u8 problems in [0, 0xff] (0xff = score 0, aligner_swsse_ee_u8.cpp:58-61);
+ * i16 problems (BT2X_DP_I16, aligner_swsse_ee_i16.cpp:58-63) hold the int16 value + 0x8000,
+ * i.e. [0, 0xffff] with 0xffff = score 0: saturating adds of non-positive scores in the
+ * signed domain are saturating subtractions of penalties here, floor 0 = 0x8000. */
 typedef struct {
 	int R, C;
-	uint8_t E[BT2X_MAX_ROWS][BT2X_MAX_COLS];
-	uint8_t F[BT2X_MAX_ROWS][BT2X_MAX_COLS];
-	uint8_t H[BT2X_MAX_ROWS][BT2X_MAX_COLS];
+	uint16_t E[BT2X_MAX_ROWS][BT2X_MAX_COLS];
+	uint16_t F[BT2X_MAX_ROWS][BT2X_MAX_COLS];
+	uint16_t H[BT2X_MAX_ROWS][BT2X_MAX_COLS];
 	uint8_t rt[BT2X_MAX_ROWS][BT2X_MAX_COLS];   /* reportedThrough bit */
 } dpmat_t;
 
@@ -520,17 +524,22 @@ int bt2o_dp_align(const bt2x_scoring* sc,
 		const bt2x_dp_in* p = &in[pi];
 		const int R = p->rdlen, C = p->ncol;
 		if(R < 1 || R > BT2X_MAX_ROWS || C < 1 || C + 1 > BT2X_MAX_COLS) { free(m); free(res); return BT2X_E_ARG; }
+		const int i16 = (p->flags & BT2X_DP_I16) != 0;
+		if(p->minsc > 0 || p->minsc < (i16 ? -32767 : -254)) { free(m); free(res); return BT2X_E_ARG; }
 		const uint8_t* rd = reads + p->read_off;
 		const uint8_t* qu = quals + p->qual_off;
 		const uint8_t* rf = refs + p->ref_off;
+		/* top: H of row -1 = score 0 (u8: 0xff; i16: 0x7fff + 0x8000) */
+		const int top = i16 ? 0xffff : 0xff;
 		m->R = R; m->C = C;
-		/* Fill: the exact saturating recurrence the striped kernel computes
-		 * (u8.cpp:249-536): H[-1][*] = 0xff, H[*][-1] = 0, E[*][0] = 0, F[0][*] = 0. */
+		/* Fill: the exact saturating recurrence the striped kernels compute (u8.cpp:249-536,
+		 * i16.cpp:253-541): H[-1][*] = top, H[*][-1] = floor, E[*][0] = floor, F[0][*] = floor;
+		 * the gap barrier subtracts top (u8: 0xff once; i16: 0x8000 added twice). */
 		int lrmax = 0, ncand = 0;
 		for(int j = 0; j < C; j++) {
 			int refm = 1 << rf[j];
 			for(int i = 0; i < R; i++) {
-				int gbar = (i < sc->gapbar || R - i - 1 < sc->gapbar) ? 0xff : 0;
+				int gbar = (i < sc->gapbar || R - i - 1 < sc->gapbar) ? top : 0;
 				int e = 0, f = 0;
 				if(j > 0) {
 					int e1 = sat(m->E[i][j - 1] - rde);
@@ -542,31 +551,39 @@ int bt2o_dp_align(const bt2x_scoring* sc,
 					int f2 = sat(m->H[i - 1][j] - rfo);
 					f = sat((f1 > f2 ? f1 : f2) - gbar);
 				}
-				int diag = (i == 0) ? 0xff : (j == 0 ? 0 : m->H[i - 1][j - 1]);
+				int diag = (i == 0) ? top : (j == 0 ? 0 : m->H[i - 1][j - 1]);
 				int pen = -sc_score(sc, rd[i], refm, qu[i] - 33);
 				int h = sat(diag - pen);
 				if(e > h) h = e;
 				if(f > h) h = f;
-				m->E[i][j] = (uint8_t)e; m->F[i][j] = (uint8_t)f; m->H[i][j] = (uint8_t)h;
+				m->E[i][j] = (uint16_t)e; m->F[i][j] = (uint16_t)f; m->H[i][j] = (uint16_t)h;
 				m->rt[i][j] = 0;
 			}
 			int lr = m->H[R - 1][j];
 			if(lr > lrmax) lrmax = lr;
-			if(lr - 0xff >= p->minsc) { cands[ncand].row = R - 1; cands[ncand].col = j; cands[ncand].score = lr; ncand++; }
+			/* candidate: lr - 0xff / lr_i16 - 0x7fff >= minsc; DpBtCandidate::score = the raw
+			 * cell value (u8.cpp:518-521, i16.cpp:526-529) */
+			if(lr - top >= p->minsc) {
+				cands[ncand].row = R - 1; cands[ncand].col = j; cands[ncand].score = i16 ? lr - 0x8000 : lr; ncand++;
+			}
 		}
 		if(ctr) { ctr->dp_cells += (uint64_t)R * C; ctr->dp_cols += C; }
 		if(debug && debug->digests) {
 			uint64_t d[3] = {0, 0, 0};
 			for(int i = 0; i < R; i++) for(int j = 0; j < C; j++) {
-				d[0] += bt2x_cell_digest(i, j, MAT_E, m->E[i][j]);
-				d[1] += bt2x_cell_digest(i, j, MAT_F, m->F[i][j]);
-				d[2] += bt2x_cell_digest(i, j, MAT_H, m->H[i][j]);
+				/* the stored value: the u8 byte, or the int16 bit pattern */
+				const uint32_t x = i16 ? 0x8000u : 0u;
+				d[0] += bt2x_cell_digest(i, j, MAT_E, m->E[i][j] ^ x);
+				d[1] += bt2x_cell_digest(i, j, MAT_F, m->F[i][j] ^ x);
+				d[2] += bt2x_cell_digest(i, j, MAT_H, m->H[i][j] ^ x);
 			}
 			memcpy(debug->digests + 3 * (size_t)pi, d, sizeof d);
 		}
 		bt2x_dp_out* o = &out[pi];
 		o->nrec = 0; o->rec_off = nrec; o->ncand = 0;
-		int score = lrmax - 0xff;
+		/* alignEnd2EndSseU8 / alignEnd2EndSseI16: score = lrmax - 0xff of the stored value
+		 * (u8.cpp:637-668; i16.cpp:642-673, where 0xff is subtracted from the int16) */
+		int score = (i16 ? lrmax - 0x8000 : lrmax) - 0xff;
 		if(score < p->minsc) { o->status = 0; o->best = score; ncand = 0; }
 		else if(lrmax == 0) { o->status = 0; o->best = INT32_MIN; ncand = 0; }
 		else {
@@ -577,7 +594,9 @@ int bt2o_dp_align(const bt2x_scoring* sc,
 		if(debug && debug->cands) {
 			uint32_t* dc = debug->cands + (size_t)pi * BT2X_MAX_COLS;
 			for(int k = 0; k < BT2X_MAX_COLS; k++)
-				dc[k] = k < ncand ? BT2X_CAND_PACK(cands[k].row, cands[k].col, cands[k].score) : 0xffffffffu;
+				dc[k] = k >= ncand ? 0xffffffffu
+				      : i16 ? BT2X_CAND_PACK16(cands[k].col, cands[k].score)
+				            : BT2X_CAND_PACK(cands[k].row, cands[k].col, cands[k].score);
 		}
 		if(!o->status) continue;
 		/* nextAlignment() until done() (aligner_sw.cpp:252-375) */

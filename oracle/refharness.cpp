@@ -93,6 +93,9 @@
 #include "unique.cpp"
 #include "simple_func.cpp"
 #include "outq.cpp"
+#ifdef ENABLE_I16
+#include "aligner_swsse_ee_i16.cpp"     // the -DENABLE_I16 build (bowtie2-align.cpp:31-33)
+#endif
 #include "aligner_swsse_ee_u8.cpp"
 #include "aligner_sw.cpp"
 #include "aligner_sw_driver.cpp"
@@ -184,12 +187,16 @@ static int cmdSeeds(int argc, char** argv) {
 }
 
 // ----------------------------------------------------------------------- dp
-static uint64_t digestMat(const SSEMatrix<false, ALN_MAX_ROWS, ALN_MAX_COLS>& m,
+// Order-independent digest of one matrix: sum of bt2x_cell_digest over cells of the
+// stored value (u8: the byte; i16: the int16 bit pattern).
+template<bool kI16>
+static uint64_t digestMat(const SSEMatrix<kI16, ALN_MAX_ROWS, ALN_MAX_COLS>& m,
                           size_t nrow, size_t ncol, int mat) {
-	uint64_t h = 0;   // order-independent: sum of bt2x_cell_digest over cells
+	uint64_t h = 0;
 	for(size_t i = 0; i < nrow; i++)
 		for(size_t j = 0; j < ncol; j++)
-			h += bt2x_cell_digest((uint32_t)i, (uint32_t)j, (uint32_t)mat, (uint32_t)(m.elt(i, j, mat) & 0xff));
+			h += bt2x_cell_digest((uint32_t)i, (uint32_t)j, (uint32_t)mat,
+			                      (uint32_t)(m.elt(i, j, mat) & (kI16 ? 0xffff : 0xff)));
 	return h;
 }
 
@@ -215,9 +222,10 @@ static int cmdDp(int argc, char** argv) {
 	Scoring sc(bonusMatch, penMmcType, penMmcMax, penMmcMin, scoreMin, nCeil, penNType, penN,
 	           penNCatPair, penRdGapConst, penRfGapConst, penRdGapLinear, penRfGapLinear, gGapBarrier);
 	FILE* fo = fopen(out.c_str(), "w");
-	fprintf(fo, "# dp idx=%s reads=%s maxhalf=%zu gapbar=%d mmp=%d,%d np=%d rdg=%d,%d rfg=%d,%d\n",
+	fprintf(fo, "# dp idx=%s reads=%s maxhalf=%zu gapbar=%d mmp=%d,%d np=%d rdg=%d,%d rfg=%d,%d sse8=%d\n",
 	        idx.c_str(), fq.c_str(), (size_t)maxhalf, (int)gGapBarrier, (int)penMmcMax, (int)penMmcMin,
-	        (int)penN, (int)penRdGapConst, (int)penRdGapLinear, (int)penRfGapConst, (int)penRfGapLinear);
+	        (int)penN, (int)penRdGapConst, (int)penRdGapLinear, (int)penRfGapConst, (int)penRfGapLinear,
+	        (int)enable8);
 	SwAligner* swap = new SwAligner();
 	SwAligner& swa = *swap;
 	RandomSource jrnd; jrnd.init(seed);
@@ -233,7 +241,9 @@ static int cmdDp(int argc, char** argv) {
 		if(rdlen >= 256 || rdlen < 2) continue;
 		TAlScore minsc = scoreMin.f<TAlScore>((double)rdlen);
 		if(minsc > 0) minsc = 0;
-		if(minsc < -254) minsc = -254;
+#ifndef ENABLE_I16
+		if(minsc < -254) minsc = -254;             // bt2_search.cpp:2484-2492
+#endif
 		int nceil = std::min((int)nCeil.f<int>((double)rdlen), (int)rdlen);
 		swa.reset();
 		if(!swa.initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, rdlen, sc)) {
@@ -262,29 +272,35 @@ static int cmdDp(int argc, char** argv) {
 			size_t nsInLeftShift = 0;
 			swa.reset();
 			swa.initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, rdlen, sc);
-			bool okRef = swa.initRef(fw, (TRefId)tidx, rect, ref, tlen, minsc, true, true,
+			bool okRef = swa.initRef(fw, (TRefId)tidx, rect, ref, tlen, minsc, enable8, true,
 			                         nwindow, nsInLeftShift);
 			if(!okRef) { fprintf(fo, "F %zu %ld %d initRef-fail\n", myidx, (long)refoff, (int)fw); continue; }
 			std::string win;
 			for(size_t i = 0; i < swa.rflen_; i++) win += DNA[firsts5[(int)swa.rf_[i]]];
 			uint32_t rseed = jrnd.nextU32();
-			fprintf(fo, "P %zu %zu %d %s %s %s %lld %lld %zu %zu %zu %lld %d %u %lld %ld %lld\n", nprob, myidx, (int)fw,
+			// the P line's last field: 1 when the problem runs the i16 kernel (enable8_ false)
+#ifdef ENABLE_I16
+			const bool useI16 = !swa.enable8_;
+#else
+			const bool useI16 = false;
+#endif
+			fprintf(fo, "P %zu %zu %d %s %s %s %lld %lld %zu %zu %zu %lld %d %u %lld %ld %lld %d\n", nprob, myidx, (int)fw,
 			        r.seq.c_str(), r.qual.c_str(), win.c_str(), (long long)rect.refl, (long long)rect.refr,
 			        (size_t)rect.triml, (size_t)rect.corel, (size_t)rect.corer, (long long)minsc, nceil, rseed,
-			        (long long)refoff, tidx, (long long)tlen);
+			        (long long)refoff, tidx, (long long)tlen, (int)useI16);
 			nprob++;
 			TAlScore best = std::numeric_limits<TAlScore>::min();
 			bool ok = swa.align(best);
-			auto& d = fw ? swa.sseU8fw_ : swa.sseU8rc_;
-			fprintf(fo, "A %d %lld %zu %016llx %016llx %016llx\n", (int)ok, (long long)best,
-			        (size_t)swa.btncand_.size(),
-			        (unsigned long long)digestMat(d.mat_, rdlen, swa.rflen_, SSEMatrixConsts::E),
-			        (unsigned long long)digestMat(d.mat_, rdlen, swa.rflen_, SSEMatrixConsts::F),
-			        (unsigned long long)digestMat(d.mat_, rdlen, swa.rflen_, SSEMatrixConsts::H));
-			if(getenv("HARNESS_DUMP") && nprob == 1) {
-				for(size_t i = 0; i < rdlen; i++) for(size_t j = 0; j < swa.rflen_; j++)
-					fprintf(stderr, "M %zu %zu %d %d %d\n", i, j, d.mat_.elt(i, j, 0), d.mat_.elt(i, j, 1), d.mat_.elt(i, j, 2));
+			uint64_t dg[3];
+			for(int mat = 0; mat < 3; mat++) {
+#ifdef ENABLE_I16
+				if(useI16) { dg[mat] = digestMat((fw ? swa.sseI16fw_ : swa.sseI16rc_).mat_, rdlen, swa.rflen_, mat); continue; }
+#endif
+				dg[mat] = digestMat((fw ? swa.sseU8fw_ : swa.sseU8rc_).mat_, rdlen, swa.rflen_, mat);
 			}
+			fprintf(fo, "A %d %lld %zu %016llx %016llx %016llx\n", (int)ok, (long long)best,
+			        (size_t)swa.btncand_.size(), (unsigned long long)dg[SSEMatrixConsts::E],
+			        (unsigned long long)dg[SSEMatrixConsts::F], (unsigned long long)dg[SSEMatrixConsts::H]);
 			fprintf(fo, "C");
 			for(size_t c = 0; c < swa.btncand_.size(); c++)
 				fprintf(fo, " %zu,%zu,%lld", swa.btncand_[c].row, swa.btncand_[c].col,

@@ -24,6 +24,8 @@ namespace {
 class OracleBackend : public Backend {
 public:
 	OracleBackend(const bt2x_index_desc& idx, const bt2x_scoring& sc) : idx_(idx), sc_(sc) {}
+	// --inject-error N: the Nth DP launch throws, as a failing GPU call would (bt2x::check)
+	int fail_at = 0;
 	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
 	                 HostVec<bt2x_seed_out>& out) override {
 		out.resize(in.size());
@@ -39,6 +41,7 @@ public:
 	              const HostVec<uint8_t>& refs, const HostVec<bt2x_dp_in>& in,
 	              HostVec<bt2x_dp_out>& out, HostVec<bt2x_aln_rec>& recs,
 	              HostVec<uint32_t>& edits) override {
+		if(fail_at > 0 && ++ndp_ == fail_at) throw bt2x::Error(BT2X_E_NODEVICE, "injected backend error");
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
 		uint32_t rec_cap = 4 * n + 64, edit_cap = 48 * n + 256;
@@ -82,6 +85,7 @@ public:
 private:
 	const bt2x_index_desc& idx_;
 	const bt2x_scoring& sc_;
+	int ndp_ = 0;
 };
 
 // --host-timing: the second run answers every launch from the first run's recorded
@@ -137,7 +141,7 @@ int main(int argc, char** argv) {
 	size_t slots = 4096;
 	int threads = 4;
 	bool host_timing = false, pipeline = true, gpu_round = true;
-	int reps = 1;
+	int reps = 1, inject = 0;
 	for(int i = 3; i < argc; i++) {
 		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
 		const std::string a = argv[i];
@@ -147,6 +151,7 @@ int main(int argc, char** argv) {
 		else if(a == "--no-pipeline") pipeline = false;
 		else if(a == "--no-gpu-round") gpu_round = false;
 		else if(a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
+		else if(a == "--inject-error" && i + 1 < argc) inject = std::atoi(argv[++i]);
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); return 1; }
 	}
 	bt2x_scoring_init(&p.sc);
@@ -154,6 +159,7 @@ int main(int argc, char** argv) {
 	RefInfo ref;
 	ref.init(index.desc(), argv[1]);
 	OracleBackend be(index.desc(), p.sc);
+	be.fail_at = inject;
 	if(host_timing) {
 		ReplayBackend rb(&be);
 		{
@@ -195,7 +201,13 @@ int main(int argc, char** argv) {
 	al.set_pipeline(pipeline);
 	al.set_gpu_round(gpu_round);
 	FastqReader fq(argv[2]);
-	const RunStats st = al.run(fq, stdout, slots, threads);
+	RunStats st;
+	try {
+		st = al.run(fq, stdout, slots, threads);
+	} catch(const std::exception& e) {               // as bt2x-align's main does
+		std::fprintf(stderr, "test_e2e_oracle: %s\n", e.what());
+		return 1;
+	}
 	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu "
 	             "tight_recs=%llu\n",
 	             (unsigned long long)st.reads, (unsigned long long)st.aligned, (unsigned long long)st.seed_launches,

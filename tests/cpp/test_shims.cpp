@@ -4,8 +4,11 @@
 //   A ok best ncand / N 1 rnd score ns gaps nedit bases refoff refns nedit edits... / N 0 rnd
 // tests/test_gpu_parity.py compares the output with tests/golden/dp_rep*.txt.xz.
 //
-// usage: test_shims <index basename> <problems.txt> <batch|single> [gapbar mm_max mm_min np rdg_c rdg_l rfg_c rfg_l]
+// usage: test_shims <index basename> <problems.txt> <batch|single> [gapbar mm_max mm_min np rdg_c rdg_l rfg_c rfg_l
+//                   [sse8]]
 // problems.txt lines: fw seq qual win refl refr triml corel corer minsc nceil rseed tlen
+// Built twice: test_shims (the stock build) and test_shims_i16 (-DENABLE_I16: the shims then
+// pick the i16 kernel as SwAligner::initRef does, aligner_sw.cpp:77-83; sse8 0 = --no-sse8).
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -92,6 +95,7 @@ int main(int argc, char** argv) {
 		sc.rdg_const = atoi(argv[8]); sc.rdg_linear = atoi(argv[9]); sc.rfg_const = atoi(argv[10]); sc.rfg_linear = atoi(argv[11]);
 		bt2x_scoring_init(&sc);
 	}
+	const bool enable8 = argc < 13 || atoi(argv[12]) != 0;
 	try {
 		bt2x::Index idx(argv[1]);
 		bt2x::Device dev(0, idx, sc);
@@ -118,7 +122,7 @@ int main(int argc, char** argv) {
 				RectStub rect{p.refl, p.refr, p.triml, p.corel, p.corer};
 				WindowRefs refs{p.refl, p.win};
 				size_t nsUpto = 0;
-				b.initRef(slot, p.fw != 0, 0, rect, refs, p.tlen, p.minsc, 0, nsUpto, pid[i]);
+				b.initRef(slot, p.fw != 0, 0, rect, refs, p.tlen, p.minsc, 0, nsUpto, pid[i], enable8);
 			}
 			b.run();
 			for(size_t i = 0; i < probs.size(); i++) {
@@ -138,7 +142,7 @@ int main(int argc, char** argv) {
 				WindowRefs refs{p.refl, p.win};
 				size_t nsUpto = 0;
 				if(!swa.initRead(fwd[i], rev[i], qf[i], qr[i], fwd[i].length(), ss) ||
-				   !swa.initRef(p.fw != 0, 0, rect, refs, p.tlen, p.minsc, true, true, 0, nsUpto)) {
+				   !swa.initRef(p.fw != 0, 0, rect, refs, p.tlen, p.minsc, enable8, true, 0, nsUpto)) {
 					fprintf(fo, "X\n"); continue;
 				}
 				int64_t best = 0;

@@ -121,6 +121,7 @@ class DpCase:
                            "triml": int(t[9]), "corel": int(t[10]), "corer": int(t[11]),
                            "minsc": int(t[12]), "nceil": int(t[13]), "rseed": int(t[14]),
                            "refoff": int(t[15]), "tidx": int(t[16]), "tlen": int(t[17]),
+                           "i16": int(t[18]) if len(t) > 18 else 0,      # refharness-i16: enable8_ off
                            "cands": [], "calls": []}
                     probs.append(cur)
                 elif t[0] == "A":
@@ -163,14 +164,17 @@ class DpCase:
             x["minsc"], x["nceil"] = p["minsc"], p["nceil"]
             x["triml"], x["corel"], x["corer"] = p["triml"], p["corel"], p["corer"]
             x["fw"] = p["fw"]
+            x["flags"] = abi.DP_I16 if p["i16"] else 0
             pr += len(c); pq += len(q); pf += len(w)
         self.reads = np.concatenate(rd) if rd else np.zeros(1, np.uint8)
         self.quals = np.concatenate(qu) if qu else np.zeros(1, np.uint8)
         self.refs = np.concatenate(rf) if rf else np.zeros(1, np.uint8)
 
 
-def replay_rng(seed: int, ntries_per_call):
-    """Reproduce RandomSource after each nextAlignment call (aligner_sw.cpp:324-336)."""
+def replay_rng(seed: int, ntries_per_call, i16: bool = False):
+    """Reproduce RandomSource after each nextAlignment call: per attempted candidate
+    reseed = nextU32() + 1, then init(reseed + 1) on the u8 path (aligner_sw.cpp:324-336)
+    or init(reseed) on the i16 path (:338-348)."""
     last = seed & 0xFFFFFFFF
     out = []
     for nt in ntries_per_call:
@@ -180,7 +184,7 @@ def replay_rng(seed: int, ntries_per_call):
             last = (1664525 * last + 1013904223) & 0xFFFFFFFF
             ret ^= last
             reseed = (ret + 1) & 0xFFFFFFFF
-            last = (reseed + 1) & 0xFFFFFFFF
+            last = reseed if i16 else (reseed + 1) & 0xFFFFFFFF
         out.append(last)
     return out
 
@@ -197,8 +201,14 @@ def compare_dp(case: DpCase, out, recs, edits, digests=None, cands=None, limit=2
         if digests is not None and list(int(v) for v in digests[i]) != p["digest"]:
             bad.append(f"prob {i}: E/F/H digest mismatch")
         if cands is not None:
-            got = [abi.cand_fields(c) for c in cands[i][: int(o["ncand"])]]
-            if got != [tuple(c) for c in p["cands"]]:
+            got = [abi.cand_fields(c, p["i16"]) for c in cands[i][: int(o["ncand"])]]
+            want = [tuple(c) for c in p["cands"]]
+            if p["i16"]:
+                rows = {c[0] for c in want}
+                want = [(None, c[1], c[2]) for c in want]
+                if rows and rows != {len(p["seq"]) - 1}:
+                    bad.append(f"prob {i}: i16 candidate outside the last row")
+            if got != want:
                 bad.append(f"prob {i}: candidate list mismatch")
         calls = p["calls"]
         nrec = int(o["nrec"])
@@ -206,7 +216,7 @@ def compare_dp(case: DpCase, out, recs, edits, digests=None, cands=None, limit=2
             bad.append(f"prob {i}: {nrec} nextAlignment calls != {len(calls)}")
         else:
             r = recs[int(o["rec_off"]): int(o["rec_off"]) + nrec]
-            rnd = replay_rng(p["rseed"], [int(x["ntries"]) for x in r])
+            rnd = replay_rng(p["rseed"], [int(x["ntries"]) for x in r], p["i16"])
             for k, (rec, exp) in enumerate(zip(r, calls)):
                 if rnd[k] != exp["rnd"] or int(rec["ok"]) != exp["ok"]:
                     bad.append(f"prob {i} call {k}: rng/ok mismatch")
@@ -229,11 +239,20 @@ def compare_dp(case: DpCase, out, recs, edits, digests=None, cands=None, limit=2
     return bad
 
 
-def dp_header_scoring(golden: str) -> dict:
-    """Scoring parameters recorded in a DP golden header line by refharness."""
+def dp_header(golden: str) -> dict:
     with open_text(golden) as f:
         h = f.readline().split()
-    kv = dict(x.split("=", 1) for x in h if "=" in x)
+    return dict(x.split("=", 1) for x in h if "=" in x)
+
+
+def dp_header_sse8(golden: str) -> int:
+    """--sse8 / --no-sse8 of a DP golden (refharness-i16 records it; older sets: 1)."""
+    return int(dp_header(golden).get("sse8", 1))
+
+
+def dp_header_scoring(golden: str) -> dict:
+    """Scoring parameters recorded in a DP golden header line by refharness."""
+    kv = dp_header(golden)
     mx, mn = (int(v) for v in kv["mmp"].split(","))
     rdc, rdl = (int(v) for v in kv["rdg"].split(","))
     rfc, rfl = (int(v) for v in kv["rfg"].split(","))

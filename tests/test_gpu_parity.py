@@ -13,7 +13,10 @@ pytestmark = pytest.mark.gpu
 
 SEED_SETS = [("lambda_virus", "lambda_longreads.fq.xz", "seeds_lambda.txt.xz"),
              ("rep", "rep_reads.fq.xz", "seeds_rep.txt.xz")]
-DP_SETS = ["dp_rep.txt.xz", "dp_rep_dpad12.txt.xz", "dp_rep_alt.txt.xz"]
+DP_SETS = ["dp_rep.txt.xz", "dp_rep_dpad12.txt.xz", "dp_rep_alt.txt.xz",
+           # the reference's i16 kernel (-DENABLE_I16 build): --no-sse8, minimum scores below
+           # the u8 floor, and that build's default (mixed u8/i16 launches)
+           "dp_rep_i16.txt.xz", "dp_rep_i16_wide.txt.xz", "dp_rep_i16_mix.txt.xz"]
 
 
 @pytest.fixture(scope="module")
@@ -130,7 +133,7 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
             out, recs, edits = ctx.dp_align(rd, qu, rf, dp, debug=False)[:3]
         finally:
             del os.environ["BT2X_DP_WAVE"]
-        _compare_out(out, eo, dp, banded=(wave == "0"))
+        _compare_out(out, eo, dp)
         for i in np.nonzero(out["nrec"] * sel)[0]:
             a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
             b = erecs[eo["rec_off"][i]: eo["rec_off"][i] + eo["nrec"][i]]
@@ -174,13 +177,18 @@ def _golden_records(gold):
 
 @pytest.mark.parametrize("gold,mode,limit", [("dp_rep.txt.xz", "batch", None),
                                              ("dp_rep_alt.txt.xz", "batch", None),
-                                             ("dp_rep_dpad12.txt.xz", "single", 400)])
+                                             ("dp_rep_dpad12.txt.xz", "single", 400),
+                                             ("dp_rep_i16.txt.xz", "batch", None),
+                                             ("dp_rep_i16_mix.txt.xz", "batch", None),
+                                             ("dp_rep_i16_wide.txt.xz", "single", 300)])
 def test_cpp_host_shims_match_golden(golden_dir, tmp_path, gold, mode, limit):
     """include/bt2x_shims.hpp driven like SwDriver drives SwAligner (initRead, initRef,
     align, nextAlignment until done, the caller's RandomSource advanced by the shim)
-    reproduces the reference's records line for line."""
+    reproduces the reference's records line for line.  The i16 goldens run the shims as a
+    -DENABLE_I16 build compiles them (tests/cpp/test_shims_i16), with the golden's sse8."""
     import subprocess
-    assert os.access(SHIM, os.X_OK), "tests/cpp/test_shims not built (__graft_entry__.build())"
+    shim = SHIM + ("_i16" if "_i16" in gold else "")
+    assert os.access(shim, os.X_OK), f"{shim} not built (__graft_entry__.build())"
     recs = _golden_records(gold)[:limit]
     pf = tmp_path / "probs.txt"
     with open(pf, "w") as f:
@@ -190,9 +198,9 @@ def test_cpp_host_shims_match_golden(golden_dir, tmp_path, gold, mode, limit):
                               t[14], t[17]]) + "\n")
     s = g.dp_header_scoring(os.path.join(g.GOLDEN, gold))
     args = [str(s[k]) for k in ("gapbar", "mm_max", "mm_min", "n_pen", "rdg_const", "rdg_linear",
-                                "rfg_const", "rfg_linear")]
+                                "rfg_const", "rfg_linear")] + [str(g.dp_header_sse8(os.path.join(g.GOLDEN, gold)))]
     base = g.materialize_index("rep", str(golden_dir))
-    r = subprocess.run([SHIM, base, str(pf), mode] + args, capture_output=True, text=True, timeout=600)
+    r = subprocess.run([shim, base, str(pf), mode] + args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     got = {}
     cur = None
@@ -210,11 +218,9 @@ def test_cpp_host_shims_match_golden(golden_dir, tmp_path, gold, mode, limit):
     for i, (_, a, ns) in enumerate(recs):
         ga, gn = got[i]
         k = 4 if mode == "batch" else 3
-        if a[1] == "1":
-            assert ga[:k] == a[:k], (i, ga, a)
-        else:
-            # a failed align(): the banded fill's best may be lower (dp_kernel.hip, _compare_out)
-            assert ga[1] == a[1] and ga[3:k] == a[3:k] and int(ga[2]) <= int(a[2]), (i, ga, a)
+        # align()'s verdict, best (exact for failed problems too: BT2X_OPT_EXACT_BEST) and
+        # candidate count, then every nextAlignment call
+        assert ga[:k] == a[:k], (i, ga, a)
         assert gn == ns, (i, gn, ns)
         ncalls += len(ns)
     assert ncalls > 0
@@ -256,10 +262,11 @@ def test_seed_kernel_lf_extension_path(golden_dir, monkeypatch):
         ctx.suffix_array(0, 1)
 
 
-def _random_dp_problems(n, seed):
+def _random_dp_problems(n, seed, i16=0.0):
     """Unframed DP problems over the ABI's whole shape range: R 1..160, ncol 1..199
     (ncol + 1 <= 200), minsc -254..0, random core diagonals / trims, both strands, N-rich
-    reads and windows, every quality; lengths mixed within waves."""
+    reads and windows, every quality; lengths mixed within waves.  A fraction `i16` are
+    BT2X_DP_I16 problems, half of them with minimum scores below the u8 floor (to -1500)."""
     rng = np.random.default_rng(seed)
     R = rng.integers(1, 161, size=n)
     R[rng.random(n) < 0.1] = 160
@@ -290,27 +297,30 @@ def _random_dp_problems(n, seed):
         lo = int(rng.integers(0, c + 20))
         x["corel"], x["corer"] = lo, lo + int(rng.integers(0, 40))
         x["fw"] = int(rng.random() < 0.5)
+        if rng.random() < i16:
+            x["flags"] = abi.DP_I16
+            if rng.random() < 0.5:
+                x["minsc"] = int(rng.integers(-1500, -254))
         pr += r; pf += c
     return np.concatenate(rd), np.concatenate(qu), np.concatenate(rf), inp
 
 
-def _compare_out(out, eo, inp, banded):
-    """align() verdicts.  The banded production fill (dp_kernel.hip, BT2X_DP_BAND) computes
-    only cells a path scoring >= minsc can use, so `best` of a failed problem (status 0)
-    may come out lower than the reference's, and stays below minsc; everything else is
-    exact."""
+def _compare_out(out, eo, inp, exact_best=True):
+    """align() verdicts, bit-exact.  Without BT2X_OPT_EXACT_BEST the banded production fill
+    (dp_kernel.hip, BT2X_DP_BAND) computes only cells a path scoring >= minsc can use, so
+    `best` of a failed problem may come out lower than the reference's, still below the
+    reference's threshold (u8: minsc; i16: the reference's own lrmax - 0xff test)."""
     np.testing.assert_array_equal(out[["status", "ncand", "nrec"]], eo[["status", "ncand", "nrec"]])
-    if not banded:
+    if exact_best:
         np.testing.assert_array_equal(out["best"], eo["best"])
         return
     ok = eo["status"] == 1
     np.testing.assert_array_equal(out["best"][ok], eo["best"][ok])
     assert (out["best"][~ok] <= eo["best"][~ok]).all()
-    assert (out["best"][~ok] < inp["minsc"][~ok].astype(np.int32)).all()
 
 
-def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, banded):
-    _compare_out(out, eo, inp, banded)
+def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=True):
+    _compare_out(out, eo, inp, exact_best)
     fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff"]
     for i in np.nonzero(out["nrec"])[0]:
         a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
@@ -321,36 +331,65 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, banded):
                                           eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
 
 
-@pytest.mark.parametrize("debug,wave,band", [(False, "0", "1"), (False, "0", "0"), (False, "1", "1"),
-                                             (True, "0", "1")])
-def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, monkeypatch):
+@pytest.mark.parametrize("debug,wave,band,i16", [(False, "0", "1", 0.0), (False, "0", "0", 0.0), (False, "1", "1", 0.0),
+                                                 (True, "0", "1", 0.0),
+                                                 (False, "0", "1", 1.0), (False, "1", "1", 1.0),
+                                                 (True, "0", "1", 1.0), (False, "0", "1", 0.3),
+                                                 (True, "0", "1", 0.3)])
+def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, monkeypatch):
     """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
     wave-per-problem mode) and debug kernels on random shapes/penalty thresholds at the ABI
-    limits vs the oracle: statuses, candidates, every nextAlignment record and edit."""
+    limits vs the oracle: statuses, bests, candidates, every nextAlignment record and edit.
+    i16: the share of BT2X_DP_I16 problems (all, or mixed into u8 launches; the 16-bit lane
+    kernels, including minimum scores below -254)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     monkeypatch.setenv("BT2X_DP_BAND", band)
-    rd, qu, rf, inp = _random_dp_problems(6000, seed=77 + int(debug))
+    rd, qu, rf, inp = _random_dp_problems(6000, seed=77 + int(debug) + int(10 * i16), i16=i16)
     ctx = ctxs["rep"][0]
     res = ctx.dp_align(rd, qu, rf, inp, debug=debug)
     eo, erecs, eedits, edig, ecands, _ = ol.dp_align(ol.default_scoring(), rd, qu, rf, inp)
     out, recs, edits = res[0], res[1], res[2]
-    _compare_dp(out, recs, edits, eo, erecs, eedits, inp, banded=(not debug and wave == "0" and band == "1"))
+    _compare_dp(out, recs, edits, eo, erecs, eedits, inp)
     if debug:
         np.testing.assert_array_equal(res[3], edig)
         np.testing.assert_array_equal(res[4], ecands)
     assert (out["status"] == 1).sum() > 1000 and (out["status"] == 0).sum() > 100
+    if i16:
+        assert ((inp["flags"] == abi.DP_I16) & (inp["minsc"] < -254) & (out["status"] == 1)).sum() > 100
 
 
+def test_dp_exact_best_option(ctxs, monkeypatch):
+    """BT2X_OPT_EXACT_BEST (default on): failed problems' best equals the reference's; off,
+    the banded lane kernel may report a lower one (documented in bt2x.h)."""
+    monkeypatch.setenv("BT2X_DP_WAVE", "0")
+    rd, qu, rf, inp = _random_dp_problems(3000, seed=5)
+    eo, erecs, eedits, _, _, _ = ol.dp_align(ol.default_scoring(), rd, qu, rf, inp)
+    ctx = ctxs["rep"][0]
+    try:
+        ctx.set_option(abi.OPT_EXACT_BEST, 0)
+        out, recs, edits = ctx.dp_align(rd, qu, rf, inp)[:3]
+        _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=False)
+        failed = eo["status"] == 0
+        assert (out["best"][failed] < eo["best"][failed]).sum() > 10     # the band's lower bound shows
+    finally:
+        ctx.set_option(abi.OPT_EXACT_BEST, 1)
+    out, recs, edits = ctx.dp_align(rd, qu, rf, inp)[:3]
+    _compare_dp(out, recs, edits, eo, erecs, eedits, inp)
+
+
+@pytest.mark.parametrize("gold", ["dp_rep_dpad12.txt.xz", "dp_rep_i16.txt.xz", "dp_rep_i16_mix.txt.xz"])
 @pytest.mark.parametrize("wave", ["0", "1"])
-def test_dp_production_kernel_on_golden(ctxs, wave, monkeypatch):
+def test_dp_production_kernel_on_golden(ctxs, wave, gold, monkeypatch):
     """The production (non-debug) kernel, in both modes, reproduces the reference records of
-    the golden set."""
+    the golden set (oracle-checked, then against the golden itself)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
-    case = g.DpCase(os.path.join(g.GOLDEN, "dp_rep_dpad12.txt.xz"))
+    case = g.DpCase(os.path.join(g.GOLDEN, gold))
     ctx = ctxs["rep"][0]
     out, recs, edits = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
     eo, erecs, eedits, _, _, _ = ol.dp_align(ol.default_scoring(), case.reads, case.quals, case.refs, case.inp)
-    _compare_dp(out, recs, edits, eo, erecs, eedits, case.inp, banded=(wave == "0"))
+    _compare_dp(out, recs, edits, eo, erecs, eedits, case.inp)
+    bad = g.compare_dp(case, out, recs, edits)
+    assert not bad, "\n".join(bad)
 
 
 def test_empty_batches(ctxs):

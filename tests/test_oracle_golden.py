@@ -14,6 +14,9 @@ import oracle_lib as ol
 SEED_SETS = [("lambda_virus", "lambda_longreads.fq.xz", "seeds_lambda.txt.xz"),
              ("rep", "rep_reads.fq.xz", "seeds_rep.txt.xz")]
 DP_SETS = ["dp_rep.txt.xz", "dp_rep_dpad12.txt.xz", "dp_rep_alt.txt.xz"]
+# the reference's i16 kernel (refharness-i16, a -DENABLE_I16 build): --no-sse8; --no-sse8
+# with minimum scores below the u8 floor; and that build's default (u8 unless minsc < -254)
+I16_DP_SETS = ["dp_rep_i16.txt.xz", "dp_rep_i16_wide.txt.xz", "dp_rep_i16_mix.txt.xz"]
 
 
 def scoring_for(golden):
@@ -60,6 +63,45 @@ def test_dp_matches_reference(gold):
     assert (out["status"] == 1).sum() > 1000 and (out["status"] == 0).sum() > 100
     assert (recs["gaps"] > 0).sum() > 100 and (recs["ns"] > 0).sum() > 10
     assert (out["nrec"] > 1).sum() > 100
+
+
+@pytest.mark.parametrize("gold", I16_DP_SETS)
+def test_dp_i16_matches_reference(gold):
+    """The oracle's i16 mode (BT2X_DP_I16: int16 cells shifted by 0x8000, no clamp of minsc,
+    the i16 reseed) vs alignEnd2EndSseI16 / backtraceNucleotidesEnd2EndSseI16 and the i16
+    nextAlignment (aligner_swsse_ee_i16.cpp, aligner_sw.cpp:338-348): statuses, bests (the
+    reference's lrmax - 0xff of the int16), E/F/H digests of the int16 cells, candidates,
+    every record and the RNG state after every call."""
+    path = os.path.join(g.GOLDEN, gold)
+    case = g.DpCase(path)
+    sc = scoring_for(path)
+    out, recs, edits, dig, cands, ctr = ol.dp_align(sc, case.reads, case.quals, case.refs, case.inp)
+    bad = g.compare_dp(case, out, recs, edits, dig, cands)
+    assert not bad, "\n".join(bad)
+    i16 = (case.inp["flags"] & g.abi.DP_I16) != 0
+    assert i16.sum() > 1000 and (out["nrec"] > 1).sum() > 500 and (recs["gaps"] > 0).sum() > 100
+    if gold == "dp_rep_i16.txt.xz":
+        assert i16.all() and (out["status"] == 0).sum() > 100
+        assert (out["best"][out["status"] == 1] > 30000).all()       # lrmax - 0xff of the int16
+    else:
+        assert (case.inp["minsc"] < -254).sum() > 1000                 # beyond the u8 kernel's range
+    if gold == "dp_rep_i16_mix.txt.xz":
+        assert 0 < (~i16).sum() and ((case.inp["minsc"] < -254) == i16).all()
+
+
+def test_dp_i16_differs_from_u8():
+    """The same problems through the u8 kernel give other RNG states (the reseed differs):
+    the i16 goldens are a distinct parity target."""
+    case = g.DpCase(os.path.join(g.GOLDEN, "dp_rep_i16.txt.xz"))
+    inp = case.inp.copy()
+    inp["flags"] = 0
+    out, recs, _, _, _, _ = ol.dp_align(ol.default_scoring(), case.reads, case.quals, case.refs, inp)
+    moved = 0
+    for i, p in enumerate(case.probs):
+        r = recs[int(out["rec_off"][i]): int(out["rec_off"][i]) + int(out["nrec"][i])]
+        rnd = g.replay_rng(p["rseed"], [int(x["ntries"]) for x in r], False)
+        moved += sum(1 for k, c in enumerate(p["calls"][:len(rnd)]) if rnd[k] != c["rnd"])
+    assert moved > 1000
 
 
 RESOLVE_SETS = [("lambda_virus", "resolve_lambda.txt.xz"), ("rep", "resolve_rep.txt.xz")]

@@ -19,6 +19,10 @@ Steps (all outputs xz-compressed under tests/golden/):
   5. e2e: the reference aligner (bowtie2-align-l, 1 thread) on the lambda and rep
      fixtures, default and --dpad 12 / non-default scoring, as sorted @PG-less SAM.
      `make_golden.py e2e` regenerates only these.
+  6. i16 (`make_golden.py i16`): the -DENABLE_I16 reference builds (refharness-i16,
+     bowtie2-align-l-i16) -- DP vectors and SAM of the signed 16-bit kernel (--no-sse8).
+  7. md5 (`make_golden.py md5`): e2e_md5.json, md5s of sets too large to commit as SAM
+     (config C2's E. coli stand-in, 50k-read lane-kernel launches, all of config C1).
 Each text golden file starts with a '#' header naming the command that produced it.
 """
 from __future__ import annotations
@@ -140,8 +144,120 @@ def tandem_goldens(tmp: str) -> None:
             fo.write(sam_records(sam))
 
 
+ALIGN16 = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l-i16")
+HARN16 = os.path.join(ROOT, "oracle", "_ref", "refharness-i16")
+WIDE_MIN = ["--score-min", "L,-0.6,-2.5", "--dpad", "12"]   # minsc below -254 from 102 bp on
+
+# the i16 DP (BASELINE config C2): -DENABLE_I16 reference builds.  dp: the
+# refharness dp set over the rep reads with --no-sse8, with a minimum score below the u8
+# floor, and the i16 build's default (u8 unless minsc < -254: mixed launches)
+I16_DP_SETS = [("dp_rep_i16", "1234", ["--no-sse8"]),
+               ("dp_rep_i16_wide", "99", ["--no-sse8"] + WIDE_MIN),
+               ("dp_rep_i16_mix", "77", WIDE_MIN)]
+I16_E2E_SETS = [("e2e_rep_i16", "rep", "rep_reads.fq", ["--no-sse8"]),
+                ("e2e_tandem_i16", "tandem", "tandem_reads.fq", ["--no-sse8"]),
+                ("e2e_rep_i16_wide", "rep", "rep_reads.fq", ["--no-sse8"] + WIDE_MIN),
+                ("e2e_rep_i16_mix", "rep", "rep_reads.fq", WIDE_MIN)]
+
+
+def i16_goldens(tmp: str) -> None:
+    """DP vectors and SAM of the reference's i16 kernel (refharness-i16, bowtie2-align-l-i16)."""
+    for idx in ("rep", "tandem"):
+        base = os.path.join(tmp, idx)
+        for k in "1234":
+            xz_unpack(os.path.join(GOLD, f"{idx}.{k}.bt2l.xz"), f"{base}.{k}.bt2l")
+    for fq in ("rep_reads.fq", "tandem_reads.fq"):
+        xz_unpack(os.path.join(GOLD, fq + ".xz"), os.path.join(tmp, fq))
+    rep, rfq = os.path.join(tmp, "rep"), os.path.join(tmp, "rep_reads.fq")
+    # the wide/mixed DP sets use reads 1450..1899 (100 and 150 bp: minsc on both sides of -254)
+    sub = os.path.join(tmp, "rep_reads_sub.fq")
+    with open(rfq) as fi, open(sub, "w") as fo:
+        for i, line in enumerate(fi):
+            if 4 * 1450 <= i < 4 * 1900:
+                fo.write(line)
+    for name, seed, opts in I16_DP_SETS:
+        out = os.path.join(tmp, name + ".txt")
+        run([HARN16, "dp", rep, rfq if name == "dp_rep_i16" else sub, out, seed] + opts)
+        xz_copy(out, os.path.join(GOLD, name + ".txt.xz"))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for name, idx, fq, opts in I16_E2E_SETS:
+        sam = os.path.join(tmp, name + ".sam")
+        run([ALIGN16, "-x", os.path.join(tmp, idx), "-U", os.path.join(tmp, fq), "-S", sam] + opts,
+            env=env, stderr=subprocess.DEVNULL)
+        with lzma.open(os.path.join(GOLD, name + ".sam.xz"), "wb", preset=9 | lzma.PRESET_EXTREME) as fo:
+            fo.write(sam_records(sam))
+
+
+# md5 goldens (tests/golden/e2e_md5.json): sets too large to commit as SAM.  md5 of the
+# sorted records minus @PG (`grep -v '^@PG' | sort | md5sum`, SURVEY.md:508's procedure).
+#   ecoli_*: config C2 -- the seeded 4.64 Mbp genome (simdata.ecoli_genome, indexed by the
+#            reference builder; FASTA and index md5s pinned) with simdata.fixture_reads
+#   ecoli_large_*: 50k x 150 bp at --dpad 12: DP launches of > 32k problems (the lane kernel)
+#   lambda_full: config C1, all 6000 example/reads/longreads.fq reads, 1 thread
+MD5_SETS = [("ecoli_i16", 10000, 100, 1, "i16", ["--no-sse8"]),
+            ("ecoli_u8", 10000, 100, 1, "u8", []),
+            ("ecoli_large_u8", 50000, 150, 3, "u8", ["--dpad", "12"]),
+            ("ecoli_large_i16", 50000, 150, 3, "i16", ["--no-sse8", "--dpad", "12"])]
+
+
+def sam_md5(path: str) -> tuple[str, int, int]:
+    import hashlib
+    with open(path, "rb") as f:
+        lines = [ln for ln in f.read().split(b"\n") if ln and not ln.startswith(b"@PG")]
+    recs = [ln for ln in lines if not ln.startswith(b"@")]
+    aligned = sum(1 for ln in recs if ln.split(b"\t")[1] != b"4")
+    data = b"".join(ln + b"\n" for ln in sorted(lines))
+    return hashlib.md5(data).hexdigest(), len(recs), aligned
+
+
+def md5_goldens(tmp: str) -> None:
+    import hashlib
+    import json
+    g = sd.ecoli_genome()
+    fa = os.path.join(tmp, "ecoli.fa")
+    sd.write_fasta(fa, g)
+    base = os.path.join(tmp, "ecoli")
+    run([BUILD, fa, base], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    md5 = lambda p: hashlib.md5(open(p, "rb").read()).hexdigest()     # noqa: E731
+    out = {"_note": "tools/make_golden.py md5: sorted SAM records minus @PG of the reference aligner "
+                    "(1 thread); genome/reads from tools/simdata.py",
+           "ecoli_fasta_md5": md5(fa), "ecoli_index_md5": {k: md5(f"{base}.{k}.bt2l") for k in "1234"},
+           "sets": {}}
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for name, n, rdlen, seed, binary, opts in MD5_SETS:
+        fq = os.path.join(tmp, f"{name}.fq")
+        sd.fixture_reads(g, fq, n, rdlen, seed)
+        sam = os.path.join(tmp, name + ".sam")
+        run([ALIGN16 if binary == "i16" else ALIGN, "-x", base, "-U", fq, "-S", sam] + opts,
+            env=env, stderr=subprocess.DEVNULL)
+        h, nrec, nal = sam_md5(sam)
+        out["sets"][name] = {"genome": "ecoli", "reads": n, "read_len": rdlen, "seed": seed, "binary": binary,
+                             "opts": opts, "md5": h, "records": nrec, "aligned": nal}
+    # C1: the shipped lambda example, every read
+    lam = os.path.join(tmp, "lambda_virus")
+    for k in "1234":
+        xz_unpack(os.path.join(GOLD, f"lambda_virus.{k}.bt2l.xz"), f"{lam}.{k}.bt2l")
+    sam = os.path.join(tmp, "lambda_full.sam")
+    run([ALIGN, "-x", lam, "-U", os.path.join(REF, "example/reads/longreads.fq"), "-S", sam],
+        env=env, stderr=subprocess.DEVNULL)
+    h, nrec, nal = sam_md5(sam)
+    out["sets"]["lambda_full"] = {"genome": "lambda_virus", "reads": nrec, "fastq": "lambda_longreads_full.fq.xz",
+                                  "binary": "u8", "opts": [], "md5": h, "records": nrec, "aligned": nal}
+    xz_copy(os.path.join(REF, "example/reads/longreads.fq"), os.path.join(GOLD, "lambda_longreads_full.fq.xz"))
+    with open(os.path.join(GOLD, "e2e_md5.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main() -> None:
     run(["make", "-C", os.path.join(ROOT, "oracle"), "ref", "oracle"])
+    for cmd, fn in (("i16", i16_goldens), ("md5", md5_goldens)):
+        if sys.argv[1:] == [cmd]:
+            tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
+            try:
+                fn(tmp)
+            finally:
+                shutil.rmtree(tmp, ignore_errors=True)
+            return
     if sys.argv[1:] == ["tandem"]:
         tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
         try:

@@ -247,3 +247,43 @@ def concat_genome(chroms):
     parts = [lut[np.frombuffer(s, dtype=np.uint8)] for _, s in chroms]
     starts = np.cumsum([0] + [len(x) for x in parts[:-1]]).astype(np.int64)
     return np.concatenate(parts), starts
+
+
+# Config C2's reference: E. coli K-12 is not available offline, so a seeded
+# synthetic genome of its length stands in (tests/golden/e2e_md5.json pins its FASTA md5).
+ECOLI_LEN = 4_641_652
+
+
+def ecoli_genome():
+    return gen_genome(ECOLI_LEN, nchrom=1, seed=1)
+
+
+def write_fastq_fixed(path: str, reads: np.ndarray, quals: np.ndarray, first_id: int = 0,
+                      append: bool = False) -> None:
+    """Fixed-length FASTQ from (n, R) code / Phred+33 arrays, vectorised: '@r<9 digits>'
+    names (ids from first_id)."""
+    n, R = reads.shape
+    rec = np.empty((n, 11 + 1 + R + 3 + R + 1), dtype=np.uint8)
+    rec[:, 0] = ord("@")
+    rec[:, 1] = ord("r")
+    ids = np.arange(first_id, first_id + n, dtype=np.int64)
+    for k in range(9):
+        rec[:, 10 - k] = ord("0") + (ids // (10 ** k)) % 10
+    rec[:, 11] = ord("\n")
+    rec[:, 12:12 + R] = ACGT[reads]
+    rec[:, 12 + R] = ord("\n")
+    rec[:, 13 + R] = ord("+")
+    rec[:, 14 + R] = ord("\n")
+    rec[:, 15 + R:15 + 2 * R] = quals
+    rec[:, 15 + 2 * R] = ord("\n")
+    with open(path, "ab" if append else "wb") as f:
+        f.write(rec.tobytes())
+
+
+def fixture_reads(chroms, path: str, n: int, rdlen: int, seed: int) -> None:
+    """n simulated fixed-length reads (sim_reads_fixed, BASELINE.md error model) of the
+    genome `chroms`, written to `path` (the e2e md5 fixtures of tests/golden/e2e_md5.json)."""
+    codes, starts = concat_genome(chroms)
+    reads, quals, _, _, _ = sim_reads_fixed(codes, starts, n, rdlen, seed=seed)
+    write_fastq_fixed(path, reads, quals)
+
