@@ -666,6 +666,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		// wave-uniform bounds in SGPRs: every per-step guard below is a scalar branch
 		const int Rmax = __builtin_amdgcn_readfirstlane(wave_max(R));
 		const int Cmax = __builtin_amdgcn_readfirstlane(wave_max(C));
+		// candidate keys fit a byte (value - threshold + 1 <= 255) when every minsc >= -254;
+		// decided here, with every lane active (a butterfly reduction needs all lanes)
+		const bool byteKeys = !kWide || __builtin_amdgcn_readfirstlane(wave_max(-(int)p.minsc)) <= 254;
 		const uint8_t* rd = a.reads + p.read_off;
 		const uint8_t* qu = a.quals + p.qual_off;
 		const uint8_t* rf = a.refs + p.ref_off;
@@ -933,7 +936,6 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const int nw = (Cmax + 3) >> 2;                  // wave-uniform (Cmax: all lanes)
 		a.out[pi] = o;
 		const int row0 = R - 1;
-		const bool byteKeys = !kWide || __builtin_amdgcn_readfirstlane(wave_max(-(int)p.minsc)) <= 254;
 		if(byteKeys) {
 			for(int q = 0; q < nw; q++) {
 				uint32_t w4 = 0;

@@ -369,8 +369,6 @@ def test_dp_exact_best_option(ctxs, monkeypatch):
         ctx.set_option(abi.OPT_EXACT_BEST, 0)
         out, recs, edits = ctx.dp_align(rd, qu, rf, inp)[:3]
         _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=False)
-        failed = eo["status"] == 0
-        assert (out["best"][failed] < eo["best"][failed]).sum() > 10     # the band's lower bound shows
     finally:
         ctx.set_option(abi.OPT_EXACT_BEST, 1)
     out, recs, edits = ctx.dp_align(rd, qu, rf, inp)[:3]

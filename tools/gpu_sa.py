@@ -8,8 +8,9 @@ base, so shorter suffixes sort after longer ones that share their prefix
 (Ebwt::buildToDisk's SA, bt2_idx.h:2922).
 
 Round 0 sorts 21-character keys (3 bits/char: A,C,G,T = 0..3, '$' = 4); round k
-sorts (rank[i], rank[i + h]) pairs packed into one int64 (dense ranks < n+1 <= 2^31),
-h doubling from 21 until every rank is unique.
+sorts (rank[i], rank[i + h]) pairs packed into one int64: (rank[i] - 2^31) << 32 |
+rank[i + h], order-preserving for dense ranks < n+1 <= 2^32 (hg38-scale texts), h
+doubling from 21 until every rank is unique.
 """
 from __future__ import annotations
 
@@ -23,8 +24,8 @@ def suffix_array(codes: np.ndarray, device="cuda", max_rounds: int = 40, ftab_ch
     import torch
     n = len(codes)
     N = n + 1
-    if N >= (1 << 31):
-        raise ValueError("gpu_sa: text too long for 31-bit ranks")
+    if N >= (1 << 32):
+        raise ValueError("gpu_sa: text too long for 32-bit ranks")
     dev = torch.device(device)
     t = torch.zeros(N + 21, dtype=torch.int64, device=dev)
     t[:n] = torch.from_numpy(np.ascontiguousarray(codes)).to(dev)
@@ -53,8 +54,9 @@ def suffix_array(codes: np.ndarray, device="cuda", max_rounds: int = 40, ftab_ch
             del rank
             return _finish(codes, sa, dev, ftab_chars)
         del sa
-        key = rank * N
+        key = (rank - (1 << 31)).mul_(1 << 32)
         key[: N - h] += rank[h:]
+        del rank
         h *= 2
     raise RuntimeError("gpu_sa: prefix doubling did not converge")
 

@@ -287,3 +287,45 @@ def fixture_reads(chroms, path: str, n: int, rdlen: int, seed: int) -> None:
     reads, quals, _, _, _ = sim_reads_fixed(codes, starts, n, rdlen, seed=seed)
     write_fastq_fixed(path, reads, quals)
 
+
+
+def sim_reads_fast(genome_codes: np.ndarray, chrom_starts: np.ndarray, n: int, rdlen: int, seed: int,
+                   sub_rate: float = 0.01, indel_frac: float = 0.10, rc_frac: float = 0.5,
+                   qmin: int = 2, qmax: int = 40, n_rate: float = 0.001):
+    """sim_reads_fixed's error model (1 % substitutions, one indel in 10 % of
+    reads, half reverse-complemented, Phred uniform qmin..qmax, rare Ns) with narrow
+    integer draws and window gathers: ~10x faster, for bench-scale read sets (a different
+    random stream than sim_reads_fixed, whose outputs the md5 fixtures pin)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    G = len(genome_codes)
+    ends = np.append(chrom_starts[1:], G)
+    isn = genome_codes > 3
+    out_pos = np.empty(0, dtype=np.int64)
+    W = rdlen + 2
+    while len(out_pos) < n:
+        p = rng.integers(0, G - W, size=int(n * 1.2) + 64)
+        c = np.searchsorted(chrom_starts, p, side="right") - 1
+        ok = p + W <= ends[c]
+        p = p[ok]
+        win = np.lib.stride_tricks.sliding_window_view(isn, W)[p]
+        out_pos = np.concatenate([out_pos, p[~win.any(axis=1)]])
+    p = out_pos[:n]
+    win = np.lib.stride_tricks.sliding_window_view(genome_codes, W)[p]       # (n, W) u8
+    j = np.arange(rdlen, dtype=np.int16)[None, :]
+    k = rng.integers(10, rdlen - 10, size=(n, 1), dtype=np.int16)
+    kind = rng.integers(0, 1 << 16, size=n, dtype=np.uint16)
+    indel = kind < int(indel_frac * 65536)
+    dele = indel & ((kind & 1) == 0)
+    ins = indel & ~dele
+    idx = j + (dele[:, None] & (j >= k)).astype(np.int16) - (ins[:, None] & (j > k)).astype(np.int16) + 1
+    reads = np.take_along_axis(win, idx.astype(np.intp), axis=1)
+    rnd = rng.integers(0, 1 << 16, size=(n, rdlen), dtype=np.uint16)
+    codes = rng.integers(0, 256, size=(n, rdlen), dtype=np.uint8) & 3
+    reads = np.where(ins[:, None] & (j == k), codes, reads)
+    reads = np.where(rnd < int(sub_rate * 65536), codes, reads)
+    reads = np.where(rnd >= 65536 - int(n_rate * 65536), np.uint8(4), reads)
+    fw = rng.random(n) >= rc_frac
+    rc = np.where(reads < 4, 3 - reads, 4).astype(np.uint8)[:, ::-1]
+    reads = np.where(fw[:, None], reads, rc)
+    quals = (rng.integers(qmin, qmax + 1, size=(n, rdlen), dtype=np.uint8) + 33).astype(np.uint8)
+    return np.ascontiguousarray(reads), quals
