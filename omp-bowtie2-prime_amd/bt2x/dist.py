@@ -49,3 +49,170 @@ def max_over_ranks(x: float, dist=None, device=None) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# ---------------------------------------------------------------- sharded aligner runs
+#
+# python -m torch.distributed.run --nproc-per-node N -m bt2x.dist [--aligner PATH] -- \
+#     <bt2x-align arguments, including -S out.sam>
+#
+# Each rank runs the aligner as a child process on its own GPU (HIP_VISIBLE_DEVICES =
+# LOCAL_RANK; this process never touches the GPU) over shard RANK/N of the read stream
+# (bt2x-align --shard, FastqReader), writing out.sam.part<RANK>.  The ranks then sum the
+# 27 ReportingMetrics counters (gloo all-reduce: the only collective; bt2_search.cpp:
+# 2867-2869 is the reference's per-thread merge of the same counters), rank 0 appends
+# the parts in rank order to out.sam -- the single run's SAM, as the shards are
+# contiguous and in order -- and prints the reference's alignment summary of the sum.
+
+METRIC_NAMES = (
+    "nread", "npaired", "nunpaired", "nconcord_uni", "nconcord_uni1", "nconcord_uni2", "nconcord_rep",
+    "nconcord_0", "ndiscord", "nunp_0_uni", "nunp_0_uni1", "nunp_0_uni2", "nunp_0_rep", "nunp_0_0",
+    "nunp_rep_uni", "nunp_rep_uni1", "nunp_rep_uni2", "nunp_rep_rep", "nunp_rep_0", "nunp_uni", "nunp_uni1",
+    "nunp_uni2", "nunp_rep", "nunp_0", "sum_best1", "sum_best2", "sum_best")   # aln_sink.h:44-170
+
+
+def parse_metrics(text: str) -> dict:
+    """The aligner's BT2X_METRICS (27 counters) and BT2X_TIMED lines from its stderr."""
+    met, timed = None, {}
+    for ln in text.splitlines():
+        if ln.startswith("BT2X_METRICS "):
+            vals = [int(v) for v in ln.split()[1:]]
+            if len(vals) != len(METRIC_NAMES):
+                raise ValueError(f"BT2X_METRICS has {len(vals)} fields, expected {len(METRIC_NAMES)}")
+            met = dict(zip(METRIC_NAMES, vals))
+        elif ln.startswith("BT2X_TIMED "):
+            for kv in ln.split()[1:]:
+                k, v = kv.split("=", 1)
+                timed[k] = v
+    if met is None:
+        raise ValueError("aligner printed no BT2X_METRICS line")
+    return {"metrics": met, "timed": timed}
+
+
+def alignment_summary(m: dict) -> str:
+    """AlnSink::printAlSumm for unpaired reads with -M's repetitive threshold (aln_sink.cpp:349-527)."""
+    def pct(a, b):
+        return f"{100.0 * a / b if b else 0.0:.2f}%"
+    nread, nun = m["nread"], m["nunpaired"]
+    out = [f"{nread} reads; of these:" if nread else f"{nread} reads"]
+    if nun:
+        more = m["nunp_uni2"] + m["nunp_rep"]
+        out += [f"  {nun} ({pct(nun, nread)}) were unpaired; of these:",
+                f"    {m['nunp_0']} ({pct(m['nunp_0'], nun)}) aligned 0 times",
+                f"    {m['nunp_uni1']} ({pct(m['nunp_uni1'], nun)}) aligned exactly 1 time",
+                f"    {more} ({pct(more, nun)}) aligned >1 times"]
+    out.append(f"{pct(m['nunp_uni'] + m['nunp_rep'], nun)} overall alignment rate")
+    return "\n".join(out) + "\n"
+
+
+def _split_out(args: list[str]) -> tuple[list[str], str | None]:
+    args = list(args)
+    for flag in ("-S", "--output"):
+        if flag in args:
+            i = args.index(flag)
+            if i + 1 >= len(args):
+                raise ValueError(f"{flag} needs a file name")
+            out = args[i + 1]
+            del args[i:i + 2]
+            return args, out
+    return args, None
+
+
+def _append(dst, path: str) -> None:
+    with open(path, "rb") as f:
+        size = os.fstat(f.fileno()).st_size
+        off = 0
+        while off < size:                       # in-kernel copy; no user-space buffer pass
+            n = os.sendfile(dst.fileno(), f.fileno(), off, size - off)
+            if n <= 0:
+                raise OSError(f"sendfile stopped at {off} of {size} bytes of {path}")
+            off += n
+
+
+def run_sharded(aligner: str, args: list[str], dist=None, set_device: bool = True) -> dict:
+    """Run `aligner args` as this rank's shard; returns the summed metrics (every rank), the
+    max of the ranks' timed-run seconds and the total reads.  Rank 0 writes the output."""
+    import subprocess
+    import sys
+    import tempfile
+    rank, world_size, local_rank = world()
+    if dist is not None and dist.is_initialized():
+        rank, world_size = dist.get_rank(), dist.get_world_size()
+    args, out = _split_out(args)
+    if out is None:                             # stdout: parts under a directory rank 0 names
+        box = [tempfile.mkdtemp(prefix="bt2x_parts_") if rank == 0 else None]
+        if dist is not None and dist.is_initialized() and world_size > 1:
+            dist.broadcast_object_list(box, src=0)
+        part_base = os.path.join(box[0], "out.sam")
+    else:
+        part_base = out
+    part = f"{part_base}.part{rank}"
+    cmd = [aligner] + args + ["-S", part, "--shard", f"{rank}/{world_size}", "--metrics"]
+    if rank > 0:
+        cmd.append("--no-hd")
+    env = dict(os.environ)
+    if set_device:
+        env["HIP_VISIBLE_DEVICES"] = str(local_rank)
+    r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    res = {"rc": r.returncode, "stderr": r.stderr}
+    try:
+        got = parse_metrics(r.stderr) if r.returncode == 0 else None
+    except ValueError as e:
+        got, res["rc"], res["stderr"] = None, 1, r.stderr + f"\n{e}\n"
+    met = got["metrics"] if got else {k: 0 for k in METRIC_NAMES}
+    t_align = float(got["timed"].get("t_align", 0)) if got else 0.0
+    ok = sum_counters({"failed": 1 if res["rc"] else 0}, dist)["failed"] == 0
+    res["metrics"] = sum_counters(met, dist)
+    res["t_align_max"] = max_over_ranks(t_align, dist)
+    res["reads"] = res["metrics"]["nread"]
+    res["ok"] = ok
+    if ok and rank == 0:
+        dst = open(out, "wb") if out else sys.stdout.buffer
+        try:
+            dst.flush()
+            for k in range(world_size):
+                _append(dst, f"{part_base}.part{k}")
+            dst.flush()
+        finally:
+            if out:
+                dst.close()
+    if dist is not None and dist.is_initialized() and world_size > 1:
+        dist.barrier()                           # parts are read before they go
+    if ok:
+        os.unlink(part)
+        if out is None and rank == 0:
+            os.rmdir(os.path.dirname(part_base))
+    return res
+
+
+def main(argv=None) -> int:
+    import argparse
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    ap = argparse.ArgumentParser(prog="python -m bt2x.dist",
+                                 description="bt2x-align over all ranks' GPUs, reads sharded (run under torch.distributed.run)")
+    ap.add_argument("--aligner", default=os.path.join(here, "bt2x-align"))
+    ap.add_argument("--no-device", action="store_true", help="do not set HIP_VISIBLE_DEVICES per rank")
+    ap.add_argument("rest", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    rest = a.rest[1:] if a.rest[:1] == ["--"] else a.rest
+    import torch.distributed as tdist
+    use_dist = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if use_dist:
+        tdist.init_process_group("gloo")
+    try:
+        res = run_sharded(a.aligner, rest, tdist if use_dist else None, set_device=not a.no_device)
+    finally:
+        if use_dist:
+            tdist.destroy_process_group()
+    rank = world()[0]
+    if res["rc"]:
+        sys.stderr.write(res["stderr"])
+    if rank == 0 and res["ok"]:
+        sys.stderr.write(alignment_summary(res["metrics"]))
+        sys.stderr.write(f"BT2X_DIST ranks={world()[1]} reads={res['reads']} t_align_max={res['t_align_max']:.4f}\n")
+    return 0 if res["ok"] else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -106,25 +106,107 @@ const uint8_t kAsc2Dna[256] = {   // alphabet.cpp:142 (A/C/G/T, either case; all
 #undef N4
 };
 
+// ------------------------------------------------------------------- summary
+
+void print_alignment_summary(const ReportingMetrics& m, std::FILE* f) {
+	using M = ReportingMetrics;
+	auto pct = [](uint64_t num, uint64_t den) { return den ? 100.0 * (double)num / (double)den : 0.0; };
+	const uint64_t nread = m.v[M::NREAD], nun = m.v[M::NUNPAIRED];
+	if(nread > 0) std::fprintf(f, "%llu reads; of these:\n", (unsigned long long)nread);
+	else std::fprintf(f, "%llu reads\n", (unsigned long long)nread);
+	if(nun > 0) {
+		std::fprintf(f, "  %llu (%.2f%%) were unpaired; of these:\n", (unsigned long long)nun, pct(nun, nread));
+		std::fprintf(f, "    %llu (%.2f%%) aligned 0 times\n", (unsigned long long)m.v[M::NUNP_0], pct(m.v[M::NUNP_0], nun));
+		std::fprintf(f, "    %llu (%.2f%%) aligned exactly 1 time\n", (unsigned long long)m.v[M::NUNP_UNI1],
+		             pct(m.v[M::NUNP_UNI1], nun));
+		const uint64_t more = m.v[M::NUNP_UNI2] + m.v[M::NUNP_REP];
+		std::fprintf(f, "    %llu (%.2f%%) aligned >1 times\n", (unsigned long long)more, pct(more, nun));
+	}
+	const uint64_t tot_al = m.v[M::NUNP_UNI] + m.v[M::NUNP_REP];
+	std::fprintf(f, "%.2f%% overall alignment rate\n", pct(tot_al, nun));
+}
+
 // ---------------------------------------------------------------- FastqReader
 
-FastqReader::FastqReader(const char* path) {
-	fd_ = ::open(path, O_RDONLY);
-	if(fd_ < 0) throw std::runtime_error(std::string("cannot open reads file ") + path);
-	struct stat sb;
-	if(::fstat(fd_, &sb) != 0) throw std::runtime_error(std::string("cannot stat ") + path);
-	len_ = (size_t)sb.st_size;
-	if(len_) {
-		void* m = ::mmap(nullptr, len_, PROT_READ, MAP_PRIVATE, fd_, 0);
-		if(m == MAP_FAILED) throw std::runtime_error(std::string("cannot map ") + path);
-		::madvise(m, len_, MADV_SEQUENTIAL);
-		map_ = (const char*)m;
+namespace {
+// first record start at or after byte `at` of a FASTQ map: a line beginning '@' whose
+// third line begins '+' (quality lines may begin with '@', never with a following
+// '+' line two lines later unless they are a header)
+size_t next_record(const char* m, size_t len, size_t at) {
+	if(at == 0) return 0;
+	size_t pos = at;
+	// start of the next line at or after `at` (at itself when the previous byte is '\n')
+	if(m[pos - 1] != '\n') {
+		const char* nl = (const char*)std::memchr(m + pos, '\n', len - pos);
+		if(!nl) return len;
+		pos = (size_t)(nl - m) + 1;
 	}
+	auto next_line = [&](size_t q) -> size_t {
+		const char* nl = (const char*)std::memchr(m + q, '\n', len - q);
+		return nl ? (size_t)(nl - m) + 1 : len;
+	};
+	while(pos < len) {
+		if(m[pos] == '@') {
+			const size_t l2 = next_line(pos);
+			const size_t l3 = l2 < len ? next_line(l2) : len;
+			if(l3 < len && m[l3] == '+') return pos;
+		}
+		pos = next_line(pos);
+	}
+	return len;
+}
+
+size_t count_lines(const char* m, size_t n) {
+	size_t k = 0;
+	for(const char* q = m; (q = (const char*)std::memchr(q, '\n', (size_t)(m + n - q))) != nullptr; q++) k++;
+	return k;
+}
+}
+
+FastqReader::FastqReader(const std::vector<std::string>& paths, int shard, int nshards) {
+	if(nshards < 1 || shard < 0 || shard >= nshards) throw std::runtime_error("bad shard " + std::to_string(shard) + "/" + std::to_string(nshards));
+	size_t total = 0;
+	for(const std::string& path : paths) {
+		File F;
+		F.fd = ::open(path.c_str(), O_RDONLY);
+		if(F.fd < 0) throw std::runtime_error("cannot open reads file " + path);
+		f_.push_back(F);
+		struct stat sb;
+		if(::fstat(F.fd, &sb) != 0) throw std::runtime_error("cannot stat " + path);
+		f_.back().len = (size_t)sb.st_size;
+		if(f_.back().len) {
+			void* m = ::mmap(nullptr, f_.back().len, PROT_READ, MAP_PRIVATE, F.fd, 0);
+			if(m == MAP_FAILED) throw std::runtime_error("cannot map " + path);
+			::madvise(m, f_.back().len, MADV_SEQUENTIAL);
+			f_.back().map = (const char*)m;
+		}
+		total += f_.back().len;
+	}
+	// this shard's byte range [lo, hi) of the concatenated stream, both snapped to record
+	// starts within their file
+	const size_t lo = (size_t)((unsigned __int128)total * (unsigned)shard / (unsigned)nshards);
+	const size_t hi = (size_t)((unsigned __int128)total * (unsigned)(shard + 1) / (unsigned)nshards);
+	size_t off = 0;
+	first_rdid_ = 0;
+	for(File& F : f_) {
+		const size_t a = std::min(std::max(lo, off) - off, F.len), b = std::min(std::max(hi, off) - off, F.len);
+		F.beg = next_record(F.map, F.len, a);
+		F.end = shard + 1 == nshards ? F.len : next_record(F.map, F.len, b);
+		if(F.end < F.beg) F.end = F.beg;
+		// records before the shard in this file: 4 lines each (a last line without '\n'
+		// still ends its record)
+		const size_t k = count_lines(F.map, F.beg);
+		first_rdid_ += F.beg == F.len && F.len && F.map[F.len - 1] != '\n' ? (k + 4) / 4 : k / 4;
+		off += F.len;
+	}
+	if(!f_.empty()) pos_ = f_[0].beg;
 }
 
 FastqReader::~FastqReader() {
-	if(map_) ::munmap((void*)map_, len_);
-	if(fd_ >= 0) ::close(fd_);
+	for(File& F : f_) {
+		if(F.map) ::munmap((void*)F.map, F.len);
+		if(F.fd >= 0) ::close(F.fd);
+	}
 }
 
 // ------------------------------------------------------------------- RefInfo
@@ -704,8 +786,16 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 	const size_t rdlen = rd.length();
 	// P0, bt2_search.cpp:2467-2553
 	int64_t minsc = P.scoreMin.f<int64_t>((double)rdlen);
-	if(minsc > 0) minsc = 0;
-	else if(minsc < -254 && !P.i16build) minsc = -254;        // stock build only
+	c->warn.clear();
+	// printEEScoreMsg (bt2_search.cpp:1870-1891, 2484-2492): the same "positive number"
+	// text for the stock build's -254 clamp
+	auto ee_warn = [&] {
+		if(!P.quiet)
+			c->warn += "Warning: minimum score function gave positive number in --end-to-end mode for read '" + rd.name +
+			           "; setting to 0 instead\n";
+	};
+	if(minsc > 0) { ee_warn(); minsc = 0; }
+	else if(minsc < -254 && !P.i16build) { ee_warn(); minsc = -254; }        // stock build only
 	PH_START();
 	Rng rnd;
 	rnd.init(rd.seed);
@@ -907,6 +997,8 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 	}
 	PH(5);
 	finish_read(P, ref_, rd, sink, rnd, c->edbuf, &c->aligned, &c->repetitive, c->sam);
+	// the finishRead counter update (aln_sink.cpp:994-1013): rs1u_ holds every alignment found
+	c->met_kind = c->repetitive ? 3 : !c->aligned ? 0 : sink.rs.size() == 1 ? 1 : 2;
 	PH(8);
 	c->req = REQ_NONE;
 	c->done = true;
@@ -1262,6 +1354,12 @@ void count(RunStats& st, const ReadCtx* c) {
 	st.reads++;
 	if(c->aligned) st.aligned++; else st.unaligned++;
 	if(c->repetitive) st.rep++;
+	using M = ReportingMetrics;
+	st.met.v[M::NREAD]++;
+	st.met.v[M::NUNPAIRED]++;
+	static constexpr int kind_field[4] = {M::NUNP_0, M::NUNP_UNI1, M::NUNP_UNI2, M::NUNP_REP};
+	st.met.v[kind_field[c->met_kind]]++;
+	if(c->met_kind == 1 || c->met_kind == 2) st.met.v[M::NUNP_UNI]++;
 	st.dps_used += c->ndp_used;
 	st.tight_recs += c->ntight;
 }
@@ -1300,6 +1398,7 @@ void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, void* ringp) {
 			c->task.h = nullptr;
 			c->done = false;
 			count(st, c);
+			if(!c->warn.empty()) std::fputs(c->warn.c_str(), stderr);
 			ring.put(c->rd.rdid, c->sam);
 			free_.push_back(c);
 		} else {
@@ -1343,14 +1442,18 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	RunStats st;
 	use_threads(threads);
 	const double t_start = now_s();
-	const std::string hdr = header();
-	std::fwrite(hdr.data(), 1, hdr.size(), out);
+	if(header_on_) {
+		const std::string hdr = header();
+		std::fwrite(hdr.data(), 1, hdr.size(), out);
+	}
 	uint64_t rdid = 0;
+	const uint64_t rdid0 = fq.first_rdid();
 	bool eof = false;
 	std::vector<FastqReader::Raw> raw;
 	std::vector<ReadCtx*> fresh;
 	OutRing ring;
 	SamWriter writer(out);
+	uint64_t written = 0;
 	if(slots < 2) slots = 2;
 	reserve_launch_buffers(pipeline_ ? slots / 2 : slots);
 	// New reads join cohort `co` (up to `cap` reads in it): decoded and run up to their
@@ -1372,7 +1475,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		st.t_alloc += now_s() - t0;
 		pool().parallel_for(nf, 64, [&](long i) {
 			ReadCtx* c = fresh[(size_t)i];
-			FastqReader::decode(raw[(size_t)i], c->rd, rdid + (uint64_t)i, p_.randSeed);
+			FastqReader::decode(raw[(size_t)i], c->rd, rdid + (uint64_t)i, p_.randSeed, rdid0 + rdid + (uint64_t)i);
 			c->task = align_read(c);
 			c->task.h.resume();
 		});
@@ -1384,7 +1487,10 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		const double t0 = now_s();
 		retire(co, st, &ring);
 		const double t1 = now_s();
-		ring.drain([&](const std::string& s) { writer.append(s); });
+		ring.drain([&](const std::string& s) { writer.append(s); written++; });
+		// input files whose last record is now out
+		while(st.t_files.size() < fq.files_done() && fq.file_end(st.t_files.size()) <= written)
+			st.t_files.push_back(now_s() - t_start);
 		st.t_io += now_s() - t0;
 		st.t_retire += t1 - t0;
 	};
@@ -1447,6 +1553,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	}
 	writer.finish();
 	if(t_run) *t_run = now_s() - t_start;
+	while(st.t_files.size() < fq.nfiles()) st.t_files.push_back(now_s() - t_start);
 #ifdef BT2X_PHASE_PROF
 	ph_print();
 #endif

@@ -413,6 +413,7 @@ struct Params {
 	int tighten = 3;
 	uint32_t randSeed = 0;          // --seed
 	bool nofw = false, norc = false;
+	bool quiet = false;             // --quiet: no per-read warnings (gQuiet)
 	// DP kernel choice (aligner_sw.cpp:77-83, bt2_search.cpp:1350-1356, 2484-2492): the stock
 	// build runs u8 only, minsc clamped to -254; a -DENABLE_I16 build (i16build) keeps minsc
 	// and runs the i16 kernel unless enable8 && minsc >= -254.  --no-sse8 implies i16build
@@ -482,6 +483,7 @@ inline int parse_align_option(Params& p, int argc, char** argv, int i) {
 	if(a == "--sse8") { p.enable8 = true; return 1; }
 	if(a == "--no-sse8") { p.enable8 = false; p.i16build = true; return 1; }
 	if(a == "--i16-build") { p.i16build = true; return 1; }    // (not a reference option)
+	if(a == "--quiet") { p.quiet = true; return 1; }
 	if(!has) return 0;
 	// --score-min / --n-ceil / -i: the policy strings of bt2_search.cpp:1436-1541, parsed
 	// by PARSE_FUNC; a malformed function is reported as an unconsumed option
@@ -533,13 +535,22 @@ inline uint32_t gen_rand_seed(const Read& r, uint32_t seed) {
 }
 
 // FASTQ input (FastqPatternSource light parse + parse, pat.cpp:1124-1220), Phred+33
-// only; '.' is N, non-alphabetic sequence characters are skipped.  The file is mapped:
-// take() finds record boundaries (four lines each) serially with memchr, decode() builds
-// the Read (codes, reverse complement, genRandSeed) and runs in parallel over records.
+// only; '.' is N, non-alphabetic sequence characters are skipped.  The files are mapped
+// and form one read stream, as bowtie2's comma-separated -U list does; take() finds
+// record boundaries (four lines each) serially with memchr, decode() builds the Read
+// (codes, reverse complement, genRandSeed) and runs in parallel over records.
+//
+// Shards (multi-GPU, one process per GPU): shard i of n reads the records that start in
+// bytes [i*T/n, (i+1)*T/n) of the concatenated files (T = their total size), each bound
+// moved to the next record start (a line beginning '@' whose third line begins '+'), so
+// the shards partition the stream in order.  Records are numbered globally
+// (first_rdid(): records before the shard, from its line count; 4-line records): a read
+// without a name is named by that number, as the reference does.
 class FastqReader {
 public:
 	struct Raw { const char* l[4]; size_t n[4]; };
-	explicit FastqReader(const char* path);
+	explicit FastqReader(const char* path) : FastqReader(std::vector<std::string>{path}) {}
+	explicit FastqReader(const std::vector<std::string>& paths, int shard = 0, int nshards = 1);
 	~FastqReader();
 	FastqReader(const FastqReader&) = delete;
 	FastqReader& operator=(const FastqReader&) = delete;
@@ -547,19 +558,33 @@ public:
 	size_t take(size_t max, std::vector<Raw>& out) {
 		size_t k = 0;
 		while(k < max) {
+			if(cur_ >= f_.size()) break;
 			Raw r;
 			const char* s;
 			size_t n;
-			do { if(!line(s, n)) return k; } while(n == 0);
+			bool got = false;
+			while(line(s, n)) { if(n) { got = true; break; } }
+			if(!got) {                           // this file's part is done: next file
+				file_done();
+				continue;
+			}
 			r.l[0] = s; r.n[0] = n;
-			for(int j = 1; j < 4; j++) { if(!line(s, n)) { s = map_ + len_; n = 0; } r.l[j] = s; r.n[j] = n; }
+			const File& F = f_[cur_];
+			for(int j = 1; j < 4; j++) { if(!line(s, n)) { s = F.map + F.end; n = 0; } r.l[j] = s; r.n[j] = n; }
 			out.push_back(r);
 			k++;
+			taken_++;
 		}
 		return k;
 	}
-	// decodes into r, reusing its buffers
-	static void decode(const Raw& raw, Read& r, uint64_t rdid, uint32_t randSeed) {
+	// global number of the shard's first record
+	uint64_t first_rdid() const { return first_rdid_; }
+	size_t nfiles() const { return f_.size(); }
+	// records of this shard up to the end of file f (f < files_done())
+	size_t files_done() const { return ends_.size(); }
+	uint64_t file_end(size_t f) const { return ends_[f]; }
+	// decodes into r, reusing its buffers; name_id numbers an unnamed read
+	static void decode(const Raw& raw, Read& r, uint64_t rdid, uint32_t randSeed, uint64_t name_id) {
 		if(raw.l[0][0] != '@') throw std::runtime_error("FASTQ record does not start with '@'");
 		r.rdid = rdid;
 		r.name.assign(raw.l[0] + 1, raw.n[0] - 1);
@@ -573,7 +598,7 @@ public:
 		if(raw.n[1] || raw.n[3]) r.qual.assign(raw.l[3], raw.n[3]);
 		if(r.qual.size() != r.fw.size())
 			throw std::runtime_error("read " + r.name + ": qualities and sequence differ in length");
-		if(r.name.empty()) r.name = std::to_string(rdid);
+		if(r.name.empty()) r.name = std::to_string(name_id);
 		const size_t L = r.fw.size();
 		r.rc.resize(L);
 		for(size_t i = 0; i < L; i++) {
@@ -583,20 +608,41 @@ public:
 		r.qualRev.assign(r.qual.rbegin(), r.qual.rend());
 		r.seed = gen_rand_seed(r, randSeed);
 	}
+	static void decode(const Raw& raw, Read& r, uint64_t rdid, uint32_t randSeed) { decode(raw, r, rdid, randSeed, rdid); }
 private:
+	struct File { const char* map = nullptr; size_t len = 0; int fd = -1; size_t beg = 0, end = 0; };
 	bool line(const char*& s, size_t& n) {
-		if(pos_ >= len_) return false;
-		s = map_ + pos_;
-		const char* nl = (const char*)std::memchr(s, '\n', len_ - pos_);
-		n = nl ? (size_t)(nl - s) : len_ - pos_;
+		const File& F = f_[cur_];
+		if(pos_ >= F.end) return false;
+		s = F.map + pos_;
+		const char* nl = (const char*)std::memchr(s, '\n', F.end - pos_);
+		n = nl ? (size_t)(nl - s) : F.end - pos_;
 		pos_ += n + (nl ? 1 : 0);
 		while(n > 0 && s[n - 1] == '\r') n--;
 		return true;
 	}
-	const char* map_ = nullptr;
-	size_t len_ = 0, pos_ = 0;
-	int fd_ = -1;
+	void file_done() {
+		ends_.push_back(taken_);
+		if(++cur_ < f_.size()) pos_ = f_[cur_].beg;
+	}
+	std::vector<File> f_;
+	size_t cur_ = 0, pos_ = 0;
+	uint64_t first_rdid_ = 0, taken_ = 0;
+	std::vector<uint64_t> ends_;
 };
+
+// bowtie2's -U list: comma-separated file names
+inline std::vector<std::string> split_list(const std::string& s) {
+	std::vector<std::string> out;
+	size_t b = 0;
+	for(;;) {
+		const size_t e = s.find(',', b);
+		out.push_back(s.substr(b, e == std::string::npos ? std::string::npos : e - b));
+		if(e == std::string::npos) break;
+		b = e + 1;
+	}
+	return out;
+}
 
 // ------------------------------------------------------------------- reference
 
@@ -864,6 +910,8 @@ struct ReadCtx {
 	bool done = false;                   // finished, record not yet handed to the writer
 	// statistics for the run summary
 	bool aligned = false, repetitive = false;
+	std::string warn;               // the read's stderr warnings (printEEScoreMsg), written at retire
+	int met_kind = 0;               // finishRead's counter: 0 nunp_0, 1 nunp_uni1, 2 nunp_uni2, 3 nunp_rep
 	uint64_t ndp_used = 0;          // DP results the walk consumed (the rest were lookahead)
 	uint64_t ntight = 0;            // nextAlignment records consumed after -M tightened minsc
 	                                // within the same DP problem
@@ -904,12 +952,29 @@ public:
 
 // -------------------------------------------------------------------- driver
 
+// ReportingMetrics (aln_sink.h:44-170), the reference's per-run alignment counters, in its
+// field order; the unpaired fields are the ones this fork fills (AlnSinkWrap::finishRead,
+// aln_sink.cpp:708-713, 990-1013).  Additive: shards sum them (bt2_search.cpp:2867-2869).
+struct ReportingMetrics {
+	enum { NREAD, NPAIRED, NUNPAIRED, NCONCORD_UNI, NCONCORD_UNI1, NCONCORD_UNI2, NCONCORD_REP, NCONCORD_0,
+	       NDISCORD, NUNP_0_UNI, NUNP_0_UNI1, NUNP_0_UNI2, NUNP_0_REP, NUNP_0_0, NUNP_REP_UNI, NUNP_REP_UNI1,
+	       NUNP_REP_UNI2, NUNP_REP_REP, NUNP_REP_0, NUNP_UNI, NUNP_UNI1, NUNP_UNI2, NUNP_REP, NUNP_0,
+	       SUM_BEST1, SUM_BEST2, SUM_BEST, N };
+	uint64_t v[N] = {};
+	void merge(const ReportingMetrics& o) { for(int k = 0; k < N; k++) v[k] += o.v[k]; }
+};
+// AlnSink::printAlSumm for unpaired reads with a repetitive threshold (-M: canRep),
+// aln_sink.cpp:349-527.
+void print_alignment_summary(const ReportingMetrics& m, std::FILE* f);
+
 struct RunStats {
 	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0;
 	uint64_t seed_launches = 0, resolve_launches = 0, dp_launches = 0;
 	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
 	uint64_t round_launches = 0, rounds = 0, round_redo = 0;
 	uint64_t dp_max_launch = 0;     // problems in the largest DP launch
+	ReportingMetrics met;
+	std::vector<double> t_files;    // when each input file's last record was written
 	double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0,
 	       t_wait = 0, t_gather = 0, t_retire = 0;
 };
@@ -923,6 +988,8 @@ public:
 	// seed rounds through bt2x_seed_round (default on; off: seed search, host ranking and
 	// prioritization, SA resolution as three requests)
 	void set_gpu_round(bool on) { gpu_round_ = on; }
+	// --no-hd: no @HD/@SQ/@PG lines (every shard but the first of a split run)
+	void set_header(bool on) { header_on_ = on; }
 	// Size both launches' buffers for `reads` reads per launch up front: page-locked
 	// buffers cost milliseconds per allocation, so growing them launch by launch is slow.
 	void reserve_launch_buffers(size_t reads);
@@ -975,7 +1042,7 @@ private:
 	void execute(Launch& L);
 	void scatter_resume(Launch& L, RunStats& st);
 	Launch launch_[2];
-	bool pipeline_ = true, gpu_round_ = true;
+	bool pipeline_ = true, gpu_round_ = true, header_on_ = true;
 	ReadCtx* take_ctx();
 	void retire(std::vector<ReadCtx*>& act, RunStats& st, void* ring);
 	// pooled read contexts (kept across runs; released by the destructor)

@@ -3,10 +3,17 @@
 // FASTQ in, SAM out.  All hot-path work runs on one GPU through libbt2x (include/bt2x.h);
 // there is no CPU fallback.
 //
-//   bt2x-align -x <index base> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N]
+//   bt2x-align -x <index base> {-U <r1.fq>[,r2.fq,...] | -1 <m1.fq> -2 <m2.fq>} [-S out.sam] [--dpad N] [-D N] [-R N]
 //              [-L N] [-i FUNC] [--score-min FUNC] [--n-ceil FUNC] [--mp MX,MN] [--np N]
 //              [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N] [--no-sse8] [--i16-build]
-//              [-p threads] [--slots N] [--device N] [--stats]
+//              [--no-hd] [-p threads] [--slots N] [--device N] [--stats]
+//              [--shard i/N] [--warmup-files K] [--metrics]
+// --shard i/N aligns the i-th of N contiguous parts of the read stream (FastqReader); the
+// N outputs concatenated in order (headers from part 0 only: --no-hd on the others) are
+// the whole run's SAM.  --warmup-files K aligns the first K files of the -U list once,
+// untimed and unwritten, before the timed run over the rest (bench.py).  --metrics prints
+// the 27 ReportingMetrics counters (BT2X_METRICS) and the run's clock (BT2X_TIMED) for a
+// launcher to sum over shards.
 // --no-sse8 runs the signed 16-bit DP as the reference's -DENABLE_I16 build does
 // (aligner_swsse_ee_i16.cpp); --i16-build emulates that build's default (u8 unless the
 // minimum score is below -254).
@@ -206,21 +213,23 @@ private:
 
 void usage() {
 	std::fprintf(stderr,
-	             "usage: bt2x-align -x <index> -U <reads.fq> [-S out.sam] [--dpad N] [-D N] [-R N] [-L N]\n"
+	             "usage: bt2x-align -x <index> -U <r1.fq>[,r2.fq,...] [-S out.sam] [--dpad N] [-D N] [-R N] [-L N]\n"
 	             "                  [-i FUNC] [--score-min FUNC] [--n-ceil FUNC] [--mp MX,MN] [--np N]\n"
 	             "                  [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N] [--no-sse8] [--i16-build]\n"
-	             "                  [-p threads] [--slots N] [--device N] [--stats]\n");
+	             "                  [--no-hd] [-p threads] [--slots N] [--device N] [--stats]\n"
+	             "                  [--shard i/N] [--warmup-files K] [--metrics]\n");
 }
 
 } // namespace
 
 int main(int argc, char** argv) {
 	tune_malloc();
-	std::string idx, fq, outp;
+	std::string idx, fq, outp, mate1, mate2;
 	Params p;
 	int threads = 16, device = 0;
 	size_t slots = 1 << 18;
-	bool stats = false, pipeline = true, gpu_round = true;
+	bool stats = false, pipeline = true, gpu_round = true, hd = true, metrics = false;
+	int shard = 0, nshards = 1, warm_files = 0;
 	std::string dump;
 	for(int i = 1; i < argc; i++) {
 		const std::string a = argv[i];
@@ -231,6 +240,8 @@ int main(int argc, char** argv) {
 		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
 		if(a == "-x") idx = val();
 		else if(a == "-U") fq = val();
+		else if(a == "-1") mate1 = val();
+		else if(a == "-2") mate2 = val();
 		else if(a == "-S") outp = val();
 		else if(a == "-p") threads = std::atoi(val());
 		else if(a == "--slots") slots = (size_t)std::atol(val());
@@ -239,10 +250,36 @@ int main(int argc, char** argv) {
 		else if(a == "--dump") dump = val();
 		else if(a == "--no-pipeline") pipeline = false;
 		else if(a == "--no-gpu-round") gpu_round = false;
+		else if(a == "--no-hd") hd = false;
+		else if(a == "--metrics") metrics = true;
+		else if(a == "--warmup-files") warm_files = std::atoi(val());
+		else if(a == "--shard") {
+			if(std::sscanf(val(), "%d/%d", &shard, &nshards) != 2 || nshards < 1 || shard < 0 || shard >= nshards) {
+				std::fprintf(stderr, "--shard takes i/N with 0 <= i < N\n");
+				return 1;
+			}
+		}
 		else if(a == "--end-to-end" || a == "--sensitive" || a == "--reorder" || a == "-q") {}
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); usage(); return 1; }
 	}
+	// -1/-2: this fork aligns mate 1 alone, as unpaired reads (bt2_search.cpp:1006-1007,
+	// 1690-1694 -- paired alignment is compiled out), so the mate-1 files are the read stream
+	if(!mate1.empty() || !mate2.empty()) {
+		if(!fq.empty()) { std::fprintf(stderr, "-U with -1/-2 is not supported\n"); return 1; }
+		if(split_list(mate1).size() != split_list(mate2).size()) {
+			std::fprintf(stderr, "Error: %zu mate files/sequences were specified with -1, but %zu\n"
+			             "mate files/sequences were specified with -2.  The same number of mate files/\n"
+			             "sequences must be specified with -1 and -2.\n", split_list(mate1).size(), split_list(mate2).size());
+			return 1;
+		}
+		fq = mate1;
+	}
 	if(idx.empty() || fq.empty()) { usage(); return 1; }
+	const std::vector<std::string> files = split_list(fq);
+	if(warm_files < 0 || (size_t)warm_files >= files.size()) {
+		std::fprintf(stderr, "--warmup-files must leave at least one -U file to time\n");
+		return 1;
+	}
 	bt2x_scoring_init(&p.sc);
 	if(p.multiseedLen < 1 || p.multiseedLen > 32) { std::fprintf(stderr, "-L must be in 1..32\n"); return 1; }
 	try {
@@ -271,8 +308,16 @@ int main(int argc, char** argv) {
 		Aligner al(p, ref, be);
 		al.set_pipeline(pipeline);
 		al.set_gpu_round(gpu_round);
-		FastqReader reader(fq.c_str());
+		al.set_header(hd);
 		pin.join();
+		if(warm_files > 0) {                           // untimed: first launches, page faults, pools
+			FastqReader wr(std::vector<std::string>(files.begin(), files.begin() + warm_files), shard, nshards);
+			std::FILE* null = std::fopen("/dev/null", "wb");
+			if(!null) throw std::runtime_error("cannot open /dev/null");
+			al.run(wr, null, slots, threads);
+			std::fclose(null);
+		}
+		FastqReader reader(std::vector<std::string>(files.begin() + warm_files, files.end()), shard, nshards);
 		struct rusage ru0;
 		getrusage(RUSAGE_SELF, &ru0);
 		const auto t_start = std::chrono::steady_clock::now();
@@ -285,14 +330,16 @@ int main(int argc, char** argv) {
 		const double t_align = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
 		struct rusage ru_end;
 		getrusage(RUSAGE_SELF, &ru_end);
-		// alignment summary (AlnSink::printAlSumm, unpaired)
-		auto pct = [&](uint64_t a) { return st.reads ? 100.0 * (double)a / (double)st.reads : 0.0; };
-		std::fprintf(stderr, "%llu reads; of these:\n", (unsigned long long)st.reads);
-		std::fprintf(stderr, "  %llu (100.00%%) were unpaired; of these:\n", (unsigned long long)st.reads);
-		std::fprintf(stderr, "    %llu (%.2f%%) aligned 0 times\n", (unsigned long long)st.unaligned, pct(st.unaligned));
-		std::fprintf(stderr, "    %llu (%.2f%%) aligned exactly 1 time\n", (unsigned long long)(st.aligned - st.rep), pct(st.aligned - st.rep));
-		std::fprintf(stderr, "    %llu (%.2f%%) aligned >1 times\n", (unsigned long long)st.rep, pct(st.rep));
-		std::fprintf(stderr, "%.2f%% overall alignment rate\n", pct(st.aligned));
+		print_alignment_summary(st.met, stderr);
+		if(metrics) {
+			std::string line = "BT2X_METRICS";
+			for(uint64_t v : st.met.v) line += " " + std::to_string(v);
+			std::fprintf(stderr, "%s\n", line.c_str());
+			std::string tf;
+			for(double t : st.t_files) { char b[32]; std::snprintf(b, sizeof b, "%s%.4f", tf.empty() ? "" : ",", t); tf += b; }
+			std::fprintf(stderr, "BT2X_TIMED reads=%llu first_rdid=%llu t_align=%.4f t_files=%s\n",
+			             (unsigned long long)st.reads, (unsigned long long)reader.first_rdid(), t_align, tf.c_str());
+		}
 		if(stats) {
 			// the whole process, then the alignment window alone
 			struct rusage ru;

@@ -136,28 +136,48 @@ private:
 
 int main(int argc, char** argv) {
 	tune_malloc();
-	if(argc < 3) { std::fprintf(stderr, "usage: test_e2e_oracle <index> <reads.fq> [--dpad N] [--slots N] [-p T]\n"); return 1; }
+	// test_e2e_oracle <index> <reads.fq> [options], or bt2x-align's -x/-U/-S form (the
+	// multi-process launcher drives it as it drives bt2x-align)
+	const char* usage = "usage: test_e2e_oracle <index> <reads.fq>[,more.fq] [--dpad N] [--slots N] [-p T] [--shard i/N] "
+	                    "[--no-hd] [--metrics] [-S out]\n";
 	Params p;
 	size_t slots = 4096;
 	int threads = 4;
-	bool host_timing = false, pipeline = true, gpu_round = true;
-	int reps = 1, inject = 0;
-	for(int i = 3; i < argc; i++) {
+	bool host_timing = false, pipeline = true, gpu_round = true, hd = true, metrics = false;
+	int reps = 1, inject = 0, shard = 0, nshards = 1;
+	std::string idx, fqs, outp;
+	std::vector<std::string> pos;
+	for(int i = 1; i < argc; i++) {
 		if(const int k = parse_align_option(p, argc, argv, i)) { i += k - 1; continue; }
 		const std::string a = argv[i];
 		if(a == "--slots" && i + 1 < argc) slots = (size_t)std::atol(argv[++i]);
 		else if(a == "-p" && i + 1 < argc) threads = std::atoi(argv[++i]);
+		else if(a == "-x" && i + 1 < argc) idx = argv[++i];
+		else if(a == "-U" && i + 1 < argc) fqs = argv[++i];
+		else if(a == "-S" && i + 1 < argc) outp = argv[++i];
 		else if(a == "--host-timing") host_timing = true;
 		else if(a == "--no-pipeline") pipeline = false;
 		else if(a == "--no-gpu-round") gpu_round = false;
+		else if(a == "--no-hd") hd = false;
+		else if(a == "--metrics") metrics = true;
 		else if(a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
 		else if(a == "--inject-error" && i + 1 < argc) inject = std::atoi(argv[++i]);
+		else if(a == "--shard" && i + 1 < argc) {
+			if(std::sscanf(argv[++i], "%d/%d", &shard, &nshards) != 2) { std::fputs(usage, stderr); return 1; }
+		}
+		else if(a[0] != '-') pos.push_back(a);
 		else { std::fprintf(stderr, "unsupported option %s\n", a.c_str()); return 1; }
 	}
+	if(idx.empty() && !pos.empty()) idx = pos[0];
+	if(fqs.empty() && pos.size() > 1) fqs = pos[1];
+	if(idx.empty() || fqs.empty()) { std::fputs(usage, stderr); return 1; }
+	const std::vector<std::string> files = split_list(fqs);
+	std::FILE* out = stdout;
+	if(!outp.empty() && !(out = std::fopen(outp.c_str(), "wb"))) { std::fprintf(stderr, "cannot open %s\n", outp.c_str()); return 1; }
 	bt2x_scoring_init(&p.sc);
-	bt2x::Index index(argv[1], true);
+	bt2x::Index index(idx.c_str(), true);
 	RefInfo ref;
-	ref.init(index.desc(), argv[1]);
+	ref.init(index.desc(), idx);
 	OracleBackend be(index.desc(), p.sc);
 	be.fail_at = inject;
 	if(host_timing) {
@@ -166,7 +186,7 @@ int main(int argc, char** argv) {
 			Aligner al0(p, ref, rb);
 			al0.set_pipeline(pipeline);
 			al0.set_gpu_round(gpu_round);
-			FastqReader fq(argv[2]);
+			FastqReader fq(files, shard, nshards);
 			std::FILE* nul = std::fopen("/dev/null", "wb");
 			al0.run(fq, nul, slots, threads);
 			std::fclose(nul);
@@ -177,7 +197,7 @@ int main(int argc, char** argv) {
 		Aligner al(p, ref, rb);
 		al.set_pipeline(pipeline);
 		al.set_gpu_round(gpu_round);
-		FastqReader fq(argv[2]);
+		FastqReader fq(files, shard, nshards);
 		struct rusage ru0, ru1;
 		getrusage(RUSAGE_SELF, &ru0);
 		const auto t0 = std::chrono::steady_clock::now();
@@ -200,13 +220,24 @@ int main(int argc, char** argv) {
 	Aligner al(p, ref, be);
 	al.set_pipeline(pipeline);
 	al.set_gpu_round(gpu_round);
-	FastqReader fq(argv[2]);
+	al.set_header(hd);
 	RunStats st;
+	uint64_t first_rdid = 0;
 	try {
-		st = al.run(fq, stdout, slots, threads);
+		FastqReader fq(files, shard, nshards);
+		first_rdid = fq.first_rdid();
+		st = al.run(fq, out, slots, threads);
 	} catch(const std::exception& e) {               // as bt2x-align's main does
 		std::fprintf(stderr, "test_e2e_oracle: %s\n", e.what());
 		return 1;
+	}
+	if(out != stdout) std::fclose(out); else std::fflush(out);
+	if(metrics) {                                     // bt2x-align --metrics' lines
+		print_alignment_summary(st.met, stderr);
+		std::string line = "BT2X_METRICS";
+		for(uint64_t v : st.met.v) line += " " + std::to_string(v);
+		std::fprintf(stderr, "%s\nBT2X_TIMED reads=%llu first_rdid=%llu t_align=0\n", line.c_str(),
+		             (unsigned long long)st.reads, (unsigned long long)first_rdid);
 	}
 	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu "
 	             "tight_recs=%llu\n",

@@ -75,3 +75,83 @@ def test_gloo_two_rank_sharded_seed_search(tmp_path):
     seeds, rep, t = open(tmp_path / "ctr.txt").read().split()
     assert int(seeds) == case.n and int(rep) == int(full["need_reporting"].sum())
     assert float(t) == 2.0
+
+
+ORACLE_DRIVER = os.path.join(ROOT, "tests", "cpp", "test_e2e_oracle")
+
+
+def test_gloo_two_rank_sharded_alignment(tmp_path):
+    """The product's multi-GPU path (python -m bt2x.dist under torch.distributed.run) with
+    gloo and world_size 2, each rank's aligner being the host driver over the CPU oracle
+    kernels (tests/cpp/test_e2e_oracle, bt2x-align's command line): the rep reads split over
+    two -U files, sharded by byte range; the concatenated SAM equals the single-process
+    run's byte for byte (and the reference golden's records), and the summary printed from
+    the all-reduced ReportingMetrics equals the reference's."""
+    import json
+    import lzma
+    import golden_io as g
+    from test_e2e import sam_records, split_stderr
+    base = g.materialize_index("rep", str(tmp_path / "idx"))
+    with lzma.open(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), "rb") as f:
+        lines = f.read().split(b"\n")
+    cut = 4 * 1301                                  # two -U files: a record boundary, uneven
+    (tmp_path / "a.fq").write_bytes(b"\n".join(lines[:cut]) + b"\n")
+    (tmp_path / "b.fq").write_bytes(b"\n".join(lines[cut:]))
+    fqs = f"{tmp_path / 'a.fq'},{tmp_path / 'b.fq'}"
+    single = subprocess.run([ORACLE_DRIVER, "-x", base, "-U", fqs, "-p", "2", "--metrics"],
+                            capture_output=True, timeout=600)
+    assert single.returncode == 0, single.stderr[-2000:]
+    out = tmp_path / "dist.sam"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1",
+               PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "omp-bowtie2-prime_amd"), os.environ.get("PYTHONPATH", "")]))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "bt2x.dist",
+           "--aligner", ORACLE_DRIVER, "--no-device", "--", "-x", base, "-U", fqs, "-p", "2", "-S", str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = out.read_bytes()
+    assert got == single.stdout
+    with lzma.open(os.path.join(g.GOLDEN, "e2e_rep.sam.xz"), "rb") as f:
+        assert sam_records(got) == sam_records(f.read())
+    with open(os.path.join(g.GOLDEN, "e2e_summary.json")) as f:
+        exp = json.load(f)["sets"]["e2e_rep"]["summary"]
+    assert split_stderr(r.stderr)[1] == split_stderr(exp)[1]
+    assert "BT2X_DIST ranks=2 reads=3560" in r.stderr
+    assert not list(tmp_path.glob("dist.sam.part*"))
+
+
+def test_shard_partition_and_metrics_sum(tmp_path):
+    """--shard i/N over 1..5 shards (byte ranges snapped to records): the parts concatenate
+    to the whole run, record ids continue across shards (first_rdid) and the shards'
+    BT2X_METRICS sum to the single run's."""
+    import golden_io as g
+    import lzma
+    base = g.materialize_index("rep", str(tmp_path / "idx"))
+    fq = tmp_path / "r.fq"
+    with lzma.open(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), "rb") as f:
+        fq.write_bytes(f.read())
+    whole = subprocess.run([ORACLE_DRIVER, "-x", base, "-U", str(fq), "-p", "2", "--metrics"], capture_output=True,
+                           timeout=600, check=True)
+    wm = bdist.parse_metrics(whole.stderr.decode())["metrics"]
+    for n in (2, 5):
+        parts, tot, nxt = [], {k: 0 for k in bdist.METRIC_NAMES}, 0
+        for i in range(n):
+            r = subprocess.run([ORACLE_DRIVER, "-x", base, "-U", str(fq), "-p", "2", "--metrics", "--shard", f"{i}/{n}"]
+                               + ([] if i == 0 else ["--no-hd"]), capture_output=True, timeout=600, check=True)
+            parts.append(r.stdout)
+            pm = bdist.parse_metrics(r.stderr.decode())
+            assert int(pm["timed"]["first_rdid"]) == nxt
+            nxt += pm["metrics"]["nread"]
+            for k, v in pm["metrics"].items():
+                tot[k] += v
+        assert b"".join(parts) == whole.stdout
+        assert tot == wm
+
+
+def test_alignment_summary_format():
+    m = {k: 0 for k in bdist.METRIC_NAMES}
+    m.update(nread=3560, nunpaired=3560, nunp_0=1284, nunp_uni=2276, nunp_uni1=1798, nunp_uni2=478)
+    assert bdist.alignment_summary(m) == (
+        "3560 reads; of these:\n  3560 (100.00%) were unpaired; of these:\n    1284 (36.07%) aligned 0 times\n"
+        "    1798 (50.51%) aligned exactly 1 time\n    478 (13.43%) aligned >1 times\n63.93% overall alignment rate\n")
+    assert bdist.alignment_summary({k: 0 for k in bdist.METRIC_NAMES}) == "0 reads\n0.00% overall alignment rate\n"

@@ -53,6 +53,28 @@ SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
 # below), and each kernel forced for every launch
 DP_MODES = {"default": None, "lane": "0", "wave": "1"}
 MD5 = os.path.join(g.GOLDEN, "e2e_md5.json")
+SUMMARY = os.path.join(g.GOLDEN, "e2e_summary.json")
+
+
+def split_stderr(text: str) -> tuple[list[str], str]:
+    """(sorted per-read warning lines, the alignment summary block) of an aligner's stderr:
+    the reference prints both (printEEScoreMsg, AlnSink::printAlSumm)."""
+    lines = text.splitlines()
+    warns = sorted(ln for ln in lines if ln.startswith("Warning:"))
+    start = next((i for i, ln in enumerate(lines) if ln.endswith(" reads; of these:") or ln.endswith(" reads")), None)
+    assert start is not None, "no alignment summary in:\n" + text[-1500:]
+    end = next(i for i in range(start, len(lines)) if lines[i].endswith("overall alignment rate"))
+    return warns, "".join(ln + "\n" for ln in lines[start:end + 1])
+
+
+def check_summary(stderr: bytes, name: str) -> None:
+    """The run's summary and warnings == the reference's (e2e_summary.json, make_golden.py summary)."""
+    with open(SUMMARY) as f:
+        exp = json.load(f)["sets"][name]["summary"]
+    got_w, got_s = split_stderr(stderr.decode())
+    exp_w, exp_s = split_stderr(exp)
+    assert got_s == exp_s, f"summary:\n{got_s}\nreference:\n{exp_s}"
+    assert got_w == exp_w, f"{len(got_w)} warnings vs the reference's {len(exp_w)}"
 
 
 def sam_records(data: bytes) -> list[bytes]:
@@ -92,7 +114,8 @@ def check(cmd: list[str], golden: str, env=None):
 def test_host_driver_vs_reference_sam(fixtures, name, idx, fq, opts):
     """Host driver + CPU oracle kernels == the reference's SAM (no GPU)."""
     assert os.access(ORACLE_DRIVER, os.X_OK), "build first: make -C tests/cpp"
-    got, err = check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4"] + opts, name)
+    got, err = check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4", "--metrics"] + opts, name)
+    check_summary(err, name)
     n_al = sum(1 for ln in got if not ln.startswith(b"@") and ln.split(b"\t")[1] != b"4")
     # (150 bp reads need --dpad <= 12 to fit ALN_MAX_COLS: SURVEY F2)
     assert n_al > {"lambda_virus": 400, "rep": 2000, "tandem": 1400}[idx]
@@ -150,7 +173,8 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     env.pop("BT2X_DP_WAVE", None)
     if DP_MODES[mode] is not None:
         env["BT2X_DP_WAVE"] = DP_MODES[mode]
-    check([ALIGN, "-x", fixtures[idx], "-U", fixtures[fq], "--slots", "1000"] + opts, name, env=env)
+    _, err = check([ALIGN, "-x", fixtures[idx], "-U", fixtures[fq], "--slots", "1000"] + opts, name, env=env)
+    check_summary(err, name)
 
 
 # ---------------------------------------------------------------- md5 goldens
@@ -217,7 +241,9 @@ def md5_opts(st) -> list[str]:
 def test_host_driver_vs_reference_md5_ecoli(ecoli, name):
     """Config C2 (u8 and the i16 kernel): host driver + CPU oracle kernels == reference."""
     base, reads = ecoli
-    check_md5([ORACLE_DRIVER, base, reads[name], "--slots", "2000", "-p", "4"] + md5_opts(md5_sets()["sets"][name]), name)
+    err = check_md5([ORACLE_DRIVER, base, reads[name], "--slots", "2000", "-p", "4", "--metrics"]
+                    + md5_opts(md5_sets()["sets"][name]), name)
+    check_summary(err, name)
 
 
 def test_host_driver_vs_reference_md5_lambda_full(tmp_path):
@@ -237,6 +263,7 @@ def test_bt2x_align_vs_reference_md5_ecoli(ecoli, name):
     large = "large" in name
     err = check_md5([ALIGN, "-x", base, "-U", reads[name], "--slots", "65536" if large else "4096", "--stats"]
                     + md5_opts(md5_sets()["sets"][name]), name)
+    check_summary(err, name)
     if large:
         mx = int(err.split(b"dp_max_launch=")[1].split()[0])
         assert mx > 32768, mx
@@ -259,3 +286,18 @@ def test_host_driver_lookahead_invariance(fixtures):
     assert outs[0] == outs[1] == outs[2]
     with lzma.open(os.path.join(g.GOLDEN, "e2e_rep_dpad12.sam.xz"), "rb") as f:
         assert outs[0] == sam_records(f.read())
+
+
+@pytest.mark.gpu
+def test_bt2x_align_mates_align_as_unpaired(fixtures, tmp_path):
+    """-1/-2 (config C4): this fork aligns mate 1 alone, as unpaired reads -- the
+    records and summary of `-1 m1 -2 m2` equal those of `-U m1` (the reference's, measured:
+    tools/make_golden.py; here the rep golden)."""
+    m2 = tmp_path / "m2.fq"
+    m2.write_bytes(open(fixtures["rep_reads.fq"], "rb").read())
+    _, err = check([ALIGN, "-x", fixtures["rep"], "-1", fixtures["rep_reads.fq"], "-2", str(m2), "--slots", "1000"],
+                   "e2e_rep")
+    check_summary(err, "e2e_rep")
+    r = subprocess.run([ALIGN, "-x", fixtures["rep"], "-1", fixtures["rep_reads.fq"], "-2", f"{m2},{m2}"],
+                       capture_output=True, timeout=120)
+    assert r.returncode == 1 and b"specified with -1, but 2" in r.stderr

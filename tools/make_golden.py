@@ -22,6 +22,8 @@ Steps (all outputs xz-compressed under tests/golden/):
   6. i16 (`make_golden.py i16`): the -DENABLE_I16 reference builds (refharness-i16,
      bowtie2-align-l-i16) -- DP vectors and SAM of the signed 16-bit kernel (--no-sse8).
   7. md5 (`make_golden.py md5`): e2e_md5.json, md5s of sets too large to commit as SAM
+  8. summary (`make_golden.py summary`): e2e_summary.json, the reference's alignment
+     summary (ReportingMetrics) for the e2e and md5 sets
      (config C2's E. coli stand-in, 50k-read lane-kernel launches, all of config C1).
 Each text golden file starts with a '#' header naming the command that produced it.
 """
@@ -248,9 +250,52 @@ def md5_goldens(tmp: str) -> None:
         json.dump(out, f, indent=1)
 
 
+def ref_summary(stderr: str) -> str:
+    """The reference's alignment summary (AlnSink::printAlSumm) from its stderr, without
+    the Timer: lines it prints alongside (bt2_search.cpp MyTimer dump)."""
+    return "".join(ln + "\n" for ln in stderr.splitlines() if ln and not ln.startswith("Timer:"))
+
+
+def summary_goldens(tmp: str) -> None:
+    """e2e_summary.json: the reference's alignment summary for the committed e2e sets and
+    the E. coli md5 sets (the metrics bt2x-align --metrics and bt2x.dist reproduce)."""
+    import json
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = {"_note": "tools/make_golden.py summary: the reference aligner's stderr summary (1 thread)", "sets": {}}
+    sets = ([(n, i, f, o, ALIGN) for n, i, f, o in E2E_SETS] +
+            [(n, "tandem", "tandem_reads.fq", o, ALIGN) for n, o in TANDEM_SETS] +
+            [(n, i, f, o, ALIGN16) for n, i, f, o in I16_E2E_SETS])
+    for name, idx, fq, opts, binary in sets:
+        base = os.path.join(tmp, idx)
+        if not os.path.exists(base + ".4.bt2l"):
+            for k in "1234":
+                xz_unpack(os.path.join(GOLD, f"{idx}.{k}.bt2l.xz"), f"{base}.{k}.bt2l")
+        rfq = os.path.join(tmp, fq)
+        if not os.path.exists(rfq):
+            xz_unpack(os.path.join(GOLD, fq + ".xz"), rfq)
+        r = subprocess.run([binary, "-x", base, "-U", rfq, "-S", os.devnull] + opts, env=env, check=True,
+                           capture_output=True, text=True)
+        out["sets"][name] = {"index": idx, "fastq": fq + ".xz", "opts": opts,
+                             "binary": "i16" if binary == ALIGN16 else "u8", "summary": ref_summary(r.stderr)}
+    g = sd.ecoli_genome()
+    fa = os.path.join(tmp, "ecoli.fa")
+    sd.write_fasta(fa, g)
+    base = os.path.join(tmp, "ecoli")
+    run([BUILD, fa, base], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    for name, n, rdlen, seed, binary, opts in MD5_SETS:
+        fq = os.path.join(tmp, f"{name}.fq")
+        sd.fixture_reads(g, fq, n, rdlen, seed)
+        r = subprocess.run([ALIGN16 if binary == "i16" else ALIGN, "-x", base, "-U", fq, "-S", os.devnull] + opts,
+                           env=env, check=True, capture_output=True, text=True)
+        out["sets"][name] = {"index": "ecoli", "reads": n, "read_len": rdlen, "seed": seed, "binary": binary,
+                             "opts": opts, "summary": ref_summary(r.stderr)}
+    with open(os.path.join(GOLD, "e2e_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main() -> None:
     run(["make", "-C", os.path.join(ROOT, "oracle"), "ref", "oracle"])
-    for cmd, fn in (("i16", i16_goldens), ("md5", md5_goldens)):
+    for cmd, fn in (("i16", i16_goldens), ("md5", md5_goldens), ("summary", summary_goldens)):
         if sys.argv[1:] == [cmd]:
             tmp = tempfile.mkdtemp(prefix="bt2x_golden_")
             try:
