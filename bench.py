@@ -1,25 +1,34 @@
 #!/usr/bin/env python3
-"""bench.py — BASELINE.json's headline metric on MI355X: 150 bp single-end reads,
-end-to-end alignment with --dpad 12 (config C3; hg38 is not available offline, so a
-seeded 1 Gbp synthetic genome stands in), reads/s and the DP kernel's HBM roofline.
+"""bench.py — BASELINE.json's headline metric on MI355X: end-to-end FASTQ -> SAM reads/s
+of 150 bp single-end reads at --dpad 12 (config C3).  hg38 is not available offline: a
+seeded 3.1 Gbp synthetic genome of 24 chromosomes stands in (tools/simdata.gen_genome:
+interspersed repeat families, low-complexity stretches, N runs), indexed on the box.
 
-Per rank (one process per GPU):
-  1. The aligner itself, bt2x-align (FASTQ -> SAM; host driver + the three gfx950
-     kernels, omp-bowtie2-prime_amd/host), runs once over the batch of --reads reads and
-     records the inputs of every GPU launch it makes (--dump): the seed searches, SA
-     resolutions and DP rounds that SwDriver::extendSeeds generates for these reads.
-     A second, undumped run gives the end-to-end wall time (`end_to_end`, FASTQ parse,
-     host logic, PCIe and SAM formatting included).
-  2. The timed hot path: one step = that exact launch sequence replayed from HBM
-     (inputs resident before the timed region) -- seed_kernel, resolve_kernel and
-     dp_fill_kernel launches in the aligner's order.
-     value = reads of all ranks / max-over-ranks wall time of K steps.
-  3. Rank 0 at N=1: the reference aligner (oracle/_ref/bowtie2-align-l, OpenMP) on a
-     bounded sample of the same FASTQ = cpu_baseline; its SAM is compared with ours
-     record by record (`parity`).
-Multi-GPU: reads sharded (each rank its own seeded batch), index replicated per GPU,
-no collective on the data path ("scaling": "weak"); the only collective is the
-max-of-times reduction for the report.
+Per rank (one process per GPU; the GPU work runs in bt2x-align, a child process):
+  setup   genome (seeded, every rank), its index (rank 0: suffix array by prefix doubling
+          on the GPU, tools/gpu_sa.py; files by bt2x_build_index_sa, byte-identical to the
+          reference builder), and the rank's reads: W warmup + K step files of
+          ceil(10M / K) reads each (tools/simdata.sim_reads_fast, BASELINE.md's error model),
+          generated in a process pool before anything touches the GPU.
+  timed   bt2x-align -U warm1,..,warmW,step1,..,stepK --warmup-files W: the W warmup files
+          run untimed inside the same process (first launches, page faults, pools), then
+          the K step files are one timed FASTQ -> SAM run: parse, the host driver, every
+          seed search / SA resolution / DP on the GPU, PCIe, SAM formatting and writing.
+          All ranks start it after a barrier; value = reads of all ranks / max over ranks
+          of the timed run's wall time (BT2X_TIMED t_align; the index load is outside it).
+  kernels rank 0: bt2x-align --dump records the GPU launches of one 1M-read file; the
+          launch sequence is replayed from HBM (inputs resident) with HIP events around
+          each launch (bt2x_last_kernel_ms, on the launch stream) -> per-kernel time,
+          the dominant kernel's roofline, and replay_reads_per_s (kernels alone).
+  cpu     rank 0 at N=1: the reference aligner (oracle/_ref/bowtie2-align-l, OpenMP)
+          on a bounded sample of the first step file (SURVEY §8(d) protocol: threads n-1
+          and n of the box's CPU share, the better one repeated to a median of 3, plus a
+          1-thread line; alignment time = wall - wall of a 1-read run (index load); the
+          reference's own Timer: phase sums reported).  Its SAM is compared with ours
+          record by record (`parity`).
+Multi-GPU: each rank aligns its own 10M-read batch ("scaling": "weak"), the index
+replicated per GPU; the ranks' only exchange is the final sum of the ReportingMetrics
+counters and the max of the times (gloo: host values, no GPU collective on the path).
 """
 from __future__ import annotations
 
@@ -27,6 +36,7 @@ import argparse
 import glob
 import json
 import os
+import shutil
 import subprocess
 import sys
 import time
@@ -41,102 +51,44 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
 ALIGN = os.path.join(ROOT, "omp-bowtie2-prime_amd", "bt2x", "bt2x-align")
 REF_ALIGN = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l")
+C3_READS = 10_000_000
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--reads", type=int, default=1 << 20, help="reads per step per GPU")
+    ap.add_argument("--steps", type=int, default=10, help="timed step files (C3's 10M reads split K ways)")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed warmup files")
+    ap.add_argument("--reads", type=int, default=C3_READS, help="timed reads per GPU (C3: 10M)")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--dpad", type=int, default=12, help="--dpad (maxhalf); 12 fits 150 bp in ALN_MAX_COLS")
-    ap.add_argument("--genome", default="synthetic", help="'synthetic' (default) or 'rep' (fixture)")
-    ap.add_argument("--genome-mb", type=float, default=1000.0)
+    ap.add_argument("--genome-mb", type=float, default=3100.0)
     ap.add_argument("--genome-seed", type=int, default=2024)
-    ap.add_argument("--host-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
-                    help="host threads of bt2x-align (the box's CPU share)")
-    ap.add_argument("--cpu-sample", type=int, default=200000,
-                    help="reads aligned by the reference aligner for cpu_baseline / parity")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
-                    help="OpenMP threads of the reference CPU baseline (the box's CPU share)")
+    ap.add_argument("--host-threads", type=int, default=0, help="bt2x-align -p (0: the rank's CPU share)")
+    ap.add_argument("--slots", type=int, default=1 << 18, help="bt2x-align --slots (reads in flight)")
+    ap.add_argument("--replay-reads", type=int, default=1 << 20, help="reads whose GPU launches are replayed")
+    ap.add_argument("--replay-steps", type=int, default=3)
+    ap.add_argument("--cpu-sample", type=int, default=800_000, help="reads of the reference CPU baseline")
+    ap.add_argument("--cpu-sample-1t", type=int, default=40_000, help="reads of its 1-thread line")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--replay-ablate", type=int, default=0,
-                    help="profiling only: BT2X_DP_ABLATE for the replay (1: DP fill without the walk); outputs invalid")
-    ap.add_argument("--prep-only", action="store_true",
-                    help="write the genome index and reads, print their paths, exit (profiling the aligner)")
-    ap.add_argument("--lookahead", type=int, default=8, help="bt2x-align --lookahead (DP problems posed per request)")
-    ap.add_argument("--slots", type=int, default=1 << 17,
-                    help="bt2x-align --slots (reads in flight) of the end-to-end run; the launch-recording run "
-                         "batches the whole --reads batch (--slots = --reads, --no-pipeline)")
-    ap.add_argument("--rss-limit-gb", type=float, default=120.0, help="kill bt2x-align above this host RSS")
+    ap.add_argument("--no-replay", action="store_true")
+    ap.add_argument("--workdir", default=os.environ.get("BT2X_BENCH_DIR", f"/tmp/bt2x_bench_{os.getuid()}"))
+    ap.add_argument("--rss-limit-gb", type=float, default=200.0, help="kill bt2x-align above this host RSS")
     return ap.parse_args()
 
 
-def workload_key(args) -> str:
-    g = f"synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}" if args.genome == "synthetic" else args.genome
-    return f"e2e|{g}|reads{args.reads}|R{args.read_len}|dpad{args.dpad}|la{args.lookahead}|round"
-
-
-def pmc_traffic(args, kernel: str):
-    """Per-step HBM bytes of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/<tag>_traffic.json, tools/pmc_traffic.py) taken on this same workload;
-    (None, None) if there is none."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
-        with open(path) as f:
-            t = json.load(f)
-        if t.get("workload") == workload_key(args) and kernel in t.get("kernels", {}):
-            return t["kernels"][kernel]["traffic_bytes"], os.path.relpath(path, ROOT)
-    return None, None
-
-
-def load_genome(args, workdir, rank=0, dist=None):
-    """-> (chroms, index basename, description).  'synthetic' (default): a seeded
-    genome-scale reference (tools/simdata.gen_genome: 24 chromosomes, interspersed
-    repeat families, low-complexity stretches, N runs) indexed here -- suffix array
-    by prefix doubling on the GPU (tools/gpu_sa.py), files by bt2x_build_index_sa
-    (byte-identical to the reference's bowtie2-build-l, tests/test_builder.py).
-    Index building is setup, outside the timed region."""
-    import golden_io as g
-    import simdata as sd
-    if args.genome == "rep":
-        import lzma
-        with lzma.open(os.path.join(g.GOLDEN, "rep.fa.xz"), "rb") as f:
-            raw = f.read()
-        path = os.path.join(workdir, f"rep{rank}.fa")
-        with open(path, "wb") as f:
-            f.write(raw)
-        chroms = sd.read_fasta(path)
-        base = g.materialize_index("rep", os.path.join(workdir, f"r{rank}"))
-        return chroms, base, "rep (300 kbp repeat-rich fixture)"
-    if args.genome != "synthetic":
-        raise SystemExit("--genome must be 'synthetic' or 'rep'")
-    import gpu_sa
-    from bt2x import lib
-    total = int(args.genome_mb * 1e6)
-    tag = f"syn{total}_s{args.genome_seed}"
-    base = os.path.join(workdir, tag)
-    fa = base + ".fa"
-    t0 = time.perf_counter()
-    chroms = sd.gen_genome(total, nchrom=24, seed=args.genome_seed)
-    # rank 0 builds (ranks share the node's /tmp); the others wait at the barrier
-    if rank == 0 and not all(os.path.exists(f"{base}.{k}.bt2l") for k in "1234"):
-        sd.write_fasta(fa, chroms)
-        codes, _ = sd.concat_genome(chroms)
-        sa, bwt, keys = gpu_sa.suffix_array(codes[codes < 4], device="cuda")
-        lib.build_index_sa(fa, base + ".tmp", sa, bwt=bwt, keys=keys)
-        for k in "1234":
-            os.replace(f"{base}.tmp.{k}.bt2l", f"{base}.{k}.bt2l")
-        del sa, bwt, keys, codes
-        os.unlink(fa)
-        import torch
-        torch.cuda.empty_cache()
-    if dist:
-        dist.barrier()
-    print(f"# genome {tag}: {total / 1e6:.0f} Mbp, index ready in {time.perf_counter() - t0:.1f} s",
-          file=sys.stderr, flush=True)
-    return chroms, base, f"synthetic {total / 1e6:.0f} Mbp (seed {args.genome_seed}, 24 chromosomes, " \
-                         f"5% repeat families, low-complexity, N runs)"
+def cpu_share() -> int:
+    """CPUs this process may use: affinity, capped by the cgroup's CPU quota (the GPU box
+    reports the whole machine's CPUs in affinity but grants a 16-CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, p = open(path).read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, int(q) // int(p)))
+        except (OSError, ValueError):
+            pass
+    return n
 
 
 def mark(msg):
@@ -146,41 +98,125 @@ def mark(msg):
             rss = next(int(ln.split()[1]) >> 10 for ln in f if ln.startswith("VmRSS"))
     except (OSError, StopIteration):
         pass
-    print(f"# {msg} (bench RSS {rss} MiB)", file=sys.stderr, flush=True)
+    print(f"# {time.strftime('%H:%M:%S')} {msg} (bench RSS {rss} MiB)", file=sys.stderr, flush=True)
 
 
-def write_fastq(path, reads, quals, first_id=0):
-    """Fixed-length FASTQ, vectorised: '@r<9 digits>' names."""
-    n, R = reads.shape
-    rec = np.empty((n, 11 + 1 + R + 3 + R + 1), dtype=np.uint8)
-    rec[:, 0] = ord("@"); rec[:, 1] = ord("r")
-    ids = np.arange(first_id, first_id + n, dtype=np.int64)
-    for k in range(9):
-        rec[:, 10 - k] = ord("0") + (ids // (10 ** k)) % 10
-    rec[:, 11] = ord("\n")
-    rec[:, 12:12 + R] = np.frombuffer(b"ACGTN", np.uint8)[reads]
-    rec[:, 12 + R] = ord("\n"); rec[:, 13 + R] = ord("+"); rec[:, 14 + R] = ord("\n")
-    rec[:, 15 + R:15 + 2 * R] = quals
-    rec[:, 15 + 2 * R] = ord("\n")
-    with open(path, "wb") as f:
-        f.write(rec.tobytes())
+def workload_key(args) -> str:
+    return (f"c3|synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}|reads{args.reads}|R{args.read_len}|"
+            f"dpad{args.dpad}|replay{args.replay_reads}")
 
 
-def run_aligner(args, base, fq, sam, gpu, dump=None):
-    """dump: record the launch sequence with the whole batch in flight (the largest
-    launches; the problems are the same at any batching); otherwise the end-to-end
-    configuration (--slots reads in flight, GPU launches overlapped with host work)."""
-    slots = args.reads if dump else args.slots
-    cmd = [ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad), "--device", str(gpu),
-           "-p", str(args.host_threads), "--slots", str(slots), "--lookahead", str(args.lookahead), "--stats"]
-    if dump:
-        cmd += ["--dump", dump, "--no-pipeline"]
+def pmc_profile(args, kernel: str):
+    """Per-launch HBM bytes and VALU figures of `kernel` from the newest committed rocprofv3
+    PMC summary (profiles/<tag>_traffic.json, tools/pmc_traffic.py) taken on this workload."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == workload_key(args) and kernel in t.get("kernels", {}):
+            return t["kernels"][kernel], os.path.relpath(path, ROOT)
+    return None, None
+
+
+# ------------------------------------------------------------------------ inputs
+
+_GEN = {}
+
+
+def _gen_file(job):
+    import simdata as sd
+    path, n, R, seed, first_id = job
+    reads, quals = sd.sim_reads_fast(_GEN["codes"], _GEN["starts"], n, R, seed)
+    sd.write_fastq_fixed(path + ".tmp", reads, quals, first_id=first_id)
+    os.replace(path + ".tmp", path)
+    return path
+
+
+def make_inputs(args, rank, world, workdir):
+    """-> (chroms, [warmup files], [step files], reads per step file).  Reads: seeded per
+    (rank, file), written by a fork pool before the GPU is touched."""
+    import multiprocessing as mp
+    import simdata as sd
     t0 = time.perf_counter()
-    errp = os.path.join(os.path.dirname(sam), "align.err")
+    chroms = sd.gen_genome(int(args.genome_mb * 1e6), nchrom=24, seed=args.genome_seed)
+    codes, starts = sd.concat_genome(chroms)
+    mark(f"genome {args.genome_mb:g} Mbp generated in {time.perf_counter() - t0:.1f} s")
+    per = -(-args.reads // args.steps)
+    rdir = os.path.join(workdir, f"rank{rank}")
+    os.makedirs(rdir, exist_ok=True)
+    jobs, warm, steps = [], [], []
+    first = 0
+    for k in range(args.warmup + args.steps):
+        n = per if k >= args.warmup else args.replay_reads       # warmup files double as the replay batch
+        if k == args.warmup + args.steps - 1:
+            n = args.reads - per * (args.steps - 1)
+        tag = f"w{k}" if k < args.warmup else f"s{k - args.warmup}"
+        path = os.path.join(rdir, f"{tag}_{n}_R{args.read_len}_g{args.genome_seed}.fq")
+        (warm if k < args.warmup else steps).append(path)
+        if not os.path.exists(path):
+            jobs.append((path, n, args.read_len, 3 + 7919 * rank + 104729 * k, first))
+        first += n
+    if jobs:
+        _GEN["codes"], _GEN["starts"] = codes, starts
+        procs = max(1, min(len(jobs), cpu_share() // max(world, 1)))
+        with mp.get_context("fork").Pool(procs) as pool:
+            for _ in pool.imap_unordered(_gen_file, jobs):
+                pass
+        _GEN.clear()
+    mark(f"rank {rank}: {len(warm)} warmup + {len(steps)} step files of {per} reads ready in "
+         f"{time.perf_counter() - t0:.1f} s")
+    return chroms, codes, warm, steps, per
+
+
+def build_index(args, chroms, codes, workdir, rank, dist):
+    """Rank 0 indexes the genome (cached in workdir); the others wait at the barrier."""
+    import simdata as sd
+    tag = f"syn{int(args.genome_mb * 1e6)}_s{args.genome_seed}"
+    base = os.path.join(workdir, tag)
+    t0 = time.perf_counter()
+    if rank == 0 and not all(os.path.exists(f"{base}.{k}.bt2l") for k in "1234"):
+        import torch
+        import gpu_sa
+        from bt2x import lib
+        fa = base + ".fa"
+        sd.write_fasta(fa, chroms)
+        sa, bwt, keys = gpu_sa.suffix_array(codes[codes < 4], device="cuda")
+        lib.build_index_sa(fa, base + ".tmp", sa, bwt=bwt, keys=keys)
+        for k in "1234":
+            os.replace(f"{base}.tmp.{k}.bt2l", f"{base}.{k}.bt2l")
+        del sa, bwt, keys
+        os.unlink(fa)
+        torch.cuda.empty_cache()
+    if dist:
+        dist.barrier()
+    mark(f"index {tag} ready in {time.perf_counter() - t0:.1f} s")
+    return base, (f"synthetic {args.genome_mb / 1e3:.2f} Gbp (seed {args.genome_seed}, 24 chromosomes, "
+                  f"5% repeat families, low-complexity stretches, N runs)")
+
+
+# ------------------------------------------------------------------------ aligner runs
+
+def kv_line(err: str, tag: str) -> dict:
+    lines = [ln for ln in err.splitlines() if ln.startswith(tag + " ")]
+    if not lines:
+        return {}
+    out = {}
+    for t in lines[-1].split()[1:]:
+        k, v = t.split("=", 1)
+        try:
+            out[k] = float(v)
+        except ValueError:
+            out[k] = v
+    return out
+
+
+def run_aligner(args, cmd, errp, what):
+    """bt2x-align as a child process (this process's GPU context, if any, stays idle), with
+    a host-RAM watchdog (the box caps a command's RAM) and a progress line every 30 s."""
+    t0 = time.perf_counter()
     with open(errp, "w") as ferr:
         p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=ferr)
-        peak = 0
-        while p.poll() is None:          # host-RAM watchdog (the box caps a command's RAM)
+        peak, last = 0, t0
+        while p.poll() is None:
             try:
                 with open(f"/proc/{p.pid}/status") as f:
                     for ln in f:
@@ -188,28 +224,21 @@ def run_aligner(args, base, fq, sam, gpu, dump=None):
                             peak = max(peak, int(ln.split()[1]) >> 10)
             except OSError:
                 pass
-            if peak > args.rss_limit_gb * 1024 or time.perf_counter() - t0 > 1500:
+            now = time.perf_counter()
+            if peak > args.rss_limit_gb * 1024 or now - t0 > 900:
                 p.kill()
                 p.wait()
                 break
+            if now - last > 30:
+                mark(f"{what}: running {now - t0:.0f} s, RSS {peak} MiB")
+                last = now
             time.sleep(0.2)
     wall = time.perf_counter() - t0
     err = open(errp).read()
     if p.returncode != 0:
-        raise SystemExit(f"bt2x-align failed (rc {p.returncode}, peak RSS {peak} MiB): {err[-3000:]}")
-    print(f"# bt2x-align {'(dump) ' if dump else ''}{wall:.1f} s, peak RSS {peak} MiB", file=sys.stderr, flush=True)
-    line = [ln for ln in err.splitlines() if ln.startswith("BT2X_STATS")][-1]
-    st = {k: float(v) for k, v in (t.split("=") for t in line.split()[1:])}
-    ru = [ln for ln in err.splitlines() if ln.startswith("BT2X_RUSAGE_ALIGN")]
-    if ru:
-        st["rusage_align"] = {k: float(v) for k, v in (t.split("=") for t in ru[-1].split()[1:])}
-    gl = [ln for ln in err.splitlines() if ln.startswith("BT2X_GPU")]
-    if gl:
-        st["gpu"] = {k: float(v) for k, v in (t.split("=") for t in gl[-1].split()[1:])}
-    st["wall_incl_index_load"] = wall
-    st["peak_rss_mib"] = peak
-    st["summary"] = [ln.strip() for ln in err.splitlines() if "aligned" in ln or "overall" in ln]
-    return st
+        raise SystemExit(f"bt2x-align ({what}) failed (rc {p.returncode}, peak RSS {peak} MiB): {err[-3000:]}")
+    mark(f"bt2x-align {what}: {wall:.1f} s, peak RSS {peak} MiB")
+    return err, wall, peak
 
 
 def load_dumps(ddir):
@@ -240,103 +269,23 @@ def load_dumps(ddir):
     return out
 
 
-def sam_records(path, limit_ids=None):
-    recs = []
-    with open(path, "rb") as f:
-        for ln in f:
-            if ln.startswith(b"@"):
-                continue
-            if limit_ids is not None and int(ln[1:10]) >= limit_ids:
-                continue
-            recs.append(ln.rstrip(b"\n"))
-    recs.sort()
-    return recs
-
-
-def cpu_reference(args, base, fq_sample, m, workdir):
-    """The reference aligner (OpenMP, --cpu-threads) on the first m reads; alignment time
-    = wall(m reads) - wall(1 read) (index load cancels)."""
-    if not os.access(REF_ALIGN, os.X_OK):
-        return None, None
-    env = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads), OMP_WAIT_POLICY="ACTIVE")
-    one = os.path.join(workdir, "one.fq")
-    with open(fq_sample, "rb") as f, open(one, "wb") as g:
-        for _ in range(4):
-            g.write(f.readline())
-    times = []
-    for fq, sam in ((one, os.path.join(workdir, "ref_one.sam")), (fq_sample, os.path.join(workdir, "ref.sam"))):
-        t0 = time.perf_counter()
-        r = subprocess.run([REF_ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad)],
-                           env=env, capture_output=True, text=True, timeout=1200)
-        times.append(time.perf_counter() - t0)
-        if r.returncode != 0:
-            print(r.stderr[-2000:], file=sys.stderr)
-            return None, None
-    dt = max(times[1] - times[0], 1e-6)
-    base_line = {"value": round(m / dt / 1e6, 6), "unit": "M reads/s", "cores": args.cpu_threads,
-                 "kind": "reference",
-                 "sample": f"first {m} reads of this batch through the reference aligner "
-                           f"(oracle/_ref/bowtie2-align-l --dpad {args.dpad}, FASTQ->SAM, OpenMP "
-                           f"{args.cpu_threads} threads): {times[1]:.2f} s minus {times[0]:.2f} s index load"}
-    return base_line, os.path.join(workdir, "ref.sam")
-
-
-def main():
-    args = parse()
+def replay(args, base, fq, rdir, gpu):
+    """Record the GPU launches bt2x-align makes for the reads of `fq` (whole file in flight),
+    replay them from HBM and time each launch with HIP events on the launch stream."""
     import torch
-    from bt2x import dist as bdist
-    rank, world, local = bdist.world()
-    # rehearsal knobs (not used by the driver): BT2X_BENCH_DEVICE pins every rank to one
-    # GPU, BT2X_BENCH_DIST_BACKEND=gloo runs the rank reductions on the host
-    gpu = int(os.environ.get("BT2X_BENCH_DEVICE", local))
-    backend = os.environ.get("BT2X_BENCH_DIST_BACKEND", "nccl")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if backend == "nccl":
-            torch.cuda.set_device(gpu)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend)
-
     from bt2x import abi, lib
-    import simdata as sd
-
-    workdir = os.path.join("/tmp", f"bt2x_bench_{os.getuid()}")
-    os.makedirs(workdir, exist_ok=True)
-    chroms, base, gdesc = load_genome(args, workdir, rank, dist)
-    genome, starts = sd.concat_genome(chroms)
-    R, n = args.read_len, args.reads
-    reads, quals, _, _, _ = sd.sim_reads_fixed(genome, starts, n, R, seed=bdist.rank_seed(3, rank))
-    del genome
-    rdir = os.path.join(workdir, f"rank{rank}")
-    os.makedirs(rdir, exist_ok=True)
-    fq = os.path.join(rdir, "reads.fq")
-    write_fastq(fq, reads, quals)
-    del reads, quals
-    mark(f"{n} reads written to {fq}")
-    if args.prep_only:
-        print(f"BT2X_DATA {base} {fq}", flush=True)
-        return
-
-    # ---- 1. the aligner: launch recording run, then the end-to-end timing run
+    n = int(os.path.basename(fq).split("_")[1])
     ddir = os.path.join(rdir, "dump")
-    for p in glob.glob(os.path.join(ddir, "*")):
-        os.unlink(p)
-    os.makedirs(ddir, exist_ok=True)
-    sam = os.path.join(rdir, "out.sam")
-    run_aligner(args, base, fq, sam, gpu, dump=ddir)
-    e2e = run_aligner(args, base, fq, sam, gpu)
+    shutil.rmtree(ddir, ignore_errors=True)
+    os.makedirs(ddir)
+    run_aligner(args, [ALIGN, "-x", base, "-U", fq, "-S", os.devnull, "--dpad", str(args.dpad), "-p",
+                       str(args.host_threads), "--slots", str(n), "--dump", ddir, "--no-pipeline"],
+                os.path.join(rdir, "dump.err"), "launch recording")
     launches = load_dumps(ddir)
-    mark(f"{len(launches)} launches loaded")
-
-    # ---- 2. replay the launch sequence from HBM
-    if args.replay_ablate:
-        os.environ["BT2X_DP_ABLATE"] = str(args.replay_ablate)
-    if world == 1 or backend != "nccl":
-        torch.cuda.set_device(gpu)
+    shutil.rmtree(ddir, ignore_errors=True)
+    torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    idx = lib.Index(base, load_offs=True)     # SA sample + text: full SA rebuilt in HBM
+    idx = lib.Index(base, load_offs=True)
     ctx = lib.Context(idx, device=gpu)
 
     def to_dev(a):
@@ -372,6 +321,7 @@ def main():
                                    torch.empty(rec_cap * abi.ALN_REC.itemsize, dtype=torch.uint8, device=dev),
                                    torch.empty(edit_cap * 4, dtype=torch.uint8, device=dev),
                                    torch.zeros(16, dtype=torch.int32, device=dev), rec_cap, edit_cap]))
+    del launches
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     kid = {"seed": abi.K_SEED, "resolve": abi.K_RESOLVE, "dp": abi.K_DP, "round": abi.K_ROUND}
@@ -398,10 +348,10 @@ def main():
             if record is not None:
                 # HIP events recorded on this stream around each launch (bt2x_last_kernel_ms);
                 # a round's seed kernel and ranking+resolution are also booked as seed / resolve
-                record[kind]["ms"] += ctx.last_kernel_ms(kid[kind])
+                record[kind] += ctx.last_kernel_ms(kid[kind])
                 if kind == "round":
-                    record["seed"]["ms"] += ctx.last_kernel_ms(abi.K_SEED)
-                    record["resolve"]["ms"] += ctx.last_kernel_ms(abi.K_RESOLVE)
+                    record["seed"] += ctx.last_kernel_ms(abi.K_SEED)
+                    record["resolve"] += ctx.last_kernel_ms(abi.K_RESOLVE)
             if counters is not None:
                 for kk in (("seed", "resolve") if kind == "round" else (kind,)):
                     for k, v in ctx.last_counters(kid[kk]).items():
@@ -413,105 +363,241 @@ def main():
                     counters["round"]["max_samples"] = max(counters["round"].get("max_samples", 0), rs["max_samples"])
 
     ctr = {k: {} for k in kid}          # algorithmic-work counters (deterministic per step)
-    for w in range(max(args.warmup, 1)):
-        step(counters=ctr if w == 0 else None)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
+    step(counters=ctr)
     torch.cuda.synchronize(dev)
     recs = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rec = {k: {"ms": 0.0} for k in kid}
+    for _ in range(args.replay_steps):
+        rec = {k: 0.0 for k in kid}
         step(rec)
         recs.append(rec)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    e2e_t = e2e["t_align"]
-    if dist:
-        dist.barrier()
-        red_dev = dev if backend == "nccl" else None
-        elapsed = bdist.max_over_ranks(elapsed, dist, red_dev)
-        e2e_t = bdist.max_over_ranks(e2e_t, dist, red_dev)
     for kind, m, b in plan:           # overflow check on the last step's arenas
         if kind == "dp":
             used = b[7][:2].cpu().numpy()
             if used[0] > b[8] or used[1] > b[9]:
                 raise SystemExit(f"DP result arena overflow {used} vs {(b[8], b[9])}")
-
-    value = n * world * args.steps / elapsed / 1e6
-    kms = {k: float(np.mean([r[k]["ms"] for r in recs])) for k in kid}
-    # algorithmic bytes: FM = 128*(2*BiLF + LF1) + 16*ftab (+ 128*LF1 + 8 per
-    # SA sample for the GroupWalk resolve); DP = 3*R*C (E,F,H) + C (window) + 10*ceil(R/16)*16
-    cs, cr, cd = ctr["seed"], ctr["resolve"], ctr["dp"]
-    fm_bytes = 128 * (2 * cs.get("n_bilf", 0) + cs.get("n_lf1", 0)) + 16 * cs.get("n_ftab", 0)
-    res_bytes = cr.get("alg_bytes", 0)
-    dp_bytes = 3 * cd.get("dp_cells", 0) + cd.get("dp_cols", 0) + units["dp"] * 10 * ((R + 15) // 16) * 16
-    kern = {"seed": (kms["seed"], fm_bytes), "resolve": (kms["resolve"], res_bytes), "dp": (kms["dp"], dp_bytes)}
-    # (round launches are booked above as their seed and resolve parts)
-    dom = max(kern, key=lambda k: kern[k][0])
-    ach = kern[dom][1] / (kern[dom][0] / 1e3) / 1e9 if kern[dom][0] > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(args, dom)
-    # the kernel's own algorithmic bytes (bt2x_counters.alg_bytes: for the DP, the 1 B
-    # traceback flag per cell it writes + window + read/quality bytes), beside §8(d)'s
-    # reference-equivalent figure above
-    own = {"seed": cs.get("alg_bytes", 0), "resolve": cr.get("alg_bytes", 0), "dp": cd.get("alg_bytes", 0)}[dom]
-    ach_own = own / (kern[dom][0] / 1e3) / 1e9 if kern[dom][0] > 0 else 0.0
+    kms = {k: float(np.mean([r[k] for r in recs])) for k in kid}
     nl = {k: sum(1 for kk, _, _ in plan if kk == k) for k in kid}
     nl["seed"] += nl["round"]
     nl["resolve"] += nl["round"]
+    ctx.close()
+    del plan
+    torch.cuda.empty_cache()
+    return {"reads": n, "elapsed": elapsed, "kms": kms, "ctr": ctr, "nl": nl, "units": units}
+
+
+def roofline(args, rp):
+    """SURVEY §8(d)'s algorithmic bytes per launch of the dominant kernel / its average
+    launch time (HIP events), with the kernel's own bytes beside it."""
+    R = args.read_len
+    cs, cr, cd = rp["ctr"]["seed"], rp["ctr"]["resolve"], rp["ctr"]["dp"]
+    kms, nl = rp["kms"], rp["nl"]
+    # FM = 128*(2*BiLF + LF1) + 16*ftab (+ 128*LF1 + 8 per SA sample for the GroupWalk
+    # resolve); DP = 3*R*C (E,F,H) + C (window) + 10*ceil(R/16)*16 (query profile)
+    fm_bytes = 128 * (2 * cs.get("n_bilf", 0) + cs.get("n_lf1", 0)) + 16 * cs.get("n_ftab", 0)
+    res_bytes = cr.get("alg_bytes", 0)
+    dp_bytes = 3 * cd.get("dp_cells", 0) + cd.get("dp_cols", 0) + rp["units"]["dp"] * 10 * ((R + 15) // 16) * 16
+    kern = {"seed": (kms["seed"], fm_bytes), "resolve": (kms["resolve"], res_bytes), "dp": (kms["dp"], dp_bytes)}
+    dom = max(kern, key=lambda k: kern[k][0])
+    ms, alg = kern[dom]
+    ach = alg / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    own = {"seed": cs.get("alg_bytes", 0), "resolve": cr.get("alg_bytes", 0), "dp": cd.get("alg_bytes", 0)}[dom]
+    ach_own = own / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    pmc, pmc_src = pmc_profile(args, dom)
+    L = max(nl[dom], 1)
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": None if pmc is None else int(pmc["traffic_bytes"] / L),
+            "alg_bytes": int(alg / L), "avg_launch_ms": round(ms / L, 4), "per": "launch", "launches_per_step": nl[dom],
+            "alg_bytes_note": "achieved/alg_bytes count SURVEY 8(d)'s full-rectangle reference-equivalent bytes "
+                              "(3 B of E/F/H per cell of every DP rectangle); the banded kernel computes "
+                              "dp_cells_computed cells and moves 1 B per computed cell: achieved_kernel",
+            "achieved_kernel": round(ach_own, 2), "frac_kernel": round(ach_own / HBM_PEAK_GBS, 4),
+            "alg_bytes_kernel": int(own / L), "pmc_src": pmc_src}
+    if pmc is not None:
+        for k in ("valu_util", "sq_wait_any_per_wave_cycle", "write_bytes"):
+            if k in pmc:
+                roof[k] = pmc[k] if k != "write_bytes" else int(pmc[k] / L)
+    kernels = {"seed_ms": round(kms["seed"], 3), "resolve_ms": round(kms["resolve"], 3), "dp_ms": round(kms["dp"], 3),
+               "seed_alg_bytes": fm_bytes, "resolve_alg_bytes": res_bytes, "dp_alg_bytes": dp_bytes,
+               "launches": nl, "units": rp["units"], "counters_seed": cs, "counters_resolve": cr,
+               "counters_dp": cd, "round_sampling": rp["ctr"]["round"], "replay_reads": rp["reads"],
+               "replay_steps": args.replay_steps,
+               "replay_reads_per_s": round(rp["reads"] * args.replay_steps / rp["elapsed"], 1),
+               "what": "the GPU launch sequence bt2x-align issues for replay_reads reads (one file, all in flight), "
+                       "replayed from HBM; kernel times from HIP events on the launch stream"}
+    return roof, kernels
+
+
+# ------------------------------------------------------------------------ CPU baseline
+
+def ref_run(args, base, fq, threads, sam):
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_WAIT_POLICY="ACTIVE")
+    t0 = time.perf_counter()
+    # (the fork's -p is a tasks-per-thread multiplier, default 10: BASELINE.md runs it as is)
+    r = subprocess.run([REF_ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad)],
+                       env=env, capture_output=True, text=True, timeout=900)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"reference aligner failed: {r.stderr[-2000:]}")
+    timers = {}
+    for ln in r.stderr.splitlines():
+        if ln.startswith("Timer:"):
+            p = ln.split()
+            if len(p) >= 4 and p[3] != "N/A":
+                timers[p[3]] = float(p[2])
+    return wall, timers
+
+
+def head_fastq(src, dst, n):
+    with open(src, "rb") as f, open(dst, "wb") as g:
+        for _ in range(4 * n):
+            ln = f.readline()
+            if not ln:
+                break
+            g.write(ln)
+
+
+def cpu_baseline(args, base, fq, rdir):
+    """the reference aligner on the box's CPU share; n-1 and n threads, the
+    better repeated to a median of 3; 1 thread on a smaller sample; alignment time = wall -
+    wall of a 1-read run at the same thread count (index load)."""
+    if not os.access(REF_ALIGN, os.X_OK):
+        return None, None
+    n = cpu_share()
+    m, m1 = args.cpu_sample, args.cpu_sample_1t
+    sample, s1, one = (os.path.join(rdir, f) for f in ("cpu_sample.fq", "cpu_1t.fq", "cpu_one.fq"))
+    head_fastq(fq, sample, m)
+    head_fastq(fq, s1, m1)
+    head_fastq(fq, one, 1)
+    sam = os.path.join(rdir, "ref.sam")
+    load = {}
+
+    def rate(threads, fqp, reads):
+        if threads not in load:
+            load[threads] = ref_run(args, base, one, threads, os.devnull)[0]
+        wall, timers = ref_run(args, base, fqp, threads, sam if fqp == sample else os.devnull)
+        return reads / max(wall - load[threads], 1e-6), wall, timers
+
+    runs = {}
+    for t in sorted({max(1, n - 1), n}):
+        runs[t] = [rate(t, sample, m)]
+        mark(f"reference aligner, {t} threads: {runs[t][-1][0]:.0f} reads/s")
+    best = max(runs, key=lambda t: runs[t][0][0])
+    while len(runs[best]) < 3:
+        runs[best].append(rate(best, sample, m))
+    med = sorted(runs[best], key=lambda r: r[0])[1]
+    one_t = rate(1, s1, m1)
+    mark(f"reference aligner: median {med[0]:.0f} reads/s at {best} threads; 1 thread {one_t[0]:.0f} reads/s")
+    # (the last sample run left its SAM at `sam`; every run over the sample aligns the same reads)
+    return {"value": round(med[0] / 1e6, 6), "unit": "M reads/s", "cores": best, "kind": "reference",
+            "sample": f"first {m} reads of step file 1 through oracle/_ref/bowtie2-align-l --dpad {args.dpad} "
+                      f"(FASTQ->SAM, OpenMP, OMP_WAIT_POLICY=ACTIVE) on this box's {n}-CPU share: "
+                      f"threads {sorted(runs)}, best repeated, median of 3; alignment time = wall - wall of a "
+                      f"1-read run (index load {load[best]:.2f} s)",
+            "runs": {str(t): [round(r[0], 1) for r in v] for t, v in runs.items()},
+            "one_thread": {"value": round(one_t[0] / 1e6, 6), "reads": m1},
+            "timer_sums_s": med[2], "cpu_share": n}, sam
+
+
+def sam_records(path, first_n=None):
+    recs = []
+    with open(path, "rb") as f:
+        for ln in f:
+            if ln.startswith(b"@"):
+                continue
+            recs.append(ln.rstrip(b"\n"))
+            if first_n is not None and len(recs) >= first_n:
+                break
+    recs.sort()
+    return recs
+
+
+# ------------------------------------------------------------------------ main
+
+def main():
+    args = parse()
+    from bt2x import dist as bdist
+    rank, world, local = bdist.world()
+    gpu = int(os.environ.get("BT2X_BENCH_DEVICE", local))
+    share = cpu_share()
+    if args.host_threads <= 0:
+        args.host_threads = max(4, share // max(world, 1))
+    workdir = args.workdir
+    os.makedirs(workdir, exist_ok=True)
+    # inputs first: the read generator forks, which must happen before the GPU is touched
+    chroms, codes, warm, steps, per = make_inputs(args, rank, world, workdir)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    base, gdesc = build_index(args, chroms, codes, workdir, rank, dist)
+    del chroms, codes
+    rdir = os.path.join(workdir, f"rank{rank}")
+
+    # ---- timed: the aligner over the step files (warmup files first, untimed)
+    need = args.reads * (args.read_len * 3)                   # SAM bytes, generously
+    out_sam = os.path.join(rdir, "out.sam")
+    if shutil.disk_usage(rdir).free < need + (8 << 30):
+        out_sam = os.devnull
+    cmd = [ALIGN, "-x", base, "-U", ",".join(warm + steps), "-S", out_sam, "--dpad", str(args.dpad),
+           "--device", str(gpu), "-p", str(args.host_threads), "--slots", str(args.slots),
+           "--warmup-files", str(len(warm)), "--metrics", "--stats"]
+    if dist:
+        dist.barrier()
+    err, wall, peak = run_aligner(args, cmd, os.path.join(rdir, "align.err"), "timed run")
+    if dist:
+        dist.barrier()
+    timed = kv_line(err, "BT2X_TIMED")
+    stats = kv_line(err, "BT2X_STATS")
+    met = bdist.parse_metrics(err)["metrics"]
+    t_align = float(timed["t_align"])
+    if met["nread"] != args.reads:
+        raise SystemExit(f"timed run aligned {met['nread']} reads, expected {args.reads}")
+    tot = bdist.sum_counters(met, dist)
+    t_max = bdist.max_over_ranks(t_align, dist)
+    value = tot["nread"] / t_max / 1e6
+    t_files = [float(x) for x in str(timed.get("t_files", "")).split(",") if x]
+
     line = {
         "metric": "M reads/s aligned (150 bp SE vs hg38) at 1/2/4/8 MI355X; % HBM-roofline",
         "value": round(value, 4), "unit": "M reads/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (seeded genome + simulated 150 bp reads, BASELINE.md error model)",
-        "config": {"workload": f"C3 stand-in: {R} bp SE, --dpad {args.dpad}, genome {gdesc}; step = the "
-                               f"GPU launch sequence bt2x-align issues to align {n} reads end to end "
-                               f"({nl['round']} seed-round launches (seed search + ranking/prioritization + SA "
-                               f"resolution), {nl['seed'] - nl['round']} seed, {nl['resolve'] - nl['round']} resolve, "
-                               f"{nl['dp']} DP launches: {units['seed']} seeds, {cr.get('n_problems', 0)} SA "
-                               f"elements, {units['dp']} DP problems), replayed from HBM",
-                   "reads_per_gpu_step": n, "read_len": R, "parallelism": f"dp{world} (read shards)",
-                   "key": workload_key(args)},
-        # achieved = algorithmic bytes per launch / average launch time (= per-step bytes / per-step
-        # kernel time); traffic (PMC, committed per step) is reported per launch to match.
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                     "traffic": None if traffic is None else int(traffic / max(nl[dom], 1)),
-                     "alg_bytes": int(kern[dom][1] / max(nl[dom], 1)),
-                     "avg_launch_ms": round(kern[dom][0] / max(nl[dom], 1), 4), "per": "launch",
-                     "alg_bytes_per_step": kern[dom][1], "traffic_per_step": traffic,
-                     "launches_per_step": nl[dom], "traffic_src": traffic_src,
-                     "alg_bytes_note": "achieved/alg_bytes count SURVEY 8(d)'s reference-equivalent bytes (3 B of "
-                                       "E/F/H per DP cell); the kernel itself moves 1 B per cell: see achieved_kernel",
-                     "achieved_kernel": round(ach_own, 2), "frac_kernel": round(ach_own / HBM_PEAK_GBS, 4),
-                     "alg_bytes_kernel": int(own / max(nl[dom], 1))},
-        "kernels": {"seed_ms": round(kms["seed"], 3), "resolve_ms": round(kms["resolve"], 3),
-                    "dp_ms": round(kms["dp"], 3), "seed_alg_bytes": fm_bytes, "resolve_alg_bytes": res_bytes,
-                    "dp_alg_bytes": dp_bytes, "launches": nl, "units": units,
-                    "counters_seed": cs, "counters_resolve": cr, "counters_dp": cd,
-                    "round_sampling": ctr["round"]},
-        "end_to_end": {"value": round(n * world / e2e_t / 1e6, 4), "unit": "M reads/s",
-                       "what": "bt2x-align FASTQ->SAM wall time (host driver, PCIe, SAM formatting; "
-                               f"index load excluded; --slots {args.slots}, launches overlapped with host "
-                               "work), max over ranks",
-                       "t_align_s": round(e2e_t, 3), "summary": e2e["summary"],
-                       "stats": {k: v for k, v in e2e.items() if k not in ("summary",)}},
+        "data": "synthetic (seeded 3.1 Gbp genome + simulated 150 bp reads, BASELINE.md error model)",
+        "config": {"workload": f"C3 stand-in: {args.reads} x {args.read_len} bp SE reads per GPU, end-to-end, "
+                               f"--dpad {args.dpad}, genome {gdesc}; value = FASTQ -> SAM reads/s of bt2x-align "
+                               f"(parse, host driver, GPU seed/resolve/DP kernels, PCIe, SAM written to "
+                               f"{'a file' if out_sam != os.devnull else '/dev/null'}), index load excluded; "
+                               f"step = one FASTQ file of {per} reads",
+                   "reads_per_gpu": args.reads, "read_len": args.read_len, "parallelism": f"dp{world} (read shards)",
+                   "host_threads": args.host_threads, "slots": args.slots, "key": workload_key(args)},
+        "end_to_end": {"t_align_s": round(t_align, 3), "t_align_max_s": round(t_max, 3),
+                       "step_done_s": [round(t, 3) for t in t_files], "wall_incl_index_load_s": round(wall, 2),
+                       "peak_rss_mib": peak, "summary": bdist.alignment_summary(tot).splitlines(),
+                       "stats": stats, "gpu": kv_line(err, "BT2X_GPU"), "rusage_align": kv_line(err, "BT2X_RUSAGE_ALIGN")},
     }
+    # ---- rank 0: kernels (replay) and, at N=1, the CPU baseline + parity
+    if rank == 0 and not args.no_replay:
+        rp = replay(args, base, warm[0] if warm else steps[0], rdir, gpu)
+        line["roofline"], line["kernels"] = roofline(args, rp)
     if rank == 0 and world == 1 and not args.no_cpu:
-        m = min(args.cpu_sample, n)
-        fqs = os.path.join(rdir, "sample.fq")
-        with open(fq, "rb") as f, open(fqs, "wb") as g:
-            rec_len = 11 + 1 + R + 3 + R + 1
-            g.write(f.read(rec_len * m))
-        ref, ref_sam = cpu_reference(args, base, fqs, m, rdir)
-        if ref is not None:
-            line["cpu_baseline"] = ref
-            ours, theirs = sam_records(sam, limit_ids=m), sam_records(ref_sam)
-            diff = sum(1 for a, b in zip(ours, theirs) if a != b) + abs(len(ours) - len(theirs))
-            line["parity"] = {"sample_reads": m, "records_differ": diff,
-                              "what": "sorted SAM records of bt2x-align vs the reference aligner on the sample"}
+        cb, ref_sam = cpu_baseline(args, base, steps[0], rdir)
+        if cb is not None:
+            line["cpu_baseline"] = cb
+            if out_sam != os.devnull:
+                ours, theirs = sam_records(out_sam, args.cpu_sample), sam_records(ref_sam)
+                diff = sum(1 for a, b in zip(ours, theirs) if a != b) + abs(len(ours) - len(theirs))
+                line["parity"] = {"sample_reads": args.cpu_sample, "records_differ": diff,
+                                  "what": "sorted SAM records of the timed run's first sample reads vs the "
+                                          "reference aligner's on the same reads"}
+            line["gpu_vs_cpu"] = round(value / cb["value"], 2) if cb["value"] else None
+    if out_sam != os.devnull and os.path.exists(out_sam):
+        os.unlink(out_sam)
+    if dist:
+        dist.barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
