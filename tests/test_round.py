@@ -74,3 +74,104 @@ def test_round_kernel_matches_host(sets):
     for name, base, fq in sets:
         st = run([base, fq, "--gpu"])
         assert st["mismatches"] == 0 and st["cases"] > 1000, (name, st)
+
+
+@pytest.mark.gpu
+def test_round_kernel_vs_reference_rank_golden(tmp_path):
+    """bt2x_seed_round against the reference's own rankSeedHits (tests/golden/rank_rep.txt.xz,
+    oracle/refharness.cpp "rank": aligner_seed.h:1000-1061 with a RandomSource seeded per
+    (read, round)).  Every read and round of the rep fixture runs through the kernel with
+    the golden's seeds, the golden's RNG seed and maxelt 0 (prioritizeSATups then samples
+    nothing, so the returned RNG state is the state after ranking): NO_HITS exactly where the
+    reference found none, and SeedResults::nonzeroOffsets(), numElts() and the RandomSource
+    state after rankSeedHits equal the reference's."""
+    import numpy as np
+    import torch
+    from bt2x import abi, lib
+    from bt2x import seeds as bseeds
+    base = g.materialize_index("rep", str(tmp_path))
+    case = g.SeedCase(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), os.path.join(g.GOLDEN, "seeds_rep.txt.xz"))
+    reads = g.read_fastq(os.path.join(g.GOLDEN, "rep_reads.fq.xz"))
+    # S rows per (read, round), in file order (the order bt2x_seed_round expects per read)
+    rows = {}
+    with g.open_text(os.path.join(g.GOLDEN, "seeds_rep.txt.xz")) as f:
+        k = 0
+        for line in f:
+            if line.startswith("S "):
+                t = line.split()
+                rows.setdefault((int(t[1]), int(t[2])), []).append(k)
+                k += 1
+    ranks = []
+    with g.open_text(os.path.join(g.GOLDEN, "rank_rep.txt.xz")) as f:
+        for line in f:
+            t = line.split()
+            if t and t[0] in ("K", "Z"):
+                ranks.append(t)
+    L = 22
+    seed_sel, rin, exp = [], [], []
+    offs = np.cumsum([0] + [2 * len(s) for _, s, _ in reads])
+    for t in ranks:
+        ridx, rnd = int(t[1]), int(t[2])
+        rdlen = len(reads[ridx][1])
+        ival = bseeds.interval(rdlen)
+        nrounds = min(2, ival)
+        offset = (ival * rnd) // nrounds
+        sl = min(L, rdlen)
+        num_offs = 1 + (rdlen - offset - sl) // ival if rdlen - offset > sl else 1
+        sel = rows.get((ridx, rnd), [])
+        r = np.zeros(1, dtype=abi.ROUND_IN)
+        r["read_off"] = offs[ridx]
+        r["seed0"] = len(seed_sel)
+        r["nseeds"] = len(sel)
+        r["num_offs"] = num_offs
+        r["rdlen"] = rdlen
+        r["interval"] = ival
+        r["offset"] = offset
+        r["seedlen"] = sl
+        if t[0] == "K":
+            assert int(t[4]) == num_offs
+            r["rnd_last"] = int(t[3])
+        else:
+            r["rnd_last"] = (ridx * 2654435761 + rnd * 97 + 1) & 0xffffffff
+        r["rnd_lastoff"] = 30                       # RandomSource::init (random_source.h:46-50)
+        seed_sel += sel
+        rin.append(r)
+        exp.append(t)
+    rin = np.concatenate(rin)
+    sin = case.inp[np.array(seed_sel, dtype=np.int64)]
+    n = len(rin)
+    dev = torch.device("cuda", 0)
+    torch.cuda.init()                           # torch's HIP runtime first, then the context
+    torch.cuda.set_device(dev)
+    ctx = lib.Context(lib.Index(base, load_offs=True))
+
+    def to_dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
+
+    d_reads, d_seeds, d_in = to_dev(case.reads), to_dev(sin), to_dev(rin)
+    d_exr = to_dev(np.zeros(1, dtype=abi.EXRANGE))
+    d_out = torch.zeros(n * abi.ROUND_OUT.itemsize, dtype=torch.uint8, device=dev)
+    cap = 8 * n + 1024
+    d_sats = torch.zeros(cap * abi.SAT.itemsize, dtype=torch.uint8, device=dev)
+    d_elts = torch.zeros(cap * abi.RESOLVE_OUT.itemsize, dtype=torch.uint8, device=dev)
+    d_exro = torch.zeros(cap * abi.EXRANGE.itemsize, dtype=torch.uint8, device=dev)
+    d_used = torch.zeros(4, dtype=torch.int32, device=dev)
+    ctx.seed_round_dev(d_reads.data_ptr(), d_seeds.data_ptr(), len(sin), d_in.data_ptr(), n, d_exr.data_ptr(), 0,
+                       d_out.data_ptr(), d_sats.data_ptr(), cap, d_elts.data_ptr(), cap, d_exro.data_ptr(), cap,
+                       d_used.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    out = d_out.cpu().numpy().view(abi.ROUND_OUT)
+    ctx.close()
+    bad, nk = [], 0
+    for i, t in enumerate(exp):
+        o = out[i]
+        if t[0] == "Z":
+            if o["status"] != 1:                    # BT2X_ROUND_NO_HITS
+                bad.append((t[:3], "status", int(o["status"])))
+            continue
+        nk += 1
+        got = (int(o["status"]), int(o["nonz"]), int(o["num_elts"]), int(o["rnd_last"]))
+        want = (0, int(t[5]), int(t[8]), int(t[13]))
+        if got != want:
+            bad.append((t[:3], got, want))
+    assert nk > 5000 and not bad, (len(bad), bad[:5])
