@@ -316,11 +316,14 @@ def replay(args, base, fq, rdir, gpu):
         else:
             m = len(parts[3])
             rec_cap, edit_cap = int(parts[4][0]) + 1024, int(parts[4][1]) + 4096   # sizes the aligner saw
-            plan.append((kind, m, [to_dev(parts[0]), to_dev(parts[1]), to_dev(parts[2]), to_dev(parts[3]),
+            fl = parts[3]["flags"]
+            lf = (abi.DPL_I16 if (fl & abi.DP_I16).any() else 0) | (abi.DPL_REF_TEXT if (fl & abi.DP_REF_TEXT).any() else 0)
+            refs = parts[2] if len(parts[2]) else np.zeros(1, dtype=np.uint8)
+            plan.append((kind, m, [to_dev(parts[0]), to_dev(parts[1]), to_dev(refs), to_dev(parts[3]),
                                    torch.empty(m * abi.DP_OUT.itemsize, dtype=torch.uint8, device=dev),
                                    torch.empty(rec_cap * abi.ALN_REC.itemsize, dtype=torch.uint8, device=dev),
                                    torch.empty(edit_cap * 4, dtype=torch.uint8, device=dev),
-                                   torch.zeros(16, dtype=torch.int32, device=dev), rec_cap, edit_cap]))
+                                   torch.zeros(16, dtype=torch.int32, device=dev), rec_cap, edit_cap, lf]))
     del launches
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
@@ -344,7 +347,7 @@ def replay(args, base, fq, rdir, gpu):
             else:
                 ctx.dp_align_dev(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), b[3].data_ptr(), m,
                                  b[4].data_ptr(), b[5].data_ptr(), b[8], b[6].data_ptr(), b[9],
-                                 b[7].data_ptr(), sh)
+                                 b[7].data_ptr(), sh, launch_flags=b[10])
             if record is not None:
                 # HIP events recorded on this stream around each launch (bt2x_last_kernel_ms);
                 # a round's seed kernel and ranking+resolution are also booked as seed / resolve

@@ -195,9 +195,14 @@ typedef struct {
 	int16_t  nceil;          /* max Ns in the reference portion                 */
 	uint16_t triml, corel, corer;
 	uint8_t  fw;             /* orientation: rc results get invertEdits()       */
-	uint8_t  flags;          /* BT2X_DP_I16                                      */
+	uint8_t  flags;          /* BT2X_DP_I16, BT2X_DP_REF_TEXT                      */
 } bt2x_dp_in;
 #define BT2X_DP_I16 1u
+/* The window comes from the index instead of refs[]: ref_off holds the text id (tidx) and
+ * the window is text tidx's [refl, refl + ncol), N (4) outside the text and in its N runs
+ * -- BitPairReference::getStretch as SwAligner::initRef calls it (aligner_sw.cpp:117-229).
+ * The context cuts it from the joined text it keeps in HBM (BT2X_CAP_REF_TEXT). */
+#define BT2X_DP_REF_TEXT 2u
 
 /* Result of align() for one problem.  Its nextAlignment() call sequence is
  * recs[rec_off .. rec_off + nrec). */
@@ -285,10 +290,13 @@ int bt2x_dp_align(bt2x_ctx* ctx,
  * then kernel scratch) in HBM.  launch_flags: BT2X_DPL_I16 when any problem carries
  * BT2X_DP_I16 (the 16-bit kernels run the launch; an i16 problem in a launch without
  * it is reported BT2X_E_ARG by the host variant, and comes back with status -1 here),
- * BT2X_DPL_EXACT_BEST for exact best of failed problems (bt2x_dp_out.best).  The host
- * variant derives both (the second from BT2X_OPT_EXACT_BEST). */
+ * BT2X_DPL_EXACT_BEST for exact best of failed problems (bt2x_dp_out.best),
+ * BT2X_DPL_REF_TEXT when any problem carries BT2X_DP_REF_TEXT (its window is cut from the
+ * index first, inside the BT2X_K_DP events).  The host variant derives all three (the
+ * second from BT2X_OPT_EXACT_BEST). */
 #define BT2X_DPL_I16 1u
 #define BT2X_DPL_EXACT_BEST 2u
+#define BT2X_DPL_REF_TEXT 4u     /* some problem is BT2X_DP_REF_TEXT */
 int bt2x_dp_align_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const uint8_t* d_quals,
                       const uint8_t* d_refs, const bt2x_dp_in* d_in, uint32_t n,
                       bt2x_dp_out* d_out, bt2x_aln_rec* d_recs, uint32_t rec_cap,
@@ -300,6 +308,12 @@ int bt2x_dp_align_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const uint8_t* d_qu
  * reads it (bowtie2 prints it only under --mapq-extra). */
 enum { BT2X_OPT_EXACT_BEST = 1 };
 int bt2x_set_option(bt2x_ctx* ctx, int option, int64_t value);
+
+/* What the context can do: BT2X_CAP_REF_TEXT -- DP problems may name their window
+ * (BT2X_DP_REF_TEXT); needs the joined text resident, i.e. an index loaded with
+ * load_offs and a text of < 2^32 rows. */
+#define BT2X_CAP_REF_TEXT 1u
+int bt2x_capabilities(const bt2x_ctx* ctx, uint32_t* caps);
 
 /* Order-independent digest of one matrix cell (shared by oracle, kernel and harness). */
 static inline uint64_t bt2x_cell_digest(uint32_t row, uint32_t col, uint32_t mat, uint32_t val) {

@@ -17,7 +17,9 @@ DP_IN = np.dtype([("read_off", "<u8"), ("qual_off", "<u8"), ("ref_off", "<u8"),
                   ("nceil", "<i2"), ("triml", "<u2"), ("corel", "<u2"), ("corer", "<u2"),
                   ("fw", "u1"), ("flags", "u1")], align=True)
 DP_I16 = 1                  # bt2x_dp_in.flags: the reference's signed 16-bit DP (--no-sse8)
-DPL_I16, DPL_EXACT_BEST = 1, 2
+DP_REF_TEXT = 2             # bt2x_dp_in.flags: window cut from the index (ref_off = text id)
+DPL_I16, DPL_EXACT_BEST, DPL_REF_TEXT = 1, 2, 4
+CAP_REF_TEXT = 1            # bt2x_capabilities
 OPT_EXACT_BEST = 1
 DP_OUT = np.dtype([("status", "<i4"), ("best", "<i4"), ("ncand", "<u2"), ("nrec", "<u2"),
                    ("rec_off", "<u4")], align=True)

@@ -45,6 +45,7 @@ FUNCS = {
                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                          ctypes.POINTER(abi.DpDebug), ctypes.c_uint32, ctypes.c_void_p]),
     "bt2x_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
+    "bt2x_capabilities": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "bt2x_resolve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
                                     ctypes.c_void_p]),
     "bt2x_resolve_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
@@ -196,10 +197,17 @@ class Context:
     def dp_align_dev(self, d_reads, d_quals, d_refs, d_in, n, d_out, d_recs, rec_cap, d_edits,
                      edit_cap, d_counters, stream=0, launch_flags=0):
         """bt2x_dp_align_dev; launch_flags: abi.DPL_I16 (some problem is BT2X_DP_I16),
-        abi.DPL_EXACT_BEST (exact best of failed problems).  d_counters: 4 x u32."""
+        abi.DPL_EXACT_BEST (exact best of failed problems), abi.DPL_REF_TEXT (some problem
+        is BT2X_DP_REF_TEXT).  d_counters: 4 x u32."""
         check(load().bt2x_dp_align_dev(self.h, d_reads, d_quals, d_refs, d_in, n, d_out, d_recs,
                                        rec_cap, d_edits, edit_cap, d_counters, None, launch_flags, stream),
               "bt2x_dp_align_dev")
+
+    def capabilities(self) -> int:
+        """bt2x_capabilities: abi.CAP_* bits."""
+        caps = ctypes.c_uint32(0)
+        check(load().bt2x_capabilities(self.h, ctypes.byref(caps)), "bt2x_capabilities")
+        return int(caps.value)
 
     def set_option(self, option: int, value: int) -> None:
         check(load().bt2x_set_option(self.h, option, int(value)), "bt2x_set_option")

@@ -150,6 +150,7 @@ struct bt2x_ctx {
 	~bt2x_ctx();
 	int device = 0;
 	hipStream_t stream = nullptr;
+	hipEvent_t sync_ev = nullptr;              // blocking-sync event: host waits sleep, not spin
 	hipEvent_t ev[BT2X_K_COUNT][2] = {};
 	bool ev_valid[BT2X_K_COUNT] = {};
 	DevIndex ix{};
@@ -162,7 +163,8 @@ struct bt2x_ctx {
 	// to resolve, per-lane workspace)
 	DevBuf b_rin, b_exr, b_rout, b_sats, b_elts, b_exro, b_used, b_sout, b_rows, b_ws, b_jobs, b_ranges, b_rcnt;
 	const uint32_t* d_resolve_n = nullptr;     // element count of the last round's resolve (HBM)
-	DevBuf scratch, b_fail;
+	DevBuf scratch, b_fail, b_in2, b_win;         // + DP windows cut from the text (BT2X_DP_REF_TEXT)
+	uint64_t npat = 0;
 	bool exact_best = true;                    // BT2X_OPT_EXACT_BEST
 	int ncu = 0;
 	uint32_t chunk_groups = 16384;             // DP chunk: 1 Mi problems, ~34 GB of traceback bytes
@@ -177,6 +179,7 @@ bt2x_ctx::~bt2x_ctx() {
 	(void)hipSetDevice(device);
 	if(stream) (void)hipStreamSynchronize(stream);
 	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch, &b_fail,
+	                 &b_in2, &b_win,
 	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws,
 	                 &b_jobs, &b_ranges, &b_rcnt})
 		b->release();
@@ -185,7 +188,21 @@ bt2x_ctx::~bt2x_ctx() {
 		if(p) (void)hipFree(p);
 	for(int k = 0; k < BT2X_K_COUNT; k++)
 		for(int j = 0; j < 2; j++) if(ev[k][j]) (void)hipEventDestroy(ev[k][j]);
+	if(sync_ev) (void)hipEventDestroy(sync_ev);
 	if(stream) (void)hipStreamDestroy(stream);
+}
+
+namespace {
+// Wait for the context's stream.  The host-pointer entry points are called from a driver
+// thread that shares the CPUs with the host's per-read work: the wait blocks on an event
+// (hipEventBlockingSync) instead of spinning in hipStreamSynchronize (BT2X_SPIN_WAIT=1
+// restores that).
+hipError_t stream_wait(bt2x_ctx* c) {
+	static const bool spin = [] { const char* e = getenv("BT2X_SPIN_WAIT"); return e && e[0] == '1'; }();
+	if(spin || !c->sync_ev) return hipStreamSynchronize(c->stream);
+	hipError_t e = hipEventRecord(c->sync_ev, c->stream);
+	return e != hipSuccess ? e : hipEventSynchronize(c->sync_ev);
+}
 }
 
 namespace {
@@ -221,6 +238,7 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	c->device = device;
 	HIPCHK(hipSetDevice(device));
 	HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	HIPCHK(hipEventCreateWithFlags(&c->sync_ev, hipEventBlockingSync | hipEventDisableTiming));
 	for(int k = 0; k < BT2X_K_COUNT; k++) {
 		HIPCHK(hipEventCreate(&c->ev[k][0]));
 		HIPCHK(hipEventCreate(&c->ev[k][1]));
@@ -282,6 +300,7 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	// SA resolution (bt2x_resolve): fragment table always; the SA sample only when no
 	// full SA was built (the resolve kernel then walks LF to it, as GroupWalk does)
 	c->ix.offs = nullptr; c->ix.rstarts = nullptr; c->ix.plen = nullptr; c->ix.nfrag = idx->nfrag;
+	c->npat = idx->npat;
 	if(idx->nfrag && idx->rstarts && idx->plen && idx->npat) {
 		HIPCHK(hipMalloc(&c->d_rstarts, 24 * idx->nfrag));
 		HIPCHK(hipMemcpy(c->d_rstarts, idx->rstarts, 24 * idx->nfrag, hipMemcpyHostToDevice));
@@ -414,7 +433,7 @@ extern "C" int bt2x_seed_search(bt2x_ctx* c, const uint8_t* reads, uint64_t read
 	                          do_extend, (bt2x_seed_out*)c->b_out.p, c->stream);
 	if(rc) return rc;
 	HIPCHK(hipMemcpyAsync(out, c->b_out.p, sizeof(bt2x_seed_out) * n, hipMemcpyDeviceToHost, c->stream));
-	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(stream_wait(c));
 	return BT2X_OK;
 }
 
@@ -458,11 +477,26 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	a.wide = (launch_flags & BT2X_DPL_I16) ? 1u : 0u;
 	a.fail_list = exact ? (uint32_t*)c->b_fail.p : nullptr;
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
+	if(launch_flags & BT2X_DPL_REF_TEXT) {
+		if(!c->ix.text || !c->ix.rstarts) return BT2X_E_ARG;
+		if((rc = c->b_in2.ensure(sizeof(bt2x_dp_in) * (size_t)(n ? n : 1))) ||
+		   (rc = c->b_win.ensure((size_t)BT2X_MAX_COLS * (n ? n : 1))))
+			return rc;
+		if((rc = bt2x_launch_windows(c->ix, d_in, n, d_refs, (bt2x_dp_in*)c->b_in2.p, (uint8_t*)c->b_win.p, s))) return rc;
+		a.in = (const bt2x_dp_in*)c->b_in2.p;
+		a.refs = (const uint8_t*)c->b_win.p;
+	}
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));
 	c->ev_valid[BT2X_K_DP] = true;
 	c->n_dp_last = n;
 	return rc;
+}
+
+extern "C" int bt2x_capabilities(const bt2x_ctx* c, uint32_t* caps) {
+	if(!c || !caps) return BT2X_E_ARG;
+	*caps = (c->ix.text && c->ix.rstarts) ? BT2X_CAP_REF_TEXT : 0u;
+	return BT2X_OK;
 }
 
 extern "C" int bt2x_dp_align(bt2x_ctx* c,
@@ -474,27 +508,29 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
                              bt2x_aln_rec* recs, uint32_t rec_cap, uint32_t* nrec_used,
                              uint32_t* edits, uint32_t edit_cap, uint32_t* nedit_used,
                              bt2x_dp_debug* debug) {
-	if(!c || (n && (!reads || !quals || !refs || !in || !out))) return BT2X_E_ARG;
+	if(!c || (n && (!reads || !quals || (!refs && refs_bytes) || !in || !out))) return BT2X_E_ARG;
 	if(nrec_used) *nrec_used = 0;
 	if(nedit_used) *nedit_used = 0;
 	if(n == 0) return BT2X_OK;
 	// shape checks: the kernel trusts these (reference limits; the u8 kernel's
 	// minsc floor, aligner_sw.cpp:77-83)
 	uint32_t launch_flags = c->exact_best ? BT2X_DPL_EXACT_BEST : 0u;
+	const bool can_text = c->ix.text && c->ix.rstarts;
 	for(uint32_t i = 0; i < n; i++) {
 		const bt2x_dp_in& p = in[i];
-		const bool i16 = (p.flags & BT2X_DP_I16) != 0;
+		const bool i16 = (p.flags & BT2X_DP_I16) != 0, text = (p.flags & BT2X_DP_REF_TEXT) != 0;
 		if(p.rdlen < 1 || p.rdlen > BT2X_MAX_ROWS || p.ncol < 1 || p.ncol + 1 > BT2X_MAX_COLS ||
 		   p.read_off + p.rdlen > reads_bytes || p.qual_off + p.rdlen > quals_bytes ||
-		   p.ref_off + p.ncol > refs_bytes || p.minsc < (i16 ? -32767 : -254) || p.minsc > 0 ||
-		   (p.flags & ~BT2X_DP_I16) != 0)
+		   (text ? (!can_text || p.ref_off >= c->npat) : p.ref_off + p.ncol > refs_bytes) ||
+		   p.minsc < (i16 ? -32767 : -254) || p.minsc > 0 || (p.flags & ~(BT2X_DP_I16 | BT2X_DP_REF_TEXT)) != 0)
 			return BT2X_E_ARG;
 		if(i16) launch_flags |= BT2X_DPL_I16;
+		if(text) launch_flags |= BT2X_DPL_REF_TEXT;
 	}
 	HIPCHK(hipSetDevice(c->device));
 	int rc;
 	if((rc = c->b_reads.ensure(reads_bytes)) || (rc = c->b_quals.ensure(quals_bytes)) ||
-	   (rc = c->b_refs.ensure(refs_bytes)) || (rc = c->b_in.ensure(sizeof(bt2x_dp_in) * n)) ||
+	   (rc = c->b_refs.ensure(refs_bytes ? refs_bytes : 1)) || (rc = c->b_in.ensure(sizeof(bt2x_dp_in) * n)) ||
 	   (rc = c->b_out.ensure(sizeof(bt2x_dp_out) * n)) ||
 	   (rc = c->b_recs.ensure(sizeof(bt2x_aln_rec) * (size_t)(rec_cap ? rec_cap : 1))) ||
 	   (rc = c->b_edits.ensure(sizeof(uint32_t) * (size_t)(edit_cap ? edit_cap : 1)))) return rc;
@@ -509,7 +545,7 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
 	}
 	HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
 	HIPCHK(hipMemcpyAsync(c->b_quals.p, quals, quals_bytes, hipMemcpyHostToDevice, c->stream));
-	HIPCHK(hipMemcpyAsync(c->b_refs.p, refs, refs_bytes, hipMemcpyHostToDevice, c->stream));
+	if(refs_bytes) HIPCHK(hipMemcpyAsync(c->b_refs.p, refs, refs_bytes, hipMemcpyHostToDevice, c->stream));
 	HIPCHK(hipMemcpyAsync(c->b_in.p, in, sizeof(bt2x_dp_in) * n, hipMemcpyHostToDevice, c->stream));
 	rc = bt2x_dp_align_dev(c, (const uint8_t*)c->b_reads.p, (const uint8_t*)c->b_quals.p,
 	                       (const uint8_t*)c->b_refs.p, (const bt2x_dp_in*)c->b_in.p, n,
@@ -520,15 +556,16 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
 	uint32_t used[4] = {0, 0, 0, 0};
 	HIPCHK(hipMemcpyAsync(used, c->d_counters, sizeof used, hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(hipMemcpyAsync(out, c->b_out.p, sizeof(bt2x_dp_out) * n, hipMemcpyDeviceToHost, c->stream));
-	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(stream_wait(c));
 	if(nrec_used) *nrec_used = used[0];
 	if(nedit_used) *nedit_used = used[1];
 	if(used[3]) return BT2X_E_ARG;                            // cannot happen: launch_flags cover in[]
 	if(used[0] > rec_cap || used[1] > edit_cap) return BT2X_E_OVERFLOW;
-	if(used[0]) HIPCHK(hipMemcpy(recs, c->b_recs.p, sizeof(bt2x_aln_rec) * used[0], hipMemcpyDeviceToHost));
-	if(used[1]) HIPCHK(hipMemcpy(edits, c->b_edits.p, sizeof(uint32_t) * used[1], hipMemcpyDeviceToHost));
-	if(dd.digests) HIPCHK(hipMemcpy(debug->digests, dd.digests, sizeof(uint64_t) * 3 * n, hipMemcpyDeviceToHost));
-	if(dd.cands) HIPCHK(hipMemcpy(debug->cands, dd.cands, sizeof(uint32_t) * BT2X_MAX_COLS * n, hipMemcpyDeviceToHost));
+	if(used[0]) HIPCHK(hipMemcpyAsync(recs, c->b_recs.p, sizeof(bt2x_aln_rec) * used[0], hipMemcpyDeviceToHost, c->stream));
+	if(used[1]) HIPCHK(hipMemcpyAsync(edits, c->b_edits.p, sizeof(uint32_t) * used[1], hipMemcpyDeviceToHost, c->stream));
+	if(dd.digests) HIPCHK(hipMemcpyAsync(debug->digests, dd.digests, sizeof(uint64_t) * 3 * n, hipMemcpyDeviceToHost, c->stream));
+	if(dd.cands) HIPCHK(hipMemcpyAsync(debug->cands, dd.cands, sizeof(uint32_t) * BT2X_MAX_COLS * n, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(stream_wait(c));
 	return BT2X_OK;
 }
 
@@ -671,12 +708,12 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 	if(rc) return rc;
 	HIPCHK(hipMemcpyAsync(used, c->b_used.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(hipMemcpyAsync(out, c->b_rout.p, sizeof(bt2x_round_out) * nreads, hipMemcpyDeviceToHost, c->stream));
-	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(stream_wait(c));
 	if(used[0] > sat_cap || used[1] > elt_cap || used[2] > exr_cap) return BT2X_E_OVERFLOW;
 	if(used[0]) HIPCHK(hipMemcpyAsync(sats, c->b_sats.p, sizeof(bt2x_sat) * used[0], hipMemcpyDeviceToHost, c->stream));
 	if(used[1]) HIPCHK(hipMemcpyAsync(elts, c->b_elts.p, sizeof(bt2x_resolve_out) * used[1], hipMemcpyDeviceToHost, c->stream));
 	if(used[2]) HIPCHK(hipMemcpyAsync(exr_out, c->b_exro.p, sizeof(bt2x_exrange) * used[2], hipMemcpyDeviceToHost, c->stream));
-	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(stream_wait(c));
 	return BT2X_OK;
 }
 
@@ -695,6 +732,6 @@ extern "C" int bt2x_resolve(bt2x_ctx* c, const bt2x_resolve_in* in, uint32_t n, 
 	                      (bt2x_resolve_out*)c->b_out.p, c->stream);
 	if(rc) return rc;
 	HIPCHK(hipMemcpyAsync(out, c->b_out.p, sizeof(bt2x_resolve_out) * n, hipMemcpyDeviceToHost, c->stream));
-	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(stream_wait(c));
 	return BT2X_OK;
 }

@@ -52,6 +52,11 @@ int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_
 int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
                            int reject, bt2x_resolve_out* d_out, unsigned long long* d_ctr, int ncu, void* stream);
 
+// DP windows cut from the resident text (window_kernel.hip): every problem's window to
+// win[i * BT2X_MAX_COLS ..), its dp_in to out[i] with ref_off rebased and the flag cleared.
+int bt2x_launch_windows(const DevIndex& ix, const bt2x_dp_in* d_in, uint32_t n, const uint8_t* d_refs,
+                        bt2x_dp_in* d_out, uint8_t* d_win, void* stream);
+
 // Seed round (round_kernel.hip): per read, finalize + rank + prioritize after its seed
 // search; sats/rows/exr_out allocated by atomics on counters[0..2].
 struct RoundLaunch {

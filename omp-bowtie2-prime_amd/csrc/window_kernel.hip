@@ -1,0 +1,88 @@
+// window_kernel.hip — DP reference windows cut from the resident index (gfx950).
+//
+// SwAligner::initRef fetches each rectangle's reference characters with
+// BitPairReference::getStretch (aligner_sw.cpp:117-229, reference.cpp:484-611): the
+// window [refl, refl + ncol) of text tidx, N (4) outside the text and in its N runs.
+// A problem flagged BT2X_DP_REF_TEXT names (tidx = ref_off, refl, ncol) instead of
+// carrying the bytes; this kernel cuts the window from the joined text the context keeps
+// in HBM (16 bases per u32, LSB-first) through the fragment table (rstarts: joined
+// offset, text id, text offset per maximal non-N stretch, in joined order), so the host
+// never touches the 0.8 GB packed text and the windows never cross PCIe.
+//
+// One wave per problem, one output byte per lane and step; every problem's window goes to
+// its slot of BT2X_MAX_COLS bytes in `win`, and its dp_in to `out` with ref_off = the
+// slot (unflagged problems are copied from `refs`), so the DP kernels run unchanged.
+// HBM-bound: per problem ~ncol/4 bytes of packed text read, ncol bytes written.
+#include <hip/hip_runtime.h>
+
+#include "bt2x_device.h"
+
+namespace {
+
+// last fragment k in [lo, hi) with toff_k <= off (lo - 1 if none); fragments of one text
+// are in text order
+__device__ __forceinline__ int64_t frag_at(const uint64_t* rs, int64_t lo, int64_t hi, int64_t off) {
+	int64_t a = lo, b = hi;                     // answer in [lo - 1, hi)
+	while(a < b) {
+		const int64_t m = (a + b) >> 1;
+		if((int64_t)rs[3 * m + 2] <= off) a = m + 1; else b = m;
+	}
+	return a - 1;
+}
+
+// first fragment k with tidx_k >= t
+__device__ __forceinline__ int64_t frag_text_lb(const uint64_t* rs, int64_t nfrag, uint64_t t) {
+	int64_t a = 0, b = nfrag;
+	while(a < b) {
+		const int64_t m = (a + b) >> 1;
+		if(rs[3 * m + 1] < t) a = m + 1; else b = m;
+	}
+	return a;
+}
+
+__global__ void __launch_bounds__(256) window_kernel(DevIndex ix, const bt2x_dp_in* __restrict__ in, uint32_t n,
+                                                     const uint8_t* __restrict__ refs, bt2x_dp_in* __restrict__ out,
+                                                     uint8_t* __restrict__ win) {
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+	if(i >= n) return;
+	bt2x_dp_in p = in[i];
+	uint8_t* w = win + (size_t)i * BT2X_MAX_COLS;
+	const uint32_t ncol = p.ncol;
+	if(p.flags & BT2X_DP_REF_TEXT) {
+		const uint64_t t = p.ref_off;
+		const int64_t nfrag = (int64_t)ix.nfrag;
+		const int64_t lo = frag_text_lb(ix.rstarts, nfrag, t), hi = frag_text_lb(ix.rstarts, nfrag, t + 1);
+		for(uint32_t c = lane; c < ncol; c += 64u) {
+			const int64_t off = p.refl + (int64_t)c;
+			uint8_t code = 4;
+			// the last non-empty fragment starting at or before off (RefInfo::stretch's rule)
+			for(int64_t k = frag_at(ix.rstarts, lo, hi, off); k >= lo; k--) {
+				const uint64_t joff = ix.rstarts[3 * k], toff = ix.rstarts[3 * k + 2];
+				const uint64_t jend = k + 1 < nfrag ? ix.rstarts[3 * (k + 1)] : ix.len;
+				if(jend == joff) continue;
+				const uint64_t j = joff + (uint64_t)(off - (int64_t)toff);
+				if(j < jend) code = (uint8_t)((ix.text[j >> 4] >> ((j & 15u) << 1)) & 3u);
+				break;
+			}
+			w[c] = code;
+		}
+	} else {
+		for(uint32_t c = lane; c < ncol; c += 64u) w[c] = refs[p.ref_off + c];
+	}
+	if(lane == 0) {
+		p.ref_off = (uint64_t)i * BT2X_MAX_COLS;
+		p.flags &= (uint8_t)~BT2X_DP_REF_TEXT;
+		out[i] = p;
+	}
+}
+
+} // namespace
+
+int bt2x_launch_windows(const DevIndex& ix, const bt2x_dp_in* d_in, uint32_t n, const uint8_t* d_refs,
+                        bt2x_dp_in* d_out, uint8_t* d_win, void* stream) {
+	if(n == 0) return BT2X_OK;
+	hipLaunchKernelGGL(window_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, ix, d_in, n, d_refs, d_out,
+	                   d_win);
+	return hipGetLastError() == hipSuccess ? BT2X_OK : BT2X_E_NODEVICE;
+}

@@ -1025,6 +1025,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 	const long n = (long)cohort.size();
 	const long nch = (n + kChunk - 1) / kChunk;
 	if((long)L.chunks.size() < nch) L.chunks.resize((size_t)nch);
+	const bool ref_index = be_.ref_from_index();
 	PH_START();
 	pool().parallel_for(nch, 1, [&](long ch) {
 		Launch::Chunk& C = L.chunks[(size_t)ch];
@@ -1039,7 +1040,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 				C.wr.push_back(c); C.nres += c->res_in.size();
 			} else if(c->req == REQ_DP) {
 				C.wd.push_back(c); C.dbytes += 2 * c->rd.length(); C.nprob += c->dps.size();
-				for(const DpWork& d : c->dps) C.rbytes += d.key.ncol;
+				if(!ref_index) for(const DpWork& d : c->dps) C.rbytes += d.key.ncol;
 			} else if(c->req == REQ_ROUND) {
 				C.wn.push_back(c); C.nbytes += 2 * c->rd.length(); C.nnseed += c->seed_in.size();
 				C.nexr += c->exRange.size();
@@ -1107,11 +1108,16 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			for(const DpWork& d : c->dps) {
 				bt2x_dp_in q = d.in;
 				q.read_off = q.qual_off = dbo + (d.key.fw ? 0 : len);
-				q.ref_off = rbo;
 				L.fb[pko] = rbo;
-				ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, L.dp_refs.data() + rbo);
+				if(ref_index) {                          // the backend cuts the window from the index
+					q.ref_off = (uint64_t)d.key.tidx;
+					q.flags |= BT2X_DP_REF_TEXT;
+				} else {
+					q.ref_off = rbo;
+					ref_.stretch((uint32_t)d.key.tidx, d.key.refl, d.key.ncol, L.dp_refs.data() + rbo);
+					rbo += d.key.ncol;
+				}
 				L.dp_in[pko++] = q;
-				rbo += d.key.ncol;
 			}
 			dbo += 2 * len;
 		}
@@ -1292,77 +1298,128 @@ private:
 	uint64_t base_ = 0;
 };
 
-// SAM output off the scheduler's thread: records are appended to 4 MiB chunks that a
-// writer thread fwrites in order.
-class SamWriter {
+// SAM output off the scheduler's thread, in input order: finished records are put into a
+// ring by read id (from the pool's threads, for ids the scheduler reserved), and a writer
+// thread moves the ready prefix into 4 MiB chunks and fwrites them.  The ring only grows
+// in reserve(), on the scheduler's thread, under the lock the writer holds while it
+// drains.
+class OrderedSamWriter {
 public:
-	explicit SamWriter(std::FILE* f) : f_(f), th_([this] { loop(); }) { cur_.reserve(kChunk + 4096); }
-	~SamWriter() { finish(); }
-	void append(const std::string& rec) {
-		cur_ += rec;
-		if(cur_.size() >= kChunk) flush();
+	explicit OrderedSamWriter(std::FILE* f) : f_(f) {
+		grow(1 << 16);
+		th_ = std::thread([this] { loop(); });
 	}
+	~OrderedSamWriter() { finish(); }
+	void reserve(uint64_t end) {                       // scheduler thread
+		if(end - base_.load(std::memory_order_acquire) <= cap_) return;
+		std::lock_guard<std::mutex> g(mu_);
+		size_t cap = cap_;
+		while(end - base_.load(std::memory_order_relaxed) > cap) cap *= 2;
+		if(cap != cap_) grow(cap);
+	}
+	void put(uint64_t id, std::string& rec) {          // any thread
+		const size_t k = id & (cap_ - 1);
+		slot_[k].swap(rec);
+		rec.clear();
+		ready_[k].store(1, std::memory_order_release);
+	}
+	void kick() {
+		{ std::lock_guard<std::mutex> g(mu_); kicked_ = true; }
+		cv_.notify_one();
+	}
+	uint64_t written() const { return base_.load(std::memory_order_acquire); }
 	void finish() {
 		if(!th_.joinable()) return;
-		flush();
 		{ std::lock_guard<std::mutex> g(mu_); stop_ = true; }
-		cv_.notify_all();
+		cv_.notify_one();
 		th_.join();
 	}
 private:
 	static constexpr size_t kChunk = 4u << 20;
-	void flush() {
-		if(cur_.empty()) return;
-		std::string next;
-		{
-			std::unique_lock<std::mutex> g(mu_);
-			full_.push_back(std::move(cur_));
-			if(!spare_.empty()) { next = std::move(spare_.back()); spare_.pop_back(); }
+	void grow(size_t cap) {                            // (lock held, or before the thread starts)
+		std::vector<std::string> s(cap);
+		std::unique_ptr<std::atomic<uint8_t>[]> r(new std::atomic<uint8_t>[cap]);
+		for(size_t i = 0; i < cap; i++) r[i].store(0, std::memory_order_relaxed);
+		const uint64_t b = base_.load(std::memory_order_relaxed);
+		for(uint64_t id = b; cap_ && id < b + cap_; id++) {
+			s[id & (cap - 1)].swap(slot_[id & (cap_ - 1)]);
+			r[id & (cap - 1)].store(ready_[id & (cap_ - 1)].load(std::memory_order_acquire), std::memory_order_relaxed);
 		}
-		cv_.notify_all();
-		cur_ = std::move(next);
-		cur_.clear();
-		cur_.reserve(kChunk + 4096);
+		slot_.swap(s);
+		ready_.swap(r);
+		cap_ = cap;
+	}
+	// moves the ready prefix (at most one chunk) into `chunk`; true if it stopped on a full chunk
+	bool drain(std::string& chunk) {
+		std::lock_guard<std::mutex> g(mu_);
+		uint64_t b = base_.load(std::memory_order_relaxed);
+		for(;;) {
+			const size_t k = b & (cap_ - 1);
+			if(!ready_[k].load(std::memory_order_acquire)) break;
+			chunk += slot_[k];
+			slot_[k].clear();
+			ready_[k].store(0, std::memory_order_relaxed);
+			base_.store(++b, std::memory_order_release);
+			if(chunk.size() >= kChunk) return true;
+		}
+		return false;
 	}
 	void loop() {
+		std::string chunk;
+		chunk.reserve(kChunk + 4096);
 		for(;;) {
-			std::string buf;
+			bool stop;
 			{
 				std::unique_lock<std::mutex> g(mu_);
-				cv_.wait(g, [&] { return stop_ || !full_.empty(); });
-				if(full_.empty()) return;
-				buf = std::move(full_.front());
-				full_.pop_front();
+				cv_.wait(g, [&] { return stop_ || kicked_; });
+				kicked_ = false;
+				stop = stop_;
 			}
-			std::fwrite(buf.data(), 1, buf.size(), f_);
-			buf.clear();
-			std::lock_guard<std::mutex> g(mu_);
-			if(spare_.size() < 4) spare_.push_back(std::move(buf));
+			bool full;
+			do {
+				full = drain(chunk);
+				if(full || (stop && !chunk.empty())) {
+					std::fwrite(chunk.data(), 1, chunk.size(), f_);
+					chunk.clear();
+				}
+			} while(full);
+			if(stop) return;
 		}
 	}
 	std::FILE* f_;
-	std::string cur_;
+	std::vector<std::string> slot_;
+	std::unique_ptr<std::atomic<uint8_t>[]> ready_;
+	size_t cap_ = 0;
+	std::atomic<uint64_t> base_{0};
 	std::mutex mu_;
 	std::condition_variable cv_;
-	std::deque<std::string> full_;
-	std::vector<std::string> spare_;
-	bool stop_ = false;
+	bool kicked_ = false, stop_ = false;
 	std::thread th_;
 };
 
-void count(RunStats& st, const ReadCtx* c) {
-	st.reads++;
-	if(c->aligned) st.aligned++; else st.unaligned++;
-	if(c->repetitive) st.rep++;
-	using M = ReportingMetrics;
-	st.met.v[M::NREAD]++;
-	st.met.v[M::NUNPAIRED]++;
-	static constexpr int kind_field[4] = {M::NUNP_0, M::NUNP_UNI1, M::NUNP_UNI2, M::NUNP_REP};
-	st.met.v[kind_field[c->met_kind]]++;
-	if(c->met_kind == 1 || c->met_kind == 2) st.met.v[M::NUNP_UNI]++;
-	st.dps_used += c->ndp_used;
-	st.tight_recs += c->ntight;
-}
+// The per-read counters retire() adds up (RunStats' share of them).
+struct RetireAcc {
+	uint64_t reads = 0, aligned = 0, unaligned = 0, rep = 0, dps_used = 0, tight_recs = 0;
+	ReportingMetrics met;
+	void count(const ReadCtx* c) {
+		reads++;
+		if(c->aligned) aligned++; else unaligned++;
+		if(c->repetitive) rep++;
+		using M = ReportingMetrics;
+		met.v[M::NREAD]++;
+		met.v[M::NUNPAIRED]++;
+		static constexpr int kind_field[4] = {M::NUNP_0, M::NUNP_UNI1, M::NUNP_UNI2, M::NUNP_REP};
+		met.v[kind_field[c->met_kind]]++;
+		if(c->met_kind == 1 || c->met_kind == 2) met.v[M::NUNP_UNI]++;
+		dps_used += c->ndp_used;
+		tight_recs += c->ntight;
+	}
+	void into(RunStats& st) const {
+		st.reads += reads; st.aligned += aligned; st.unaligned += unaligned; st.rep += rep;
+		st.dps_used += dps_used; st.tight_recs += tight_recs;
+		st.met.merge(met);
+	}
+};
 }
 
 WorkPool& Aligner::pool() { return *pool_; }
@@ -1387,19 +1444,29 @@ Aligner::~Aligner() {
 	if(pool_) pool().parallel_for(n, 256, [&](long i) { ctxs_[(size_t)i].reset(); });
 }
 
-// Retire the finished reads of `act` (their records go to the ring, their contexts back
-// to the pool); the others stay in `act`.
-void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, void* ringp) {
-	OutRing& ring = *static_cast<OutRing*>(ringp);
+// Retire the finished reads of `act` (their records go to `put`, their contexts back to
+// the pool); the others stay in `act`.  Parallel over 1024-read chunks, each with its own
+// counters; then a serial compaction.
+void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, const std::function<void(uint64_t, std::string&)>& put) {
+	const long n = (long)act.size(), nch = (n + 1023) / 1024;
+	std::vector<RetireAcc> acc((size_t)nch);
+	pool().parallel_for(nch, 1, [&](long ch) {
+		RetireAcc& a = acc[(size_t)ch];
+		for(long i = ch * 1024; i < std::min(n, (ch + 1) * 1024); i++) {
+			ReadCtx* c = act[(size_t)i];
+			if(!c->done) continue;
+			c->task.h.destroy();
+			c->task.h = nullptr;
+			a.count(c);
+			if(!c->warn.empty()) std::fputs(c->warn.c_str(), stderr);
+			put(c->rd.rdid, c->sam);
+		}
+	});
+	for(const RetireAcc& a : acc) a.into(st);
 	size_t w = 0;
 	for(ReadCtx* c : act) {
 		if(c->done) {
-			c->task.h.destroy();
-			c->task.h = nullptr;
 			c->done = false;
-			count(st, c);
-			if(!c->warn.empty()) std::fputs(c->warn.c_str(), stderr);
-			ring.put(c->rd.rdid, c->sam);
 			free_.push_back(c);
 		} else {
 			act[w++] = c;
@@ -1451,9 +1518,8 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	bool eof = false;
 	std::vector<FastqReader::Raw> raw;
 	std::vector<ReadCtx*> fresh;
-	OutRing ring;
-	SamWriter writer(out);
-	uint64_t written = 0;
+	OrderedSamWriter writer(out);
+	const auto put = [&writer](uint64_t id, std::string& rec) { writer.put(id, rec); };
 	if(slots < 2) slots = 2;
 	reserve_launch_buffers(pipeline_ ? slots / 2 : slots);
 	// New reads join cohort `co` (up to `cap` reads in it): decoded and run up to their
@@ -1471,7 +1537,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		t0 = now_s();
 		fresh.resize((size_t)nf);
 		for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
-		ring.reserve(rdid + (uint64_t)nf);
+		writer.reserve(rdid + (uint64_t)nf);
 		st.t_alloc += now_s() - t0;
 		pool().parallel_for(nf, 64, [&](long i) {
 			ReadCtx* c = fresh[(size_t)i];
@@ -1485,10 +1551,11 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	};
 	auto retire_write = [&](std::vector<ReadCtx*>& co) {
 		const double t0 = now_s();
-		retire(co, st, &ring);
+		retire(co, st, put);
 		const double t1 = now_s();
-		ring.drain([&](const std::string& s) { writer.append(s); written++; });
-		// input files whose last record is now out
+		writer.kick();
+		// input files whose last record is out
+		const uint64_t written = writer.written();
 		while(st.t_files.size() < fq.files_done() && fq.file_end(st.t_files.size()) <= written)
 			st.t_files.push_back(now_s() - t_start);
 		st.t_io += now_s() - t0;
@@ -1586,7 +1653,7 @@ std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threa
 		act.insert(act.end(), fresh.begin(), fresh.end());
 		if(act.empty()) break;
 		step(act, st);
-		retire(act, st, &ring);
+		retire(act, st, [&ring](uint64_t id, std::string& rec) { ring.put(id, rec); });
 		ring.drain([&](const std::string& s) { out += s; });
 	}
 	if(stp) *stp = st;

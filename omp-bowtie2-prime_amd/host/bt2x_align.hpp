@@ -52,6 +52,7 @@
 #include <stdexcept>
 #include <string>
 #include <utility>
+#include <functional>
 #include <vector>
 
 #include "bt2x.h"
@@ -948,6 +949,9 @@ public:
 	                        const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr,
 	                        uint32_t maxelt, HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats,
 	                        HostVec<bt2x_resolve_out>& elts, HostVec<bt2x_exrange>& exr_out) = 0;
+	// true: DP problems name their reference window (BT2X_DP_REF_TEXT: ref_off = tidx) and
+	// the backend cuts it from the index; false: the driver fills refs (RefInfo::stretch)
+	virtual bool ref_from_index() const { return false; }
 };
 
 // -------------------------------------------------------------------- driver
@@ -1044,7 +1048,9 @@ private:
 	Launch launch_[2];
 	bool pipeline_ = true, gpu_round_ = true, header_on_ = true;
 	ReadCtx* take_ctx();
-	void retire(std::vector<ReadCtx*>& act, RunStats& st, void* ring);
+	// put(id, record) takes a finished read's SAM record; it is called from the pool's
+	// threads, for distinct ids
+	void retire(std::vector<ReadCtx*>& act, RunStats& st, const std::function<void(uint64_t, std::string&)>& put);
 	// pooled read contexts (kept across runs; released by the destructor)
 	std::vector<std::unique_ptr<ReadCtx>> ctxs_;
 	std::vector<ReadCtx*> free_;

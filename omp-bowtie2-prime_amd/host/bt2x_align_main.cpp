@@ -78,7 +78,14 @@ private:
 // Product backend: every request kind is one bt2x C-ABI call on the context's GPU.
 class HipBackend : public Backend {
 public:
-	explicit HipBackend(bt2x_ctx* ctx) : ctx_(ctx) {}
+	explicit HipBackend(bt2x_ctx* ctx) : ctx_(ctx) {
+		uint32_t caps = 0;
+		bt2x::check(bt2x_capabilities(ctx, &caps), "bt2x_capabilities");
+		ref_text_ = (caps & BT2X_CAP_REF_TEXT) != 0 && !(std::getenv("BT2X_HOST_WINDOWS") && std::getenv("BT2X_HOST_WINDOWS")[0] == '1');
+	}
+	// DP windows cut on the GPU from the resident text (BT2X_DP_REF_TEXT), unless the
+	// context lacks it or BT2X_HOST_WINDOWS=1 asks for host-side windows
+	bool ref_from_index() const override { return ref_text_; }
 	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
 	                 HostVec<bt2x_seed_out>& out) override {
 		out.resize(in.size());
@@ -160,6 +167,7 @@ public:
 	} gs;
 private:
 	bt2x_ctx* ctx_;
+	bool ref_text_ = false;
 	double sat_per_read_ = 16, elt_per_read_ = 64;
 };
 
@@ -168,6 +176,7 @@ private:
 class DumpBackend : public Backend {
 public:
 	DumpBackend(Backend& inner, const std::string& dir) : in_(inner), dir_(dir) {}
+	bool ref_from_index() const override { return in_.ref_from_index(); }
 	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
 	                 HostVec<bt2x_seed_out>& out) override {
 		write("seed", {{reads.data(), reads.size()}, {in.data(), in.size() * sizeof(bt2x_seed_in)}});

@@ -9,6 +9,7 @@
 //
 //   test_e2e_oracle <index base> <reads.fq> [--dpad N] [--slots N] [-p T]
 #include <chrono>
+#include <csignal>
 #include <sys/resource.h>
 #include <cstdio>
 #include <cstdlib>
@@ -193,6 +194,7 @@ int main(int argc, char** argv) {
 		}
 		for(int rep = 0; rep < reps; rep++) {
 		rb.rewind();
+		if(std::getenv("SPROF_WAIT")) std::raise(SIGUSR2);   // tools/sprof.c: profile the replay only
 		// the timed run starts from an empty context pool, as bt2x-align does
 		Aligner al(p, ref, rb);
 		al.set_pipeline(pipeline);

@@ -123,6 +123,20 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     assert (out["status"] == 1).sum() > 20000
     assert (recs["nbuf"] > recs["nedit"]).sum() > 1000      # failed attempts' leftovers are exercised
 
+    # the same problems naming their windows (BT2X_DP_REF_TEXT: cut on the GPU from the
+    # resident joined text through the fragment table, N runs included): identical results
+    assert ctx.capabilities() & abi.CAP_REF_TEXT
+    dp2 = dp.copy()
+    dp2["ref_off"] = np.asarray(tidx, dtype=np.uint64)[np.nonzero(keep)[0]]
+    dp2["flags"] |= abi.DP_REF_TEXT
+    assert any((c == 4).any() for c in ref)                  # the fixture's N runs reach windows
+    out2, recs2, edits2, dig2, cands2 = ctx.dp_align(rd, qu, rf, dp2, debug=True)
+    np.testing.assert_array_equal(out2[["status", "best", "ncand", "nrec"]], eo[["status", "best", "ncand", "nrec"]])
+    np.testing.assert_array_equal(dig2, edig)
+    np.testing.assert_array_equal(cands2, ecands)
+    o3, r3, e3 = ctx.dp_align(rd, qu, np.zeros(0, np.uint8), dp2, debug=False)[:3]   # no refs at all
+    _compare_out(o3, eo, dp)
+
     # the production kernels without debug outputs: lane-per-problem and wave-per-problem
     # (the small-launch mode), every record and the whole edit-buffer image
     sel = np.arange(len(dp)) < 12000

@@ -55,8 +55,8 @@ def main():
     fq = os.path.join(wd, f"{tag}_r{args.reads}_L{args.read_len}.fq")
     if not os.path.exists(fq):
         genome, starts = sd.concat_genome(chroms)
-        reads, quals, _, _, _ = sd.sim_reads_fixed(genome, starts, args.reads, args.read_len, seed=3)
-        bench.write_fastq(fq, reads, quals)
+        reads, quals = sd.sim_reads_fast(genome, starts, args.reads, args.read_len, seed=3)
+        sd.write_fastq_fixed(fq, reads, quals)
     sam = os.path.join(wd, "out.sam")
     cmd = [args.driver, base, fq, "--host-timing", "-p", str(args.p),
            "--slots", str(args.slots), "--dpad", str(args.dpad)] + extra
