@@ -230,6 +230,31 @@ class Context:
               "bt2x_resolve_dev")
 
     # ------------------------------------------------------------ seed round
+    def seed_round(self, reads, seeds, inp, exr, maxelt, sat_cap=None, elt_cap=None, exr_cap=None):
+        """bt2x_seed_round (host buffers) -> (round_out, sats, elts, exr_out); arenas grown
+        and the call repeated once on BT2X_E_OVERFLOW."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        seeds = np.ascontiguousarray(seeds, dtype=abi.SEED_IN)
+        inp = np.ascontiguousarray(inp, dtype=abi.ROUND_IN)
+        exr = np.ascontiguousarray(exr if len(exr) else np.zeros(0, dtype=abi.EXRANGE), dtype=abi.EXRANGE)
+        n = len(inp)
+        sat_cap = sat_cap or 16 * n + 1024
+        elt_cap = elt_cap or 64 * n + 1024
+        exr_cap = exr_cap or 4 * n + 256
+        out = np.zeros(n, dtype=abi.ROUND_OUT)
+        sats = np.zeros(sat_cap, dtype=abi.SAT)
+        elts = np.zeros(elt_cap, dtype=abi.RESOLVE_OUT)
+        exro = np.zeros(exr_cap, dtype=abi.EXRANGE)
+        used = (ctypes.c_uint32 * 3)()
+        rc = load().bt2x_seed_round(self.h, abi.ptr(reads), reads.nbytes, abi.ptr(seeds), len(seeds), abi.ptr(inp), n,
+                                    abi.ptr(exr), len(exr), maxelt, abi.ptr(out), abi.ptr(sats), sat_cap,
+                                    abi.ptr(elts), elt_cap, abi.ptr(exro), exr_cap, used)
+        if rc == abi.E_OVERFLOW:
+            return self.seed_round(reads, seeds, inp, exr, maxelt, max(sat_cap, used[0]), max(elt_cap, used[1]),
+                                   max(exr_cap, used[2]))
+        check(rc, "bt2x_seed_round")
+        return out, sats[: used[0]], elts[: used[1]], exro[: used[2]]
+
     def seed_round_dev(self, d_reads, d_seeds, nseeds, d_in, nreads, d_exr, maxelt, d_out, d_sats, sat_cap,
                        d_elts, elt_cap, d_exr_out, exr_cap, d_used, stream=0):
         """bt2x_seed_round_dev: seed search + ranking/prioritization + SA resolution of a

@@ -86,7 +86,6 @@ def test_round_kernel_vs_reference_rank_golden(tmp_path):
     reference found none, and SeedResults::nonzeroOffsets(), numElts() and the RandomSource
     state after rankSeedHits equal the reference's."""
     import numpy as np
-    import torch
     from bt2x import abi, lib
     from bt2x import seeds as bseeds
     base = g.materialize_index("rep", str(tmp_path))
@@ -140,27 +139,8 @@ def test_round_kernel_vs_reference_rank_golden(tmp_path):
     rin = np.concatenate(rin)
     sin = case.inp[np.array(seed_sel, dtype=np.int64)]
     n = len(rin)
-    dev = torch.device("cuda", 0)
-    torch.cuda.init()                           # torch's HIP runtime first, then the context
-    torch.cuda.set_device(dev)
     ctx = lib.Context(lib.Index(base, load_offs=True))
-
-    def to_dev(a):
-        return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to(dev)
-
-    d_reads, d_seeds, d_in = to_dev(case.reads), to_dev(sin), to_dev(rin)
-    d_exr = to_dev(np.zeros(1, dtype=abi.EXRANGE))
-    d_out = torch.zeros(n * abi.ROUND_OUT.itemsize, dtype=torch.uint8, device=dev)
-    cap = 8 * n + 1024
-    d_sats = torch.zeros(cap * abi.SAT.itemsize, dtype=torch.uint8, device=dev)
-    d_elts = torch.zeros(cap * abi.RESOLVE_OUT.itemsize, dtype=torch.uint8, device=dev)
-    d_exro = torch.zeros(cap * abi.EXRANGE.itemsize, dtype=torch.uint8, device=dev)
-    d_used = torch.zeros(4, dtype=torch.int32, device=dev)
-    ctx.seed_round_dev(d_reads.data_ptr(), d_seeds.data_ptr(), len(sin), d_in.data_ptr(), n, d_exr.data_ptr(), 0,
-                       d_out.data_ptr(), d_sats.data_ptr(), cap, d_elts.data_ptr(), cap, d_exro.data_ptr(), cap,
-                       d_used.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
-    torch.cuda.synchronize(dev)
-    out = d_out.cpu().numpy().view(abi.ROUND_OUT)
+    out = ctx.seed_round(case.reads, sin, rin, np.zeros(0, dtype=abi.EXRANGE), 0)[0]
     ctx.close()
     bad, nk = [], 0
     for i, t in enumerate(exp):
