@@ -310,7 +310,7 @@ def replay(args, base, fq, rdir, gpu):
                                    int(meta[0]),
                                    torch.empty(m * abi.ROUND_OUT.itemsize, dtype=torch.uint8, device=dev),
                                    torch.empty(caps[0] * abi.SAT.itemsize, dtype=torch.uint8, device=dev), caps[0],
-                                   torch.empty(caps[1] * abi.RESOLVE_OUT.itemsize, dtype=torch.uint8, device=dev), caps[1],
+                                   torch.empty(caps[1] * abi.ELT.itemsize, dtype=torch.uint8, device=dev), caps[1],
                                    torch.empty(caps[2] * abi.EXRANGE.itemsize, dtype=torch.uint8, device=dev), caps[2],
                                    torch.zeros(4, dtype=torch.int32, device=dev)]))
         else:

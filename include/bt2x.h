@@ -355,6 +355,16 @@ typedef struct {
 } bt2x_resolve_out;
 #define BT2X_NO_TIDX 0xffffffffu
 
+/* One element of a seed round (bt2x_seed_round): the reference coordinate of
+ * bt2x_resolve_out without the joined offset and the text length (the caller's
+ * plen[tidx]), 16 bytes across PCIe instead of 32.  tidx = BT2X_NO_TIDX (toff = 0): the
+ * row lies in no fragment. */
+typedef struct {
+	uint64_t toff;           /* textoff: offset into reference tidx                      */
+	uint32_t tidx;
+	uint32_t straddled;      /* 1 if the hit runs past its fragment's end                 */
+} bt2x_elt;
+
 /* With the resident full suffix array this is one 4-byte lookup per element; without
  * it (texts of 2^32 rows or more, BT2X_FULL_SA=0) the kernel walks LF to the SA sample
  * exactly like GWState (<= 2^offRate - 1 steps).  Needs an index loaded with
@@ -442,7 +452,7 @@ int bt2x_seed_round(bt2x_ctx* ctx, const uint8_t* reads, uint64_t reads_bytes,
                     const bt2x_exrange* exr, uint32_t nexr, uint32_t maxelt,
                     bt2x_round_out* out,
                     bt2x_sat* sats, uint32_t sat_cap,
-                    bt2x_resolve_out* elts, uint32_t elt_cap,
+                    bt2x_elt* elts, uint32_t elt_cap,
                     bt2x_exrange* exr_out, uint32_t exr_cap,
                     uint32_t used[3]);
 /* Device-pointer variant (inputs resident in HBM; used: 3 x u32 in HBM).  Events:
@@ -451,7 +461,7 @@ int bt2x_seed_round(bt2x_ctx* ctx, const uint8_t* reads, uint64_t reads_bytes,
 int bt2x_seed_round_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const bt2x_seed_in* d_seeds, uint32_t nseeds,
                         const bt2x_round_in* d_in, uint32_t nreads, const bt2x_exrange* d_exr, uint32_t maxelt,
                         bt2x_round_out* d_out, bt2x_sat* d_sats, uint32_t sat_cap,
-                        bt2x_resolve_out* d_elts, uint32_t elt_cap, bt2x_exrange* d_exr_out, uint32_t exr_cap,
+                        bt2x_elt* d_elts, uint32_t elt_cap, bt2x_exrange* d_exr_out, uint32_t exr_cap,
                         uint32_t* d_used, void* stream);
 
 /* Page-locked host memory for the buffers a caller hands to the host-pointer entry points

@@ -243,7 +243,7 @@ class Context:
         exr_cap = exr_cap or 4 * n + 256
         out = np.zeros(n, dtype=abi.ROUND_OUT)
         sats = np.zeros(sat_cap, dtype=abi.SAT)
-        elts = np.zeros(elt_cap, dtype=abi.RESOLVE_OUT)
+        elts = np.zeros(elt_cap, dtype=abi.ELT)
         exro = np.zeros(exr_cap, dtype=abi.EXRANGE)
         used = (ctypes.c_uint32 * 3)()
         rc = load().bt2x_seed_round(self.h, abi.ptr(reads), reads.nbytes, abi.ptr(seeds), len(seeds), abi.ptr(inp), n,

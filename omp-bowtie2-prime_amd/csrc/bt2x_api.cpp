@@ -577,7 +577,7 @@ extern "C" int bt2x_abi_sizes(uint32_t* out, int n) {
 	                      (uint32_t)sizeof(bt2x_index_desc), (uint32_t)sizeof(bt2x_counters),
 	                      (uint32_t)sizeof(bt2x_resolve_in), (uint32_t)sizeof(bt2x_resolve_out),
 	                      (uint32_t)sizeof(bt2x_round_in), (uint32_t)sizeof(bt2x_round_out),
-	                      (uint32_t)sizeof(bt2x_sat), (uint32_t)sizeof(bt2x_exrange)};
+	                      (uint32_t)sizeof(bt2x_sat), (uint32_t)sizeof(bt2x_exrange), (uint32_t)sizeof(bt2x_elt)};
 	const int m = (int)(sizeof s / sizeof s[0]);
 	for(int i = 0; i < n && i < m; i++) out[i] = s[i];
 	return m;
@@ -613,7 +613,7 @@ extern "C" int bt2x_resolve_dev(bt2x_ctx* c, const bt2x_resolve_in* d_in, uint32
 extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt2x_seed_in* d_seeds, uint32_t nseeds,
                                    const bt2x_round_in* d_in, uint32_t nreads, const bt2x_exrange* d_exr,
                                    uint32_t maxelt, bt2x_round_out* d_out, bt2x_sat* d_sats, uint32_t sat_cap,
-                                   bt2x_resolve_out* d_elts, uint32_t elt_cap, bt2x_exrange* d_exr_out,
+                                   bt2x_elt* d_elts, uint32_t elt_cap, bt2x_exrange* d_exr_out,
                                    uint32_t exr_cap, uint32_t* d_used, void* stream) {
 	if(!c || !d_used) return BT2X_E_ARG;
 	if(!c->ix.sa && !c->ix.offs) return BT2X_E_ARG;        // index loaded without load_offs
@@ -670,7 +670,7 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
                                const bt2x_exrange* exr, uint32_t nexr, uint32_t maxelt,
                                bt2x_round_out* out,
                                bt2x_sat* sats, uint32_t sat_cap,
-                               bt2x_resolve_out* elts, uint32_t elt_cap,
+                               bt2x_elt* elts, uint32_t elt_cap,
                                bt2x_exrange* exr_out, uint32_t exr_cap,
                                uint32_t used[3]) {
 	if(!c || !used || (nreads && (!in || !out)) || (nseeds && (!reads || !seeds))) return BT2X_E_ARG;
@@ -693,7 +693,7 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 	   (rc = c->b_exr.ensure(sizeof(bt2x_exrange) * (size_t)(nexr ? nexr : 1))) ||
 	   (rc = c->b_rout.ensure(sizeof(bt2x_round_out) * nreads)) ||
 	   (rc = c->b_sats.ensure(sizeof(bt2x_sat) * (size_t)(sat_cap ? sat_cap : 1))) ||
-	   (rc = c->b_elts.ensure(sizeof(bt2x_resolve_out) * (size_t)(elt_cap ? elt_cap : 1))) ||
+	   (rc = c->b_elts.ensure(sizeof(bt2x_elt) * (size_t)(elt_cap ? elt_cap : 1))) ||
 	   (rc = c->b_exro.ensure(sizeof(bt2x_exrange) * (size_t)(exr_cap ? exr_cap : 1))) ||
 	   (rc = c->b_used.ensure(4 * sizeof(uint32_t)))) return rc;
 	if(reads_bytes) HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
@@ -703,7 +703,7 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 	rc = bt2x_seed_round_dev(c, (const uint8_t*)c->b_reads.p, (const bt2x_seed_in*)c->b_in.p, nseeds,
 	                         (const bt2x_round_in*)c->b_rin.p, nreads, (const bt2x_exrange*)c->b_exr.p, maxelt,
 	                         (bt2x_round_out*)c->b_rout.p, (bt2x_sat*)c->b_sats.p, sat_cap,
-	                         (bt2x_resolve_out*)c->b_elts.p, elt_cap, (bt2x_exrange*)c->b_exro.p, exr_cap,
+	                         (bt2x_elt*)c->b_elts.p, elt_cap, (bt2x_exrange*)c->b_exro.p, exr_cap,
 	                         (uint32_t*)c->b_used.p, c->stream);
 	if(rc) return rc;
 	HIPCHK(hipMemcpyAsync(used, c->b_used.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
@@ -711,7 +711,7 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 	HIPCHK(stream_wait(c));
 	if(used[0] > sat_cap || used[1] > elt_cap || used[2] > exr_cap) return BT2X_E_OVERFLOW;
 	if(used[0]) HIPCHK(hipMemcpyAsync(sats, c->b_sats.p, sizeof(bt2x_sat) * used[0], hipMemcpyDeviceToHost, c->stream));
-	if(used[1]) HIPCHK(hipMemcpyAsync(elts, c->b_elts.p, sizeof(bt2x_resolve_out) * used[1], hipMemcpyDeviceToHost, c->stream));
+	if(used[1]) HIPCHK(hipMemcpyAsync(elts, c->b_elts.p, sizeof(bt2x_elt) * used[1], hipMemcpyDeviceToHost, c->stream));
 	if(used[2]) HIPCHK(hipMemcpyAsync(exr_out, c->b_exro.p, sizeof(bt2x_exrange) * used[2], hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(stream_wait(c));
 	return BT2X_OK;

@@ -51,6 +51,8 @@ int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_
 // element count in HBM (*d_n, at most cap): persistent grid-stride launch
 int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
                            int reject, bt2x_resolve_out* d_out, unsigned long long* d_ctr, int ncu, void* stream);
+int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
+                           int reject, bt2x_elt* d_out, unsigned long long* d_ctr, int ncu, void* stream);
 
 // DP windows cut from the resident text (window_kernel.hip): every problem's window to
 // win[i * BT2X_MAX_COLS ..), its dp_in to out[i] with ref_off rebased and the flag cleared.

@@ -674,14 +674,23 @@ sa_resolve_kernel(DevIndex ix, const bt2x_resolve_in* __restrict__ in, uint32_t 
 }
 
 // The same over a count that lives in HBM (written by the kernel that produced the
-// elements), grid-stride; at most cap elements.
+// elements), grid-stride; at most cap elements.  Out: bt2x_resolve_out, or the seed
+// round's 16-byte bt2x_elt.
+__device__ __forceinline__ void put_elt(bt2x_resolve_out* out, uint32_t i, const bt2x_resolve_out& o) { out[i] = o; }
+__device__ __forceinline__ void put_elt(bt2x_elt* out, uint32_t i, const bt2x_resolve_out& o) {
+	bt2x_elt e;
+	e.toff = o.toff; e.tidx = o.tidx; e.straddled = o.straddled;
+	out[i] = e;
+}
+
+template<class Out>
 __global__ void __launch_bounds__(256)
 sa_resolve_kernel_dn(DevIndex ix, const bt2x_resolve_in* __restrict__ in, const uint32_t* __restrict__ d_n,
-                     uint32_t cap, int reject, bt2x_resolve_out* __restrict__ out, unsigned long long* __restrict__ ctr) {
+                     uint32_t cap, int reject, Out* __restrict__ out, unsigned long long* __restrict__ ctr) {
 	const uint32_t n = min(*d_n, cap);
 	uint32_t steps = 0;
 	for(uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-		out[i] = resolve_one(ix, in[i], reject, steps);
+		put_elt(out, i, resolve_one(ix, in[i], reject, steps));
 	if(ctr) {
 		uint64_t s = steps;
 		for(int k = 32; k >= 1; k >>= 1) s += __shfl_xor(s, k);
@@ -745,15 +754,28 @@ int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }
 
-int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
-                           int reject, bt2x_resolve_out* d_out, unsigned long long* d_ctr, int ncu, void* stream) {
+namespace {
+template<class Out>
+int launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
+                      int reject, Out* d_out, unsigned long long* d_ctr, int ncu, void* stream) {
 	if(cap == 0) return 0;
 	if(!ix.sa && !ix.offs) return BT2X_E_ARG;
 	uint32_t blocks = (uint32_t)(ncu > 0 ? ncu : 256) * 8u;
 	if(blocks > (cap + 255) / 256) blocks = (cap + 255) / 256;
-	hipLaunchKernelGGL(sa_resolve_kernel_dn, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+	hipLaunchKernelGGL(sa_resolve_kernel_dn<Out>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
 	                   ix, d_in, d_n, cap, reject, d_out, d_ctr);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
+}
+}
+
+int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
+                           int reject, bt2x_resolve_out* d_out, unsigned long long* d_ctr, int ncu, void* stream) {
+	return launch_resolve_dn(ix, d_in, d_n, cap, reject, d_out, d_ctr, ncu, stream);
+}
+
+int bt2x_launch_resolve_dn(const DevIndex& ix, const bt2x_resolve_in* d_in, const uint32_t* d_n, uint32_t cap,
+                           int reject, bt2x_elt* d_out, unsigned long long* d_ctr, int ncu, void* stream) {
+	return launch_resolve_dn(ix, d_in, d_n, cap, reject, d_out, d_ctr, ncu, stream);
 }
 
 int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_t n, int reject,

@@ -626,10 +626,13 @@ int ExtendWalk::next(int64_t minsc, DpKey& k) {
 		uint32_t rdoff = sp.rdoff;
 		if(!fw) rdoff = (uint32_t)(rdlen_ - rdoff - sp.seedlen);
 		const uint16_t elt = rands_[i_].next(*rnd_);
-		const bt2x_resolve_out& wr = (*res_)[(*firstRow_)[i_] + elt];
+		const bt2x_elt& wr = (*res_)[(*firstRow_)[i_] + elt];
 		neltLeft_--;
-		const int64_t tidx = wr.tidx == BT2X_NO_TIDX ? 0 : (int64_t)wr.tidx;
-		const int64_t toff = (int64_t)wr.toff, tlen = (int64_t)wr.tlen;
+		// (no fragment: tidx, toff and tlen stay 0, the caller's initial values,
+		// aligner_sw_driver.cpp:392)
+		const bool none = wr.tidx == BT2X_NO_TIDX;
+		const int64_t tidx = none ? 0 : (int64_t)wr.tidx;
+		const int64_t toff = (int64_t)wr.toff, tlen = none ? 0 : (int64_t)plen_[wr.tidx];
 		const int64_t refoff = toff - (int64_t)rdoff;
 		const Coord refcoord(tidx, refoff, fw);
 		if(seen_->locusPresent(refcoord)) { prm_->nRedundants++; continue; }
@@ -853,7 +856,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		c->sats.clear(); c->exNew.clear();
 		bool redo = !gpu_round_;
 		if(!redo) {
-			co_await Awaiter{c, REQ_ROUND};                          // fills round_out, sats, res_out, exNew
+			co_await Awaiter{c, REQ_ROUND};                          // fills round_out, sats, elts, exNew
 			PH_START();
 			redo = c->round_out.status == BT2X_ROUND_REDO;
 			if(redo) { c->sats.clear(); c->exNew.clear(); }
@@ -893,7 +896,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		{
 			prm.nDpFail = 0;
 			const int64_t perfectScore = 0;
-			c->walk.reset(P, satpos, rand_ns, c->firstRow, c->res_out, nelt_, rdlen);
+			c->walk.reset(P, satpos, rand_ns, c->firstRow, c->elts, ref_.lens(), nelt_, rdlen);
 			c->walk.bind(&rnd, &prm, &c->seenDiags);
 			for(;;) {
 				DpKey key;
@@ -1202,7 +1205,7 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 			c->round_out = o;
 			if(o.status == BT2X_ROUND_OK) {
 				c->sats.assign(L.round_sats.begin() + o.sat0, L.round_sats.begin() + o.sat0 + o.nsat);
-				c->res_out.assign(L.round_elts.begin() + o.elt0, L.round_elts.begin() + o.elt0 + o.nelt);
+				c->elts.assign(L.round_elts.begin() + o.elt0, L.round_elts.begin() + o.elt0 + o.nelt);
 				c->exNew.assign(L.round_exr_out.begin() + o.exr0, L.round_exr_out.begin() + o.exr0 + o.nexr);
 			}
 			c->req = REQ_NONE;
@@ -1214,7 +1217,12 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 			c->seed_out.assign(L.seed_out.begin() + (long)L.sk[i], L.seed_out.begin() + (long)L.sk[i + 1]);
 		} else if(i < nws + nwr) {
 			const long r = i - nws;
-			c->res_out.assign(L.res_out.begin() + (long)L.rk[r], L.res_out.begin() + (long)L.rk[r + 1]);
+			// the three-request path's resolves as round elements
+			c->elts.resize((size_t)(L.rk[r + 1] - L.rk[r]));
+			for(size_t k = 0; k < c->elts.size(); k++) {
+				const bt2x_resolve_out& o = L.res_out[L.rk[r] + k];
+				c->elts[k] = bt2x_elt{o.toff, o.tidx, o.straddled};
+			}
 		} else {
 			const long r = i - nws - nwr;
 			for(size_t j = 0; j < c->dps.size(); j++) {
@@ -1489,7 +1497,7 @@ struct LaunchSizes {
 std::vector<size_t> Aligner::launch_buffer_bytes(const Params& p, size_t reads) {
 	const LaunchSizes z(p, reads);
 	return {z.nr * 320, z.nr * 24 * sizeof(bt2x_seed_in), z.nr * sizeof(bt2x_round_in), z.nr * 4 * sizeof(bt2x_exrange),
-	        z.nr * sizeof(bt2x_round_out), z.nr * 64 * sizeof(bt2x_sat), z.nr * 64 * sizeof(bt2x_resolve_out),
+	        z.nr * sizeof(bt2x_round_out), z.nr * 64 * sizeof(bt2x_sat), z.nr * 64 * sizeof(bt2x_elt),
 	        z.nr * 4 * sizeof(bt2x_exrange), z.nd * 320, z.nd * 320, z.np * 210, z.np * sizeof(bt2x_dp_in),
 	        z.np * sizeof(bt2x_dp_out), (z.np * 4 + 64) * sizeof(bt2x_aln_rec), (z.np * 48 + 256) * sizeof(uint32_t)};
 }

@@ -656,6 +656,7 @@ public:
 	size_t nrefs() const { return names_.size(); }
 	const std::string& name(size_t i) const { return names_[i]; }
 	uint64_t len(size_t i) const { return plen_[i]; }
+	const uint64_t* lens() const { return plen_.data(); }
 	// codes of reference tidx over [off, off+n); positions outside a fragment are N
 	void stretch(uint32_t tidx, int64_t off, size_t n, uint8_t* out) const;
 private:
@@ -817,10 +818,11 @@ void host_round(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_see
 class ExtendWalk {
 public:
 	static constexpr int PROBLEM = 0;
+	// res: the round's elements; plen: reference lengths (plen[tidx] = the element's tlen)
 	void reset(const Params& P, const std::vector<SatPos>& sat, const std::vector<uint32_t>& rand_ns,
-	           const std::vector<uint32_t>& firstRow, const std::vector<bt2x_resolve_out>& res, size_t nelt,
-	           size_t rdlen) {
-		P_ = &P; sat_ = &sat; firstRow_ = &firstRow; res_ = &res; neltLeft_ = nelt; rdlen_ = rdlen;
+	           const std::vector<uint32_t>& firstRow, const std::vector<bt2x_elt>& res, const uint64_t* plen,
+	           size_t nelt, size_t rdlen) {
+		P_ = &P; sat_ = &sat; firstRow_ = &firstRow; res_ = &res; plen_ = plen; neltLeft_ = nelt; rdlen_ = rdlen;
 		rands_.resize(sat.size());
 		for(size_t i = 0; i < sat.size(); i++) rands_[i].init(rand_ns[i]);
 		i_ = 0; first_ = true; inPass_ = false;
@@ -837,7 +839,8 @@ private:
 	const Params* P_ = nullptr;
 	const std::vector<SatPos>* sat_ = nullptr;
 	const std::vector<uint32_t>* firstRow_ = nullptr;
-	const std::vector<bt2x_resolve_out>* res_ = nullptr;
+	const std::vector<bt2x_elt>* res_ = nullptr;
+	const uint64_t* plen_ = nullptr;
 	size_t neltLeft_ = 0, rdlen_ = 0;
 	std::vector<SmallRandom1toN> rands_;
 	size_t i_ = 0;
@@ -886,7 +889,7 @@ struct ReadCtx {
 	std::vector<bt2x_seed_in> seed_in;   // read_off: 0 = patFw, rdlen = patRc
 	std::vector<bt2x_seed_out> seed_out;
 	std::vector<bt2x_resolve_in> res_in;
-	std::vector<bt2x_resolve_out> res_out;
+	std::vector<bt2x_elt> elts;      // the round's elements (bt2x_seed_round, or converted resolves)
 	std::vector<DpWork> dps;             // the problems posed by the current DP request
 	// DP results of this read (memo by DpKey; records and edit images in arenas)
 	std::vector<DpMemo> memo;
@@ -948,7 +951,7 @@ public:
 	virtual void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
 	                        const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr,
 	                        uint32_t maxelt, HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats,
-	                        HostVec<bt2x_resolve_out>& elts, HostVec<bt2x_exrange>& exr_out) = 0;
+	                        HostVec<bt2x_elt>& elts, HostVec<bt2x_exrange>& exr_out) = 0;
 	// true: DP problems name their reference window (BT2X_DP_REF_TEXT: ref_off = tidx) and
 	// the backend cuts it from the index; false: the driver fills refs (RefInfo::stretch)
 	virtual bool ref_from_index() const { return false; }
@@ -1029,7 +1032,7 @@ private:
 		HostVec<bt2x_exrange> round_exr, round_exr_out;
 		HostVec<bt2x_round_out> round_out;
 		HostVec<bt2x_sat> round_sats;
-		HostVec<bt2x_resolve_out> round_elts;
+		HostVec<bt2x_elt> round_elts;
 		double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_gather = 0;
 		// gather's per-chunk lists, sizes and bases
 		struct Chunk {

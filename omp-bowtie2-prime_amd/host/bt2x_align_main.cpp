@@ -98,7 +98,7 @@ public:
 	}
 	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
 	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
-	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_elt>& elts,
 	                HostVec<bt2x_exrange>& exr_out) override {
 		const auto t0 = std::chrono::steady_clock::now();
 		const uint32_t n = (uint32_t)in.size();
@@ -131,7 +131,7 @@ public:
 		gs.round_h2d += reads.size() + seeds.size() * sizeof(bt2x_seed_in) + n * sizeof(bt2x_round_in) +
 		                exr.size() * sizeof(bt2x_exrange);
 		gs.round_d2h += n * sizeof(bt2x_round_out) + sats.size() * sizeof(bt2x_sat) +
-		                elts.size() * sizeof(bt2x_resolve_out) + exr_out.size() * sizeof(bt2x_exrange);
+		                elts.size() * sizeof(bt2x_elt) + exr_out.size() * sizeof(bt2x_exrange);
 		gs.t_round_call += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 	}
 	void dp_align(const HostVec<uint8_t>& reads, const HostVec<uint8_t>& quals,
@@ -188,7 +188,7 @@ public:
 	}
 	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
 	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
-	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_elt>& elts,
 	                HostVec<bt2x_exrange>& exr_out) override {
 		in_.seed_round(reads, seeds, in, exr, maxelt, out, sats, elts, exr_out);
 		const uint64_t meta[4] = {maxelt, sats.size(), elts.size(), exr_out.size()};   // arena sizes the replay needs

@@ -61,7 +61,7 @@ public:
 	// the oracle SA resolution: the contract of bt2x_seed_round on the CPU
 	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
 	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
-	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_elt>& elts,
 	                HostVec<bt2x_exrange>& exr_out) override {
 		HostVec<bt2x_seed_out> so;
 		seed_search(reads, seeds, so);
@@ -81,7 +81,10 @@ public:
 		}
 		sats.assign(sv.begin(), sv.end());
 		exr_out.assign(xv.begin(), xv.end());
-		resolve(HostVec<bt2x_resolve_in>(rows.begin(), rows.end()), elts);
+		HostVec<bt2x_resolve_out> ro;
+		resolve(HostVec<bt2x_resolve_in>(rows.begin(), rows.end()), ro);
+		elts.resize(ro.size());
+		for(size_t k = 0; k < ro.size(); k++) elts[k] = bt2x_elt{ro[k].toff, ro[k].tidx, ro[k].straddled};
 	}
 private:
 	const bt2x_index_desc& idx_;
@@ -111,7 +114,7 @@ public:
 	}
 	void seed_round(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& seeds,
 	                const HostVec<bt2x_round_in>& in, const HostVec<bt2x_exrange>& exr, uint32_t maxelt,
-	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_resolve_out>& elts,
+	                HostVec<bt2x_round_out>& out, HostVec<bt2x_sat>& sats, HostVec<bt2x_elt>& elts,
 	                HostVec<bt2x_exrange>& exr_out) override {
 		if(rec_) {
 			rec_->seed_round(reads, seeds, in, exr, maxelt, out, sats, elts, exr_out);
@@ -122,7 +125,7 @@ public:
 		}
 	}
 private:
-	struct Round { HostVec<bt2x_round_out> out; HostVec<bt2x_sat> sats; HostVec<bt2x_resolve_out> elts;
+	struct Round { HostVec<bt2x_round_out> out; HostVec<bt2x_sat> sats; HostVec<bt2x_elt> elts;
 	               HostVec<bt2x_exrange> exr; };
 	std::vector<Round> rounds_;
 	size_t kn_ = 0;

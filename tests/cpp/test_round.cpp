@@ -206,7 +206,7 @@ int main(int argc, char** argv) {
 			}
 			std::vector<bt2x_round_out> out(in.size());
 			std::vector<bt2x_sat> sats(in.size() * 420);
-			std::vector<bt2x_resolve_out> elts(in.size() * 420);
+			std::vector<bt2x_elt> elts(in.size() * 420);
 			std::vector<bt2x_exrange> exro(in.size() * 130);
 			uint32_t used[3];
 			const int rc = bt2x_seed_round(dev.ctx(), rb.data(), rb.size(), seeds.data(), (uint32_t)seeds.size(), in.data(),
@@ -230,7 +230,8 @@ int main(int argc, char** argv) {
 					if(!hr.empty() && bt2x_resolve(dev.ctx(), hr.data(), (uint32_t)hr.size(), 0, ho.data()) != BT2X_OK) return 1;
 					bool eq = ho.size() == out[r].nelt;
 					for(size_t k = 0; eq && k < ho.size(); k++)
-						eq = std::memcmp(&ho[k], &elts[out[r].elt0 + k], sizeof(bt2x_resolve_out)) == 0;
+						eq = ho[k].toff == elts[out[r].elt0 + k].toff && ho[k].tidx == elts[out[r].elt0 + k].tidx &&
+						     ho[k].straddled == elts[out[r].elt0 + k].straddled;
 					b.rows = eq ? a.rows : std::vector<uint64_t>{};
 				}
 				std::string why;
