@@ -16,7 +16,8 @@ Per rank (one process per GPU; the GPU work runs in bt2x-align, a child process)
           seed search / SA resolution / DP on the GPU, PCIe, SAM formatting and writing.
           All ranks start it after a barrier; value = reads of all ranks / max over ranks
           of the timed run's wall time (BT2X_TIMED t_align; the index load is outside it).
-  kernels rank 0: bt2x-align --dump records the GPU launches of one 1M-read file; the
+  kernels rank 0: bt2x-align --dump records the GPU launches of one 1M-read file (a cohort
+          of the timed run's size in flight, so the launches have its shapes); the
           launch sequence is replayed from HBM (inputs resident) with HIP events around
           each launch (bt2x_last_kernel_ms, on the launch stream) -> per-kernel time,
           the dominant kernel's roofline, and replay_reads_per_s (kernels alone).
@@ -65,7 +66,7 @@ def parse():
     ap.add_argument("--genome-mb", type=float, default=3100.0)
     ap.add_argument("--genome-seed", type=int, default=2024)
     ap.add_argument("--host-threads", type=int, default=0, help="bt2x-align -p (0: the rank's CPU share)")
-    ap.add_argument("--slots", type=int, default=1 << 18, help="bt2x-align --slots (reads in flight)")
+    ap.add_argument("--slots", type=int, default=1 << 17, help="bt2x-align --slots (reads in flight)")
     ap.add_argument("--replay-reads", type=int, default=1 << 20, help="reads whose GPU launches are replayed")
     ap.add_argument("--replay-steps", type=int, default=3)
     ap.add_argument("--cpu-sample", type=int, default=800_000, help="reads of the reference CPU baseline")
@@ -278,8 +279,11 @@ def replay(args, base, fq, rdir, gpu):
     ddir = os.path.join(rdir, "dump")
     shutil.rmtree(ddir, ignore_errors=True)
     os.makedirs(ddir)
+    # one cohort of the timed run's size in flight (--slots / 2, its pipeline's cohorts): the
+    # replayed launches have the shapes the end-to-end run launches
     run_aligner(args, [ALIGN, "-x", base, "-U", fq, "-S", os.devnull, "--dpad", str(args.dpad), "-p",
-                       str(args.host_threads), "--slots", str(n), "--dump", ddir, "--no-pipeline"],
+                       str(args.host_threads), "--slots", str(max(1, args.slots // 2)), "--dump", ddir,
+                       "--no-pipeline"],
                 os.path.join(rdir, "dump.err"), "launch recording")
     launches = load_dumps(ddir)
     shutil.rmtree(ddir, ignore_errors=True)
@@ -429,8 +433,9 @@ def roofline(args, rp):
                "counters_dp": cd, "round_sampling": rp["ctr"]["round"], "replay_reads": rp["reads"],
                "replay_steps": args.replay_steps,
                "replay_reads_per_s": round(rp["reads"] * args.replay_steps / rp["elapsed"], 1),
-               "what": "the GPU launch sequence bt2x-align issues for replay_reads reads (one file, all in flight), "
-                       "replayed from HBM; kernel times from HIP events on the launch stream"}
+               "what": "the GPU launch sequence bt2x-align issues for replay_reads reads (one file; cohorts of "
+                       "--slots/2 reads in flight, as in the timed run), replayed from HBM; kernel times from HIP "
+                       "events on the launch stream"}
     return roof, kernels
 
 

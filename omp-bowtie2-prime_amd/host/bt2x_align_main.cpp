@@ -236,7 +236,7 @@ int main(int argc, char** argv) {
 	std::string idx, fq, outp, mate1, mate2;
 	Params p;
 	int threads = 16, device = 0;
-	size_t slots = 1 << 18;
+	size_t slots = 1 << 17;
 	bool stats = false, pipeline = true, gpu_round = true, hd = true, metrics = false;
 	int shard = 0, nshards = 1, warm_files = 0;
 	std::string dump;

@@ -44,7 +44,7 @@ def main() -> None:
     ap.add_argument("--src", default="gpurun_out")
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--workload", required=True, help="bench.py workload key of the profiled run")
-    ap.add_argument("--cmd", default="python3 bench.py --steps 5 --warmup 2 --no-cpu")
+    ap.add_argument("--cmd", default="python3 bench.py --no-cpu")
     ap.add_argument("--replays", type=int, default=0,
                     help="bench steps in the profiled run (warmup + steps): traffic is then reported per step "
                          "(all launches of the op in one replay), as bench.py times it")
@@ -55,16 +55,18 @@ def main() -> None:
     shutil.copy(os.path.join(a.src, "prof_kt", "run_kernel_stats.csv"),
                 os.path.join(out, f"{a.tag}_kernel_stats.csv"))
     def replay_rows(path):
-        """Rows of the process that issued the most of our dispatches: bench.py's replay
-        (the bt2x-align runs it starts are child processes with fewer launches)."""
+        """Rows of bench.py's own process, i.e. the kernel replay: of the processes that ran
+        our kernels (bench.py, and the bt2x-align runs it starts as children, which finish
+        first) the one whose first dispatch came last."""
         with open(path) as f:
             rows = [r for r in csv.DictReader(f) if short(r["Kernel_Name"])]
         pid = "Process_Id" if rows and "Process_Id" in rows[0] else None
         if pid:
-            cnt = defaultdict(int)
+            first = {}
             for r in rows:
-                cnt[r[pid]] += 1
-            keep = max(cnt, key=cnt.get)
+                t = int(r.get("Start_Timestamp") or r.get("Start_Time") or 0)
+                first[r[pid]] = min(first.get(r[pid], t), t)
+            keep = max(first, key=first.get)
             rows = [r for r in rows if r[pid] == keep]
         return rows
 
@@ -116,6 +118,38 @@ def main() -> None:
                              "per": "step" if a.replays else "launch",
                              "avg_duration_ms": round(per_call(dur[k]) / 1e6, 4) if dur.get(k) else None,
                              "per_kernel_ms": {n: round(sum(v) / len(v) / 1e6, 4) for n, v in dur[k].items()}}
+    # SQ counters (prof_sq): per step of the replay, per DP kernel; VALU utilisation =
+    # VALU instructions / (kernel time x issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles
+    # per wave64 VALU op), SQ_WAIT_ANY per wave-cycle (MI355X_MICROARCH.md PMC section)
+    sq_path = os.path.join(a.src, "prof_sq", "run_counter_collection.csv")
+    if os.path.exists(sq_path) and a.replays:
+        sq = defaultdict(lambda: defaultdict(float))
+        for r in replay_rows(sq_path):
+            sq[kname(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        issue_peak = 256 * 4 * 2.4e9 / 2
+        out_sq = {"what": "SQ counters of the DP kernels per bench replay step (tools/gpujobs/profile_r03.sh, "
+                          "rocprofv3 --pmc); time per step from the kernel trace",
+                  "workload": a.workload, "kernels": {}}
+        for kn, c in sq.items():
+            if "dp_" not in kn:
+                continue
+            c = {k: v / a.replays for k, v in c.items()}
+            t = sum(sum(v) for n, v in dur["dp"].items() if n == kn) / 1e9 / a.replays if dur.get("dp") else 0
+            e = dict(c)
+            if c.get("SQ_WAVE_CYCLES"):
+                e["wait_any_per_wave_cycle"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
+                e["active_per_wave_cycle"] = c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+            if t:
+                e["time_s_per_step"] = t
+                e["valu_util"] = c.get("SQ_INSTS_VALU", 0) / (t * issue_peak)
+            out_sq["kernels"][kn] = e
+        with open(os.path.join(out, f"{a.tag}_dp_sq.json"), "w") as g:
+            json.dump(out_sq, g, indent=1)
+        fill = out_sq["kernels"].get("dp_fill_kernel", {})
+        if "dp" in res["kernels"] and fill:
+            res["kernels"]["dp"]["valu_util"] = round(fill.get("valu_util", 0), 4)
+            res["kernels"]["dp"]["sq_wait_any_per_wave_cycle"] = round(fill.get("wait_any_per_wave_cycle", 0), 4)
+            res["kernels"]["dp"]["sq_src"] = f"profiles/{a.tag}_dp_sq.json"
     with open(os.path.join(out, f"{a.tag}_traffic.json"), "w") as g:
         json.dump(res, g, indent=1)
     print(json.dumps(res, indent=1))
