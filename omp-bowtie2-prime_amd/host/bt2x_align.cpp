@@ -605,7 +605,7 @@ long find_memo(const std::vector<DpMemo>& memo, const DpKey& k) {
 
 int ExtendWalk::next(int64_t minsc, DpKey& k) {
 	const Params& P = *P_;
-	const size_t n = (uint16_t)sat_->size();                // gws_size is a uint16_t
+	const size_t n = (uint16_t)nsat_;                       // gws_size is a uint16_t
 	for(;;) {
 		if(!inPass_) {                                       // while(neltLeft > 0)
 			if(neltLeft_ == 0) return EXTEND_EXHAUSTED_CANDIDATES;
@@ -613,8 +613,8 @@ int ExtendWalk::next(int64_t minsc, DpKey& k) {
 			inPass_ = true; i_ = 0; first_ = true;
 		}
 		if(i_ >= n) { inPass_ = false; continue; }
-		const SatPos& sp = (*sat_)[i_];
-		const bool is_small = sp.size < kNsm;
+		const bt2x_sat& sp = sat_[i_];
+		const bool is_small = sp.rand_n < kNsm;
 		if(rands_[i_].done() || !(first_ || is_small)) { i_++; first_ = true; continue; }
 		if(minsc == 0) return EXTEND_PERFECT_SCORE;
 		if(prm_->nExDps >= P.mxDp || prm_->nMateDps >= P.mxDp) return EXTEND_EXCEEDED_HARD_LIMIT;
@@ -622,7 +622,7 @@ int ExtendWalk::next(int64_t minsc, DpKey& k) {
 		if(prm_->nExIters >= P.mxIter) return EXTEND_EXCEEDED_HARD_LIMIT;
 		prm_->nExIters++;
 		first_ = false;
-		const bool fw = sp.fw;
+		const bool fw = sp.fw != 0;
 		uint32_t rdoff = sp.rdoff;
 		if(!fw) rdoff = (uint32_t)(rdlen_ - rdoff - sp.seedlen);
 		const uint16_t elt = rands_[i_].next(*rnd_);
@@ -875,19 +875,11 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		const bt2x_round_out& ro = c->round_out;
 		if(ro.status == BT2X_ROUND_NO_HITS) break;                   // no seed hits: done
 		c->exRange.insert(c->exRange.end(), c->exNew.begin(), c->exNew.end());
-		// the extension list (SATupleAndPos) and each entry's first element
-		std::vector<SatPos>& satpos = c->satpos;
-		std::vector<uint32_t>& rand_ns = c->rand_ns;
-		satpos.clear(); rand_ns.clear(); c->firstRow.clear();
+		// the extension list (SATupleAndPos: the round's bt2x_sat entries) and each entry's
+		// first element
+		c->firstRow.resize(c->sats.size());
 		uint32_t e0 = 0;
-		for(const bt2x_sat& st : c->sats) {
-			SatPos sp;
-			sp.size = st.rand_n; sp.fw = st.fw != 0; sp.rdoff = st.rdoff; sp.seedlen = st.seedlen;
-			satpos.push_back(sp);
-			rand_ns.push_back(st.rand_n);
-			c->firstRow.push_back(e0);
-			e0 += st.rand_n;
-		}
+		for(size_t k = 0; k < c->sats.size(); k++) { c->firstRow[k] = e0; e0 += c->sats[k].rand_n; }
 		const size_t nelt_ = ro.nelt;
 		PH(4);
 
@@ -896,7 +888,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		{
 			prm.nDpFail = 0;
 			const int64_t perfectScore = 0;
-			c->walk.reset(P, satpos, rand_ns, c->firstRow, c->elts, ref_.lens(), nelt_, rdlen);
+			c->walk.reset(P, c->sats, c->firstRow, c->elts, ref_.lens(), nelt_, rdlen);
 			c->walk.bind(&rnd, &prm, &c->seenDiags);
 			for(;;) {
 				DpKey key;

@@ -593,7 +593,7 @@ public:
 		r.fw.reserve(raw.n[1]);
 		for(size_t i = 0; i < raw.n[1]; i++) {
 			const unsigned char c = (unsigned char)(raw.l[1][i] == '.' ? 'N' : raw.l[1][i]);
-			if(std::isalpha(c)) r.fw.push_back(kAsc2Dna[c]);
+			if((unsigned)((c | 32u) - 'a') < 26u) r.fw.push_back(kAsc2Dna[c]);   // isalpha, "C" locale
 		}
 		r.qual.clear();
 		if(raw.n[1] || raw.n[3]) r.qual.assign(raw.l[3], raw.n[3]);
@@ -819,12 +819,14 @@ class ExtendWalk {
 public:
 	static constexpr int PROBLEM = 0;
 	// res: the round's elements; plen: reference lengths (plen[tidx] = the element's tlen)
-	void reset(const Params& P, const std::vector<SatPos>& sat, const std::vector<uint32_t>& rand_ns,
-	           const std::vector<uint32_t>& firstRow, const std::vector<bt2x_elt>& res, const uint64_t* plen,
-	           size_t nelt, size_t rdlen) {
-		P_ = &P; sat_ = &sat; firstRow_ = &firstRow; res_ = &res; plen_ = plen; neltLeft_ = nelt; rdlen_ = rdlen;
+	// sat: the extension list (bt2x_seed_round's order; rand_n = the entry's element count)
+	template<class SatVec>
+	void reset(const Params& P, const SatVec& sat, const std::vector<uint32_t>& firstRow,
+	           const std::vector<bt2x_elt>& res, const uint64_t* plen, size_t nelt, size_t rdlen) {
+		P_ = &P; firstRow_ = &firstRow; res_ = &res; plen_ = plen; neltLeft_ = nelt; rdlen_ = rdlen;
 		rands_.resize(sat.size());
-		for(size_t i = 0; i < sat.size(); i++) rands_[i].init(rand_ns[i]);
+		for(size_t i = 0; i < sat.size(); i++) rands_[i].init(sat[i].rand_n);
+		sat_ = sat.data(); nsat_ = sat.size();
 		i_ = 0; first_ = true; inPass_ = false;
 	}
 	void bind(Rng* rnd, Prm* prm, SeenDiags* seen) { rnd_ = rnd; prm_ = prm; seen_ = seen; }
@@ -837,7 +839,8 @@ public:
 private:
 	static constexpr uint64_t kNsm = 5;                          // prioritizeSATups' nsm
 	const Params* P_ = nullptr;
-	const std::vector<SatPos>* sat_ = nullptr;
+	const bt2x_sat* sat_ = nullptr;
+	size_t nsat_ = 0;
 	const std::vector<uint32_t>* firstRow_ = nullptr;
 	const std::vector<bt2x_elt>* res_ = nullptr;
 	const uint64_t* plen_ = nullptr;
@@ -901,8 +904,7 @@ struct ReadCtx {
 	std::vector<bt2x_sat> sats;
 	std::vector<bt2x_exrange> exRange, exNew;           // extendSeeds' exRange (both strands)
 	RoundScratch rs;
-	std::vector<SatPos> satpos;
-	std::vector<uint32_t> rand_ns, firstRow;
+	std::vector<uint32_t> firstRow;
 	// extendSeeds state
 	SeenDiags seenDiags, seen2;
 	ExtendWalk walk, ahead;

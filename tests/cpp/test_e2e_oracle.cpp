@@ -24,7 +24,11 @@ using namespace bt2x::host;
 namespace {
 class OracleBackend : public Backend {
 public:
-	OracleBackend(const bt2x_index_desc& idx, const bt2x_scoring& sc) : idx_(idx), sc_(sc) {}
+	OracleBackend(const bt2x_index_desc& idx, const bt2x_scoring& sc, const RefInfo* ref = nullptr)
+		: idx_(idx), sc_(sc), ref_(ref) {}
+	// with a RefInfo: DP problems name their windows (BT2X_DP_REF_TEXT) as with the GPU
+	// backend, and the windows are cut here
+	bool ref_from_index() const override { return ref_ != nullptr; }
 	// --inject-error N: the Nth DP launch throws, as a failing GPU call would (bt2x::check)
 	int fail_at = 0;
 	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
@@ -45,11 +49,28 @@ public:
 		if(fail_at > 0 && ++ndp_ == fail_at) throw bt2x::Error(BT2X_E_NODEVICE, "injected backend error");
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
+		const uint8_t* rf = refs.data();
+		const bt2x_dp_in* pin = in.data();
+		std::vector<uint8_t> win;
+		std::vector<bt2x_dp_in> in2;
+		if(ref_) {                                           // BitPairReference::getStretch per problem
+			in2.assign(in.begin(), in.end());
+			for(bt2x_dp_in& q : in2) {
+				if(!(q.flags & BT2X_DP_REF_TEXT)) continue;
+				const size_t o = win.size();
+				win.resize(o + q.ncol);
+				ref_->stretch((uint32_t)q.ref_off, q.refl, q.ncol, win.data() + o);
+				q.ref_off = o;
+				q.flags &= (uint8_t)~BT2X_DP_REF_TEXT;
+			}
+			rf = win.data();
+			pin = in2.data();
+		}
 		uint32_t rec_cap = 4 * n + 64, edit_cap = 48 * n + 256;
 		for(int attempt = 0; attempt < 2; attempt++) {
 			recs.resize(rec_cap); edits.resize(edit_cap);
 			uint32_t nrec = 0, ned = 0;
-			const int rc = bt2o_dp_align(&sc_, reads.data(), quals.data(), refs.data(), in.data(), n, out.data(),
+			const int rc = bt2o_dp_align(&sc_, reads.data(), quals.data(), rf, pin, n, out.data(),
 			                             recs.data(), rec_cap, &nrec, edits.data(), edit_cap, &ned, nullptr, nullptr);
 			if(rc == BT2X_E_OVERFLOW && attempt == 0) { rec_cap = nrec; edit_cap = ned; continue; }
 			if(rc != 0) throw std::runtime_error("oracle dp");
@@ -89,6 +110,7 @@ public:
 private:
 	const bt2x_index_desc& idx_;
 	const bt2x_scoring& sc_;
+	const RefInfo* ref_;
 	int ndp_ = 0;
 };
 
@@ -96,7 +118,8 @@ private:
 // outputs (the driver is deterministic), so its wall time is the host driver's alone.
 class ReplayBackend : public Backend {
 public:
-	explicit ReplayBackend(Backend* rec) : rec_(rec) {}
+	explicit ReplayBackend(Backend* rec) : rec_(rec), ref_index_(rec->ref_from_index()) {}
+	bool ref_from_index() const override { return ref_index_; }
 	void rewind() { rec_ = nullptr; k_ = kr_ = kd_ = kn_ = 0; }
 	void seed_search(const HostVec<uint8_t>& reads, const HostVec<bt2x_seed_in>& in,
 	                 HostVec<bt2x_seed_out>& out) override {
@@ -131,6 +154,7 @@ private:
 	size_t kn_ = 0;
 	struct Dp { HostVec<bt2x_dp_out> out; HostVec<bt2x_aln_rec> recs; HostVec<uint32_t> edits; };
 	Backend* rec_;
+	bool ref_index_;
 	size_t k_ = 0, kr_ = 0, kd_ = 0;
 	std::vector<HostVec<bt2x_seed_out>> seeds_;
 	std::vector<HostVec<bt2x_resolve_out>> res_;
@@ -147,7 +171,7 @@ int main(int argc, char** argv) {
 	Params p;
 	size_t slots = 4096;
 	int threads = 4;
-	bool host_timing = false, pipeline = true, gpu_round = true, hd = true, metrics = false;
+	bool host_timing = false, pipeline = true, gpu_round = true, hd = true, metrics = false, host_windows = false;
 	int reps = 1, inject = 0, shard = 0, nshards = 1;
 	std::string idx, fqs, outp;
 	std::vector<std::string> pos;
@@ -163,6 +187,7 @@ int main(int argc, char** argv) {
 		else if(a == "--no-pipeline") pipeline = false;
 		else if(a == "--no-gpu-round") gpu_round = false;
 		else if(a == "--no-hd") hd = false;
+		else if(a == "--host-windows") host_windows = true;
 		else if(a == "--metrics") metrics = true;
 		else if(a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
 		else if(a == "--inject-error" && i + 1 < argc) inject = std::atoi(argv[++i]);
@@ -182,7 +207,9 @@ int main(int argc, char** argv) {
 	bt2x::Index index(idx.c_str(), true);
 	RefInfo ref;
 	ref.init(index.desc(), idx);
-	OracleBackend be(index.desc(), p.sc);
+	// windows named by the problems and cut by the backend (the GPU backend's mode), or cut by
+	// the driver (--host-windows)
+	OracleBackend be(index.desc(), p.sc, host_windows ? nullptr : &ref);
 	be.fail_at = inject;
 	if(host_timing) {
 		ReplayBackend rb(&be);

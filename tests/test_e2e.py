@@ -130,6 +130,13 @@ def test_host_driver_vs_reference_sam(fixtures, name, idx, fq, opts):
         assert tight > 100, tight
 
 
+@pytest.mark.parametrize("name,idx,fq,opts", [SETS[1], SETS[9]], ids=[SETS[1][0], SETS[9][0]])
+def test_host_driver_host_cut_windows(fixtures, name, idx, fq, opts):
+    """The same with the DP reference windows cut by the driver (RefInfo::stretch) instead of
+    named for the backend to cut (BT2X_DP_REF_TEXT, the GPU backend's default)."""
+    check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4", "--host-windows"] + opts, name)
+
+
 @pytest.mark.parametrize("name,idx,fq,opts", [SETS[1], SETS[4]], ids=[SETS[1][0], SETS[4][0]])
 def test_host_driver_vs_reference_sam_three_requests(fixtures, name, idx, fq, opts):
     """The same with every seed round as seed search + host ranking/prioritization + SA

@@ -60,7 +60,9 @@ def main() -> None:
         first) the one whose first dispatch came last."""
         with open(path) as f:
             rows = [r for r in csv.DictReader(f) if short(r["Kernel_Name"])]
-        pid = "Process_Id" if rows and "Process_Id" in rows[0] else None
+        # (rocprofv3 writes one table for all processes; without a process column the
+        # issuing thread tells them apart)
+        pid = next((k for k in ("Process_Id", "Thread_Id") if rows and k in rows[0]), None)
         if pid:
             first = {}
             for r in rows:
