@@ -1098,8 +1098,9 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			L.wd[i] = c; L.qb[i] = dbo; L.pb[i] = pko;
 			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)dbo);
 			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.dp_reads.begin() + (long)(dbo + len));
-			std::copy(c->rd.qual.begin(), c->rd.qual.end(), L.dp_quals.begin() + (long)dbo);
-			std::copy(c->rd.qualRev.begin(), c->rd.qualRev.end(), L.dp_quals.begin() + (long)(dbo + len));
+			// (memcpy: char -> uint8_t through std::copy is a scalar byte loop)
+			std::memcpy(L.dp_quals.data() + dbo, c->rd.qual.data(), len);
+			std::memcpy(L.dp_quals.data() + dbo + len, c->rd.qualRev.data(), len);
 			for(const DpWork& d : c->dps) {
 				bt2x_dp_in q = d.in;
 				q.read_off = q.qual_off = dbo + (d.key.fw ? 0 : len);
