@@ -540,15 +540,19 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        bdist.init_quiet(dist)
     base, gdesc = build_index(args, chroms, codes, workdir, rank, dist)
     del chroms, codes
     rdir = os.path.join(workdir, f"rank{rank}")
 
     # ---- timed: the aligner over the step files (warmup files first, untimed)
-    need = args.reads * (args.read_len * 3)                   # SAM bytes, generously
+    # every rank writes its SAM to the node's disk when all of them fit (the same choice at
+    # every N, so the per-GPU work does not change with N); else /dev/null everywhere
+    need = args.reads * (args.read_len * 3)                   # SAM bytes per rank, generously
+    if dist:
+        dist.barrier()                                        # every rank's inputs are on disk
     out_sam = os.path.join(rdir, "out.sam")
-    if shutil.disk_usage(rdir).free < need + (8 << 30):
+    if shutil.disk_usage(rdir).free < world * need + (8 << 30):
         out_sam = os.devnull
     cmd = [ALIGN, "-x", base, "-U", ",".join(warm + steps), "-S", out_sam, "--dpad", str(args.dpad),
            "--device", str(gpu), "-p", str(args.host_threads), "--slots", str(args.slots),

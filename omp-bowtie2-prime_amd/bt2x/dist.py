@@ -11,6 +11,24 @@ from __future__ import annotations
 import os
 
 
+def init_quiet(dist, backend: str = "gloo") -> None:
+    """dist.init_process_group(backend) with the backend's connection chatter ("[Gloo] Rank
+    0 is connected to ...", written to fd 1 by the C++ side) kept off stdout, where the
+    bench's one JSON line and SAM output go."""
+    import sys
+    sys.stdout.flush()
+    saved = os.dup(1)
+    null = os.open(os.devnull, os.O_WRONLY)
+    try:
+        os.dup2(null, 1)
+        dist.init_process_group(backend)
+        dist.barrier()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(null)
+
+
 def world() -> tuple[int, int, int]:
     """(rank, world_size, local_rank) from the torch.distributed.run environment."""
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
@@ -199,7 +217,7 @@ def main(argv=None) -> int:
     import torch.distributed as tdist
     use_dist = int(os.environ.get("WORLD_SIZE", "1")) > 1
     if use_dist:
-        tdist.init_process_group("gloo")
+        init_quiet(tdist)
     try:
         res = run_sharded(a.aligner, rest, tdist if use_dist else None, set_device=not a.no_device)
     finally:
