@@ -1090,22 +1090,11 @@ uint32_t dp_wave_max() {                        // read per launch (tests switch
 	return (w && w[0] == '0') ? 0u : (w && w[0] == '1') ? 0xffffffffu : (x ? (uint32_t)atoll(x) : 32768u);
 }
 
-// BT2X_DP_SPREAD=k (experiments): at most k fill workgroups per CU, through dynamic LDS,
-// so a launch of fewer groups than resident slots spreads over every CU
-size_t dp_spread_lds(uint32_t groups, int ncu) {
-	const char* e = getenv("BT2X_DP_SPREAD");
-	const int k = e ? atoi(e) : 0;
-	if(k <= 0 || (int64_t)groups >= (int64_t)ncu * 12) return 0;
-	const size_t per = (size_t)160 * 1024 / (size_t)k;
-	const size_t stat = (size_t)(kCols / 4) * 64 * 4;        // the kernel's static LDS
-	return per > stat + 256 ? per - stat - 256 : 0;
-}
-
 template<bool kDebug, bool kFused>
 void launch_fill(bool wide, uint32_t grid, hipStream_t s, const DevScoring& sc, const DpLaunch& a, uint32_t base,
-                 uint32_t np, size_t dyn = 0) {
-	if(wide) hipLaunchKernelGGL((dp_fill_kernel<kDebug, kFused, true>), dim3(grid), dim3(64), dyn, s, sc, a, base, np);
-	else hipLaunchKernelGGL((dp_fill_kernel<kDebug, kFused, false>), dim3(grid), dim3(64), dyn, s, sc, a, base, np);
+                 uint32_t np) {
+	if(wide) hipLaunchKernelGGL((dp_fill_kernel<kDebug, kFused, true>), dim3(grid), dim3(64), 0, s, sc, a, base, np);
+	else hipLaunchKernelGGL((dp_fill_kernel<kDebug, kFused, false>), dim3(grid), dim3(64), 0, s, sc, a, base, np);
 }
 } // namespace
 
@@ -1144,7 +1133,7 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.fused[dbg ? 1 : 0][wide ? 1 : 0];
 		if(fb > groups_all) fb = groups_all;
 		if(dbg) launch_fill<true, true>(wide, fb, s, sc, a, 0u, a0.n);
-		else launch_fill<false, true>(wide, fb, s, sc, a, 0u, a0.n, dp_spread_lds(groups_all, a0.ncu));
+		else launch_fill<false, true>(wide, fb, s, sc, a, 0u, a0.n);
 	} else {
 		a.walk_scratch = a0.scratch + (size_t)a0.chunk_groups * kGroupBytes;
 		const uint32_t chunk = a0.chunk_groups * 64;
