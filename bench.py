@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--slots", type=int, default=1 << 17, help="bt2x-align --slots (reads in flight)")
     ap.add_argument("--replay-reads", type=int, default=1 << 20, help="reads whose GPU launches are replayed")
     ap.add_argument("--replay-steps", type=int, default=3)
+    ap.add_argument("--replay-slots", type=int, default=0,
+                    help="reads in flight while recording the replayed launches (0: the timed run's cohort, --slots/2)")
     ap.add_argument("--cpu-sample", type=int, default=800_000, help="reads of the reference CPU baseline")
     ap.add_argument("--cpu-sample-1t", type=int, default=40_000, help="reads of its 1-thread line")
     ap.add_argument("--no-cpu", action="store_true")
@@ -104,7 +106,7 @@ def mark(msg):
 
 def workload_key(args) -> str:
     return (f"c3|synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}|reads{args.reads}|R{args.read_len}|"
-            f"dpad{args.dpad}|replay{args.replay_reads}")
+            f"dpad{args.dpad}|replay{args.replay_reads}|inflight{args.replay_slots or max(1, args.slots // 2)}")
 
 
 def pmc_profile(args, kernel: str):
@@ -282,7 +284,7 @@ def replay(args, base, fq, rdir, gpu):
     # one cohort of the timed run's size in flight (--slots / 2, its pipeline's cohorts): the
     # replayed launches have the shapes the end-to-end run launches
     run_aligner(args, [ALIGN, "-x", base, "-U", fq, "-S", os.devnull, "--dpad", str(args.dpad), "-p",
-                       str(args.host_threads), "--slots", str(max(1, args.slots // 2)), "--dump", ddir,
+                       str(args.host_threads), "--slots", str(args.replay_slots or max(1, args.slots // 2)), "--dump", ddir,
                        "--no-pipeline"],
                 os.path.join(rdir, "dump.err"), "launch recording")
     launches = load_dumps(ddir)

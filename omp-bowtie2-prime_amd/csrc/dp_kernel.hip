@@ -65,6 +65,18 @@ __device__ __forceinline__ size_t tb_addr(int row, int col, int lane) {
 	return ((((size_t)(col >> 1) * kPairWords + (st >> 1)) * 64 + lane) << 2) + ((st & 1) << 1) + (col & 1);
 }
 
+// Byte offsets of diagonal moves in that layout: (r, 2p+1) -> (r-1, 2p) is -257 (same
+// pair, one step pair up, high column -> low), (r, 2p) -> (r-1, 2p-1) is kDiag1Even (one
+// column pair left); two diagonal moves are always kDiag2.
+constexpr int kDiag1Even = -(kPairWords * 256) + 1;
+constexpr int kDiag2 = -257 + kDiag1Even;
+__device__ __forceinline__ uint32_t tb_load(__amdgpu_buffer_rsrc_t src, uint32_t off) {
+	return __builtin_amdgcn_raw_buffer_load_b8(src, (int)off, 0, 0);   // out of range: 0
+}
+
+// true when no active lane has `c` set (a wave-uniform value)
+__device__ __forceinline__ bool wave_none(bool c) { return __builtin_amdgcn_ballot_w64(c) == 0; }
+
 // traceback flag bits (1 = the equality does NOT hold); TB_MM: read and reference
 // bases differ or either is N (the diagonal move records an edit)
 enum { TB_DNE = 1, TB_FNE = 2, TB_FONE = 4, TB_EONE = 8, TB_MM = 0x10, TB_MARK = 0x80 };
@@ -124,13 +136,98 @@ __device__ __forceinline__ uint32_t row_info(int rdc, bool gbar, int mm) {
 	return (uint32_t)rdc | (gbar ? 8u : 0u) | ((uint32_t)mm << 4);
 }
 
+// An edit whose characters are not looked up yet (the walk records row, type and
+// reference column only): pos | type << 12 | kEditPending | col << 16.
+constexpr uint32_t kEditPending = 0x8000u;
+__device__ __forceinline__ uint32_t pend_edit(int pos, int type, int col) {
+	return ((uint32_t)pos & 0x3ffu) | ((uint32_t)type << 12) | kEditPending | ((uint32_t)col << 16);
+}
+// the read row an edit refers to (a read gap is recorded at row + 1, aligner_sw's convention)
+__device__ __forceinline__ int pending_row(uint32_t e) {
+	return (int)(e & 0x3ffu) - ((((e >> 12) & 7u) == EDIT_READ_GAP) ? 1 : 0);
+}
+__device__ __forceinline__ uint32_t pending_chars_of(uint32_t e, int rdc, int refc) {
+	const int type = (int)((e >> 12) & 7u);
+	const uint32_t pos = e & 0x3ffu;
+	return type == EDIT_MM ? pack_edit(pos, EDIT_MM, mask_chr(refc), acgtn(rdc))
+	     : type == EDIT_REF_GAP ? pack_edit(pos, EDIT_REF_GAP, '-', acgtn(rdc))
+	                            : pack_edit(pos, EDIT_READ_GAP, mask_chr(refc), '-');
+}
+__device__ __forceinline__ uint32_t pending_chars(uint32_t e, const uint8_t* rd, const uint8_t* rf) {
+	return pending_chars_of(e, rd[pending_row(e)], rf[(e >> 16) & 0xffu]);
+}
+// Resolve the pending entries [0, ne) of a finished backtrace in place: characters, and
+// for mismatches the penalty (N: npen, else the quality's) and the N count the reference
+// accumulates as it walks (u8.cpp backtrace).  Eight entries per batch, loads together.
+__device__ __forceinline__ void resolve_edits(const DevScoring& sc, uint32_t* stage_ed, int lane, int ne,
+                                              const uint8_t* rd, const uint8_t* rf, const uint8_t* qu,
+                                              int* bscore, int* ns) {
+	for(int k0 = 0; k0 < ne; k0 += 8) {
+		uint32_t v[8];
+#pragma unroll
+		for(int u = 0; u < 8; u++) v[u] = stage_ed[(size_t)min(k0 + u, ne - 1) * 64 + lane];
+		int rdc[8], refc[8], q[8];
+#pragma unroll
+		for(int u = 0; u < 8; u++) {
+			const int r = pending_row(v[u]);
+			rdc[u] = rd[r]; refc[u] = rf[(v[u] >> 16) & 0xffu]; q[u] = qu[r];
+		}
+		int pen[8];
+#pragma unroll
+		for(int u = 0; u < 8; u++) {
+			const int q0 = q[u] - 33;
+			pen[u] = sc.mmpen[q0 < 0 ? 0 : (q0 > 255 ? 255 : q0)];
+		}
+#pragma unroll
+		for(int u = 0; u < 8; u++) {
+			if(k0 + u >= ne) break;
+			const uint32_t e = v[u];
+			if(!(e & kEditPending)) continue;                  // resolved already (gap-barrier rows)
+			if(((e >> 12) & 7u) == EDIT_MM) {
+				const bool amb = rdc[u] > 3 || refc[u] > 3;
+				*bscore -= amb ? sc.npen : pen[u];
+				*ns += amb ? 1 : 0;
+			}
+			stage_ed[(size_t)(k0 + u) * 64 + lane] = pending_chars_of(e, rdc[u], refc[u]);
+		}
+	}
+}
+
 // Copy the edit-buffer entries [0, hi) written by one nextAlignment call to the edits
-// arena; returns their offset (0 when nothing was written).
-__device__ __forceinline__ uint32_t publish_edbuf(const DpLaunch& a, const uint32_t* stage_ed, int lane, int hi) {
+// arena; returns their offset (0 when nothing was written).  A successful call's own
+// entries [0, ns) are still in walk order: they are published in ned() order -- reversed
+// (fw), or with positions mirrored over `extent` (the reverse-complement strand's
+// invertEdits, edit.cpp:50-78) -- which is exactly what the reference's buffer holds
+// after the call.  Eight entries per batch: the loads go out together instead of one
+// dependent round trip per entry.
+__device__ __forceinline__ uint32_t publish_edbuf(const DpLaunch& a, const uint32_t* stage_ed, int lane, int hi,
+                                                  const uint8_t* rd, const uint8_t* rf,
+                                                  int ns = 0, bool fw = true, int extent = 0) {
 	if(hi <= 0) return 0;
 	const uint32_t eo = atomicAdd(&a.counters[1], (uint32_t)hi);
-	if(eo + (uint32_t)hi <= a.edit_cap)
-		for(int k = 0; k < hi; k++) a.edits[eo + k] = stage_ed[(size_t)k * 64 + lane];
+	if(eo + (uint32_t)hi <= a.edit_cap) {
+		for(int k0 = 0; k0 < hi; k0 += 8) {
+			uint32_t v[8];
+#pragma unroll
+			for(int u = 0; u < 8; u++) {
+				const int k = min(k0 + u, hi - 1);
+				const int src = (k < ns && fw) ? ns - 1 - k : k;
+				v[u] = stage_ed[(size_t)src * 64 + lane];
+			}
+#pragma unroll
+			for(int u = 0; u < 8; u++) {
+				const int k = k0 + u;
+				if(k >= hi) break;
+				uint32_t e = v[u];
+				if(e & kEditPending) e = pending_chars(e, rd, rf);
+				if(k < ns && !fw) {
+					const uint32_t pos = (uint32_t)extent - (e & 0x3ffu) - (((e >> 12) & 7u) == 1u /*read gap*/ ? 0u : 1u);
+					e = (e & ~0x3ffu) | (pos & 0x3ffu);
+				}
+				a.edits[eo + k] = e;
+			}
+		}
+	}
 	return eo;
 }
 
@@ -139,7 +236,7 @@ __device__ __forceinline__ uint32_t publish_edbuf(const DpLaunch& a, const uint3
 // backtraced over the fill's traceback bytes; records and edits staged per lane.
 __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunch& a, uint32_t pi,
                                              int lane, uint8_t* gslot, uint32_t* stage_ed,
-                                             bt2x_aln_rec* stage_rec, unsigned long long& st_bt) {
+                                             bt2x_aln_rec* stage_rec, unsigned long long& st_bt, bool refN) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 	const uint32_t gl = (uint32_t)lane;
 	const __amdgpu_buffer_rsrc_t dirsrc =
@@ -222,93 +319,114 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 					row -= kb; col -= kb;
 					tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)tb_addr(row, col, gl), 0, 0);
 				}
+				// The walk reads one byte per step, each depending on the move decided from the
+				// last: a chain of cache-missing loads (the fill's bytes left L2 long ago).  Most
+				// moves are diagonal, so the bytes of the next kLook-1 cells down the current
+				// diagonal are kept in flight: a ring of registers (q0..q7, rotated by unrolling
+				// the step kLook times, never moved -- a move would wait for the load) refilled
+				// one cell per diagonal step, and reloaded from the new cell after a gap move.
+				// The current attempt never revisits its own cells and earlier attempts' marks
+				// were stored before these loads, so a ring byte is the byte the reference reads.
 				uint32_t bo = (uint32_t)tb_addr(row, col, gl);
-				while(true) {
-					st_bt++;
-					if(tb & TB_MARK) { ok = false; break; }         // reportedThrough
-					const int diag = col - row + (int)p.triml;
-					over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);
-					if(row == 0) {
-						__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)bo, 0, 0);
-						tb_end = tb;
-						break;
-					}
-					// the reference's fixed priority over the cell's flags (u8.cpp:843-990):
-					// H: diag > F (H-up / F-up) > E (H-left / E-left); E/F prefer the open
-					const uint32_t dne = tb & TB_DNE, fne = (tb >> 1) & 1u;
-					const uint32_t fext = (tb >> 2) & 1u, eext = (tb >> 3) & 1u;
-					const bool inH = ct == 2;
-					const bool isD = inH && !dne;
-					const bool isF = (ct == 1) || (inH && dne && !fne);
-					const int drow = (isD || isF) ? 1 : 0, dcol = isF ? 0 : 1;
-					const int nct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);
-					// byte-offset delta of the move (tb_addr's pair/step layout)
-					const int st = row + (col & 1);
-					const int dD = (col & 1) ? -257 : -(kPairWords * 256) + 1;
-					const int dU = (st & 1) ? -2 : -254;
-					const int dL = (col & 1) ? ((row & 1) ? -255 : -3) : ((row & 1) ? -(kPairWords * 256) + 255 : -(kPairWords * 256) + 3);
-					const uint32_t cbo = bo;
-					bo = (uint32_t)((int)bo + (isD ? dD : isF ? dU : dL));
-					const int crow = row, ccol = col;
-					row -= drow; col -= dcol; ct = nct;
-					const uint32_t ctb = tb;
-					tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)bo, 0, 0);
-					__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)cbo, 0, 0);   // setReportedThrough
-					if(crow == row0) mlo = ccol;
-					if(isD) {
-						if(ctb & TB_MM) {
-							const int rdc = rd[crow], refc = rf[ccol];
-							const bool amb = rdc > 3 || refc > 3;
-							const int q0 = (int)qu[crow] - 33;
-							const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
-							stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(refc), acgtn(rdc));
-							ne++;
-							bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
-							if(amb) ns++;
-						}
-					} else {
-						const bool open = nct == 2;
-						const uint32_t e = isF ? pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rd[crow]))
-						                       : pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(rf[ccol]), '-');
-						stage_ed[(size_t)ne * 64 + lane] = e;
-						ne++;
-						bscore -= isF ? (open ? rfo : rfe) : (open ? rdo : rde);
-						gaps++;
-					}
+				uint32_t q0 = tb, q1, q2, q3, q4, q5, q6, q7;
+				{
+					const int d1 = (col & 1) ? -257 : kDiag1Even;
+					q1 = tb_load(dirsrc, bo + d1);               q2 = tb_load(dirsrc, bo + kDiag2);
+					q3 = tb_load(dirsrc, bo + kDiag2 + d1);      q4 = tb_load(dirsrc, bo + 2 * kDiag2);
+					q5 = tb_load(dirsrc, bo + 2 * kDiag2 + d1);  q6 = tb_load(dirsrc, bo + 3 * kDiag2);
+					q7 = tb_load(dirsrc, bo + 3 * kDiag2 + d1);
 				}
+				bool fin = false;
+#define BT2X_WALK_STEP(T0, T1, T2, T3, T4, T5, T6, T7)                                                        \
+				{                                                                                     \
+					const uint32_t ctb = T0;                                                          \
+					uint32_t nbo = bo + 4 * kDiag2;  /* the next ring load; finished lanes: harmless */ \
+					if(fin) {}                                                                        \
+					else if(st_bt++, ctb & TB_MARK) { ok = false; fin = true; }  /* reportedThrough */ \
+					else {                                                                            \
+						const int diag = col - row + (int)p.triml;                                    \
+						over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);   \
+						if(row == 0) {                                                                \
+							__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)bo, 0, 0); \
+							tb_end = ctb;                                                             \
+							fin = true;                                                               \
+						} else {                                                                      \
+							/* the reference's fixed priority over the cell's flags (u8.cpp:843-990): \
+							   H: diag > F (H-up / F-up) > E (H-left / E-left); E/F prefer the open */ \
+							const uint32_t dne = ctb & TB_DNE, fne = (ctb >> 1) & 1u;                 \
+							const uint32_t fext = (ctb >> 2) & 1u, eext = (ctb >> 3) & 1u;            \
+							const bool inH = ct == 2;                                                 \
+							const bool isD = inH && !dne;                                             \
+							const bool isF = (ct == 1) || (inH && dne && !fne);                       \
+							const int nct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);          \
+							/* byte-offset deltas of the moves (tb_addr's pair/step layout) */        \
+							const int st = row + (col & 1);                                           \
+							const int dU = (st & 1) ? -2 : -254;                                      \
+							const int dL = (col & 1) ? ((row & 1) ? -255 : -3)                        \
+							                         : ((row & 1) ? kDiag1Even + 254 : kDiag1Even + 2); \
+							const uint32_t cbo = bo;                                                  \
+							const int crow = row, ccol = col;                                         \
+							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;                \
+							if(crow == row0) mlo = ccol;                                              \
+							/* the move's edit, characters (and a mismatch's penalty) resolved after  \
+							   the walk (resolve_edits): no read/reference loads in the chain */      \
+							if(!isD || (ctb & TB_MM)) {                                               \
+								stage_ed[(size_t)ne * 64 + lane] =                                    \
+									isD ? pend_edit(crow, EDIT_MM, ccol)                              \
+									    : isF ? pend_edit(crow, EDIT_REF_GAP, ccol) : pend_edit(crow + 1, EDIT_READ_GAP, ccol); \
+								ne++;                                                                 \
+							}                                                                         \
+							if(!isD) {                                                                \
+								const bool open = nct == 2;                                           \
+								bscore -= isF ? (open ? rfo : rfe) : (open ? rdo : rde);              \
+								gaps++;                                                               \
+							}                                                                         \
+							if(isD) {                                                                 \
+								bo = cbo + ((ccol & 1) ? -257 : kDiag1Even);                          \
+							} else {                                                                  \
+								bo = cbo + (isF ? dU : dL);                                           \
+								const int d1 = (col & 1) ? -257 : kDiag1Even;                         \
+								T1 = tb_load(dirsrc, bo);                  T2 = tb_load(dirsrc, bo + d1); \
+								T3 = tb_load(dirsrc, bo + kDiag2);         T4 = tb_load(dirsrc, bo + kDiag2 + d1); \
+								T5 = tb_load(dirsrc, bo + 2 * kDiag2);     T6 = tb_load(dirsrc, bo + 2 * kDiag2 + d1); \
+								T7 = tb_load(dirsrc, bo + 3 * kDiag2);     nbo = bo + 3 * kDiag2 + d1;    \
+							}                                                                         \
+							__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)cbo, 0, 0); /* setReportedThrough */ \
+						}                                                                             \
+					}                                                                                 \
+					/* one unconditional def per step: a load under a divergent branch would be \
+					   merged by a register copy, which waits for it */                          \
+					T0 = tb_load(dirsrc, nbo);                                                        \
+				}
+				// lanes that finish idle to the end of the wave's step: the exits are wave-uniform
+				// (no divergent loop exits, whose joins would copy -- and so wait for -- the
+				// ring registers)
+				while(true) {
+					BT2X_WALK_STEP(q0, q1, q2, q3, q4, q5, q6, q7) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q1, q2, q3, q4, q5, q6, q7, q0) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q2, q3, q4, q5, q6, q7, q0, q1) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q3, q4, q5, q6, q7, q0, q1, q2) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q4, q5, q6, q7, q0, q1, q2, q3) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q5, q6, q7, q0, q1, q2, q3, q4) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q6, q7, q0, q1, q2, q3, q4, q5) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q7, q0, q1, q2, q3, q4, q5, q6) if(wave_none(!fin)) break;
+				}
+#undef BT2X_WALK_STEP
 				if(!ok || !over_core) { hi = max(hi, ne); continue; }
 				if(tb_end & TB_MM) {                     // the final (row 0) cell
-					const int rdc = rd[row], refc = rf[col];
-					const bool amb = rdc > 3 || refc > 3;
-					const int q0 = (int)qu[row] - 33;
-					const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
-					stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
+					stage_ed[(size_t)ne * 64 + lane] = pend_edit(row, EDIT_MM, col);
 					ne++;
-					bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
-					if(amb) ns++;
 				}
+				resolve_edits(sc, stage_ed, lane, ne, rd, rf, qu, &bscore, &ns);
 				if(ns > p.nceil) { hi = max(hi, ne); continue; }
+				// reference Ns under the alignment: only windows holding an N (flagged by the
+				// fill) scan their columns
 				int refns = 0;
-				for(int k = col; k <= col0; k++) refns += (rf[k] > 3);
-				const int trimBeg = 0;
-				const int extent = R - trimBeg - (R - row0 - 1);
-				// the edit list in ned() order, in place: reverse(), pos -= trimBeg, and for
-				// the reverse-complement strand invertEdits() (reverse again, mirror pos;
-				// edit.cpp:50-78)
-				if(p.fw) {
-					for(int k = 0; k < ne / 2; k++) {
-						const uint32_t x = stage_ed[(size_t)k * 64 + lane];
-						stage_ed[(size_t)k * 64 + lane] = stage_ed[(size_t)(ne - 1 - k) * 64 + lane];
-						stage_ed[(size_t)(ne - 1 - k) * 64 + lane] = x;
-					}
-				} else {
-					for(int k = 0; k < ne; k++) {
-						const uint32_t e = stage_ed[(size_t)k * 64 + lane];
-						const uint32_t pos = (uint32_t)extent - ((e & 0x3ffu) - (uint32_t)trimBeg)
-						                     - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
-						stage_ed[(size_t)k * 64 + lane] = (e & ~0x3ffu) | (pos & 0x3ffu);
-					}
-				}
+				if(refN)
+					for(int k = col; k <= col0; k++) refns += (rf[k] > 3);
+				// trimBeg = 0; ned() order (reverse(), and for the reverse-complement strand
+				// invertEdits(), edit.cpp:50-78) is applied as the entries are published
+				const int extent = R - (R - row0 - 1);
 				hi = max(hi, ne);
 				found = true;
 				bt2x_aln_rec r;
@@ -316,7 +434,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				r.score = (int16_t)bscore; r.ns = (uint16_t)ns; r.gaps = (uint16_t)gaps;
 				r.nedit = (uint16_t)ne; r.bases_aligned = (uint16_t)(extent - ne);
 				r.refns = (uint16_t)refns; r.refoff = (int64_t)col + p.refl;
-				r.edit_off = publish_edbuf(a, stage_ed, lane, hi); r.nbuf = (uint32_t)hi;
+				r.edit_off = publish_edbuf(a, stage_ed, lane, hi, rd, rf, ne, p.fw != 0, extent); r.nbuf = (uint32_t)hi;
 				stage_rec[(size_t)nrec * 64 + lane] = r;
 				break;
 			}
@@ -324,7 +442,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				bt2x_aln_rec r;
 				r.ntries = (uint16_t)ntries; r.ok = 0; r.pad0 = 0; r.score = 0; r.ns = 0; r.gaps = 0;
 				r.nedit = 0; r.bases_aligned = 0; r.refns = 0; r.refoff = 0;
-				r.edit_off = publish_edbuf(a, stage_ed, lane, hi); r.nbuf = (uint32_t)hi;
+				r.edit_off = publish_edbuf(a, stage_ed, lane, hi, rd, rf); r.nbuf = (uint32_t)hi;
 				stage_rec[(size_t)nrec * 64 + lane] = r;
 				nrec++;
 				break;
@@ -746,6 +864,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const __amdgpu_buffer_rsrc_t dirsrc =
 			__builtin_amdgcn_make_buffer_rsrc(dir, 0, (int)(kDirBytesLane * 64u), 0x00020000);
 		int refa = C > 0 ? rf[0] : 4, refb = C > 1 ? rf[1] : 4;
+		uint32_t refN = 0;                              // an N in the window's columns [0, C)
 		for(int pp = 0; pp < npairs; pp++) {
 			const int j0 = 2 * pp;
 			// opaque per pair: keeps the per-step guards and last-row compares from being
@@ -767,6 +886,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			const uint32_t refc2 = (uint32_t)ca | ((uint32_t)cb << 16);
 			// N reference columns: every row pays the N penalty
 			const uint32_t coln = (ca > 3 ? 0x0000ffffu : 0u) | (cb > 3 ? 0xffff0000u : 0u);
+			refN |= ((ca > 3) & (j0 < C)) | ((cb > 3) & (j0 + 1 < C));
 			// traceback stores through a buffer resource: lane offset in a VGPR, the step
 			// offset in an SGPR (no per-store 64-bit address arithmetic)
 			const uint32_t pbase = (uint32_t)pp * kPairWords * 256u;
@@ -998,7 +1118,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		if(kFused) {
 			uint8_t* wslot = gslot + kGroupBytes;
 			walk_problem(sc, a, pi, lane, gslot, reinterpret_cast<uint32_t*>(wslot + kEditOff),
-			             reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt);
+			             reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0);
 		}
 	}
 	if(a.stats) {
@@ -1034,7 +1154,7 @@ dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const uint32_t q = grp * 64 + lane;
 		if(q < nprob) {
 			const uint32_t pi = base + q;
-			walk_problem(sc, a, pi, lane, a.scratch + (size_t)grp * kGroupBytes, stage_ed, stage_rec, st_bt);
+			walk_problem(sc, a, pi, lane, a.scratch + (size_t)grp * kGroupBytes, stage_ed, stage_rec, st_bt, true);
 		}
 	}
 	if(a.stats) {

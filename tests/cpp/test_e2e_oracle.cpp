@@ -237,6 +237,7 @@ int main(int argc, char** argv) {
 		const RunStats st = al.run(fq, stdout, slots, threads, &t_run);
 		const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 		getrusage(RUSAGE_SELF, &ru1);
+		if(std::getenv("SPROF_WAIT")) std::raise(SIGUSR2);   // ... and not the teardown
 		auto sec = [](const timeval& a, const timeval& b) { return (b.tv_sec - a.tv_sec) + (b.tv_usec - a.tv_usec) * 1e-6; };
 		std::fprintf(stderr, "HOST_TIMING rusage user=%.3f sys=%.3f minflt=%ld vcsw=%ld\n", sec(ru0.ru_utime, ru1.ru_utime),
 		             sec(ru0.ru_stime, ru1.ru_stime), ru1.ru_minflt - ru0.ru_minflt, ru1.ru_nvcsw - ru0.ru_nvcsw);

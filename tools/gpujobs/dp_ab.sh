@@ -1,0 +1,8 @@
+# DP replay A/B: ablations at cohort and whole-file shapes
+mkdir -p gpurun_out
+for s in 65536 1048576; do
+timeout -k 10 300 python -u tools/dp_replay.py --slots $s "" BT2X_DP_ABLATE=2 BT2X_DP_ABLATE=1 BT2X_DP_BAND=0 \
+  > gpurun_out/r03_dp_ab_$s.log 2>&1
+rc=$?; echo "slots $s rc=$rc"; grep -E "config|launches|Error|error" gpurun_out/r03_dp_ab_$s.log | tail -8
+[ $rc -eq 0 ] || exit $rc
+done

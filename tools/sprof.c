@@ -26,7 +26,7 @@
 static void* g_pc[MAXS][DEPTH];
 static atomic_int g_n;
 static volatile sig_atomic_t g_on = 1;          // SPROF_WAIT=1: off until the program raises SIGUSR2
-static void on_usr2(int sig) { (void)sig; g_on = 1; }
+static void on_usr2(int sig) { (void)sig; g_on = !g_on; }   // each SIGUSR2 toggles sampling
 
 static void on_prof(int sig, siginfo_t* si, void* uc_) {
 	(void)sig; (void)si;
