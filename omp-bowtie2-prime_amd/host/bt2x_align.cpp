@@ -495,6 +495,8 @@ void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, 
 		else if(sk.exitUnpair == Sink::EXIT_WITH_ALIGNMENTS) nunpair = std::min<uint64_t>(sk.n, 1);
 	}
 	o.clear();
+	// one allocation per record at most (name, SEQ, QUAL, CIGAR/MD and the tags)
+	o.reserve(rd.name.size() + 2 * rd.length() + 384);
 	append_name(o, rd.name);
 	if(nunpair == 0) {
 		*aligned = false; *rep = unpairMax;

@@ -337,8 +337,12 @@ public:
 	bool overlap(const AlnRes& r, const uint32_t* ned, size_t n) {
 		if(alns_.empty()) return false;
 		rows(r, ned, n, tmp_);
+		// the runs of each row lie inside the alignment's reference span [lo, hi): spans that
+		// do not meet rule a pair out without the per-row scan (a repetitive read reports
+		// many alignments at distinct loci; the scan over all of them was quadratic)
+		const int64_t lo = span_lo(tmp_), hi = span_hi(tmp_);
 		for(const Aln& a : alns_) {
-			if(a.refid != r.refid || a.fw != r.fw) continue;
+			if(a.refid != r.refid || a.fw != r.fw || a.hi <= lo || hi <= a.lo) continue;
 			const int64_t* o = runs_.data() + a.run0;
 			for(size_t i = 0; i < rdlen_; i++) {
 				const int64_t l = std::max(o[2 * i], tmp_[2 * i]), rr = std::min(o[2 * i + 1], tmp_[2 * i + 1]);
@@ -349,11 +353,15 @@ public:
 	}
 	void add(const AlnRes& r, const uint32_t* ned, size_t n) {
 		rows(r, ned, n, tmp_);
-		alns_.push_back({r.refid, r.fw, runs_.size()});
+		alns_.push_back({r.refid, r.fw, runs_.size(), span_lo(tmp_), span_hi(tmp_)});
 		runs_.insert(runs_.end(), tmp_.begin(), tmp_.end());
 	}
 private:
-	struct Aln { int64_t refid; bool fw; size_t run0; };
+	struct Aln { int64_t refid; bool fw; size_t run0; int64_t lo, hi; };
+	// rows' runs move right monotonically (left_{i+1} >= left_i): the first row's left and
+	// the last row's right bound every run
+	int64_t span_lo(const std::vector<int64_t>& t) const { return rdlen_ ? t[0] : 0; }
+	int64_t span_hi(const std::vector<int64_t>& t) const { return rdlen_ ? t[2 * rdlen_ - 1] : 0; }
 	void rows(const AlnRes& r, const uint32_t* ned0, size_t n, std::vector<int64_t>& out) {
 		const uint32_t* ned = ned0;
 		if(!r.fw) { invert_poss(ned0, n, rdlen_, inv_); ned = inv_.data(); }

@@ -213,22 +213,22 @@ int main(int argc, char** argv) {
 	be.fail_at = inject;
 	if(host_timing) {
 		ReplayBackend rb(&be);
+		// one aligner for the recording pass and the timed replays, as bt2x-align keeps one
+		// for its --warmup-files run and the timed run (pooled read contexts, warm heap)
+		Aligner al(p, ref, rb);
+		al.set_pipeline(pipeline);
+		al.set_gpu_round(gpu_round);
 		{
-			Aligner al0(p, ref, rb);
-			al0.set_pipeline(pipeline);
-			al0.set_gpu_round(gpu_round);
 			FastqReader fq(files, shard, nshards);
 			std::FILE* nul = std::fopen("/dev/null", "wb");
-			al0.run(fq, nul, slots, threads);
+			al.run(fq, nul, slots, threads);
 			std::fclose(nul);
 		}
 		for(int rep = 0; rep < reps; rep++) {
 		rb.rewind();
-		if(std::getenv("SPROF_WAIT")) std::raise(SIGUSR2);   // tools/sprof.c: profile the replay only
-		// the timed run starts from an empty context pool, as bt2x-align does
-		Aligner al(p, ref, rb);
-		al.set_pipeline(pipeline);
-		al.set_gpu_round(gpu_round);
+		// tools/sprof.c: profile the replay only (SPROF_SKIP=k: not the first k replays)
+		const bool prof = std::getenv("SPROF_WAIT") && rep >= (std::getenv("SPROF_SKIP") ? std::atoi(std::getenv("SPROF_SKIP")) : 0);
+		if(prof) std::raise(SIGUSR2);
 		FastqReader fq(files, shard, nshards);
 		struct rusage ru0, ru1;
 		getrusage(RUSAGE_SELF, &ru0);
@@ -237,7 +237,7 @@ int main(int argc, char** argv) {
 		const RunStats st = al.run(fq, stdout, slots, threads, &t_run);
 		const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 		getrusage(RUSAGE_SELF, &ru1);
-		if(std::getenv("SPROF_WAIT")) std::raise(SIGUSR2);   // ... and not the teardown
+		if(prof) std::raise(SIGUSR2);   // ... and not the teardown
 		auto sec = [](const timeval& a, const timeval& b) { return (b.tv_sec - a.tv_sec) + (b.tv_usec - a.tv_usec) * 1e-6; };
 		std::fprintf(stderr, "HOST_TIMING rusage user=%.3f sys=%.3f minflt=%ld vcsw=%ld\n", sec(ru0.ru_utime, ru1.ru_utime),
 		             sec(ru0.ru_stime, ru1.ru_stime), ru1.ru_minflt - ru0.ru_minflt, ru1.ru_nvcsw - ru0.ru_nvcsw);
