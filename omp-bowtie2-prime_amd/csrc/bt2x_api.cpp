@@ -163,7 +163,7 @@ struct bt2x_ctx {
 	// to resolve, per-lane workspace)
 	DevBuf b_rin, b_exr, b_rout, b_sats, b_elts, b_exro, b_used, b_sout, b_rows, b_ws, b_jobs, b_ranges, b_rcnt;
 	const uint32_t* d_resolve_n = nullptr;     // element count of the last round's resolve (HBM)
-	DevBuf scratch, b_fail, b_in2, b_win;         // + DP windows cut from the text (BT2X_DP_REF_TEXT)
+	DevBuf scratch, b_fail, b_heavy, b_in2, b_win;         // + DP windows cut from the text (BT2X_DP_REF_TEXT)
 	uint64_t npat = 0;
 	bool exact_best = true;                    // BT2X_OPT_EXACT_BEST
 	int ncu = 0;
@@ -178,7 +178,7 @@ struct bt2x_ctx {
 bt2x_ctx::~bt2x_ctx() {
 	(void)hipSetDevice(device);
 	if(stream) (void)hipStreamSynchronize(stream);
-	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch, &b_fail,
+	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch, &b_fail, &b_heavy,
 	                 &b_in2, &b_win,
 	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws,
 	                 &b_jobs, &b_ranges, &b_rcnt})
@@ -319,8 +319,8 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	bt2x_scoring s;
 	if(sc) s = *sc; else bt2x_scoring_default(&s);
 	c->sc = to_dev(s);
-	HIPCHK(hipMalloc((void**)&c->d_stats, 16 * sizeof(unsigned long long)));
-	HIPCHK(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
+	HIPCHK(hipMalloc((void**)&c->d_stats, 32 * sizeof(unsigned long long)));
+	HIPCHK(hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)));
 	HIPCHK(hipMalloc((void**)&c->d_counters, 16 * sizeof(uint32_t)));
 	hipDeviceProp_t prop;
 	HIPCHK(hipGetDeviceProperties(&prop, device));
@@ -476,6 +476,19 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	{ const char* bd = getenv("BT2X_DP_BAND"); a.band = (bd && bd[0] == '0') ? 0u : 1u; }
 	a.wide = (launch_flags & BT2X_DPL_I16) ? 1u : 0u;
 	a.fail_list = exact ? (uint32_t*)c->b_fail.p : nullptr;
+	// lane-kernel walks past `heavy` steps are redone by the wave kernel, traceback in LDS
+	// (BT2X_DP_HEAVY=0: never); read per launch (tests switch it)
+	{
+		const char* hv = getenv("BT2X_DP_HEAVY");
+		a.heavy = hv ? (uint32_t)atol(hv) : 1024u;
+		if(a.heavy && !d_debug) {
+			if((rc = c->b_heavy.ensure(sizeof(uint32_t) * ((size_t)n + 1)))) return rc;
+			a.heavy_list = (uint32_t*)c->b_heavy.p;
+			HIPCHK(hipMemsetAsync(a.heavy_list, 0, sizeof(uint32_t), s));
+		}
+	}
+	static const bool prof = [] { const char* e = getenv("BT2X_DP_PROF"); return e && e[0] == '1'; }();
+	if(prof) { a.prof = c->d_stats + 16; HIPCHK(hipMemsetAsync(a.prof, 0, 11 * sizeof(unsigned long long), s)); }
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
 	if(launch_flags & BT2X_DPL_REF_TEXT) {
 		if(!c->ix.text || !c->ix.rstarts) return BT2X_E_ARG;
@@ -488,6 +501,19 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	}
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));
+	if(prof) {                                   // development: where a lane-kernel wave's time goes
+		unsigned long long pv[11];
+		HIPCHK(hipStreamSynchronize(s));
+		HIPCHK(hipMemcpy(pv, a.prof, sizeof pv, hipMemcpyDeviceToHost));
+		float ms = 0;
+		hipEventElapsedTime(&ms, c->ev[BT2X_K_DP][0], c->ev[BT2X_K_DP][1]);
+		uint32_t nheavy = 0;
+		if(a.heavy_list) HIPCHK(hipMemcpy(&nheavy, a.heavy_list, sizeof nheavy, hipMemcpyDeviceToHost));
+		std::fprintf(stderr, "BT2X_DP_PROF n=%u ms=%.3f groups=%llu fill_cyc=%llu walk_cyc=%llu walk_steps=%llu cand_iters=%llu "
+		             "max_wave_cyc=%llu max_fill_cyc=%llu max_walk_cyc=%llu heavy=%u lane_work_sum=%llu "
+		             "wave_lane_max_sum=%llu lane_max=%llu\n",
+		             n, ms, pv[4], pv[0], pv[1], pv[2], pv[3], pv[5], pv[6], pv[7], nheavy, pv[8], pv[9], pv[10]);
+	}
 	c->ev_valid[BT2X_K_DP] = true;
 	c->n_dp_last = n;
 	return rc;

@@ -103,6 +103,11 @@ struct DpLaunch {
 	uint32_t wide;                 // 1: the 16-bit lane kernels (some problem is BT2X_DP_I16)
 	uint32_t* fail_list;           // n entries, or NULL: queue the banded fill's failed problems for
 	                               // the exact-best pass (BT2X_DPL_EXACT_BEST)
+	uint32_t* heavy_list;          // [0]: count, then problem indices: problems whose walk the lane
+	                               // kernel hands to the wave kernel (more than `heavy` candidates)
+	uint32_t heavy;
+	unsigned long long* prof;      // development (BT2X_DP_PROF=1): lane-kernel fill cycles, walk
+	                               // cycles, walk wave-steps, candidate wave-iterations, groups
 };
 size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups);
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream);

@@ -74,6 +74,11 @@ __device__ __forceinline__ uint32_t tb_load(__amdgpu_buffer_rsrc_t src, uint32_t
 	return __builtin_amdgcn_raw_buffer_load_b8(src, (int)off, 0, 0);   // out of range: 0
 }
 
+// 1 in the lowest active lane, else 0 (summed over lanes: wave iterations)
+__device__ __forceinline__ unsigned first_active(int lane) {
+	const uint64_t e = __builtin_amdgcn_read_exec();
+	return (e & (~e + 1)) == (1ull << lane) ? 1u : 0u;
+}
 // true when no active lane has `c` set (a wave-uniform value)
 __device__ __forceinline__ bool wave_none(bool c) { return __builtin_amdgcn_ballot_w64(c) == 0; }
 
@@ -236,7 +241,8 @@ __device__ __forceinline__ uint32_t publish_edbuf(const DpLaunch& a, const uint3
 // backtraced over the fill's traceback bytes; records and edits staged per lane.
 __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunch& a, uint32_t pi,
                                              int lane, uint8_t* gslot, uint32_t* stage_ed,
-                                             bt2x_aln_rec* stage_rec, unsigned long long& st_bt, bool refN) {
+                                             bt2x_aln_rec* stage_rec, unsigned long long& st_bt, bool refN,
+                                             unsigned long long* pw = nullptr) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 	const uint32_t gl = (uint32_t)lane;
 	const __amdgpu_buffer_rsrc_t dirsrc =
@@ -252,14 +258,35 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 		const int ncand = o.ncand;
 		const int row0 = R - 1;
 		int ndone = 0, nrec = 0;
-		// Candidate starts are fetched ahead: the next candidate's column two attempts early
-		// and its start byte one attempt early.  A byte fetched before the attempt in
-		// between reflects every earlier attempt's marks; that attempt's own marks in the
-		// start row are the columns [mlo, mhi] it left behind (start-row moves go left only).
+		// Step budget (a.heavy; 0: none).  A walk runs one chain of HBM round trips per
+		// step, and at cohort launch sizes (about one group per wave) its wave, and so
+		// the launch, waits for its longest lane: a problem past the budget (a repeat
+		// walked attempt after attempt) is dropped here -- nothing of it is kept but
+		// edit-arena space -- and redone by the wave kernel with its traceback in LDS.
+		const int budget = (a.heavy_list && a.heavy) ? (int)a.heavy : 0x7fffffff;
+		int steps = 0;
+		bool aborted = false;
+		// Candidate starts are fetched ahead: the next candidate's column two attempts early,
+		// and the bytes of its first eight cells down its diagonal (its start cell first) one
+		// attempt early -- the walk's ring (below) for that attempt, so a short attempt (most
+		// are: they run into an earlier path's marks within a few cells) waits on nothing.
+		// Bytes fetched before the attempt in between reflect every earlier attempt's marks;
+		// that attempt's own marks on those cells are recorded in `cmask` (bit i: the cell i
+		// rows up the diagonal) and applied when the ring is taken.
 		int c_next = cands[gl];
-		uint32_t b_next = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)tb_addr(row0, c_next, gl), 0, 0);
+		uint32_t n0, n1, n2, n3, n4, n5, n6, n7;
+#define BT2X_RING_LOAD(A0, A1, A2, A3, A4, A5, A6, A7, BO, COL)                                          \
+		{                                                                                         \
+			const uint32_t bo_ = (BO);                                                            \
+			const int d1_ = ((COL) & 1) ? -257 : kDiag1Even;                                      \
+			A0 = tb_load(dirsrc, bo_);                      A1 = tb_load(dirsrc, bo_ + d1_);      \
+			A2 = tb_load(dirsrc, bo_ + kDiag2);             A3 = tb_load(dirsrc, bo_ + kDiag2 + d1_); \
+			A4 = tb_load(dirsrc, bo_ + 2 * kDiag2);         A5 = tb_load(dirsrc, bo_ + 2 * kDiag2 + d1_); \
+			A6 = tb_load(dirsrc, bo_ + 3 * kDiag2);         A7 = tb_load(dirsrc, bo_ + 3 * kDiag2 + d1_); \
+		}
+		BT2X_RING_LOAD(n0, n1, n2, n3, n4, n5, n6, n7, (uint32_t)tb_addr(row0, c_next, gl), c_next)
 		int c_next2 = ncand > 1 ? cands[64 + gl] : 0;
-		int mlo = 1, mhi = 0;                                  // last attempt's start-row marks
+		uint32_t cmask = 0;                                    // last attempt's marks on the next ring
 		// stage_ed doubles as the reference's per-read edit buffer (SwResult::alres.ned_,
 		// bt2x.h "edit-buffer image"): attempts write it from index 0, a success leaves its
 		// final list there; hi = entries written during the current call.
@@ -267,16 +294,23 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 			int ntries = 0, hi = 0;
 			bool found = false;
 			while(ndone < ncand) {
+				if(pw) pw[1] += first_active(lane);       // development counters (BT2X_DP_PROF)
 				const int col0 = c_next;
-				uint32_t tb = b_next;
-				if(col0 >= mlo && col0 <= mhi) tb = TB_MARK;
+				const uint32_t M = TB_MARK;
+				uint32_t q0 = n0 | ((cmask & 1u) ? M : 0u), q1 = n1 | ((cmask & 2u) ? M : 0u);
+				uint32_t q2 = n2 | ((cmask & 4u) ? M : 0u), q3 = n3 | ((cmask & 8u) ? M : 0u);
+				uint32_t q4 = n4 | ((cmask & 16u) ? M : 0u), q5 = n5 | ((cmask & 32u) ? M : 0u);
+				uint32_t q6 = n6 | ((cmask & 64u) ? M : 0u), q7 = n7 | ((cmask & 128u) ? M : 0u);
+				const uint32_t tb = q0;
 				ndone++;
+				int dnx = -(1 << 20);                              // the next candidate's diagonal
 				if(ndone < ncand) {
 					c_next = c_next2;
-					b_next = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)tb_addr(row0, c_next, gl), 0, 0);
+					dnx = c_next - row0;
+					BT2X_RING_LOAD(n0, n1, n2, n3, n4, n5, n6, n7, (uint32_t)tb_addr(row0, c_next, gl), c_next)
 					if(ndone + 1 < ncand) c_next2 = cands[(size_t)(ndone + 1) * 64 + gl];
 				}
-				mlo = 1; mhi = 0;
+				cmask = 0;
 				// candidate start cell already traversed -> skipped, no RNG draw
 				if(tb & TB_MARK) continue;
 				ntries++;
@@ -285,69 +319,31 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				int row = row0, col = col0, ct = 2 /*H*/, bscore = 0, ns = 0, gaps = 0, ne = 0;
 				bool over_core = false, ok = true;
 				uint32_t tb_end = 0;
-				mlo = col0; mhi = col0;
-				// One dependent load per step: the next cell's byte is issued before this
-				// cell's mark store, so the in-order vmcnt never waits on a store.  Moves are
-				// decided branch-free and the byte offset is updated incrementally (32-bit,
-				// buffer addressing); read/reference/quality bytes only where TB_MM says an
-				// edit is recorded.
-				// The bottom gap-barrier rows (R-gapbar .. R-1) hold no E or F (open and extend
-				// are barred there, E[i][0] = 0), so every cell there has h == d and the walk
-				// moves diagonally; and no earlier attempt has marked these cells (an attempt
-				// enters them only from its own start cell, and each start column is tried
-				// once).  Those moves need no traceback byte: only their mismatch edits, from
-				// independent loads of read and reference bytes.  Their marks are never read,
-				// so they are not written.
-				const int kb = min(min(sc.gapbar, row0), col0);
-				if(kb > 0) {
-					const int diag = col0 - row0 + (int)p.triml;
-					over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);
-					for(int t = 0; t < kb; t++) {
-						const int crow = row0 - t, ccol = col0 - t;
-						const int rdc = rd[crow], refc = rf[ccol];
-						if(rdc != refc || rdc > 3 || refc > 3) {
-							const bool amb = rdc > 3 || refc > 3;
-							const int q0 = (int)qu[crow] - 33;
-							const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
-							stage_ed[(size_t)ne * 64 + lane] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(refc), acgtn(rdc));
-							ne++;
-							bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
-							if(amb) ns++;
-						}
-					}
-					st_bt += (unsigned long long)kb;
-					row -= kb; col -= kb;
-					tb = __builtin_amdgcn_raw_buffer_load_b8(dirsrc, (int)tb_addr(row, col, gl), 0, 0);
-				}
 				// The walk reads one byte per step, each depending on the move decided from the
 				// last: a chain of cache-missing loads (the fill's bytes left L2 long ago).  Most
-				// moves are diagonal, so the bytes of the next kLook-1 cells down the current
-				// diagonal are kept in flight: a ring of registers (q0..q7, rotated by unrolling
-				// the step kLook times, never moved -- a move would wait for the load) refilled
-				// one cell per diagonal step, and reloaded from the new cell after a gap move.
-				// The current attempt never revisits its own cells and earlier attempts' marks
-				// were stored before these loads, so a ring byte is the byte the reference reads.
+				// moves are diagonal (all of them in the bottom gap-barrier rows, which hold no E
+				// or F), so the bytes of the next seven cells down the current diagonal are kept
+				// in flight: a ring of registers (q0..q7, rotated by unrolling the step kLook
+				// times, never moved -- a move would wait for the load) refilled one cell per
+				// diagonal step, and reloaded from the new cell after a gap move.  The current
+				// attempt never revisits its own cells and earlier attempts' marks were stored
+				// before these loads (or are patched in from cmask), so a ring byte is the byte
+				// the reference reads.
 				uint32_t bo = (uint32_t)tb_addr(row, col, gl);
-				uint32_t q0 = tb, q1, q2, q3, q4, q5, q6, q7;
-				{
-					const int d1 = (col & 1) ? -257 : kDiag1Even;
-					q1 = tb_load(dirsrc, bo + d1);               q2 = tb_load(dirsrc, bo + kDiag2);
-					q3 = tb_load(dirsrc, bo + kDiag2 + d1);      q4 = tb_load(dirsrc, bo + 2 * kDiag2);
-					q5 = tb_load(dirsrc, bo + 2 * kDiag2 + d1);  q6 = tb_load(dirsrc, bo + 3 * kDiag2);
-					q7 = tb_load(dirsrc, bo + 3 * kDiag2 + d1);
-				}
 				bool fin = false;
 #define BT2X_WALK_STEP(T0, T1, T2, T3, T4, T5, T6, T7)                                                        \
 				{                                                                                     \
 					const uint32_t ctb = T0;                                                          \
 					uint32_t nbo = bo + 4 * kDiag2;  /* the next ring load; finished lanes: harmless */ \
 					if(fin) {}                                                                        \
+					else if(++steps > budget) { ok = false; fin = true; aborted = true; }             \
 					else if(st_bt++, ctb & TB_MARK) { ok = false; fin = true; }  /* reportedThrough */ \
 					else {                                                                            \
 						const int diag = col - row + (int)p.triml;                                    \
 						over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);   \
 						if(row == 0) {                                                                \
 							__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)bo, 0, 0); \
+							if(col == dnx && row0 < 8) cmask |= 1u << row0;                           \
 							tb_end = ctb;                                                             \
 							fin = true;                                                               \
 						} else {                                                                      \
@@ -367,7 +363,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 							const uint32_t cbo = bo;                                                  \
 							const int crow = row, ccol = col;                                         \
 							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;                \
-							if(crow == row0) mlo = ccol;                                              \
+							if(ccol - crow == dnx && row0 - crow < 8) cmask |= 1u << (row0 - crow);   \
 							/* the move's edit, characters (and a mismatch's penalty) resolved after  \
 							   the walk (resolve_edits): no read/reference loads in the chain */      \
 							if(!isD || (ctb & TB_MM)) {                                               \
@@ -402,6 +398,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				// (no divergent loop exits, whose joins would copy -- and so wait for -- the
 				// ring registers)
 				while(true) {
+					if(pw) pw[0] += first_active(lane);
 					BT2X_WALK_STEP(q0, q1, q2, q3, q4, q5, q6, q7) if(wave_none(!fin)) break;
 					BT2X_WALK_STEP(q1, q2, q3, q4, q5, q6, q7, q0) if(wave_none(!fin)) break;
 					BT2X_WALK_STEP(q2, q3, q4, q5, q6, q7, q0, q1) if(wave_none(!fin)) break;
@@ -412,6 +409,8 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 					BT2X_WALK_STEP(q7, q0, q1, q2, q3, q4, q5, q6) if(wave_none(!fin)) break;
 				}
 #undef BT2X_WALK_STEP
+#undef BT2X_RING_LOAD
+				if(aborted) break;
 				if(!ok || !over_core) { hi = max(hi, ne); continue; }
 				if(tb_end & TB_MM) {                     // the final (row 0) cell
 					stage_ed[(size_t)ne * 64 + lane] = pend_edit(row, EDIT_MM, col);
@@ -438,6 +437,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				stage_rec[(size_t)nrec * 64 + lane] = r;
 				break;
 			}
+			if(aborted) break;
 			if(!found) {
 				bt2x_aln_rec r;
 				r.ntries = (uint16_t)ntries; r.ok = 0; r.pad0 = 0; r.score = 0; r.ns = 0; r.gaps = 0;
@@ -448,6 +448,10 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 				break;
 			}
 			nrec++;
+		}
+		if(aborted) {                                 // the wave kernel redoes the whole call
+			a.heavy_list[1 + atomicAdd(&a.heavy_list[0], 1u)] = pi;
+			return;
 		}
 		const uint32_t ro = atomicAdd(&a.counters[0], (uint32_t)nrec);
 		if(ro + (uint32_t)nrec <= a.rec_cap)
@@ -485,23 +489,29 @@ __device__ __forceinline__ void dp_verdict(bool i16, int lrmax, int minsc, int n
 	else { status = ncand > 0 ? 1 : 0; best = score; }
 }
 
-// kBestOnly: the exact `best` of the problems the banded lane kernel failed
-// (a.fail_list[0 .. a.counters[2])): the whole rectangle's last-row maximum, nothing else.
-template<bool kBestOnly>
+// kMode 0: every problem of the launch.  kMode 1 (kBestOnly): the exact `best` of the
+// problems the banded lane kernel failed (a.fail_list[0 .. a.counters[2])): the whole
+// rectangle's last-row maximum, nothing else.  kMode 2: the problems the lane kernel handed
+// over after its fill (a.heavy_list): the whole call, their walks at LDS latency.
+template<int kMode>
 __global__ void __launch_bounds__(64)
 dp_wave_kernel(DevScoring sc, DpLaunch a) {
+	constexpr bool kBestOnly = kMode == 1;
 	__shared__ uint32_t tbw[kBestOnly ? 1 : kWaveTbWords];
 	__shared__ uint8_t refw[kCols], cands[kCols];
 	__shared__ uint16_t lastrow[kCols];
 	__shared__ uint32_t stage_ed[kBestOnly ? 1 : kEditStage];
+	// the walk's read codes and per-row mismatch penalties (quality -> mmpen), at LDS latency
+	__shared__ uint8_t rdw[kBestOnly ? 1 : kRows];
+	__shared__ uint16_t penw[kBestOnly ? 1 : kRows];
 	uint8_t* tbb = reinterpret_cast<uint8_t*>(tbw);
 	const int lane = threadIdx.x;
 	bt2x_aln_rec* stage_rec = kBestOnly ? nullptr : reinterpret_cast<bt2x_aln_rec*>(a.scratch + (size_t)blockIdx.x * kWaveRecStageBytes);
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0;
 	const uint32_t rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
-	const uint32_t nwork = kBestOnly ? min(a.counters[2], a.n) : a.n;
+	const uint32_t nwork = kMode == 1 ? min(a.counters[2], a.n) : kMode == 2 ? min(a.heavy_list[0], a.n) : a.n;
 	for(uint32_t k = blockIdx.x; k < nwork; k += gridDim.x) {
-		const uint32_t pi = kBestOnly ? a.fail_list[k] : k;
+		const uint32_t pi = kMode == 1 ? a.fail_list[k] : kMode == 2 ? a.heavy_list[1 + k] : k;
 		const bt2x_dp_in p = a.in[pi];
 		const int R = p.rdlen, C = p.ncol;
 		const bool i16 = (p.flags & BT2X_DP_I16) != 0;
@@ -512,6 +522,12 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 		const int L = (R + 3) >> 2;                 // lanes holding rows
 		const int S = 4 * L;                        // bytes per traceback column
 		for(int j = lane; j < C; j += 64) refw[j] = rf[j];
+		if(!kBestOnly)
+			for(int i = lane; i < R; i += 64) {
+				const int q0 = (int)qu[i] - 33;
+				rdw[i] = rd[i];
+				penw[i] = (uint16_t)sc.mmpen[q0 < 0 ? 0 : (q0 > 255 ? 255 : q0)];
+			}
 		// this lane's rows: read code (7 = N), mismatch penalty, gap-barred open/extend
 		uint32_t rc[4], mm[4], rdoe[4], rfoe[4], rfee[4];
 #pragma unroll
@@ -589,8 +605,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			__syncthreads();
 			continue;
 		}
-		st_cells += (unsigned long long)R * C;
-		st_cols += C;
+		if(kMode == 0) { st_cells += (unsigned long long)R * C; st_cols += C; }   // (mode 2: the lane kernel counted them)
 		bt2x_dp_out o;
 		o.nrec = 0; o.rec_off = 0;
 		o.status = status; o.best = best; o.ncand = status ? (uint16_t)nc : (uint16_t)0;
@@ -649,17 +664,15 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 							tbb[cbo] = (uint8_t)TB_MARK;               // setReportedThrough
 							if(isD) {
 								if(ctb & TB_MM) {
-									const int rdc = rd[crow], refc = refw[ccol];
+									const int rdc = rdw[crow], refc = refw[ccol];
 									const bool amb = rdc > 3 || refc > 3;
-									const int q0 = (int)qu[crow] - 33;
-									const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
 									stage_ed[ne++] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(refc), acgtn(rdc));
-									bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
+									bscore -= amb ? sc.npen : (int)penw[crow];
 									if(amb) ns++;
 								}
 							} else {
 								const bool open = nct == 2;
-								stage_ed[ne++] = isF ? pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rd[crow]))
+								stage_ed[ne++] = isF ? pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rdw[crow]))
 								                     : pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(refw[ccol]), '-');
 								bscore -= isF ? (open ? rfo_ : rfe_) : (open ? rdo_ : rde_);
 								gaps++;
@@ -667,12 +680,10 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 						}
 						if(!ok || !over_core) { hi = max(hi, ne); continue; }
 						if(tb_end & TB_MM) {
-							const int rdc = rd[row], refc = refw[col];
+							const int rdc = rdw[row], refc = refw[col];
 							const bool amb = rdc > 3 || refc > 3;
-							const int q0 = (int)qu[row] - 33;
-							const int qq = q0 < 0 ? 0 : (q0 > 255 ? 255 : q0);
 							stage_ed[ne++] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
-							bscore -= amb ? sc.npen : (int)sc.mmpen[qq];
+							bscore -= amb ? sc.npen : (int)penw[row];
 							if(amb) ns++;
 						}
 						if(ns > p.nceil) { hi = max(hi, ne); continue; }
@@ -734,10 +745,12 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 		__syncthreads();
 	}
 	if(!kBestOnly && a.stats && lane == 0) {
-		atomicAdd(&a.stats[0], st_cells);
-		atomicAdd(&a.stats[1], st_cols);
+		if(kMode == 0) {
+			atomicAdd(&a.stats[0], st_cells);
+			atomicAdd(&a.stats[1], st_cols);
+			atomicAdd(&a.stats[3], st_cells);          // whole rectangles
+		}
 		atomicAdd(&a.stats[2], st_bt);
-		atomicAdd(&a.stats[3], st_cells);              // whole rectangles
 	}
 }
 
@@ -763,7 +776,11 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 	const uint32_t one2 = opaque(0x00010001u);
 
+	unsigned long long pw[2] = {0, 0}, t_fill = 0, t_walk = 0, ngrp = 0;     // BT2X_DP_PROF
+	unsigned long long mx_fill = 0, mx_walk = 0, mylen_sum = 0, mylen_max = 0;
+	const unsigned long long t_start = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
+		const unsigned long long t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 		uint8_t* gslot = kFused ? a.scratch + (size_t)blockIdx.x * (kGroupBytes + kWalkSlotBytes)
 		                        : a.scratch + (size_t)grp * kGroupBytes;
 		uint32_t* dir = reinterpret_cast<uint32_t*>(gslot + kDirOff);
@@ -1117,8 +1134,32 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			for(int k = ncand; k < kCols; k++) a.cands[(size_t)pi * kCols + k] = 0xffffffffu;
 		if(kFused) {
 			uint8_t* wslot = gslot + kGroupBytes;
+			const unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+			const unsigned long long bt0 = st_bt;
 			walk_problem(sc, a, pi, lane, gslot, reinterpret_cast<uint32_t*>(wslot + kEditOff),
-			             reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0);
+			             reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, a.prof ? pw : nullptr);
+			if(a.prof) {
+				const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+				t_fill += t1 - t0; t_walk += t2 - t1; ngrp++;
+				mx_fill = max(mx_fill, t1 - t0); mx_walk = max(mx_walk, t2 - t1);
+				// this lane's serial work (walk steps + candidates) and the wave's maximum of it
+				mylen_sum += st_bt - bt0 + (unsigned long long)ncand;
+				mylen_max = max(mylen_max, st_bt - bt0 + (unsigned long long)ncand);
+			}
+		}
+	}
+	if(a.prof) {
+		unsigned long long w0 = pw[0], w1 = pw[1], ls = mylen_sum, lm = mylen_max;
+		for(int d = 32; d > 0; d >>= 1) {
+			w0 += __shfl_xor(w0, d); w1 += __shfl_xor(w1, d); ls += __shfl_xor(ls, d);
+			const unsigned long long o = __shfl_xor(lm, d); lm = lm > o ? lm : o;
+		}
+		if(lane == 0) {
+			atomicAdd(&a.prof[0], t_fill); atomicAdd(&a.prof[1], t_walk);
+			atomicAdd(&a.prof[2], w0); atomicAdd(&a.prof[3], w1); atomicAdd(&a.prof[4], ngrp);
+			atomicMax(&a.prof[5], __builtin_amdgcn_s_memtime() - t_start);
+			atomicMax(&a.prof[6], mx_fill); atomicMax(&a.prof[7], mx_walk);
+			atomicAdd(&a.prof[8], ls); atomicAdd(&a.prof[9], lm); atomicMax(&a.prof[10], lm);
 		}
 	}
 	if(a.stats) {
@@ -1188,7 +1229,7 @@ struct DpOccupancy {
 		fill[0][1] = blocks_per_cu((const void*)dp_fill_kernel<false, false, true>);
 		fill[1][1] = blocks_per_cu((const void*)dp_fill_kernel<true, false, true>);
 		walk = blocks_per_cu((const void*)dp_walk_kernel);
-		wave = blocks_per_cu((const void*)dp_wave_kernel<true>);
+		wave = blocks_per_cu((const void*)dp_wave_kernel<1>);
 	}
 };
 const DpOccupancy& occupancy() { static const DpOccupancy o; return o; }
@@ -1246,7 +1287,7 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
 		if(wb > slots) wb = (uint32_t)slots;
 		if(wb > a0.n) wb = a0.n;
-		hipLaunchKernelGGL(dp_wave_kernel<false>, dim3(wb), dim3(64), 0, s, sc, a);
+		hipLaunchKernelGGL(dp_wave_kernel<0>, dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
 	if(!dp_split_mode()) {
@@ -1273,7 +1314,14 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 	// exact best of the problems the banded fill failed (queued in a.fail_list)
 	if(a0.fail_list && a0.band && !dbg) {
 		const uint32_t wb = (uint32_t)a0.ncu * (uint32_t)occ.wave;
-		hipLaunchKernelGGL(dp_wave_kernel<true>, dim3(wb), dim3(64), 0, s, sc, a);
+		hipLaunchKernelGGL(dp_wave_kernel<1>, dim3(wb), dim3(64), 0, s, sc, a);
+	}
+	// the walks the lane kernel handed over (a.heavy_list): one wave per problem
+	if(a0.heavy_list && !dbg && !dp_split_mode()) {
+		uint32_t wb = (uint32_t)a0.ncu * 4u;
+		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
+		if(wb > slots) wb = (uint32_t)slots;
+		hipLaunchKernelGGL(dp_wave_kernel<2>, dim3(wb), dim3(64), 0, s, sc, a);
 	}
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }

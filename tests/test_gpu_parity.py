@@ -345,19 +345,25 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=True):
                                           eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
 
 
-@pytest.mark.parametrize("debug,wave,band,i16", [(False, "0", "1", 0.0), (False, "0", "0", 0.0), (False, "1", "1", 0.0),
-                                                 (True, "0", "1", 0.0),
-                                                 (False, "0", "1", 1.0), (False, "1", "1", 1.0),
-                                                 (True, "0", "1", 1.0), (False, "0", "1", 0.3),
-                                                 (True, "0", "1", 0.3)])
-def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, monkeypatch):
+@pytest.mark.parametrize("debug,wave,band,i16,heavy", [(False, "0", "1", 0.0, None), (False, "0", "0", 0.0, None),
+                                                       (False, "1", "1", 0.0, None), (True, "0", "1", 0.0, None),
+                                                       (False, "0", "1", 1.0, None), (False, "1", "1", 1.0, None),
+                                                       (True, "0", "1", 1.0, None), (False, "0", "1", 0.3, None),
+                                                       (True, "0", "1", 0.3, None),
+                                                       (False, "0", "1", 0.0, "0"), (False, "0", "1", 0.0, "1"),
+                                                       (False, "0", "1", 0.3, "1"), (False, "0", "0", 1.0, "2")])
+def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, monkeypatch):
     """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
     wave-per-problem mode) and debug kernels on random shapes/penalty thresholds at the ABI
     limits vs the oracle: statuses, bests, candidates, every nextAlignment record and edit.
     i16: the share of BT2X_DP_I16 problems (all, or mixed into u8 launches; the 16-bit lane
-    kernels, including minimum scores below -254)."""
+    kernels, including minimum scores below -254).  heavy: BT2X_DP_HEAVY, the walk-step budget
+    past which the lane kernel drops a problem for the wave kernel to redo (0: never; 1 and 2:
+    nearly every successful problem, mid-walk; default 1024)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     monkeypatch.setenv("BT2X_DP_BAND", band)
+    if heavy is not None:
+        monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
     rd, qu, rf, inp = _random_dp_problems(6000, seed=77 + int(debug) + int(10 * i16), i16=i16)
     ctx = ctxs["rep"][0]
     res = ctx.dp_align(rd, qu, rf, inp, debug=debug)
@@ -390,11 +396,14 @@ def test_dp_exact_best_option(ctxs, monkeypatch):
 
 
 @pytest.mark.parametrize("gold", ["dp_rep_dpad12.txt.xz", "dp_rep_i16.txt.xz", "dp_rep_i16_mix.txt.xz"])
-@pytest.mark.parametrize("wave", ["0", "1"])
-def test_dp_production_kernel_on_golden(ctxs, wave, gold, monkeypatch):
-    """The production (non-debug) kernel, in both modes, reproduces the reference records of
-    the golden set (oracle-checked, then against the golden itself)."""
+@pytest.mark.parametrize("wave,heavy", [("0", None), ("1", None), ("0", "1")])
+def test_dp_production_kernel_on_golden(ctxs, wave, heavy, gold, monkeypatch):
+    """The production (non-debug) kernel, in both modes and with walks handed to the wave
+    kernel, reproduces the reference records of the golden set (oracle-checked, then against
+    the golden itself)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
+    if heavy is not None:
+        monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
     case = g.DpCase(os.path.join(g.GOLDEN, gold))
     ctx = ctxs["rep"][0]
     out, recs, edits = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
