@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--cpu-sample-1t", type=int, default=40_000, help="reads of its 1-thread line")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-replay", action="store_true")
+    ap.add_argument("--no-replay-whole", action="store_true",
+                    help="skip the second replay with the whole file in flight (the kernels at their widest launches)")
     ap.add_argument("--workdir", default=os.environ.get("BT2X_BENCH_DIR", f"/tmp/bt2x_bench_{os.getuid()}"))
     ap.add_argument("--rss-limit-gb", type=float, default=200.0, help="kill bt2x-align above this host RSS")
     return ap.parse_args()
@@ -435,9 +437,10 @@ def roofline(args, rp):
                "counters_dp": cd, "round_sampling": rp["ctr"]["round"], "replay_reads": rp["reads"],
                "replay_steps": args.replay_steps,
                "replay_reads_per_s": round(rp["reads"] * args.replay_steps / rp["elapsed"], 1),
-               "what": "the GPU launch sequence bt2x-align issues for replay_reads reads (one file; cohorts of "
-                       "--slots/2 reads in flight, as in the timed run), replayed from HBM; kernel times from HIP "
-                       "events on the launch stream"}
+               "what": f"the GPU launch sequence bt2x-align issues for replay_reads reads (one file; "
+                       f"{args.replay_slots or max(1, args.slots // 2)} reads in flight"
+                       f"{'' if args.replay_slots else ', a cohort of the timed run'}), replayed from HBM; "
+                       "kernel times from HIP events on the launch stream"}
     return roof, kernels
 
 
@@ -597,6 +600,20 @@ def main():
     if rank == 0 and not args.no_replay:
         rp = replay(args, base, warm[0] if warm else steps[0], rdir, gpu)
         line["roofline"], line["kernels"] = roofline(args, rp)
+        if not args.no_replay_whole and not args.replay_slots:
+            # the same reads with the whole file in flight: the widest launches the aligner
+            # makes (round 2's replay shape), beside the timed run's cohort shapes above
+            wargs = argparse.Namespace(**vars(args))
+            wargs.replay_slots = args.replay_reads
+            rpw = replay(wargs, base, warm[0] if warm else steps[0], rdir, gpu)
+            rw, kw = roofline(wargs, rpw)
+            line["kernels_whole_file"] = {
+                "what": "the same replay with the whole file in flight (--replay-slots = replay_reads): "
+                        f"{kw['launches']['dp']} DP launches instead of {line['kernels']['launches']['dp']}",
+                "dp_ms": kw["dp_ms"], "seed_ms": kw["seed_ms"], "resolve_ms": kw["resolve_ms"],
+                "replay_reads_per_s": kw["replay_reads_per_s"], "launches": kw["launches"],
+                "roofline": {k: rw[k] for k in ("kernel", "achieved", "peak", "unit", "frac", "avg_launch_ms",
+                                                "achieved_kernel", "frac_kernel", "traffic", "pmc_src")}}
     if rank == 0 and world == 1 and not args.no_cpu:
         cb, ref_sam = cpu_baseline(args, base, steps[0], rdir)
         if cb is not None:
