@@ -79,6 +79,8 @@ __device__ __forceinline__ unsigned first_active(int lane) {
 	const uint64_t e = __builtin_amdgcn_read_exec();
 	return (e & (~e + 1)) == (1ull << lane) ? 1u : 0u;
 }
+// a value every active lane holds alike, as such (scalar registers, SALU arithmetic)
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 // true when no active lane has `c` set (a wave-uniform value)
 __device__ __forceinline__ bool wave_none(bool c) { return __builtin_amdgcn_ballot_w64(c) == 0; }
 
@@ -623,7 +625,9 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			cands[rank] = (uint8_t)j;
 		}
 		__syncthreads();
-		// ---- SwAligner::nextAlignment until done(), on lane 0 (see walk_problem)
+		// ---- SwAligner::nextAlignment until done(), on lane 0 (see walk_problem).  Every
+		// value read from LDS is made wave-uniform (readfirstlane), so the walk's arithmetic
+		// runs on the scalar unit: one chain of LDS round trips and SALU ops per step.
 		if(lane == 0) {
 			if(o.status != 0 && o.ncand > 0 && a.ablate != 1) {
 				const int rdo_ = sc.rdo, rde_ = sc.rde, rfo_ = sc.rfo, rfe_ = sc.rfe;
@@ -633,16 +637,16 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 					int ntries = 0, hi = 0;
 					bool found = false;
 					while(ndone < ncand) {
-						const int col0 = cands[ndone];
+						const int col0 = (int)uni(cands[ndone]);
 						ndone++;
-						if(tbb[col0 * S + row0] & TB_MARK) continue;
+						if(uni(tbb[col0 * S + row0]) & TB_MARK) continue;
 						ntries++;
 						if(a.ablate == 2) continue;
 						int row = row0, col = col0, ct = 2, bscore = 0, ns = 0, gaps = 0, ne = 0;
 						bool over_core = false, ok = true;
 						uint32_t tb_end = 0;
 						int bo = col * S + row;
-						uint32_t tb = tbb[bo];
+						uint32_t tb = uni(tbb[bo]);
 						while(true) {
 							st_bt++;
 							if(tb & TB_MARK) { ok = false; break; }
@@ -660,35 +664,35 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 							const int crow = row, ccol = col;
 							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;
 							const uint32_t ctb = tb;
-							tb = tbb[bo];
+							tb = uni(tbb[bo]);
 							tbb[cbo] = (uint8_t)TB_MARK;               // setReportedThrough
 							if(isD) {
 								if(ctb & TB_MM) {
-									const int rdc = rdw[crow], refc = refw[ccol];
+									const int rdc = (int)uni(rdw[crow]), refc = (int)uni(refw[ccol]);
 									const bool amb = rdc > 3 || refc > 3;
 									stage_ed[ne++] = pack_edit((uint32_t)crow, EDIT_MM, mask_chr(refc), acgtn(rdc));
-									bscore -= amb ? sc.npen : (int)penw[crow];
+									bscore -= amb ? sc.npen : (int)uni(penw[crow]);
 									if(amb) ns++;
 								}
 							} else {
 								const bool open = nct == 2;
-								stage_ed[ne++] = isF ? pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn(rdw[crow]))
-								                     : pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr(refw[ccol]), '-');
+								stage_ed[ne++] = isF ? pack_edit((uint32_t)crow, EDIT_REF_GAP, '-', acgtn((int)uni(rdw[crow])))
+								                     : pack_edit((uint32_t)crow + 1, EDIT_READ_GAP, mask_chr((int)uni(refw[ccol])), '-');
 								bscore -= isF ? (open ? rfo_ : rfe_) : (open ? rdo_ : rde_);
 								gaps++;
 							}
 						}
 						if(!ok || !over_core) { hi = max(hi, ne); continue; }
 						if(tb_end & TB_MM) {
-							const int rdc = rdw[row], refc = refw[col];
+							const int rdc = (int)uni(rdw[row]), refc = (int)uni(refw[col]);
 							const bool amb = rdc > 3 || refc > 3;
 							stage_ed[ne++] = pack_edit((uint32_t)row, EDIT_MM, mask_chr(refc), acgtn(rdc));
-							bscore -= amb ? sc.npen : (int)penw[row];
+							bscore -= amb ? sc.npen : (int)uni(penw[row]);
 							if(amb) ns++;
 						}
 						if(ns > p.nceil) { hi = max(hi, ne); continue; }
 						int refns = 0;
-						for(int k2 = col; k2 <= col0; k2++) refns += (refw[k2] > 3);
+						for(int k2 = col; k2 <= col0; k2++) refns += (uni(refw[k2]) > 3);
 						const int extent = R - (R - row0 - 1);
 						if(p.fw) {
 							for(int k2 = 0; k2 < ne / 2; k2++) {
