@@ -19,6 +19,7 @@
 #include <climits>
 
 #include <fcntl.h>
+#include <future>
 #include <malloc.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -1525,6 +1526,27 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	const auto put = [&writer](uint64_t id, std::string& rec) { writer.put(id, rec); };
 	if(slots < 2) slots = 2;
 	reserve_launch_buffers(pipeline_ ? slots / 2 : slots);
+	// FASTQ records are taken ahead on a helper thread (the record scan is serial): one batch
+	// of a cohort's size is in flight while the scheduler resumes, retires and gathers; refill
+	// consumes the taken records and starts the next batch.  The reader is touched by one
+	// thread at a time (the main thread only after collecting the batch in flight).
+	const size_t batch = pipeline_ ? slots / 2 : slots;
+	std::vector<FastqReader::Raw> ahead, incoming;
+	size_t ahead_pos = 0;
+	bool src_eof = false;
+	std::future<size_t> ahead_f;
+	auto start_ahead = [&] {
+		if(src_eof) return;
+		incoming.clear();
+		ahead_f = std::async(std::launch::async, [&fq, &incoming, batch] { return fq.take(batch, incoming); });
+	};
+	auto collect = [&] {
+		if(!ahead_f.valid()) return;
+		if(ahead_f.get() < batch) src_eof = true;
+		ahead.erase(ahead.begin(), ahead.begin() + (long)ahead_pos);
+		ahead_pos = 0;
+		ahead.insert(ahead.end(), incoming.begin(), incoming.end());
+	};
 	// New reads join cohort `co` (up to `cap` reads in it): decoded and run up to their
 	// first request, in parallel.
 	auto refill = [&](std::vector<ReadCtx*>& co, size_t cap) {
@@ -1532,7 +1554,17 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		raw.clear();
 		if(!eof && co.size() < cap) {
 			const size_t want = cap - co.size();
-			if(fq.take(want, raw) < want) eof = true;
+			collect();
+			const size_t n = std::min(want, ahead.size() - ahead_pos);
+			raw.insert(raw.end(), ahead.begin() + (long)ahead_pos, ahead.begin() + (long)(ahead_pos + n));
+			ahead_pos += n;
+			if(n < want && !src_eof && fq.take(want - n, raw) < want - n) src_eof = true;
+			if(src_eof && ahead_pos == ahead.size()) eof = true;
+			// input files whose last record is out (the reader is idle here)
+			const uint64_t written = writer.written();
+			while(st.t_files.size() < fq.files_done() && fq.file_end(st.t_files.size()) <= written)
+				st.t_files.push_back(now_s() - t_start);
+			start_ahead();
 		}
 		st.t_io += now_s() - t0;
 		const long nf = (long)raw.size();
@@ -1557,10 +1589,6 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		retire(co, st, put);
 		const double t1 = now_s();
 		writer.kick();
-		// input files whose last record is out
-		const uint64_t written = writer.written();
-		while(st.t_files.size() < fq.files_done() && fq.file_end(st.t_files.size()) <= written)
-			st.t_files.push_back(now_s() - t_start);
 		st.t_io += now_s() - t0;
 		st.t_retire += t1 - t0;
 	};
@@ -1621,6 +1649,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		}
 		join();
 	}
+	if(ahead_f.valid()) ahead_f.get();            // (a batch taken past the end: empty)
 	writer.finish();
 	if(t_run) *t_run = now_s() - t_start;
 	while(st.t_files.size() < fq.nfiles()) st.t_files.push_back(now_s() - t_start);
