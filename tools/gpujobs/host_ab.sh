@@ -1,4 +1,5 @@
 # host-driver A/B on the bench's C3 inputs: bt2x-align (this tree) vs bt2x-align-prev, alternated
+# (bt2x-align-prev: the previous host driver, built by hand from an older commit with the same g++ line as host/Makefile)
 mkdir -p gpurun_out
 timeout -k 10 600 python -u bench.py --no-cpu --no-replay > gpurun_out/hab_bench.json 2> gpurun_out/hab_bench.err
 rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/hab_bench.err; [ $rc -eq 0 ] || exit $rc
