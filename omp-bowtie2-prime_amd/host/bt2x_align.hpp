@@ -332,7 +332,7 @@ struct AlnRes {
 // the same reference and strand.
 class RedundantAlns {
 public:
-	void init(size_t rdlen) { rdlen_ = rdlen; alns_.clear(); runs_.clear(); }
+	void init(size_t rdlen) { rdlen_ = rdlen; alns_.clear(); runs_.clear(); eds_.clear(); }
 	// ned: the alignment's own edits in ned() order (5'-relative for rc)
 	bool overlap(const AlnRes& r, const uint32_t* ned, size_t n) {
 		if(alns_.empty()) return false;
@@ -341,8 +341,15 @@ public:
 		// do not meet rule a pair out without the per-row scan (a repetitive read reports
 		// many alignments at distinct loci; the scan over all of them was quadratic)
 		const int64_t lo = span_lo(tmp_), hi = span_hi(tmp_);
-		for(const Aln& a : alns_) {
+		for(Aln& a : alns_) {
 			if(a.refid != r.refid || a.fw != r.fw || a.hi <= lo || hi <= a.lo) continue;
+			if(a.run0 < 0) {                               // its rows, kept from now on
+				AlnRes ar;
+				ar.refid = a.refid; ar.fw = a.fw; ar.refoff = a.refoff;
+				rows(ar, eds_.data() + a.e0, a.ne, tmp2_);
+				a.run0 = (int64_t)runs_.size();
+				runs_.insert(runs_.end(), tmp2_.begin(), tmp2_.end());
+			}
 			const int64_t* o = runs_.data() + a.run0;
 			for(size_t i = 0; i < rdlen_; i++) {
 				const int64_t l = std::max(o[2 * i], tmp_[2 * i]), rr = std::min(o[2 * i + 1], tmp_[2 * i + 1]);
@@ -351,13 +358,16 @@ public:
 		}
 		return false;
 	}
+	// Most reads report one alignment, which no other is ever compared with: an added
+	// alignment keeps its span and edits, and its per-row runs are built the first time a
+	// later alignment's span meets it.
 	void add(const AlnRes& r, const uint32_t* ned, size_t n) {
 		rows(r, ned, n, tmp_);
-		alns_.push_back({r.refid, r.fw, runs_.size(), span_lo(tmp_), span_hi(tmp_)});
-		runs_.insert(runs_.end(), tmp_.begin(), tmp_.end());
+		alns_.push_back({r.refid, r.fw, r.refoff, (uint32_t)eds_.size(), (uint32_t)n, -1, span_lo(tmp_), span_hi(tmp_)});
+		eds_.insert(eds_.end(), ned, ned + n);
 	}
 private:
-	struct Aln { int64_t refid; bool fw; size_t run0; int64_t lo, hi; };
+	struct Aln { int64_t refid; bool fw; int64_t refoff; uint32_t e0, ne; int64_t run0; int64_t lo, hi; };
 	// rows' runs move right monotonically (left_{i+1} >= left_i): the first row's left and
 	// the last row's right bound every run
 	int64_t span_lo(const std::vector<int64_t>& t) const { return rdlen_ ? t[0] : 0; }
@@ -388,8 +398,8 @@ private:
 	}
 	size_t rdlen_ = 0;
 	std::vector<Aln> alns_;
-	std::vector<int64_t> runs_, tmp_;
-	std::vector<uint32_t> inv_;
+	std::vector<int64_t> runs_, tmp_, tmp2_;
+	std::vector<uint32_t> eds_, inv_;
 };
 
 // ------------------------------------------------------------------------ parameters
