@@ -1301,6 +1301,7 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		else launch_fill<false, true>(wide, fb, s, sc, a, 0u, a0.n);
 	} else {
 		a.walk_scratch = a0.scratch + (size_t)a0.chunk_groups * kGroupBytes;
+		a.heavy_list = nullptr;                  // no redo pass here: the walk kernel walks everything
 		const uint32_t chunk = a0.chunk_groups * 64;
 		for(uint32_t base = 0; base < a0.n; base += chunk) {
 			const uint32_t np = (a0.n - base < chunk) ? a0.n - base : chunk;
