@@ -359,7 +359,7 @@ def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, mo
     i16: the share of BT2X_DP_I16 problems (all, or mixed into u8 launches; the 16-bit lane
     kernels, including minimum scores below -254).  heavy: BT2X_DP_HEAVY, the walk-step budget
     past which the lane kernel drops a problem for the wave kernel to redo (0: never; 1 and 2:
-    nearly every successful problem, mid-walk; default 1024)."""
+    nearly every successful problem, mid-walk; default 896)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     monkeypatch.setenv("BT2X_DP_BAND", band)
     if heavy is not None:
