@@ -55,7 +55,7 @@ REF_ALIGN = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l")
 C3_READS = 10_000_000
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10, help="timed step files (C3's 10M reads split K ways)")
@@ -79,7 +79,11 @@ def parse():
                     help="skip the second replay with the whole file in flight (the kernels at their widest launches)")
     ap.add_argument("--workdir", default=os.environ.get("BT2X_BENCH_DIR", f"/tmp/bt2x_bench_{os.getuid()}"))
     ap.add_argument("--rss-limit-gb", type=float, default=200.0, help="kill bt2x-align above this host RSS")
-    return ap.parse_args()
+    ap.add_argument("--aligner", default=ALIGN,
+                    help="aligner binary (tests: tests/cpp/test_e2e_oracle, the host driver over the CPU oracle)")
+    ap.add_argument("--cpu-index", action="store_true",
+                    help="index the genome with the host builder (bt2x_build_index) instead of the GPU suffix sort")
+    return ap.parse_args(argv)
 
 
 def cpu_share() -> int:
@@ -163,9 +167,14 @@ def make_inputs(args, rank, world, workdir):
     if jobs:
         _GEN["codes"], _GEN["starts"] = codes, starts
         procs = max(1, min(len(jobs), cpu_share() // max(world, 1)))
-        with mp.get_context("fork").Pool(procs) as pool:
+        pool = mp.get_context("fork").Pool(procs)
+        try:
             for _ in pool.imap_unordered(_gen_file, jobs):
                 pass
+            pool.close()
+        finally:
+            pool.terminate()
+            pool.join()                     # the workers are reaped, not left behind
         _GEN.clear()
     mark(f"rank {rank}: {len(warm)} warmup + {len(steps)} step files of {per} reads ready in "
          f"{time.perf_counter() - t0:.1f} s")
@@ -179,18 +188,21 @@ def build_index(args, chroms, codes, workdir, rank, dist):
     base = os.path.join(workdir, tag)
     t0 = time.perf_counter()
     if rank == 0 and not all(os.path.exists(f"{base}.{k}.bt2l") for k in "1234"):
-        import torch
-        import gpu_sa
         from bt2x import lib
         fa = base + ".fa"
         sd.write_fasta(fa, chroms)
-        sa, bwt, keys = gpu_sa.suffix_array(codes[codes < 4], device="cuda")
-        lib.build_index_sa(fa, base + ".tmp", sa, bwt=bwt, keys=keys)
+        if getattr(args, "cpu_index", False):
+            lib.build_index(fa, base + ".tmp")
+        else:
+            import torch
+            import gpu_sa
+            sa, bwt, keys = gpu_sa.suffix_array(codes[codes < 4], device="cuda")
+            lib.build_index_sa(fa, base + ".tmp", sa, bwt=bwt, keys=keys)
+            del sa, bwt, keys
+            torch.cuda.empty_cache()
         for k in "1234":
             os.replace(f"{base}.tmp.{k}.bt2l", f"{base}.{k}.bt2l")
-        del sa, bwt, keys
         os.unlink(fa)
-        torch.cuda.empty_cache()
     if dist:
         dist.barrier()
     mark(f"index {tag} ready in {time.perf_counter() - t0:.1f} s")
@@ -464,27 +476,40 @@ def ref_run(args, base, fq, threads, sam):
     return wall, timers
 
 
-def head_fastq(src, dst, n):
-    with open(src, "rb") as f, open(dst, "wb") as g:
-        for _ in range(4 * n):
-            ln = f.readline()
-            if not ln:
+def head_fastq(srcs, dst, n) -> int:
+    """The first n records of the stream of FASTQ files `srcs` (in order) into dst; returns
+    the records written (fewer than n when the stream is shorter).  A sample larger than
+    one step file continues into the next ones, so it is always the first reads of the
+    timed run (the step files are its -U list after the warmup files)."""
+    if isinstance(srcs, str):
+        srcs = [srcs]
+    got = 0
+    with open(dst, "wb") as g:
+        for src in srcs:
+            with open(src, "rb") as f:
+                while got < n:
+                    rec = [f.readline() for _ in range(4)]
+                    if not rec[0]:
+                        break
+                    g.write(b"".join(rec))
+                    got += 1
+            if got >= n:
                 break
-            g.write(ln)
+    return got
 
 
-def cpu_baseline(args, base, fq, rdir):
+def cpu_baseline(args, base, fqs, rdir):
     """the reference aligner on the box's CPU share; n-1 and n threads, the
     better repeated to a median of 3; 1 thread on a smaller sample; alignment time = wall -
     wall of a 1-read run at the same thread count (index load)."""
     if not os.access(REF_ALIGN, os.X_OK):
         return None, None
     n = cpu_share()
-    m, m1 = args.cpu_sample, args.cpu_sample_1t
     sample, s1, one = (os.path.join(rdir, f) for f in ("cpu_sample.fq", "cpu_1t.fq", "cpu_one.fq"))
-    head_fastq(fq, sample, m)
-    head_fastq(fq, s1, m1)
-    head_fastq(fq, one, 1)
+    # m, m1: the reads the samples really hold (the timed run may have fewer than asked)
+    m = head_fastq(fqs, sample, args.cpu_sample)
+    m1 = head_fastq(fqs, s1, args.cpu_sample_1t)
+    head_fastq(fqs, one, 1)
     sam = os.path.join(rdir, "ref.sam")
     load = {}
 
@@ -506,7 +531,8 @@ def cpu_baseline(args, base, fq, rdir):
     mark(f"reference aligner: median {med[0]:.0f} reads/s at {best} threads; 1 thread {one_t[0]:.0f} reads/s")
     # (the last sample run left its SAM at `sam`; every run over the sample aligns the same reads)
     return {"value": round(med[0] / 1e6, 6), "unit": "M reads/s", "cores": best, "kind": "reference",
-            "sample": f"first {m} reads of step file 1 through oracle/_ref/bowtie2-align-l --dpad {args.dpad} "
+            "sample_reads": m,
+            "sample": f"first {m} reads of the timed run (step files in order) through oracle/_ref/bowtie2-align-l --dpad {args.dpad} "
                       f"(FASTQ->SAM, OpenMP, OMP_WAIT_POLICY=ACTIVE) on this box's {n}-CPU share: "
                       f"threads {sorted(runs)}, best repeated, median of 3; alignment time = wall - wall of a "
                       f"1-read run (index load {load[best]:.2f} s)",
@@ -528,6 +554,31 @@ def sam_records(path, first_n=None):
     return recs
 
 
+def parity(ours_sam, ref_sam, n) -> dict:
+    """Our timed run's first n SAM records (records are written in input order) against
+    the reference aligner's records for the same n reads, compared sorted."""
+    ours, theirs = sam_records(ours_sam, n), sam_records(ref_sam)
+    diff = sum(1 for a, b in zip(ours, theirs) if a != b) + abs(len(ours) - len(theirs))
+    return {"sample_reads": n, "records_ours": len(ours), "records_reference": len(theirs), "records_differ": diff,
+            "what": "sorted SAM records of the timed run's first sample_reads reads vs the reference "
+                    "aligner's on the same reads"}
+
+
+def host_threads(args, share: int, world: int) -> tuple[int, str]:
+    """bt2x-align -p per rank: the node's CPU share split over the ranks.  One rank keeps
+    ~11 cores busy at the current host cost per read, so a share that leaves
+    a rank fewer than kRankCores is reported (not silently raised)."""
+    kRankCores = 12
+    if args.host_threads > 0:
+        return args.host_threads, "set by --host-threads"
+    t = max(1, share // max(world, 1))
+    note = f"{share}-CPU share / {world} rank(s)"
+    if t < kRankCores:
+        note += (f": below the ~{kRankCores} host cores one rank uses at full rate (DESIGN.md §6) -- "
+                 "this run is host-bound by its CPU share")
+    return t, note
+
+
 # ------------------------------------------------------------------------ main
 
 def main():
@@ -536,8 +587,7 @@ def main():
     rank, world, local = bdist.world()
     gpu = int(os.environ.get("BT2X_BENCH_DEVICE", local))
     share = cpu_share()
-    if args.host_threads <= 0:
-        args.host_threads = max(4, share // max(world, 1))
+    args.host_threads, threads_note = host_threads(args, share, world)
     workdir = args.workdir
     os.makedirs(workdir, exist_ok=True)
     # inputs first: the read generator forks, which must happen before the GPU is touched
@@ -559,7 +609,7 @@ def main():
     out_sam = os.path.join(rdir, "out.sam")
     if shutil.disk_usage(rdir).free < world * need + (8 << 30):
         out_sam = os.devnull
-    cmd = [ALIGN, "-x", base, "-U", ",".join(warm + steps), "-S", out_sam, "--dpad", str(args.dpad),
+    cmd = [args.aligner, "-x", base, "-U", ",".join(warm + steps), "-S", out_sam, "--dpad", str(args.dpad),
            "--device", str(gpu), "-p", str(args.host_threads), "--slots", str(args.slots),
            "--warmup-files", str(len(warm)), "--metrics", "--stats"]
     if dist:
@@ -590,7 +640,8 @@ def main():
                                f"{'a file' if out_sam != os.devnull else '/dev/null'}), index load excluded; "
                                f"step = one FASTQ file of {per} reads",
                    "reads_per_gpu": args.reads, "read_len": args.read_len, "parallelism": f"dp{world} (read shards)",
-                   "host_threads": args.host_threads, "slots": args.slots, "key": workload_key(args)},
+                   "host_threads": args.host_threads, "host_threads_note": threads_note, "cpu_share": share,
+                   "slots": args.slots, "key": workload_key(args)},
         "end_to_end": {"t_align_s": round(t_align, 3), "t_align_max_s": round(t_max, 3),
                        "step_done_s": [round(t, 3) for t in t_files], "wall_incl_index_load_s": round(wall, 2),
                        "peak_rss_mib": peak, "summary": bdist.alignment_summary(tot).splitlines(),
@@ -615,15 +666,11 @@ def main():
                 "roofline": {k: rw[k] for k in ("kernel", "achieved", "peak", "unit", "frac", "avg_launch_ms",
                                                 "achieved_kernel", "frac_kernel", "traffic", "pmc_src")}}
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb, ref_sam = cpu_baseline(args, base, steps[0], rdir)
+        cb, ref_sam = cpu_baseline(args, base, steps, rdir)
         if cb is not None:
             line["cpu_baseline"] = cb
             if out_sam != os.devnull:
-                ours, theirs = sam_records(out_sam, args.cpu_sample), sam_records(ref_sam)
-                diff = sum(1 for a, b in zip(ours, theirs) if a != b) + abs(len(ours) - len(theirs))
-                line["parity"] = {"sample_reads": args.cpu_sample, "records_differ": diff,
-                                  "what": "sorted SAM records of the timed run's first sample reads vs the "
-                                          "reference aligner's on the same reads"}
+                line["parity"] = parity(out_sam, ref_sam, cb["sample_reads"])
             line["gpu_vs_cpu"] = round(value / cb["value"], 2) if cb["value"] else None
     if out_sam != os.devnull and os.path.exists(out_sam):
         os.unlink(out_sam)

@@ -287,7 +287,16 @@ int bt2x_dp_align(bt2x_ctx* ctx,
                   bt2x_dp_debug* debug);
 
 /* Device-pointer variant: all buffers in HBM; counters (4 x u32: recs used, edits used,
- * then kernel scratch) in HBM.  launch_flags: BT2X_DPL_I16 when any problem carries
+ * then kernel scratch) in HBM.  "Edits used" is the arena's high-water mark and may exceed
+ * the entries the records reference: a problem whose backtrace walk the lane kernel hands
+ * over to the wave kernel (the step budget, BT2X_DP_HEAVY) has already published the edit
+ * images of its earlier nextAlignment calls, and the wave kernel publishes the whole call
+ * sequence again; the dead ranges are never referenced, and since a retry with the
+ * reported size repeats the same hand-overs, that size is what the launch needs.
+ * The context's per-launch device buffers (heavy list, failed list, GPU-cut windows) are
+ * shared by all calls: calls on one context must be serialised, whatever their streams
+ * (like every other entry point; use one context per concurrent stream).
+ * launch_flags: BT2X_DPL_I16 when any problem carries
  * BT2X_DP_I16 (the 16-bit kernels run the launch; an i16 problem in a launch without
  * it is reported BT2X_E_ARG by the host variant, and comes back with status -1 here),
  * BT2X_DPL_EXACT_BEST for exact best of failed problems (bt2x_dp_out.best),

@@ -123,6 +123,41 @@ def alignment_summary(m: dict) -> str:
     return "\n".join(out) + "\n"
 
 
+def rank_device(local_rank: int, env=None) -> str:
+    """The GPU of local rank k: the k-th entry of an existing HIP_VISIBLE_DEVICES (or
+    ROCR_VISIBLE_DEVICES) mask, so a job launched on a subset of a node's GPUs stays on
+    it; the k-th GPU of the node when neither is set."""
+    env = os.environ if env is None else env
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        mask = [d.strip() for d in env.get(var, "").split(",") if d.strip()]
+        if mask:
+            if local_rank >= len(mask):
+                raise ValueError(f"local rank {local_rank} but {var}={env[var]} names {len(mask)} devices")
+            if var == "ROCR_VISIBLE_DEVICES":
+                return str(local_rank)         # HIP numbers the ROCR-visible devices from 0
+            return mask[local_rank]
+    return str(local_rank)
+
+
+def aligner_messages(stderr: str) -> str:
+    """An aligner's stderr minus its launcher-facing lines (BT2X_*) and its alignment
+    summary: what a single run leaves for the user (per-read warnings)."""
+    out, lines, i = [], stderr.splitlines(keepends=True), 0
+    while i < len(lines):
+        ln = lines[i]
+        if ln.startswith("BT2X_"):
+            i += 1
+            continue
+        if ln.rstrip("\n").endswith(" reads; of these:") or ln.rstrip("\n") == "0 reads":
+            while i < len(lines) and not lines[i].rstrip("\n").endswith("overall alignment rate"):
+                i += 1
+            i += 1
+            continue
+        out.append(ln)
+        i += 1
+    return "".join(out)
+
+
 def _split_out(args: list[str]) -> tuple[list[str], str | None]:
     args = list(args)
     for flag in ("-S", "--output"):
@@ -170,9 +205,14 @@ def run_sharded(aligner: str, args: list[str], dist=None, set_device: bool = Tru
         cmd.append("--no-hd")
     env = dict(os.environ)
     if set_device:
-        env["HIP_VISIBLE_DEVICES"] = str(local_rank)
+        env["HIP_VISIBLE_DEVICES"] = rank_device(local_rank, env)
     r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     res = {"rc": r.returncode, "stderr": r.stderr}
+    if r.returncode == 0:
+        # the per-read warnings a single run prints (printEEScoreMsg), not the launcher's
+        # own lines or the shard's summary (rank 0 prints the summed one)
+        sys.stderr.write(aligner_messages(r.stderr))
+        sys.stderr.flush()
     try:
         got = parse_metrics(r.stderr) if r.returncode == 0 else None
     except ValueError as e:

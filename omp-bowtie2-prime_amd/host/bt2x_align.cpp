@@ -157,14 +157,36 @@ size_t next_record(const char* m, size_t len, size_t at) {
 	return len;
 }
 
-size_t count_lines(const char* m, size_t n) {
-	size_t k = 0;
-	for(const char* q = m; (q = (const char*)std::memchr(q, '\n', (size_t)(m + n - q))) != nullptr; q++) k++;
+// records in m[0, n) as FastqReader::take() finds them: empty lines (after stripping
+// '\r') are skipped, and a record is a non-empty header line plus the next three lines
+uint64_t count_records(const char* m, size_t n) {
+	uint64_t k = 0;
+	size_t pos = 0;
+	auto line = [&](size_t& len) -> bool {
+		if(pos >= n) return false;
+		const char* s = m + pos;
+		const char* nl = (const char*)std::memchr(s, '\n', n - pos);
+		len = nl ? (size_t)(nl - s) : n - pos;
+		pos += len + (nl ? 1 : 0);
+		while(len > 0 && s[len - 1] == '\r') len--;
+		return true;
+	};
+	size_t len = 0;
+	while(line(len)) {
+		if(!len) continue;
+		for(int j = 1; j < 4; j++) if(!line(len)) break;
+		k++;
+	}
 	return k;
 }
 }
 
-FastqReader::FastqReader(const std::vector<std::string>& paths, int shard, int nshards) {
+uint64_t FastqReader::count_file_records(const std::string& path) {
+	FastqReader r(std::vector<std::string>{path});
+	return r.f_.empty() || !r.f_[0].len ? 0 : count_records(r.f_[0].map, r.f_[0].len);
+}
+
+FastqReader::FastqReader(const std::vector<std::string>& paths, int shard, int nshards, uint64_t rdid_base) {
 	if(nshards < 1 || shard < 0 || shard >= nshards) throw std::runtime_error("bad shard " + std::to_string(shard) + "/" + std::to_string(nshards));
 	size_t total = 0;
 	for(const std::string& path : paths) {
@@ -188,16 +210,15 @@ FastqReader::FastqReader(const std::vector<std::string>& paths, int shard, int n
 	const size_t lo = (size_t)((unsigned __int128)total * (unsigned)shard / (unsigned)nshards);
 	const size_t hi = (size_t)((unsigned __int128)total * (unsigned)(shard + 1) / (unsigned)nshards);
 	size_t off = 0;
-	first_rdid_ = 0;
+	first_rdid_ = rdid_base;
 	for(File& F : f_) {
 		const size_t a = std::min(std::max(lo, off) - off, F.len), b = std::min(std::max(hi, off) - off, F.len);
 		F.beg = next_record(F.map, F.len, a);
 		F.end = shard + 1 == nshards ? F.len : next_record(F.map, F.len, b);
 		if(F.end < F.beg) F.end = F.beg;
-		// records before the shard in this file: 4 lines each (a last line without '\n'
-		// still ends its record)
-		const size_t k = count_lines(F.map, F.beg);
-		first_rdid_ += F.beg == F.len && F.len && F.map[F.len - 1] != '\n' ? (k + 4) / 4 : k / 4;
+		// records before the shard in this file, counted as take() reads them (blank lines
+		// between records are not records)
+		if(F.beg) first_rdid_ += count_records(F.map, F.beg);
 		off += F.len;
 	}
 	if(!f_.empty()) pos_ = f_[0].beg;

@@ -563,13 +563,17 @@ inline uint32_t gen_rand_seed(const Read& r, uint32_t seed) {
 // bytes [i*T/n, (i+1)*T/n) of the concatenated files (T = their total size), each bound
 // moved to the next record start (a line beginning '@' whose third line begins '+'), so
 // the shards partition the stream in order.  Records are numbered globally
-// (first_rdid(): records before the shard, from its line count; 4-line records): a read
-// without a name is named by that number, as the reference does.
+// (first_rdid(): rdid_base plus the records before the shard, counted as take() finds
+// them): a read without a name is named by that number, as the reference does.
+// rdid_base numbers a stream that continues an earlier one (bt2x-align --warmup-files:
+// the timed files follow the warmup files in the -U list).
 class FastqReader {
 public:
 	struct Raw { const char* l[4]; size_t n[4]; };
 	explicit FastqReader(const char* path) : FastqReader(std::vector<std::string>{path}) {}
-	explicit FastqReader(const std::vector<std::string>& paths, int shard = 0, int nshards = 1);
+	explicit FastqReader(const std::vector<std::string>& paths, int shard = 0, int nshards = 1, uint64_t rdid_base = 0);
+	// records of a whole file, as take() counts them
+	static uint64_t count_file_records(const std::string& path);
 	~FastqReader();
 	FastqReader(const FastqReader&) = delete;
 	FastqReader& operator=(const FastqReader&) = delete;

@@ -11,7 +11,8 @@
 // --shard i/N aligns the i-th of N contiguous parts of the read stream (FastqReader); the
 // N outputs concatenated in order (headers from part 0 only: --no-hd on the others) are
 // the whole run's SAM.  --warmup-files K aligns the first K files of the -U list once,
-// untimed and unwritten, before the timed run over the rest (bench.py).  --metrics prints
+// untimed and unwritten, before the timed run over the rest (bench.py); unnamed reads of
+// the rest keep their numbers in the whole list.  --metrics prints
 // the 27 ReportingMetrics counters (BT2X_METRICS) and the run's clock (BT2X_TIMED) for a
 // launcher to sum over shards.
 // --no-sse8 runs the signed 16-bit DP as the reference's -DENABLE_I16 build does
@@ -326,7 +327,11 @@ int main(int argc, char** argv) {
 			al.run(wr, null, slots, threads);
 			std::fclose(null);
 		}
-		FastqReader reader(std::vector<std::string>(files.begin() + warm_files, files.end()), shard, nshards);
+		// unnamed reads of the timed files are numbered after the warmup files' records, as in
+		// one run over the whole -U list
+		uint64_t warm_records = 0;
+		for(int k = 0; k < warm_files; k++) warm_records += FastqReader::count_file_records(files[(size_t)k]);
+		FastqReader reader(std::vector<std::string>(files.begin() + warm_files, files.end()), shard, nshards, warm_records);
 		struct rusage ru0;
 		getrusage(RUSAGE_SELF, &ru0);
 		const auto t_start = std::chrono::steady_clock::now();

@@ -172,7 +172,7 @@ int main(int argc, char** argv) {
 	size_t slots = 4096;
 	int threads = 4;
 	bool host_timing = false, pipeline = true, gpu_round = true, hd = true, metrics = false, host_windows = false;
-	int reps = 1, inject = 0, shard = 0, nshards = 1;
+	int reps = 1, inject = 0, shard = 0, nshards = 1, warm_files = 0;
 	std::string idx, fqs, outp;
 	std::vector<std::string> pos;
 	for(int i = 1; i < argc; i++) {
@@ -189,6 +189,11 @@ int main(int argc, char** argv) {
 		else if(a == "--no-hd") hd = false;
 		else if(a == "--host-windows") host_windows = true;
 		else if(a == "--metrics") metrics = true;
+		// bt2x-align's bench options (bench.py drives this binary as it drives bt2x-align in the
+		// CPU test of its multi-rank path): --device and --stats are accepted and ignored
+		else if(a == "--device" && i + 1 < argc) ++i;
+		else if(a == "--stats") {}
+		else if(a == "--warmup-files" && i + 1 < argc) warm_files = std::atoi(argv[++i]);
 		else if(a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
 		else if(a == "--inject-error" && i + 1 < argc) inject = std::atoi(argv[++i]);
 		else if(a == "--shard" && i + 1 < argc) {
@@ -256,10 +261,22 @@ int main(int argc, char** argv) {
 	al.set_header(hd);
 	RunStats st;
 	uint64_t first_rdid = 0;
+	double t_align = 0;
+	if(warm_files < 0 || (size_t)warm_files >= files.size()) { std::fprintf(stderr, "--warmup-files must leave a file\n"); return 1; }
 	try {
-		FastqReader fq(files, shard, nshards);
+		uint64_t warm_records = 0;
+		if(warm_files > 0) {                              // untimed, unwritten (bt2x-align --warmup-files)
+			FastqReader wr(std::vector<std::string>(files.begin(), files.begin() + warm_files), shard, nshards);
+			std::FILE* nul = std::fopen("/dev/null", "wb");
+			al.run(wr, nul, slots, threads);
+			std::fclose(nul);
+			for(int k = 0; k < warm_files; k++) warm_records += FastqReader::count_file_records(files[(size_t)k]);
+		}
+		FastqReader fq(std::vector<std::string>(files.begin() + warm_files, files.end()), shard, nshards, warm_records);
 		first_rdid = fq.first_rdid();
+		const auto t0 = std::chrono::steady_clock::now();
 		st = al.run(fq, out, slots, threads);
+		t_align = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 	} catch(const std::exception& e) {               // as bt2x-align's main does
 		std::fprintf(stderr, "test_e2e_oracle: %s\n", e.what());
 		return 1;
@@ -269,8 +286,10 @@ int main(int argc, char** argv) {
 		print_alignment_summary(st.met, stderr);
 		std::string line = "BT2X_METRICS";
 		for(uint64_t v : st.met.v) line += " " + std::to_string(v);
-		std::fprintf(stderr, "%s\nBT2X_TIMED reads=%llu first_rdid=%llu t_align=0\n", line.c_str(),
-		             (unsigned long long)st.reads, (unsigned long long)first_rdid);
+		std::string tf;
+		for(double t : st.t_files) { char b[32]; std::snprintf(b, sizeof b, "%s%.4f", tf.empty() ? "" : ",", t); tf += b; }
+		std::fprintf(stderr, "%s\nBT2X_TIMED reads=%llu first_rdid=%llu t_align=%.4f t_files=%s\n", line.c_str(),
+		             (unsigned long long)st.reads, (unsigned long long)first_rdid, t_align, tf.c_str());
 	}
 	std::fprintf(stderr, "reads=%llu aligned=%llu seed_launches=%llu resolve_launches=%llu dp_launches=%llu dps=%llu "
 	             "tight_recs=%llu\n",

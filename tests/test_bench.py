@@ -1,0 +1,87 @@
+"""bench.py's harness on CPU: the CPU-baseline sample and the parity comparison under the
+driver's step split (a sample larger than one step file), and the N>1 path under
+torch.distributed.run (gloo, world size 2) with the host driver over the CPU oracle
+kernels as the aligner (tests/cpp/test_e2e_oracle, bt2x-align's command line)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+ORACLE_DRIVER = os.path.join(ROOT, "tests", "cpp", "test_e2e_oracle")
+
+
+def _fq(path, first, n):
+    with open(path, "w") as f:
+        for i in range(first, first + n):
+            f.write(f"@r{i}\nACGT\n+\nIIII\n")
+
+
+def test_head_fastq_spans_step_files(tmp_path):
+    # the driver's --steps 20 makes step files of 500 k reads, smaller than the 800 k sample
+    files = [str(tmp_path / f"s{k}.fq") for k in range(3)]
+    for k, p in enumerate(files):
+        _fq(p, 5 * k, 5)
+    dst = str(tmp_path / "sample.fq")
+    assert bench.head_fastq(files, dst, 8) == 8
+    assert open(dst).read().split("\n")[0::4][:8] == [f"@r{i}" for i in range(8)]
+    assert bench.head_fastq(files, dst, 100) == 15                 # the stream is shorter
+    assert bench.head_fastq(files[0], dst, 3) == 3
+
+
+def test_parity_compares_the_same_reads(tmp_path):
+    ours, ref = tmp_path / "ours.sam", tmp_path / "ref.sam"
+    recs = [f"r{i}\t0\tchr\t{i}\t42" for i in range(10)]
+    ours.write_text("@HD\tVN:1.0\n" + "".join(r + "\n" for r in recs))
+    ref.write_text("@HD\tVN:1.0\n" + "".join(r + "\n" for r in reversed(recs[:6])))
+    p = bench.parity(str(ours), str(ref), 6)
+    assert p["records_differ"] == 0 and p["records_ours"] == p["records_reference"] == 6
+    ref.write_text("".join(r + "\n" for r in recs[:5]) + "r5\t16\tchr\t5\t42\n")
+    assert bench.parity(str(ours), str(ref), 6)["records_differ"] == 1
+
+
+def test_host_threads_split_is_reported():
+    class A:
+        host_threads = 0
+    t, note = bench.host_threads(A(), 128, 8)
+    assert t == 16 and "below" not in note
+    t, note = bench.host_threads(A(), 16, 8)
+    assert t == 2 and "host-bound" in note
+    A.host_threads = 5
+    assert bench.host_threads(A(), 16, 8) == (5, "set by --host-threads")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_on_cpu(tmp_path):
+    """bench.py --gpus 2 as the driver launches it (torch.distributed.run, one process per
+    rank): per-rank inputs, rank 0 indexes while rank 1 waits at the barrier, both align
+    after a barrier, the counters are summed and the time is the max over ranks; rank 0
+    prints one JSON line whose value counts both ranks' reads."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", BT2X_BENCH_DIR=str(tmp_path / "work"))
+    reads = 1200
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--reads", str(reads), "--genome-mb", "0.25",
+           "--replay-reads", "200", "--slots", "512", "--host-threads", "2", "--no-replay", "--no-cpu",
+           "--cpu-index", "--aligner", ORACLE_DRIVER]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["scaling"] == "weak"
+    e = line["end_to_end"]
+    assert e["summary"][0] == f"{2 * reads} reads; of these:"
+    assert abs(line["value"] - 2 * reads / e["t_align_max_s"] / 1e6) < 1e-3
+    assert e["t_align_max_s"] >= e["t_align_s"] > 0
+    assert line["config"]["host_threads"] == 2

@@ -155,3 +155,96 @@ def test_alignment_summary_format():
         "3560 reads; of these:\n  3560 (100.00%) were unpaired; of these:\n    1284 (36.07%) aligned 0 times\n"
         "    1798 (50.51%) aligned exactly 1 time\n    478 (13.43%) aligned >1 times\n63.93% overall alignment rate\n")
     assert bdist.alignment_summary({k: 0 for k in bdist.METRIC_NAMES}) == "0 reads\n0.00% overall alignment rate\n"
+
+
+def test_rank_device_honours_visible_mask():
+    assert bdist.rank_device(0, {}) == "0" and bdist.rank_device(3, {}) == "3"
+    assert bdist.rank_device(1, {"HIP_VISIBLE_DEVICES": "4,5,6,7"}) == "5"
+    assert bdist.rank_device(0, {"HIP_VISIBLE_DEVICES": " 6 , 7"}) == "6"
+    assert bdist.rank_device(2, {"ROCR_VISIBLE_DEVICES": "1,3,5"}) == "2"
+    with pytest.raises(ValueError):
+        bdist.rank_device(2, {"HIP_VISIBLE_DEVICES": "4,5"})
+
+
+def test_aligner_messages_keeps_warnings_only():
+    err = ("Warning: minimum score function gave positive number in --end-to-end mode for read 'r1; setting to 0 instead\n"
+           "10 reads; of these:\n  10 (100.00%) were unpaired; of these:\n    0 (0.00%) aligned 0 times\n"
+           "    10 (100.00%) aligned exactly 1 time\n    0 (0.00%) aligned >1 times\n100.00% overall alignment rate\n"
+           "BT2X_METRICS 1 2 3\nBT2X_TIMED reads=10 t_align=0\nsomething else\n")
+    assert bdist.aligner_messages(err) == (
+        "Warning: minimum score function gave positive number in --end-to-end mode for read 'r1; setting to 0 instead\n"
+        "something else\n")
+
+
+def test_gloo_two_rank_sharded_warnings(tmp_path):
+    """A sharded run prints the per-read warnings a single run prints (here the stock
+    build's -254 clamp of a wide --score-min, printEEScoreMsg), not only the summary."""
+    import golden_io as g
+    import lzma
+    from test_e2e import split_stderr
+    base = g.materialize_index("rep", str(tmp_path / "idx"))
+    fq = tmp_path / "r.fq"
+    with lzma.open(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), "rb") as f:
+        fq.write_bytes(b"\n".join(f.read().split(b"\n")[:4 * 400]) + b"\n")
+    wide = ["--score-min", "L,-0.6,-4", "--dpad", "12"]
+    single = subprocess.run([ORACLE_DRIVER, "-x", base, "-U", str(fq), "-p", "2", "--metrics"] + wide,
+                            capture_output=True, text=True, timeout=600)
+    assert single.returncode == 0, single.stderr[-2000:]
+    exp_w, exp_s = split_stderr(single.stderr)
+    assert len(exp_w) > 20
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1",
+               PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "omp-bowtie2-prime_amd"), os.environ.get("PYTHONPATH", "")]))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "bt2x.dist",
+           "--aligner", ORACLE_DRIVER, "--no-device", "--", "-x", base, "-U", str(fq), "-p", "2",
+           "-S", str(tmp_path / "o.sam")] + wide
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got_w, got_s = split_stderr(r.stderr)
+    assert got_w == exp_w and got_s == exp_s
+
+
+def _fastq_blank_unnamed(path, lines, every=7):
+    """The records of `lines` (4-line FASTQ) with blank lines between some records and
+    every `every`-th record unnamed ('@' alone)."""
+    out = []
+    for k in range(len(lines) // 4):
+        rec = lines[4 * k:4 * k + 4]
+        if k % every == 3:
+            rec = [b"@"] + rec[1:]
+        out += rec
+        if k % 5 == 1:
+            out.append(b"")
+        if k % 11 == 2:
+            out += [b"", b""]
+    path.write_bytes(b"\n".join(out) + b"\n")
+
+
+def test_shards_and_warmup_number_unnamed_reads_globally(tmp_path):
+    """Unnamed reads are named by their number in the whole read stream: shards of a FASTQ
+    with blank lines between records (first_rdid counts records as take() reads them,
+    not lines / 4), and the timed files after --warmup-files K (numbered after the warmup
+    files' records)."""
+    import golden_io as g
+    import lzma
+    base = g.materialize_index("rep", str(tmp_path / "idx"))
+    with lzma.open(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), "rb") as f:
+        lines = f.read().split(b"\n")[:4 * 600]
+    a, b = tmp_path / "a.fq", tmp_path / "b.fq"
+    _fastq_blank_unnamed(a, lines[:4 * 250])
+    _fastq_blank_unnamed(b, lines[4 * 250:])
+    fqs = f"{a},{b}"
+    whole = subprocess.run([ORACLE_DRIVER, "-x", base, "-U", fqs, "-p", "2", "--no-hd"], capture_output=True,
+                           timeout=600, check=True).stdout
+    names = [ln.split(b"\t")[0] for ln in whole.splitlines()]
+    assert b"3" in names and b"253" in names                  # unnamed reads numbered in the stream
+    parts = []
+    for i in range(3):
+        r = subprocess.run([ORACLE_DRIVER, "-x", base, "-U", fqs, "-p", "2", "--no-hd", "--shard", f"{i}/3"],
+                           capture_output=True, timeout=600, check=True)
+        parts.append(r.stdout)
+    assert b"".join(parts) == whole
+    r = subprocess.run([ORACLE_DRIVER, "-x", base, "-U", fqs, "-p", "2", "--no-hd", "--warmup-files", "1", "--metrics"],
+                       capture_output=True, timeout=600, check=True)
+    assert int(bdist.parse_metrics(r.stderr.decode())["timed"]["first_rdid"]) == 250
+    assert r.stdout == b"".join(ln + b"\n" for ln in whole.splitlines()[250:])
