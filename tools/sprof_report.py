@@ -61,6 +61,30 @@ def main():
         for fn, c in callers.most_common(top):
             print(f"{100 * c / n:6.2f} {fn}")
         return
+    if "--lines" in sys.argv:                   # self samples by source line (build with -g)
+        lines_c = collections.Counter()
+        for mod in addrs:
+            pass
+        firsts = collections.defaultdict(list)
+        for fr in samples:
+            if fr and ":" in fr[0]:
+                mod, off = fr[0].rsplit(":", 1)
+                firsts[mod].append(off)
+        for mod, offs in firsts.items():
+            uniq = sorted(set(offs))
+            r = subprocess.run(["addr2line", "-i", "-C", "-e", mod] + ["0x" + o for o in uniq],
+                               capture_output=True, text=True)
+            # with -i an address may print several lines (inline chain): keep the first
+            out, k = {}, 0
+            outl = r.stdout.splitlines()
+            r2 = subprocess.run(["addr2line", "-C", "-e", mod] + ["0x" + o for o in uniq], capture_output=True, text=True)
+            for o, ln in zip(uniq, r2.stdout.splitlines()):
+                out[o] = ln.rsplit("/", 1)[-1]
+            for o in offs:
+                lines_c[out.get(o, "?")] += 1
+        for ln, c in lines_c.most_common(top):
+            print(f"{100 * c / n:6.2f} {ln}")
+        return
     key = incl_c if "--incl" in sys.argv else self_c
     for fn, c in key.most_common(top):
         print(f"{100 * self_c[fn] / n:6.2f} {100 * incl_c[fn] / n:6.2f} {fn}")
