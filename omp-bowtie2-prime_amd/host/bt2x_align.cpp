@@ -857,7 +857,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 				const uint32_t depth = i * interval + offset;
 				const uint32_t st = fw ? depth : (uint32_t)(rdlen - depth - L);
 				bool ok = true;
-				for(uint32_t k = 0; k < L; k++) if(s[st + k] > 3) { ok = false; break; }
+				if(rd.nN) for(uint32_t k = 0; k < L; k++) if(s[st + k] > 3) { ok = false; break; }
 				if(!ok) continue;
 				bt2x_seed_in si;
 				std::memset(&si, 0, sizeof(si));

@@ -336,13 +336,15 @@ public:
 	// ned: the alignment's own edits in ned() order (5'-relative for rc)
 	bool overlap(const AlnRes& r, const uint32_t* ned, size_t n) {
 		if(alns_.empty()) return false;
-		rows(r, ned, n, tmp_);
 		// the runs of each row lie inside the alignment's reference span [lo, hi): spans that
 		// do not meet rule a pair out without the per-row scan (a repetitive read reports
 		// many alignments at distinct loci; the scan over all of them was quadratic)
-		const int64_t lo = span_lo(tmp_), hi = span_hi(tmp_);
+		int64_t lo, hi;
+		span(r, ned, n, lo, hi);
+		bool have_rows = false;
 		for(Aln& a : alns_) {
 			if(a.refid != r.refid || a.fw != r.fw || a.hi <= lo || hi <= a.lo) continue;
+			if(!have_rows) { rows(r, ned, n, tmp_); have_rows = true; }
 			if(a.run0 < 0) {                               // its rows, kept from now on
 				AlnRes ar;
 				ar.refid = a.refid; ar.fw = a.fw; ar.refoff = a.refoff;
@@ -362,16 +364,33 @@ public:
 	// alignment keeps its span and edits, and its per-row runs are built the first time a
 	// later alignment's span meets it.
 	void add(const AlnRes& r, const uint32_t* ned, size_t n) {
-		rows(r, ned, n, tmp_);
-		alns_.push_back({r.refid, r.fw, r.refoff, (uint32_t)eds_.size(), (uint32_t)n, -1, span_lo(tmp_), span_hi(tmp_)});
+		int64_t lo, hi;
+		span(r, ned, n, lo, hi);
+		alns_.push_back({r.refid, r.fw, r.refoff, (uint32_t)eds_.size(), (uint32_t)n, -1, lo, hi});
 		eds_.insert(eds_.end(), ned, ned + n);
 	}
 private:
 	struct Aln { int64_t refid; bool fw; int64_t refoff; uint32_t e0, ne; int64_t run0; int64_t lo, hi; };
 	// rows' runs move right monotonically (left_{i+1} >= left_i): the first row's left and
-	// the last row's right bound every run
-	int64_t span_lo(const std::vector<int64_t>& t) const { return rdlen_ ? t[0] : 0; }
-	int64_t span_hi(const std::vector<int64_t>& t) const { return rdlen_ ? t[2 * rdlen_ - 1] : 0; }
+	// the last row's right bound every run.  From rows() below: left_0 = refoff,
+	// left_{i+1} = left_i + 1 + [read gaps at pos i+1] - [ref gap at pos i], and the last
+	// row's right = its left + 1, so the span is [refoff, refoff + rdlen + read gaps at
+	// pos 1..rdlen-1 - ref gaps at pos 0..rdlen-2) of the (inverted, for rc) edits: O(edits)
+	// instead of the O(rdlen) row pass (it runs for every reported alignment).
+	void span(const AlnRes& r, const uint32_t* ned, size_t n, int64_t& lo, int64_t& hi) const {
+		lo = rdlen_ ? r.refoff : 0;
+		if(!rdlen_) { hi = 0; return; }
+		int64_t d = 0;
+		const int64_t L = (int64_t)rdlen_;
+		for(size_t k = 0; k < n; k++) {
+			const uint32_t t = e_type(ned[k]);
+			int64_t p = (int64_t)e_pos(ned[k]);
+			if(!r.fw) p = L - p - (t == ET_READ_GAP ? 0 : 1);         // invert_poss
+			if(t == ET_READ_GAP && p >= 1 && p <= L - 1) d++;
+			else if(t == ET_REF_GAP && p >= 0 && p <= L - 2) d--;
+		}
+		hi = r.refoff + L + d;
+	}
 	void rows(const AlnRes& r, const uint32_t* ned0, size_t n, std::vector<int64_t>& out) {
 		const uint32_t* ned = ned0;
 		if(!r.fw) { invert_poss(ned0, n, rdlen_, inv_); ned = inv_.data(); }
@@ -537,6 +556,7 @@ struct Read {
 	std::vector<uint8_t> fw, rc;    // patFw / patRc codes 0..4
 	std::string qual, qualRev;      // Phred+33
 	uint32_t seed = 0;
+	uint32_t nN = 1;                // Ns in the read (decode counts them; 1 = not counted: scan)
 	size_t length() const { return fw.size(); }
 };
 
@@ -611,24 +631,37 @@ public:
 		if(raw.l[0][0] != '@') throw std::runtime_error("FASTQ record does not start with '@'");
 		r.rdid = rdid;
 		r.name.assign(raw.l[0] + 1, raw.n[0] - 1);
-		r.fw.clear();
-		r.fw.reserve(raw.n[1]);
-		for(size_t i = 0; i < raw.n[1]; i++) {
-			const unsigned char c = (unsigned char)(raw.l[1][i] == '.' ? 'N' : raw.l[1][i]);
-			if((unsigned)((c | 32u) - 'a') < 26u) r.fw.push_back(kAsc2Dna[c]);   // isalpha, "C" locale
+		// sequence: '.' is N, non-alphabetic characters are skipped (isalpha, "C" locale);
+		// written through a pointer into the resized buffer (no per-character push_back)
+		const size_t n1 = raw.n[1];
+		r.fw.resize(n1);
+		uint8_t* fw = r.fw.data();
+		size_t L = 0;
+		uint32_t nN = 0;
+		const unsigned char* sq = reinterpret_cast<const unsigned char*>(raw.l[1]);
+		for(size_t i = 0; i < n1; i++) {
+			const unsigned char c = sq[i] == '.' ? (unsigned char)'N' : sq[i];
+			const uint8_t code = kAsc2Dna[c];
+			const unsigned alpha = (unsigned)((c | 32u) - 'a') < 26u;
+			fw[L] = code;
+			nN += (code > 3) & alpha;
+			L += alpha;
 		}
+		r.fw.resize(L);
+		r.nN = nN;
 		r.qual.clear();
 		if(raw.n[1] || raw.n[3]) r.qual.assign(raw.l[3], raw.n[3]);
-		if(r.qual.size() != r.fw.size())
+		if(r.qual.size() != L)
 			throw std::runtime_error("read " + r.name + ": qualities and sequence differ in length");
 		if(r.name.empty()) r.name = std::to_string(name_id);
-		const size_t L = r.fw.size();
 		r.rc.resize(L);
+		uint8_t* rc = r.rc.data();
 		for(size_t i = 0; i < L; i++) {
-			const uint8_t c = r.fw[L - 1 - i];
-			r.rc[i] = c < 4 ? (uint8_t)(3 - c) : (uint8_t)4;
+			const uint8_t c = fw[L - 1 - i];
+			rc[i] = c < 4 ? (uint8_t)(3 - c) : (uint8_t)4;
 		}
-		r.qualRev.assign(r.qual.rbegin(), r.qual.rend());
+		r.qualRev.resize(L);
+		std::reverse_copy(r.qual.begin(), r.qual.end(), r.qualRev.begin());
 		r.seed = gen_rand_seed(r, randSeed);
 	}
 	static void decode(const Raw& raw, Read& r, uint64_t rdid, uint32_t randSeed) { decode(raw, r, rdid, randSeed, rdid); }
