@@ -170,6 +170,7 @@ struct bt2x_ctx {
 	uint32_t chunk_groups = 16384;             // DP chunk: 1 Mi problems, ~34 GB of traceback bytes
 	uint32_t* d_queue = nullptr;
 	unsigned long long* d_stats = nullptr;     // [0..2] seed, [4..6] dp, [8..10] resolve
+	uint8_t* d_mmpen = nullptr;                // sc.mmpen in HBM (DpLaunch::mmpen)
 	uint32_t* d_counters = nullptr;
 	uint64_t n_seed_last = 0, n_dp_last = 0, n_resolve_last = 0;
 	uint32_t n_round_last = 0;
@@ -184,7 +185,7 @@ bt2x_ctx::~bt2x_ctx() {
 	                 &b_jobs, &b_ranges, &b_rcnt})
 		b->release();
 	for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen, (void*)d_stats,
-	               (void*)d_counters, (void*)d_queue})
+	               (void*)d_counters, (void*)d_queue, (void*)d_mmpen})
 		if(p) (void)hipFree(p);
 	for(int k = 0; k < BT2X_K_COUNT; k++)
 		for(int j = 0; j < 2; j++) if(ev[k][j]) (void)hipEventDestroy(ev[k][j]);
@@ -319,6 +320,8 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	bt2x_scoring s;
 	if(sc) s = *sc; else bt2x_scoring_default(&s);
 	c->sc = to_dev(s);
+	HIPCHK(hipMalloc(&c->d_mmpen, sizeof c->sc.mmpen));
+	HIPCHK(hipMemcpy(c->d_mmpen, c->sc.mmpen, sizeof c->sc.mmpen, hipMemcpyHostToDevice));
 	HIPCHK(hipMalloc((void**)&c->d_stats, 32 * sizeof(unsigned long long)));
 	HIPCHK(hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)));
 	HIPCHK(hipMalloc((void**)&c->d_counters, 16 * sizeof(uint32_t)));
@@ -469,6 +472,7 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	a.reads = d_reads; a.quals = d_quals; a.refs = d_refs; a.in = d_in; a.n = n; a.out = d_out;
 	a.recs = d_recs; a.rec_cap = rec_cap; a.edits = d_edits; a.edit_cap = edit_cap;
 	a.counters = d_counters; a.stats = c->d_stats + 4;
+	a.mmpen = c->d_mmpen;
 	a.digests = d_debug ? d_debug->digests : nullptr;
 	a.cands = d_debug ? d_debug->cands : nullptr;
 	a.scratch = (uint8_t*)c->scratch.p; a.chunk_groups = groups; a.ncu = c->ncu; a.queue = c->d_queue;
@@ -490,15 +494,16 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	static const bool prof = [] { const char* e = getenv("BT2X_DP_PROF"); return e && e[0] == '1'; }();
 	if(prof) { a.prof = c->d_stats + 16; HIPCHK(hipMemsetAsync(a.prof, 0, 11 * sizeof(unsigned long long), s)); }
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
-	if(launch_flags & BT2X_DPL_REF_TEXT) {
-		if(!c->ix.text || !c->ix.rstarts) return BT2X_E_ARG;
-		if((rc = c->b_in2.ensure(sizeof(bt2x_dp_in) * (size_t)(n ? n : 1))) ||
-		   (rc = c->b_win.ensure((size_t)BT2X_MAX_COLS * (n ? n : 1))))
-			return rc;
-		if((rc = bt2x_launch_windows(c->ix, d_in, n, d_refs, (bt2x_dp_in*)c->b_in2.p, (uint8_t*)c->b_win.p, s))) return rc;
-		a.in = (const bt2x_dp_in*)c->b_in2.p;
-		a.refs = (const uint8_t*)c->b_win.p;
-	}
+	// every problem's window goes to a BT2X_MAX_COLS-byte slot (cut from the index for
+	// BT2X_DP_REF_TEXT problems, copied from d_refs for the others): the fill kernel reads
+	// its window as aligned dwords, 16 columns per load
+	if((launch_flags & BT2X_DPL_REF_TEXT) && (!c->ix.text || !c->ix.rstarts)) return BT2X_E_ARG;
+	if((rc = c->b_in2.ensure(sizeof(bt2x_dp_in) * (size_t)(n ? n : 1))) ||
+	   (rc = c->b_win.ensure((size_t)BT2X_MAX_COLS * (n ? n : 1))))
+		return rc;
+	if((rc = bt2x_launch_windows(c->ix, d_in, n, d_refs, (bt2x_dp_in*)c->b_in2.p, (uint8_t*)c->b_win.p, s))) return rc;
+	a.in = (const bt2x_dp_in*)c->b_in2.p;
+	a.refs = (const uint8_t*)c->b_win.p;
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));
 	if(prof) {                                   // development: where a lane-kernel wave's time goes

@@ -108,6 +108,8 @@ struct DpLaunch {
 	uint32_t heavy;
 	unsigned long long* prof;      // development (BT2X_DP_PROF=1): lane-kernel fill cycles, walk
 	                               // cycles, walk wave-steps, candidate wave-iterations, groups
+	const uint8_t* mmpen;          // DevScoring::mmpen in HBM (256 B): the kernels index it per lane,
+	                               // which a kernel-argument array would turn into SGPR spills
 };
 size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups);
 int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a, void* stream);

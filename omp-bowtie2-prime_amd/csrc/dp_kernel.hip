@@ -143,6 +143,28 @@ __device__ __forceinline__ uint32_t row_info(int rdc, bool gbar, int mm) {
 	return (uint32_t)rdc | (gbar ? 8u : 0u) | ((uint32_t)mm << 4);
 }
 
+// A byte string s[0, n) read as dwords: bytes4(k) = s[4k .. 4k+3] (byte r of the result is
+// s[4k+r]; bytes at positions >= n are unspecified).  Loads are dword-aligned and clamped
+// to the dword holding s[n-1], so they never touch a dword that holds no byte of the
+// string (nor a page the string does not reach); unaligned strings are shifted into place
+// with v_alignbyte.  n >= 1.
+struct ByteStr {
+	const uint32_t* base;         // the dword holding s[0]
+	uint32_t sh;                  // s[0]'s byte within it
+	int lastw;                    // index (from base) of the dword holding s[n-1]
+};
+__device__ __forceinline__ ByteStr byte_str(const uint8_t* s, int n) {
+	ByteStr b;
+	b.sh = (uint32_t)((uintptr_t)s & 3u);
+	b.base = reinterpret_cast<const uint32_t*>(s - b.sh);      // (pointer arithmetic: stays a global pointer)
+	b.lastw = (int)((b.sh + (uint32_t)n - 1u) >> 2);
+	return b;
+}
+__device__ __forceinline__ uint32_t bs_word(const ByteStr& b, int w) { return b.base[w < b.lastw ? w : b.lastw]; }
+__device__ __forceinline__ uint32_t bs_bytes4(const ByteStr& b, int k) {
+	return __builtin_amdgcn_alignbyte(bs_word(b, k + 1), bs_word(b, k), b.sh);
+}
+
 // An edit whose characters are not looked up yet (the walk records row, type and
 // reference column only): pos | type << 12 | kEditPending | col << 16.
 constexpr uint32_t kEditPending = 0x8000u;
@@ -166,8 +188,8 @@ __device__ __forceinline__ uint32_t pending_chars(uint32_t e, const uint8_t* rd,
 // Resolve the pending entries [0, ne) of a finished backtrace in place: characters, and
 // for mismatches the penalty (N: npen, else the quality's) and the N count the reference
 // accumulates as it walks (u8.cpp backtrace).  Eight entries per batch, loads together.
-__device__ __forceinline__ void resolve_edits(const DevScoring& sc, uint32_t* stage_ed, int lane, int ne,
-                                              const uint8_t* rd, const uint8_t* rf, const uint8_t* qu,
+__device__ __forceinline__ void resolve_edits(const DevScoring& sc, const uint8_t* mmpen, uint32_t* stage_ed, int lane,
+                                              int ne, const uint8_t* rd, const uint8_t* rf, const uint8_t* qu,
                                               int* bscore, int* ns) {
 	for(int k0 = 0; k0 < ne; k0 += 8) {
 		uint32_t v[8];
@@ -183,7 +205,7 @@ __device__ __forceinline__ void resolve_edits(const DevScoring& sc, uint32_t* st
 #pragma unroll
 		for(int u = 0; u < 8; u++) {
 			const int q0 = q[u] - 33;
-			pen[u] = sc.mmpen[q0 < 0 ? 0 : (q0 > 255 ? 255 : q0)];
+			pen[u] = mmpen[q0 < 0 ? 0 : (q0 > 255 ? 255 : q0)];
 		}
 #pragma unroll
 		for(int u = 0; u < 8; u++) {
@@ -241,7 +263,7 @@ __device__ __forceinline__ uint32_t publish_edbuf(const DpLaunch& a, const uint3
 // SwAligner::nextAlignment until done() for problem pi (lane gl of the group whose fill
 // output starts at gslot): its candidates in order, each not already reportedThrough
 // backtraced over the fill's traceback bytes; records and edits staged per lane.
-__device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunch& a, uint32_t pi,
+__device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t* mmpen, const DpLaunch& a, uint32_t pi,
                                              int lane, uint8_t* gslot, uint32_t* stage_ed,
                                              bt2x_aln_rec* stage_rec, unsigned long long& st_bt, bool refN,
                                              unsigned long long* pw = nullptr) {
@@ -418,7 +440,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const DpLaunc
 					stage_ed[(size_t)ne * 64 + lane] = pend_edit(row, EDIT_MM, col);
 					ne++;
 				}
-				resolve_edits(sc, stage_ed, lane, ne, rd, rf, qu, &bscore, &ns);
+				resolve_edits(sc, mmpen, stage_ed, lane, ne, rd, rf, qu, &bscore, &ns);
 				if(ns > p.nceil) { hi = max(hi, ne); continue; }
 				// reference Ns under the alignment: only windows holding an N (flagged by the
 				// fill) scan their columns
@@ -491,15 +513,237 @@ __device__ __forceinline__ void dp_verdict(bool i16, int lrmax, int minsc, int n
 	else { status = ncand > 0 ? 1 : 0; best = score; }
 }
 
+// ------------------------------------------------ the nextAlignment sequence, wave-parallel
+// SwAligner::nextAlignment until done() (aligner_sw.cpp:252-375) over a problem whose
+// traceback bytes are in LDS (tbb: column-major, S bytes per column), with all 64 lanes.
+// A backtrace (u8.cpp:746-1352) is a chain of dependent steps: the serial walk costs one
+// LDS round trip per step, and a repeat's candidates, walked one after another, reach
+// tens of thousands of steps.  Here:
+//  * Free paths, kParBatch candidates at a time, one per lane: the moves depend only on
+//    the cells' flags (never on marks), so each candidate's path from its start cell is
+//    walked independently, up to row 0 or to a cell marked by an attempt already
+//    validated (none of this batch marks anything).  Cells are kept as (row, col) u16.
+//  * Validation in DpBtCandidate order, all lanes on one attempt, 64 cells per round: the
+//    reference's attempt k walks its path until the first cell some earlier attempt
+//    marked (reportedThrough; a marked start cell: skipped, no RNG draw) or to row 0.  A
+//    ballot over the chunk's marks finds that cell; the walked cells are marked, their
+//    edits (the move to the path's next cell: diagonal with TB_MM, F up = ref gap, E left
+//    = read gap; open/extend from the cell's own E/F flag) are staged by prefix count,
+//    and score, N count, gaps and the core-diagonal test are lane sums.
+// Every mark, record, edit-buffer image and ntries equals the serial walk's: the same
+// attempts walk the same cells in the same order; only the order of marking within one
+// attempt differs, and no attempt reads its own cells.
+constexpr int kParBatch = 56;
+constexpr int kPathStride = 362;      // u16 cells per path (>= kRows + kCols - 1); 181 dwords: odd
+constexpr size_t kParPathBytes = (size_t)kParBatch * kPathStride * 2;
+
+__device__ __forceinline__ int wave_sum(int v) {
+	for(int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+	return v;
+}
+
+__device__ __forceinline__ void walk_wave_par(const DevScoring& sc, const DpLaunch& a, const bt2x_dp_in& p,
+                                              bt2x_dp_out& o, int lane, uint8_t* tbb, int S, const uint8_t* cands,
+                                              const uint8_t* rdw, const uint16_t* penw, const uint8_t* refw,
+                                              uint32_t* stage_ed, bt2x_aln_rec* stage_rec, uint16_t* path,
+                                              uint16_t* plen, unsigned long long& st_bt) {
+	const int R = p.rdlen, row0 = R - 1, ncand = o.ncand;
+	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
+	const uint64_t lt = (1ull << lane) - 1ull;
+	int ndone = 0, nrec = 0, b0 = 0, bn = 0;
+	while(ndone < ncand) {
+		int ntries = 0, hi = 0;
+		bool found = false;
+		while(ndone < ncand) {
+			const int k = ndone++;
+			if(k >= b0 + bn) {
+				// ---- free paths of candidates [k, k + nb)
+				const int nb = min(kParBatch, ncand - k);
+				if(lane < nb) {
+					int row = row0, col = cands[k + lane], ct = 2, n = 0;
+					uint16_t* pp = path + lane * kPathStride;
+					while(true) {
+						const uint32_t tb = tbb[col * S + row];
+						pp[n++] = (uint16_t)(row | (col << 8));
+						if((tb & TB_MARK) || row == 0) break;
+						const uint32_t dne = tb & TB_DNE, fne = (tb >> 1) & 1u;
+						const uint32_t fext = (tb >> 2) & 1u, eext = (tb >> 3) & 1u;
+						const bool inH = ct == 2;
+						const bool isD = inH && !dne;
+						const bool isF = (ct == 1) || (inH && dne && !fne);
+						ct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);
+						row -= (isD || isF) ? 1 : 0;
+						col -= isF ? 0 : 1;
+					}
+					plen[lane] = (uint16_t)n;
+				}
+				b0 = k; bn = nb;
+				__syncthreads();
+			}
+			const int len = (int)uni(plen[k - b0]);
+			const uint16_t* pk = path + (k - b0) * kPathStride;
+			if(a.ablate == 2) {                                   // profiling: no backtrace walks
+				if(!(uni(tbb[(pk[0] >> 8) * S + (pk[0] & 0xff)]) & TB_MARK)) ntries++;
+				continue;
+			}
+			// ---- validation: attempt k over its path, 64 cells per round
+			int ne = 0, walked = 0;
+			bool stopped = false, skip = false, termMM = false;
+			bool over = false;
+			int pen_l = 0, ns_l = 0, gaps_l = 0;
+			for(int c0 = 0; c0 < len; c0 += 64) {
+				const int idx = c0 + lane;
+				const bool v = idx < len;
+				const uint32_t cell = v ? pk[idx] : 0u;
+				const int row = (int)(cell & 0xffu), col = (int)(cell >> 8);
+				const int off = col * S + row;
+				const uint32_t tb = v ? tbb[off] : 0u;
+				const uint64_t mk = __builtin_amdgcn_ballot_w64(v && (tb & TB_MARK));
+				if(c0 == 0 && (mk & 1ull)) { skip = true; break; }      // start cell reportedThrough
+				const int nwk = mk ? (int)__builtin_ctzll(mk) : min(64, len - c0);
+				const bool w = lane < nwk;
+				const uint32_t ncell = (w && idx + 1 < len) ? pk[idx + 1] : cell;
+				const int nrow = (int)(ncell & 0xffu), ncl = (int)(ncell >> 8);
+				const bool term = w && row == 0;                       // a completed path's last cell
+				const bool isD = nrow != row && ncl != col, isF = nrow != row && ncl == col;
+				const bool mmE = w && !term && isD && (tb & TB_MM);
+				const bool gapE = w && !term && !isD;
+				const uint64_t eb = __builtin_amdgcn_ballot_w64(mmE || gapE);
+				if(mmE || gapE) {
+					const int pos = ne + (int)__builtin_popcountll(eb & lt);
+					stage_ed[pos] = mmE ? pack_edit((uint32_t)row, EDIT_MM, mask_chr(refw[col]), acgtn(rdw[row]))
+					              : isF ? pack_edit((uint32_t)row, EDIT_REF_GAP, '-', acgtn(rdw[row]))
+					                    : pack_edit((uint32_t)row + 1, EDIT_READ_GAP, mask_chr(refw[col]), '-');
+				}
+				ne += (int)__builtin_popcountll(eb);
+				if(w) {
+					const int diag = col - row + (int)p.triml;
+					over |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);
+					if(mmE) {
+						const bool amb = rdw[row] > 3 || refw[col] > 3;
+						pen_l += amb ? npen : (int)penw[row];
+						ns_l += amb ? 1 : 0;
+					}
+					if(gapE) {
+						const bool open = isF ? !(tb & TB_FONE) : !(tb & TB_EONE);
+						pen_l += isF ? (open ? rfo : rfe) : (open ? rdo : rde);
+						gaps_l++;
+					}
+					if(term) termMM = (tb & TB_MM) != 0;
+					tbb[off] = (uint8_t)TB_MARK;                           // setReportedThrough
+				}
+				walked += nwk;
+				if(mk) { stopped = true; break; }
+			}
+			__syncthreads();                                          // the marks, for the next attempt
+			if(skip) continue;
+			ntries++;
+			st_bt += (unsigned long long)(walked + (stopped ? 1 : 0));
+			if(stopped) { hi = max(hi, ne); continue; }
+			if(__builtin_amdgcn_ballot_w64(over) == 0) { hi = max(hi, ne); continue; }
+			// the final (row 0) cell's mismatch
+			const uint32_t tcell = uni(pk[len - 1]);
+			const int tcol = (int)(tcell >> 8);
+			termMM = __builtin_amdgcn_ballot_w64(termMM) != 0;
+			int bscore = -wave_sum(pen_l), ns = wave_sum(ns_l);
+			const int gaps = wave_sum(gaps_l);
+			if(termMM) {
+				const int rdc = (int)uni(rdw[0]), refc = (int)uni(refw[tcol]);
+				const bool amb = rdc > 3 || refc > 3;
+				if(lane == 0) stage_ed[ne] = pack_edit(0u, EDIT_MM, mask_chr(refc), acgtn(rdc));
+				ne++;
+				bscore -= amb ? npen : (int)uni(penw[0]);
+				ns += amb ? 1 : 0;
+			}
+			if(ns > p.nceil) { hi = max(hi, ne); __syncthreads(); continue; }
+			// reference Ns under the alignment: columns [tcol, col0]
+			const int col0 = (int)(uni(pk[0]) >> 8);
+			int refns = 0;
+			for(int c = tcol + lane; c <= col0; c += 64) refns += refw[c] > 3 ? 1 : 0;
+			refns = wave_sum(refns);
+			const int extent = R;
+			hi = max(hi, ne);
+			found = true;
+			__syncthreads();
+			// ned() order of the alignment's own entries [0, ne), in place: reverse (fw) or
+			// mirror positions (rc, invertEdits, edit.cpp:50-78)
+			uint32_t ev[(kEditStage + 63) / 64];
+#pragma unroll
+			for(int q = 0; q < (kEditStage + 63) / 64; q++) {
+				const int i = q * 64 + lane;
+				ev[q] = 0;
+				if(i < ne) {
+					uint32_t e = stage_ed[p.fw ? ne - 1 - i : i];
+					if(!p.fw) {
+						const uint32_t pos = (uint32_t)extent - (e & 0x3ffu) - (((e >> 12) & 7u) == EDIT_READ_GAP ? 0u : 1u);
+						e = (e & ~0x3ffu) | (pos & 0x3ffu);
+					}
+					ev[q] = e;
+				}
+			}
+			__syncthreads();
+#pragma unroll
+			for(int q = 0; q < (kEditStage + 63) / 64; q++) {
+				const int i = q * 64 + lane;
+				if(i < ne) stage_ed[i] = ev[q];
+			}
+			__syncthreads();
+			uint32_t eo = 0;
+			if(hi > 0) {
+				if(lane == 0) eo = atomicAdd(&a.counters[1], (uint32_t)hi);
+				eo = uni(eo);
+				if(eo + (uint32_t)hi <= a.edit_cap) for(int i = lane; i < hi; i += 64) a.edits[eo + i] = stage_ed[i];
+			}
+			if(lane == 0) {
+				bt2x_aln_rec r;
+				r.ntries = (uint16_t)ntries; r.ok = 1; r.pad0 = 0;
+				r.score = (int16_t)bscore; r.ns = (uint16_t)ns; r.gaps = (uint16_t)gaps;
+				r.nedit = (uint16_t)ne; r.bases_aligned = (uint16_t)(extent - ne);
+				r.refns = (uint16_t)refns; r.refoff = (int64_t)tcol + p.refl;
+				r.edit_off = eo; r.nbuf = (uint32_t)hi;
+				stage_rec[nrec] = r;
+			}
+			break;
+		}
+		if(!found) {
+			uint32_t eo = 0;
+			if(hi > 0) {
+				if(lane == 0) eo = atomicAdd(&a.counters[1], (uint32_t)hi);
+				eo = uni(eo);
+				if(eo + (uint32_t)hi <= a.edit_cap) for(int i = lane; i < hi; i += 64) a.edits[eo + i] = stage_ed[i];
+			}
+			if(lane == 0) {
+				bt2x_aln_rec r;
+				r.ntries = (uint16_t)ntries; r.ok = 0; r.pad0 = 0; r.score = 0; r.ns = 0; r.gaps = 0;
+				r.nedit = 0; r.bases_aligned = 0; r.refns = 0; r.refoff = 0;
+				r.edit_off = eo; r.nbuf = (uint32_t)hi;
+				stage_rec[nrec] = r;
+			}
+			nrec++;
+			break;
+		}
+		nrec++;
+	}
+	uint32_t ro = 0;
+	if(lane == 0) ro = atomicAdd(&a.counters[0], (uint32_t)nrec);
+	ro = uni(ro);
+	__syncthreads();                                                  // stage_rec (lane 0's stores)
+	if(ro + (uint32_t)nrec <= a.rec_cap) for(int i = lane; i < nrec; i += 64) a.recs[ro + i] = stage_rec[i];
+	o.nrec = (uint16_t)nrec; o.rec_off = ro;
+}
+
 // kMode 0: every problem of the launch.  kMode 1 (kBestOnly): the exact `best` of the
 // problems the banded lane kernel failed (a.fail_list[0 .. a.counters[2])): the whole
 // rectangle's last-row maximum, nothing else.  kMode 2: the problems the lane kernel handed
 // over after its fill (a.heavy_list): the whole call, their walks at LDS latency.
-template<int kMode>
+// kPar: the nextAlignment sequence with every lane (walk_wave_par) instead of lane 0.
+template<int kMode, bool kPar = false>
 __global__ void __launch_bounds__(64)
 dp_wave_kernel(DevScoring sc, DpLaunch a) {
 	constexpr bool kBestOnly = kMode == 1;
 	__shared__ uint32_t tbw[kBestOnly ? 1 : kWaveTbWords];
+	__shared__ uint16_t pathw[kPar ? kParBatch * kPathStride : 1];
+	__shared__ uint16_t plenw[kPar ? kParBatch : 1];
 	__shared__ uint8_t refw[kCols], cands[kCols];
 	__shared__ uint16_t lastrow[kCols];
 	__shared__ uint32_t stage_ed[kBestOnly ? 1 : kEditStage];
@@ -528,7 +772,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			for(int i = lane; i < R; i += 64) {
 				const int q0 = (int)qu[i] - 33;
 				rdw[i] = rd[i];
-				penw[i] = (uint16_t)sc.mmpen[q0 < 0 ? 0 : (q0 > 255 ? 255 : q0)];
+				penw[i] = (uint16_t)a.mmpen[q0 < 0 ? 0 : (q0 > 255 ? 255 : q0)];
 			}
 		// this lane's rows: read code (7 = N), mismatch penalty, gap-barred open/extend
 		uint32_t rc[4], mm[4], rdoe[4], rfoe[4], rfee[4];
@@ -542,7 +786,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 				q = q < 0 ? 0 : (q > 255 ? 255 : q);
 				gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
 				const int b = rd[i];
-				if(b <= 3) { c = (uint32_t)b; m = (uint32_t)sc.mmpen[q]; }
+				if(b <= 3) { c = (uint32_t)b; m = (uint32_t)a.mmpen[q]; }
 			}
 			rc[r] = c; mm[r] = m;
 			const uint32_t bar = gbar ? 0x10000u : 0u, r0 = (i == 0) ? 0x10000u : 0u;   // row 0 has no F
@@ -625,6 +869,13 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			cands[rank] = (uint8_t)j;
 		}
 		__syncthreads();
+		if(kPar) {
+			if(o.status != 0 && o.ncand > 0 && a.ablate != 1)
+				walk_wave_par(sc, a, p, o, lane, tbb, S, cands, rdw, penw, refw, stage_ed, stage_rec, pathw, plenw, st_bt);
+			if(lane == 0) a.out[pi] = o;
+			__syncthreads();
+			continue;
+		}
 		// ---- SwAligner::nextAlignment until done(), on lane 0 (see walk_problem).  Every
 		// value read from LDS is made wave-uniform (readfirstlane), so the walk's arithmetic
 		// runs on the scalar unit: one chain of LDS round trips and SALU ops per step.
@@ -774,8 +1025,13 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 	// LDS: the row info during the fill, then the last DP row (4 column keys per dword)
 	// for candidate ordering.  12.8 KiB per wave.
 	__shared__ uint32_t lds[(kCols / 4) * 64];
+	// the mismatch penalty by quality (DevScoring::mmpen), looked up per lane and row
+	__shared__ uint32_t pen4[64];
+	const uint8_t* pen_lds = reinterpret_cast<const uint8_t*>(pen4);
 	constexpr int kStateWords = kWide ? kRows / 2 : kRowWords;   // H/E state dwords per lane
 	const int lane = threadIdx.x;
+	pen4[lane] = reinterpret_cast<const uint32_t*>(a.mmpen)[lane];
+	__syncthreads();
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0, st_comp = 0;
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 	const uint32_t one2 = opaque(0x00010001u);
@@ -814,28 +1070,39 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const int thr = (int)p.minsc + top;
 		// ------------- row info (rows >= R: N, barred) ------------------------------
 		// 4 rows per dword, in LDS for the whole fill (constant per problem; the region
-		// holds the last row after the fill)
+		// holds the last row after the fill).  The read's codes and qualities come in 16
+		// rows at a time as dwords (a chain of byte loads per row would make this prologue
+		// a tenth of the fill), the penalty per quality from the LDS table.
 		const uint32_t kNone = row_info(7, true, npen);
+		const ByteStr rds = byte_str(rd, R > 0 ? R : 1), qus = byte_str(qu, R > 0 ? R : 1);
 #pragma unroll
-		for(int blk = 0; blk < kRowWords; blk++) {
-			uint32_t w = kNone * 0x01010101u;
-			if(blk * 4 < Rmax) {
-				w = 0;
+		for(int c16 = 0; c16 < kRows / 16; c16++) {
+			if(c16 * 16 < Rmax) {                                     // wave-uniform
+				uint32_t rw[4], qw[4];
 #pragma unroll
-				for(int r = 0; r < 4; r++) {
-					const int i = blk * 4 + r;
-					uint32_t b = kNone;
-					if(i < R) {
-						int q = (int)qu[i] - 33;
-						q = q < 0 ? 0 : (q > 255 ? 255 : q);
-						const bool gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
-						const int rc = rd[i];
-						b = rc > 3 ? row_info(7, gbar, npen) : row_info(rc, gbar, sc.mmpen[q]);
+				for(int k = 0; k < 4; k++) { rw[k] = bs_bytes4(rds, 4 * c16 + k); qw[k] = bs_bytes4(qus, 4 * c16 + k); }
+#pragma unroll
+				for(int k = 0; k < 4; k++) {
+					uint32_t w = 0;
+#pragma unroll
+					for(int r = 0; r < 4; r++) {
+						const int i = 16 * c16 + 4 * k + r;
+						uint32_t b = kNone;
+						if(i < R) {
+							int q = (int)((qw[k] >> (8 * r)) & 0xffu) - 33;
+							q = q < 0 ? 0 : q;
+							const bool gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
+							const int rc = (int)((rw[k] >> (8 * r)) & 0xffu);
+							b = rc > 3 ? row_info(7, gbar, npen) : row_info(rc, gbar, pen_lds[q]);
+						}
+						w |= b << (8 * r);
 					}
-					w |= b << (8 * r);
+					lds[(4 * c16 + k) * 64 + lane] = w;
 				}
+			} else {
+#pragma unroll
+				for(int k = 0; k < 4; k++) lds[(4 * c16 + k) * 64 + lane] = kNone * 0x01010101u;
 			}
-			lds[blk * 64 + lane] = w;
 		}
 		// ------------- fill: two columns per sweep, per-row state in VGPRs ------------
 		// H and E of the previous column: u8 4 rows per dword (40 + 40 dwords for 160
@@ -884,7 +1151,16 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const int npairs = (Cmax + 1) >> 1;
 		const __amdgpu_buffer_rsrc_t dirsrc =
 			__builtin_amdgcn_make_buffer_rsrc(dir, 0, (int)(kDirBytesLane * 64u), 0x00020000);
-		int refa = C > 0 ? rf[0] : 4, refb = C > 1 ? rf[1] : 4;
+		// The window's codes as dwords, 16 columns per load at every eighth pair: a load per
+		// pair made every pair wait for the previous pair's traceback stores (vmcnt counts
+		// loads and stores in issue order, and the compiler cannot count the band's
+		// stores), now one pair in eight does.  (Loads kept in flight across pairs are worse:
+		// the loop's register rotation copies them, and each copy waits.)  Windows sit in
+		// BT2X_MAX_COLS-byte slots (the window pass), so the dwords are aligned; loads are
+		// clamped to the window's last dword.
+		const uint32_t* rfw = reinterpret_cast<const uint32_t*>(rf);
+		const int lastw = ((C > 0 ? C : 1) - 1) >> 2;
+		uint32_t cw0 = 0, cw1 = 0, cw2 = 0, cw3 = 0;
 		uint32_t refN = 0;                              // an N in the window's columns [0, C)
 		for(int pp = 0; pp < npairs; pp++) {
 			const int j0 = 2 * pp;
@@ -901,9 +1177,18 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			// row-info loads stay inside the pair (hoisted out of it they would hold all 40
 			// words in VGPRs)
 			asm volatile("" ::: "memory");
-			const int ca = refa, cb = refb;
-			refa = (j0 + 2 < C) ? rf[j0 + 2] : 4;      // prefetch the next pair's bases
-			refb = (j0 + 3 < C) ? rf[j0 + 3] : 4;
+			if((pp & 7) == 0) {                           // wave-uniform: the next 16 columns
+				const int w0 = pp >> 1;
+				cw0 = rfw[min(w0, lastw)]; cw1 = rfw[min(w0 + 1, lastw)];
+				cw2 = rfw[min(w0 + 2, lastw)]; cw3 = rfw[min(w0 + 3, lastw)];
+				// consumed here, so the wait for them stays inside this branch (at the join it
+				// would run at every pair)
+				asm volatile("" : "+v"(cw0), "+v"(cw1), "+v"(cw2), "+v"(cw3));
+			}
+			const uint32_t wsel = (pp & 4) ? ((pp & 2) ? cw3 : cw2) : ((pp & 2) ? cw1 : cw0);
+			const uint32_t wsh = (uint32_t)(pp & 1) * 16u;
+			const int ca = (j0 < C) ? (int)((wsel >> wsh) & 0xffu) : 4;
+			const int cb = (j0 + 1 < C) ? (int)((wsel >> (wsh + 8u)) & 0xffu) : 4;
 			const uint32_t refc2 = (uint32_t)ca | ((uint32_t)cb << 16);
 			// N reference columns: every row pays the N penalty
 			const uint32_t coln = (ca > 3 ? 0x0000ffffu : 0u) | (cb > 3 ? 0xffff0000u : 0u);
@@ -1140,7 +1425,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			uint8_t* wslot = gslot + kGroupBytes;
 			const unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 			const unsigned long long bt0 = st_bt;
-			walk_problem(sc, a, pi, lane, gslot, reinterpret_cast<uint32_t*>(wslot + kEditOff),
+			walk_problem(sc, pen_lds, a, pi, lane, gslot, reinterpret_cast<uint32_t*>(wslot + kEditOff),
 			             reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, a.prof ? pw : nullptr);
 			if(a.prof) {
 				const unsigned long long t2 = __builtin_amdgcn_s_memtime();
@@ -1199,7 +1484,7 @@ dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const uint32_t q = grp * 64 + lane;
 		if(q < nprob) {
 			const uint32_t pi = base + q;
-			walk_problem(sc, a, pi, lane, a.scratch + (size_t)grp * kGroupBytes, stage_ed, stage_rec, st_bt, true);
+			walk_problem(sc, a.mmpen, a, pi, lane, a.scratch + (size_t)grp * kGroupBytes, stage_ed, stage_rec, st_bt, true);
 		}
 	}
 	if(a.stats) {
@@ -1249,6 +1534,14 @@ bool dp_split_mode() {
 // Largest launch run one wave per problem (BT2X_DP_WAVE=0: never, =1: always; else
 // BT2X_DP_WAVE_MAX problems, default 32768: below that a lane-per-problem launch does not
 // fill the chip and costs its serial R x C fill anyway).
+// The nextAlignment sequence of the wave kernel on every lane (walk_wave_par): the walks the
+// lane kernel hands over (default on; BT2X_DP_PARWALK=0: lane 0 as before) and, with
+// BT2X_DP_PARWALK=2, the small launches too.  Read per launch (tests switch it).
+int dp_parwalk() {
+	const char* e = getenv("BT2X_DP_PARWALK");
+	return e ? (e[0] - '0') : 1;
+}
+
 uint32_t dp_wave_max() {                        // read per launch (tests switch modes)
 	const char* w = getenv("BT2X_DP_WAVE");
 	const char* x = getenv("BT2X_DP_WAVE_MAX");
@@ -1291,7 +1584,8 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
 		if(wb > slots) wb = (uint32_t)slots;
 		if(wb > a0.n) wb = a0.n;
-		hipLaunchKernelGGL(dp_wave_kernel<0>, dim3(wb), dim3(64), 0, s, sc, a);
+		if(dp_parwalk() >= 2) hipLaunchKernelGGL((dp_wave_kernel<0, true>), dim3(wb), dim3(64), 0, s, sc, a);
+		else hipLaunchKernelGGL((dp_wave_kernel<0, false>), dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
 	if(!dp_split_mode()) {
@@ -1326,7 +1620,8 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		uint32_t wb = (uint32_t)a0.ncu * 4u;
 		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
 		if(wb > slots) wb = (uint32_t)slots;
-		hipLaunchKernelGGL(dp_wave_kernel<2>, dim3(wb), dim3(64), 0, s, sc, a);
+		if(dp_parwalk() >= 1) hipLaunchKernelGGL((dp_wave_kernel<2, true>), dim3(wb), dim3(64), 0, s, sc, a);
+		else hipLaunchKernelGGL((dp_wave_kernel<2, false>), dim3(wb), dim3(64), 0, s, sc, a);
 	}
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }

@@ -224,6 +224,19 @@ FastqReader::FastqReader(const std::vector<std::string>& paths, int shard, int n
 	if(!f_.empty()) pos_ = f_[0].beg;
 }
 
+void FastqReader::populate_ahead() {
+#ifndef MADV_POPULATE_READ
+#define MADV_POPULATE_READ 22
+#endif
+	constexpr size_t kWindow = 64u << 20;
+	const File& F = f_[cur_];
+	const size_t page = 4096;
+	const size_t a = pos_ & ~(page - 1);
+	const size_t b = std::min(F.end, pos_ + kWindow);
+	if(b > a && F.map) ::madvise((void*)(F.map + a), b - a, MADV_POPULATE_READ);
+	pop_end_ = b >= F.end ? (size_t)-1 : b;
+}
+
 FastqReader::~FastqReader() {
 	for(File& F : f_) {
 		if(F.map) ::munmap((void*)F.map, F.len);
@@ -1547,24 +1560,29 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	const auto put = [&writer](uint64_t id, std::string& rec) { writer.put(id, rec); };
 	if(slots < 2) slots = 2;
 	reserve_launch_buffers(pipeline_ ? slots / 2 : slots);
-	// FASTQ records are taken ahead on a helper thread (the record scan is serial): one batch
-	// of a cohort's size is in flight while the scheduler resumes, retires and gathers; refill
-	// consumes the taken records and starts the next batch.  The reader is touched by one
-	// thread at a time (the main thread only after collecting the batch in flight).
+	// FASTQ records are taken ahead on a helper thread (the record scan is serial): while
+	// fewer than a cohort's worth of taken records wait, one batch of a cohort's size is in
+	// flight while the scheduler resumes, retires and gathers; refill decodes straight from
+	// the taken records (no copies of the record list).  The reader is touched by one thread
+	// at a time (the main thread only after collecting the batch in flight).
 	const size_t batch = pipeline_ ? slots / 2 : slots;
 	std::vector<FastqReader::Raw> ahead, incoming;
 	size_t ahead_pos = 0;
 	bool src_eof = false;
 	std::future<size_t> ahead_f;
 	auto start_ahead = [&] {
-		if(src_eof) return;
+		if(src_eof || ahead_f.valid() || ahead.size() - ahead_pos >= batch) return;
 		incoming.clear();
 		ahead_f = std::async(std::launch::async, [&fq, &incoming, batch] { return fq.take(batch, incoming); });
 	};
+	std::vector<uint64_t> file_ends;           // the reader's file_end() values, copied while it is idle
+	auto note_files = [&] { while(file_ends.size() < fq.files_done()) file_ends.push_back(fq.file_end(file_ends.size())); };
 	auto collect = [&] {
 		if(!ahead_f.valid()) return;
 		if(ahead_f.get() < batch) src_eof = true;
-		ahead.erase(ahead.begin(), ahead.begin() + (long)ahead_pos);
+		note_files();
+		if(ahead_pos == ahead.size()) { ahead.swap(incoming); ahead_pos = 0; return; }
+		ahead.erase(ahead.begin(), ahead.begin() + (long)ahead_pos);      // the remainder: < one batch
 		ahead_pos = 0;
 		ahead.insert(ahead.end(), incoming.begin(), incoming.end());
 	};
@@ -1573,23 +1591,33 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	auto refill = [&](std::vector<ReadCtx*>& co, size_t cap) {
 		double t0 = now_s();
 		raw.clear();
+		const FastqReader::Raw* src = nullptr;
+		long nf = 0;
 		if(!eof && co.size() < cap) {
 			const size_t want = cap - co.size();
-			collect();
+			if(ahead.size() - ahead_pos < want) collect();
 			const size_t n = std::min(want, ahead.size() - ahead_pos);
-			raw.insert(raw.end(), ahead.begin() + (long)ahead_pos, ahead.begin() + (long)(ahead_pos + n));
-			ahead_pos += n;
-			if(n < want && !src_eof && fq.take(want - n, raw) < want - n) src_eof = true;
-			if(src_eof && ahead_pos == ahead.size()) eof = true;
-			// input files whose last record is out (the reader is idle here)
+			if(n < want && !src_eof) {
+				// (the helper is idle here: collect() joined it) the rest synchronously
+				raw.insert(raw.end(), ahead.begin() + (long)ahead_pos, ahead.begin() + (long)(ahead_pos + n));
+				ahead_pos += n;
+				if(fq.take(want - n, raw) < want - n) src_eof = true;
+				note_files();
+				src = raw.data();
+				nf = (long)raw.size();
+			} else {
+				src = ahead.data() + ahead_pos;
+				nf = (long)n;
+				ahead_pos += n;
+			}
+			if(src_eof && ahead_pos == ahead.size() && !ahead_f.valid()) eof = true;
+			// input files whose last record is out
 			const uint64_t written = writer.written();
-			while(st.t_files.size() < fq.files_done() && fq.file_end(st.t_files.size()) <= written)
+			while(st.t_files.size() < file_ends.size() && file_ends[st.t_files.size()] <= written)
 				st.t_files.push_back(now_s() - t_start);
-			start_ahead();
 		}
 		st.t_io += now_s() - t0;
-		const long nf = (long)raw.size();
-		if(!nf) return;
+		if(!nf) { start_ahead(); return; }
 		t0 = now_s();
 		fresh.resize((size_t)nf);
 		for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
@@ -1597,10 +1625,12 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		st.t_alloc += now_s() - t0;
 		pool().parallel_for(nf, 64, [&](long i) {
 			ReadCtx* c = fresh[(size_t)i];
-			FastqReader::decode(raw[(size_t)i], c->rd, rdid + (uint64_t)i, p_.randSeed, rdid0 + rdid + (uint64_t)i);
+			FastqReader::decode(src[i], c->rd, rdid + (uint64_t)i, p_.randSeed, rdid0 + rdid + (uint64_t)i);
 			c->task = align_read(c);
 			c->task.h.resume();
 		});
+		// (the decoded records are consumed: the helper may refill `incoming` from here on)
+		start_ahead();
 		rdid += (uint64_t)nf;
 		st.t_host += now_s() - t0;
 		co.insert(co.end(), fresh.begin(), fresh.end());

@@ -602,6 +602,7 @@ public:
 		size_t k = 0;
 		while(k < max) {
 			if(cur_ >= f_.size()) break;
+			if(pos_ >= pop_end_) populate_ahead();
 			Raw r;
 			const char* s;
 			size_t n;
@@ -667,6 +668,12 @@ public:
 	static void decode(const Raw& raw, Read& r, uint64_t rdid, uint32_t randSeed) { decode(raw, r, rdid, randSeed, rdid); }
 private:
 	struct File { const char* map = nullptr; size_t len = 0; int fd = -1; size_t beg = 0, end = 0; };
+	// Map the next window of the current file's part into the page table in one call
+	// (MADV_POPULATE_READ) instead of one minor fault per 4 KiB page as the scan reaches it
+	// (~0.7 M faults per 10 M reads); take() runs on the reader's helper thread, so this
+	// stays off the scheduler's path.  A kernel without it just faults as before.
+	void populate_ahead();
+	size_t pop_end_ = 0;
 	bool line(const char*& s, size_t& n) {
 		const File& F = f_[cur_];
 		if(pos_ >= F.end) return false;
@@ -680,6 +687,7 @@ private:
 	void file_done() {
 		ends_.push_back(taken_);
 		if(++cur_ < f_.size()) pos_ = f_[cur_].beg;
+		pop_end_ = 0;
 	}
 	std::vector<File> f_;
 	size_t cur_ = 0, pos_ = 0;

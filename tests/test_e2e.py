@@ -51,7 +51,7 @@ SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
 # the DP kernel modes each set runs through on the GPU: the launcher's default
 # (lane-per-problem banded kernel above BT2X_DP_WAVE_MAX problems, wave per problem
 # below), and each kernel forced for every launch
-DP_MODES = {"default": None, "lane": "0", "wave": "1", "hostwin": "host", "handover": "handover"}
+DP_MODES = {"default": None, "lane": "0", "wave": "1", "hostwin": "host", "handover": "handover", "parwave": "parwave"}
 MD5 = os.path.join(g.GOLDEN, "e2e_md5.json")
 SUMMARY = os.path.join(g.GOLDEN, "e2e_summary.json")
 
@@ -167,6 +167,7 @@ def test_host_driver_slot_count_invariance(fixtures):
 
 GPU_CASES = [(s, m) for s in SETS for m in DP_MODES
              if m == "default" or (m in ("hostwin", "handover") and s[0] in ("e2e_rep", "e2e_rep_i16_mix"))
+             or (m == "parwave" and s[0] in ("e2e_rep", "e2e_tandem", "e2e_tandem_i16", "e2e_rep_i16_mix"))
              or (m in ("lane", "wave") and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem", "e2e_rep_i16",
                                                     "e2e_tandem_i16", "e2e_rep_i16_mix"))]
 
@@ -182,11 +183,15 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     env.pop("BT2X_DP_WAVE", None)
     env.pop("BT2X_HOST_WINDOWS", None)
     env.pop("BT2X_DP_HEAVY", None)
+    env.pop("BT2X_DP_PARWALK", None)
     if DP_MODES[mode] == "host":
         env["BT2X_HOST_WINDOWS"] = "1"          # DP windows cut on the host (RefInfo::stretch)
     elif DP_MODES[mode] == "handover":
         env["BT2X_DP_WAVE"] = "0"
         env["BT2X_DP_HEAVY"] = "2"
+    elif DP_MODES[mode] == "parwave":             # wave per problem, its parallel walk
+        env["BT2X_DP_WAVE"] = "1"
+        env["BT2X_DP_PARWALK"] = "2"
     elif DP_MODES[mode] is not None:
         env["BT2X_DP_WAVE"] = DP_MODES[mode]
     _, err = check([ALIGN, "-x", fixtures[idx], "-U", fixtures[fq], "--slots", "1000"] + opts, name, env=env)

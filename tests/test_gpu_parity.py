@@ -141,12 +141,17 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     # (the small-launch mode), every record and the whole edit-buffer image
     sel = np.arange(len(dp)) < 12000
     fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff", "nbuf"]
-    for wave in ("0", "1"):
+    # (and every successful walk handed to the wave kernel's parallel walk; the wave mode
+    # with the parallel walk)
+    for wave, env in (("0", {}), ("1", {}), ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"})):
         os.environ["BT2X_DP_WAVE"] = wave
+        os.environ.update(env)
         try:
             out, recs, edits = ctx.dp_align(rd, qu, rf, dp, debug=False)[:3]
         finally:
             del os.environ["BT2X_DP_WAVE"]
+            for k in env:
+                del os.environ[k]
         _compare_out(out, eo, dp)
         for i in np.nonzero(out["nrec"] * sel)[0]:
             a = recs[out["rec_off"][i]: out["rec_off"][i] + out["nrec"][i]]
@@ -345,25 +350,32 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=True):
                                           eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
 
 
-@pytest.mark.parametrize("debug,wave,band,i16,heavy", [(False, "0", "1", 0.0, None), (False, "0", "0", 0.0, None),
-                                                       (False, "1", "1", 0.0, None), (True, "0", "1", 0.0, None),
-                                                       (False, "0", "1", 1.0, None), (False, "1", "1", 1.0, None),
-                                                       (True, "0", "1", 1.0, None), (False, "0", "1", 0.3, None),
-                                                       (True, "0", "1", 0.3, None),
-                                                       (False, "0", "1", 0.0, "0"), (False, "0", "1", 0.0, "1"),
-                                                       (False, "0", "1", 0.3, "1"), (False, "0", "0", 1.0, "2")])
-def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, monkeypatch):
+@pytest.mark.parametrize("debug,wave,band,i16,heavy,parwalk", [
+    (False, "0", "1", 0.0, None, None), (False, "0", "0", 0.0, None, None),
+    (False, "1", "1", 0.0, None, None), (True, "0", "1", 0.0, None, None),
+    (False, "0", "1", 1.0, None, None), (False, "1", "1", 1.0, None, None),
+    (True, "0", "1", 1.0, None, None), (False, "0", "1", 0.3, None, None),
+    (True, "0", "1", 0.3, None, None),
+    (False, "0", "1", 0.0, "0", None), (False, "0", "1", 0.0, "1", None),
+    (False, "0", "1", 0.3, "1", None), (False, "0", "0", 1.0, "2", None),
+    (False, "0", "1", 0.0, "1", "0"), (False, "1", "1", 0.0, None, "2"), (False, "1", "1", 1.0, None, "2"),
+    (False, "1", "1", 0.3, None, "2")])
+def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, parwalk, monkeypatch):
     """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
     wave-per-problem mode) and debug kernels on random shapes/penalty thresholds at the ABI
     limits vs the oracle: statuses, bests, candidates, every nextAlignment record and edit.
     i16: the share of BT2X_DP_I16 problems (all, or mixed into u8 launches; the 16-bit lane
     kernels, including minimum scores below -254).  heavy: BT2X_DP_HEAVY, the walk-step budget
     past which the lane kernel drops a problem for the wave kernel to redo (0: never; 1 and 2:
-    nearly every successful problem, mid-walk; default 896)."""
+    nearly every successful problem, mid-walk; default 896).  parwalk: BT2X_DP_PARWALK, the
+    wave kernel's nextAlignment sequence on all lanes (walk_wave_par; default: for the walks
+    handed over, 2: the small-launch mode too, 0: lane 0 everywhere)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     monkeypatch.setenv("BT2X_DP_BAND", band)
     if heavy is not None:
         monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
+    if parwalk is not None:
+        monkeypatch.setenv("BT2X_DP_PARWALK", parwalk)
     rd, qu, rf, inp = _random_dp_problems(6000, seed=77 + int(debug) + int(10 * i16), i16=i16)
     ctx = ctxs["rep"][0]
     res = ctx.dp_align(rd, qu, rf, inp, debug=debug)
@@ -396,14 +408,17 @@ def test_dp_exact_best_option(ctxs, monkeypatch):
 
 
 @pytest.mark.parametrize("gold", ["dp_rep_dpad12.txt.xz", "dp_rep_i16.txt.xz", "dp_rep_i16_mix.txt.xz"])
-@pytest.mark.parametrize("wave,heavy", [("0", None), ("1", None), ("0", "1")])
-def test_dp_production_kernel_on_golden(ctxs, wave, heavy, gold, monkeypatch):
+@pytest.mark.parametrize("wave,heavy,parwalk", [("0", None, None), ("1", None, None), ("0", "1", None),
+                                                ("1", None, "2"), ("0", "1", "0")])
+def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, gold, monkeypatch):
     """The production (non-debug) kernel, in both modes and with walks handed to the wave
-    kernel, reproduces the reference records of the golden set (oracle-checked, then against
-    the golden itself)."""
+    kernel (its parallel walk, and lane 0's), reproduces the reference records of the golden
+    set (oracle-checked, then against the golden itself)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     if heavy is not None:
         monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
+    if parwalk is not None:
+        monkeypatch.setenv("BT2X_DP_PARWALK", parwalk)
     case = g.DpCase(os.path.join(g.GOLDEN, gold))
     ctx = ctxs["rep"][0]
     out, recs, edits = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
