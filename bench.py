@@ -81,6 +81,10 @@ def parse(argv=None):
     ap.add_argument("--rss-limit-gb", type=float, default=200.0, help="kill bt2x-align above this host RSS")
     ap.add_argument("--aligner", default=ALIGN,
                     help="aligner binary (tests: tests/cpp/test_e2e_oracle, the host driver over the CPU oracle)")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the configs C2 and C5 legs (rank 0 at N=1: E. coli 1M x 100 bp --no-sse8; 5M x 400 bp)")
+    ap.add_argument("--c2-reads", type=int, default=1_000_000)
+    ap.add_argument("--c5-reads", type=int, default=5_000_000)
     ap.add_argument("--cpu-index", action="store_true",
                     help="index the genome with the host builder (bt2x_build_index) instead of the GPU suffix sort")
     return ap.parse_args(argv)
@@ -164,6 +168,17 @@ def make_inputs(args, rank, world, workdir):
         if not os.path.exists(path):
             jobs.append((path, n, args.read_len, 3 + 7919 * rank + 104729 * k, first))
         first += n
+    c5 = []
+    if rank == 0 and world == 1 and not args.no_legs and args.c5_reads > 0:
+        nf = 10
+        for k in range(nf):
+            n = args.c5_reads // nf + (1 if k < args.c5_reads % nf else 0)
+            path = os.path.join(rdir, f"c5_{k}_{n}_R400_g{args.genome_seed}.fq")
+            c5.append(path)
+            if not os.path.exists(path):
+                jobs.append((path, n, 400, 5 + 104729 * k, first))
+            first += n
+    args.c5_files = c5
     if jobs:
         _GEN["codes"], _GEN["starts"] = codes, starts
         procs = max(1, min(len(jobs), cpu_share() // max(world, 1)))
@@ -554,6 +569,99 @@ def sam_records(path, first_n=None):
     return recs
 
 
+def timed_align(args, base, files, warm, rdir, tag, extra):
+    """bt2x-align over `files` (the first `warm` untimed) -> (t_align, metrics, stats, stderr)."""
+    from bt2x import dist as bdist
+    out = os.path.join(rdir, f"{tag}.sam")
+    cmd = [args.aligner, "-x", base, "-U", ",".join(files), "-S", out, "-p", str(args.host_threads),
+           "--slots", str(args.slots), "--warmup-files", str(warm), "--metrics", "--stats"] + extra
+    err, wall, peak = run_aligner(args, cmd, os.path.join(rdir, f"{tag}.err"), f"{tag} timed run")
+    timed = kv_line(err, "BT2X_TIMED")
+    return float(timed["t_align"]), bdist.parse_metrics(err)["metrics"], kv_line(err, "BT2X_STATS"), out, peak
+
+
+def ref_baseline(args, binary, base, fqs, rdir, n, extra, tag):
+    """The reference aligner (binary) on the first n reads of fqs with the box's CPU share:
+    reads/s (alignment time = wall - wall of a 1-read run) and its SAM."""
+    share = cpu_share()
+    sample, one = os.path.join(rdir, f"{tag}_sample.fq"), os.path.join(rdir, f"{tag}_one.fq")
+    m = head_fastq(fqs, sample, n)
+    head_fastq(fqs, one, 1)
+    sam = os.path.join(rdir, f"{tag}_ref.sam")
+    env = dict(os.environ, OMP_NUM_THREADS=str(share), OMP_WAIT_POLICY="ACTIVE")
+    walls = []
+    for fq, dst in ((one, os.devnull), (sample, sam)):
+        t0 = time.perf_counter()
+        r = subprocess.run([binary, "-x", base, "-U", fq, "-S", dst] + extra, env=env, capture_output=True, text=True,
+                           timeout=900)
+        walls.append(time.perf_counter() - t0)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference aligner failed: {r.stderr[-2000:]}")
+    return {"value": round(m / max(walls[1] - walls[0], 1e-6) / 1e6, 6), "unit": "M reads/s", "cores": share,
+            "kind": "reference", "sample_reads": m,
+            "sample": f"first {m} reads through {os.path.relpath(binary, ROOT)} {' '.join(extra)} on the box's "
+                      f"{share}-CPU share, one run; alignment time = wall - wall of a 1-read run"}, sam
+
+
+def extra_legs(args, c3_base, rdir):
+    """BASELINE.json's other single-GPU configs, beside the C3 headline (rank 0, N=1):
+    C2 -- the E. coli stand-in (4.64 Mbp, simdata.ecoli_genome), 1M x 100 bp reads,
+          --no-sse8: the i16 DP kernel end to end (the reference's -DENABLE_I16 build beside
+          it, and a SAM comparison on its sample);
+    C5 -- 5M x 400 bp reads on the C3 genome: every read is unaligned by the reference's
+          rules (rdlen >= 256, bt2_search.cpp:2475-2496), so this measures throughput only
+          (FASTQ parse and SAM formatting; the GPU has nothing to do)."""
+    import simdata as sd
+    from bt2x import lib
+    legs = {}
+    # ---- C2
+    chroms = sd.ecoli_genome()
+    codes, starts = sd.concat_genome(chroms)
+    base = os.path.join(args.workdir, "ecoli")
+    if not os.path.exists(base + ".4.bt2l"):
+        sd.write_fasta(base + ".fa", chroms)
+        lib.build_index(base + ".fa", base)
+    files = []
+    for k, (n, seed) in enumerate(((args.c2_reads // 10, 17), (args.c2_reads, 11))):
+        path = os.path.join(rdir, f"c2_{k}_{n}_R100.fq")
+        if not os.path.exists(path):
+            reads, quals = sd.sim_reads_fast(codes, starts, n, 100, seed)
+            sd.write_fastq_fixed(path + ".tmp", reads, quals, first_id=0 if k == 0 else args.c2_reads // 10)
+            os.replace(path + ".tmp", path)
+        files.append(path)
+    t, met, stats, out, peak = timed_align(args, base, files, 1, rdir, "c2", ["--no-sse8"])
+    leg = {"workload": f"C2 stand-in: {args.c2_reads} x 100 bp SE reads vs the seeded 4.64 Mbp E. coli stand-in, "
+                       "--no-sse8 (the i16 DP kernel; the reference's -DENABLE_I16 build), FASTQ -> SAM",
+           "value": round(met["nread"] / t / 1e6, 4), "unit": "M reads/s", "t_align_s": round(t, 3),
+           "reads": met["nread"], "aligned": met["nunp_uni"] + met["nunp_rep"], "stats": stats, "peak_rss_mib": peak}
+    ref16 = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l-i16")
+    if not args.no_cpu and os.access(ref16, os.X_OK):
+        cb, rsam = ref_baseline(args, ref16, base, files[1:], rdir, 200_000, ["--no-sse8"], "c2")
+        leg["cpu_baseline"] = cb
+        leg["parity"] = parity(out, rsam, cb["sample_reads"])
+        leg["gpu_vs_cpu"] = round(leg["value"] / cb["value"], 2) if cb["value"] else None
+    os.unlink(out)
+    legs["C2"] = leg
+    # ---- C5
+    c5 = getattr(args, "c5_files", [])
+    if c5:
+        t, met, stats, out, peak = timed_align(args, c3_base, c5, 1, rdir, "c5", [])
+        n = met["nread"]
+        leg = {"workload": f"C5 stand-in: {args.c5_reads} x 400 bp SE reads vs the C3 genome (the first file of "
+                           f"{os.path.basename(c5[0]).split('_')[2]} reads untimed); every record unaligned as in the "
+                           "reference (reads of 256 bp or more), so throughput only: FASTQ parse + SAM",
+               "value": round(n / t / 1e6, 4), "unit": "M reads/s", "t_align_s": round(t, 3), "reads": n,
+               "aligned": met["nunp_uni"] + met["nunp_rep"], "peak_rss_mib": peak}
+        if not args.no_cpu and os.access(REF_ALIGN, os.X_OK):
+            cb, rsam = ref_baseline(args, REF_ALIGN, c3_base, c5[1:], rdir, 500_000, [], "c5")
+            leg["cpu_baseline"] = cb
+            leg["parity"] = parity(out, rsam, cb["sample_reads"])
+            leg["gpu_vs_cpu"] = round(leg["value"] / cb["value"], 2) if cb["value"] else None
+        os.unlink(out)
+        legs["C5"] = leg
+    return legs
+
+
 def parity(ours_sam, ref_sam, n) -> dict:
     """Our timed run's first n SAM records (records are written in input order) against
     the reference aligner's records for the same n reads, compared sorted."""
@@ -674,6 +782,8 @@ def main():
             line["gpu_vs_cpu"] = round(value / cb["value"], 2) if cb["value"] else None
     if out_sam != os.devnull and os.path.exists(out_sam):
         os.unlink(out_sam)
+    if rank == 0 and world == 1 and not args.no_legs:
+        line["configs_other"] = extra_legs(args, base, rdir)
     if dist:
         dist.barrier()
     if rank == 0:

@@ -85,3 +85,24 @@ def test_bench_two_ranks_on_cpu(tmp_path):
     assert abs(line["value"] - 2 * reads / e["t_align_max_s"] / 1e6) < 1e-3
     assert e["t_align_max_s"] >= e["t_align_s"] > 0
     assert line["config"]["host_threads"] == 2
+
+
+def test_bench_one_rank_with_config_legs_on_cpu(tmp_path):
+    """bench.py at N=1 with the C2 (E. coli, --no-sse8) and C5 (400 bp) legs, at toy sizes,
+    through the host driver over the CPU oracle: every leg reports a rate, C5 aligns nothing
+    (reads of 256 bp or more), and the reference baselines and parity run where the
+    reference binaries are built."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", BT2X_BENCH_DIR=str(tmp_path / "work"))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--reads", "600",
+           "--genome-mb", "0.25", "--replay-reads", "200", "--slots", "512", "--host-threads", "2", "--no-replay",
+           "--cpu-index", "--aligner", ORACLE_DRIVER, "--c2-reads", "1500", "--c5-reads", "1000",
+           "--cpu-sample", "300", "--cpu-sample-1t", "100"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    legs = line["configs_other"]
+    assert legs["C2"]["reads"] == 1500 and legs["C2"]["value"] > 0 and legs["C2"]["aligned"] > 1400
+    assert legs["C5"]["reads"] == 900 and legs["C5"]["aligned"] == 0          # the first file is untimed
+    if os.access(os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l"), os.X_OK):
+        assert line["parity"]["records_differ"] == 0 and line["parity"]["sample_reads"] == 300
+        assert legs["C2"]["parity"]["records_differ"] == 0 and legs["C5"]["parity"]["records_differ"] == 0

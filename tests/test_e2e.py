@@ -258,9 +258,10 @@ def md5_opts(st) -> list[str]:
     return [o for o in st["opts"]]
 
 
-@pytest.mark.parametrize("name", ["ecoli_u8", "ecoli_i16"])
+@pytest.mark.parametrize("name", ["ecoli_u8", "ecoli_i16", "ecoli_c5_400", "ecoli_long_200"])
 def test_host_driver_vs_reference_md5_ecoli(ecoli, name):
-    """Config C2 (u8 and the i16 kernel): host driver + CPU oracle kernels == reference."""
+    """Config C2 (u8 and the i16 kernel) and config C5's 400 bp reads (and 200 bp ones): host
+    driver + CPU oracle kernels == reference."""
     base, reads = ecoli
     err = check_md5([ORACLE_DRIVER, base, reads[name], "--slots", "2000", "-p", "4", "--metrics"]
                     + md5_opts(md5_sets()["sets"][name]), name)
@@ -275,11 +276,14 @@ def test_host_driver_vs_reference_md5_lambda_full(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["ecoli_u8", "ecoli_i16", "ecoli_large_u8", "ecoli_large_i16"])
+@pytest.mark.parametrize("name", ["ecoli_u8", "ecoli_i16", "ecoli_large_u8", "ecoli_large_i16", "ecoli_c5_400",
+                                  "ecoli_long_200"])
 def test_bt2x_align_vs_reference_md5_ecoli(ecoli, name):
-    """Config C2 and the 50k-read sets on the MI355X.  The large sets run with every read in
-    flight (--slots 65536): DP launches of more than 32k problems take the banded lane
-    kernel (checked from the run's launch statistics)."""
+    """Config C2, the 50k-read sets and config C5's fixed-length 400 bp reads (every record
+    unaligned: reads of 256 bp or more never reach the seed search, bt2_search.cpp:2475-2496)
+    on the MI355X.  The large sets run with every read in flight (--slots 65536): DP launches
+    of more than 32k problems take the banded lane kernel (checked from the run's launch
+    statistics)."""
     base, reads = ecoli
     large = "large" in name
     err = check_md5([ALIGN, "-x", base, "-U", reads[name], "--slots", "65536" if large else "4096", "--stats"]

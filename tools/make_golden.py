@@ -195,11 +195,16 @@ def i16_goldens(tmp: str) -> None:
 #   ecoli_*: config C2 -- the seeded 4.64 Mbp genome (simdata.ecoli_genome, indexed by the
 #            reference builder; FASTA and index md5s pinned) with simdata.fixture_reads
 #   ecoli_large_*: 50k x 150 bp at --dpad 12: DP launches of > 32k problems (the lane kernel)
+#   ecoli_c5_400: config C5's read shape, 20k fixed-length 400 bp reads: every read is
+#            unaligned (rdlen >= 256, bt2_search.cpp:2475-2496)
+#   ecoli_long_200: 200 bp reads (161..255: seeded, then initRead's 160-row cap, F2)
 #   lambda_full: config C1, all 6000 example/reads/longreads.fq reads, 1 thread
 MD5_SETS = [("ecoli_i16", 10000, 100, 1, "i16", ["--no-sse8"]),
             ("ecoli_u8", 10000, 100, 1, "u8", []),
             ("ecoli_large_u8", 50000, 150, 3, "u8", ["--dpad", "12"]),
-            ("ecoli_large_i16", 50000, 150, 3, "i16", ["--no-sse8", "--dpad", "12"])]
+            ("ecoli_large_i16", 50000, 150, 3, "i16", ["--no-sse8", "--dpad", "12"]),
+            ("ecoli_c5_400", 20000, 400, 5, "u8", []),
+            ("ecoli_long_200", 4000, 200, 5, "u8", [])]
 
 
 def sam_md5(path: str) -> tuple[str, int, int]:
