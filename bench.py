@@ -169,7 +169,7 @@ def make_inputs(args, rank, world, workdir):
             jobs.append((path, n, args.read_len, 3 + 7919 * rank + 104729 * k, first))
         first += n
     c5 = []
-    if rank == 0 and world == 1 and not args.no_legs and args.c5_reads > 0:
+    if rank == 0 and world == 1 and not getattr(args, "no_legs", True) and getattr(args, "c5_reads", 0) > 0:
         nf = 10
         for k in range(nf):
             n = args.c5_reads // nf + (1 if k < args.c5_reads % nf else 0)

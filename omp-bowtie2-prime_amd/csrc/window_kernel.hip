@@ -53,11 +53,17 @@ __global__ void __launch_bounds__(256) window_kernel(DevIndex ix, const bt2x_dp_
 		const uint64_t t = p.ref_off;
 		const int64_t nfrag = (int64_t)ix.nfrag;
 		const int64_t lo = frag_text_lb(ix.rstarts, nfrag, t), hi = frag_text_lb(ix.rstarts, nfrag, t + 1);
+		// one search per problem (every lane the same addresses: broadcast loads), then each
+		// column moves forward from the window start's fragment; a window rarely crosses one
+		// (per-column binary searches made this kernel a chain of dependent loads per column)
+		const int64_t k0 = frag_at(ix.rstarts, lo, hi, p.refl);
 		for(uint32_t c = lane; c < ncol; c += 64u) {
 			const int64_t off = p.refl + (int64_t)c;
 			uint8_t code = 4;
+			int64_t kc = k0 < lo ? lo - 1 : k0;
+			while(kc + 1 < hi && (int64_t)ix.rstarts[3 * (kc + 1) + 2] <= off) kc++;
 			// the last non-empty fragment starting at or before off (RefInfo::stretch's rule)
-			for(int64_t k = frag_at(ix.rstarts, lo, hi, off); k >= lo; k--) {
+			for(int64_t k = kc; k >= lo; k--) {
 				const uint64_t joff = ix.rstarts[3 * k], toff = ix.rstarts[3 * k + 2];
 				const uint64_t jend = k + 1 < nfrag ? ix.rstarts[3 * (k + 1)] : ix.len;
 				if(jend == joff) continue;

@@ -38,3 +38,44 @@ def test_integration_md_uses_the_compiled_glue():
     for call in ("swa.initRead(rd.patFw, rd.patRc, rd.qual, rd.qualRev, rdlen, sc)", "swa.align(best)",
                  "swa.nextAlignment(v, (int64_t)minsc, rnd)", "swa.done()"):
         assert call in check
+
+
+# ------------------------------------------------------------------ the drop-in, executed
+# oracle/ref_glue_build.py builds the reference aligner itself with the two patches
+# applied -- its searchAllSeedsDoAll and its SwAligner (initRead / initRef / align /
+# nextAlignment / done) routed through libbt2x.so via include/bt2x_ref_glue.hpp and
+# include/bt2x_shims.hpp -- into oracle/_ref/bowtie2-align-l-bt2x[-i16] (built here, where
+# /root/reference exists; the binaries travel to the GPU box).  Its SAM, alignment summary
+# and warnings must equal the stock reference's (the committed e2e goldens).
+PATCHED = {"u8": os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l-bt2x"),
+           "i16": os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l-bt2x-i16")}
+DROPIN_SETS = [("e2e_rep", "rep", "rep_reads.fq", [], "u8"),
+               ("e2e_tandem", "tandem", "tandem_reads.fq", [], "u8"),
+               ("e2e_rep_dpad12", "rep", "rep_reads.fq", ["--dpad", "12"], "u8"),
+               ("e2e_rep_i16", "rep", "rep_reads.fq", ["--no-sse8"], "i16")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,idx,fq,opts,build", DROPIN_SETS, ids=[s[0] for s in DROPIN_SETS])
+def test_patched_reference_aligner_on_gpu(tmp_path, name, idx, fq, opts, build):
+    import lzma
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import golden_io as g
+    from test_e2e import check_summary, sam_records
+    binary = PATCHED[build]
+    if not os.access(binary, os.X_OK):
+        pytest.skip("oracle/_ref/ has no patched reference build (needs /root/reference where it is built)")
+    base = g.materialize_index(idx, str(tmp_path))
+    reads = tmp_path / fq
+    with lzma.open(os.path.join(g.GOLDEN, fq + ".xz"), "rb") as f:
+        reads.write_bytes(f.read())
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run([binary, "-x", base, "-U", str(reads)] + opts, capture_output=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    with lzma.open(os.path.join(g.GOLDEN, name + ".sam.xz"), "rb") as f:
+        exp = sam_records(f.read())
+    got = sam_records(r.stdout)
+    bad = [(a, b) for a, b in zip(got, exp) if a != b]
+    assert len(got) == len(exp) and not bad, (len(got), len(exp), bad[:1])
+    check_summary(b"\n".join(ln for ln in r.stderr.split(b"\n") if not ln.startswith(b"Timer:")), name)

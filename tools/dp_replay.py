@@ -40,7 +40,7 @@ def main():
     import bench
 
     ns = argparse.Namespace(genome_mb=args.genome_mb, genome_seed=2024, reads=args.reads, steps=1, warmup=0,
-                            read_len=150, replay_reads=args.reads, dpad=args.dpad)
+                            read_len=150, replay_reads=args.reads, dpad=args.dpad, no_legs=True)
     os.makedirs(args.workdir, exist_ok=True)
     chroms, codes, warm, steps, per = bench.make_inputs(ns, 0, 1, args.workdir)
     base, _ = bench.build_index(ns, chroms, codes, args.workdir, 0, None)
