@@ -22,26 +22,31 @@ namespace glue {
 
 // The seed batch of MultiSeedAligner as one GPU call.  The reference's extension walks
 // seq[-ii] over the `lim` read characters left of the seed (SeedResults::get_rel_offs,
-// aligner_seed.h:1155); the kernel gets those characters in read order, then the seed.
-// Returns false on a device error (the caller's `throw 1`).
+// aligner_seed.h:1155), and the seed itself is read[lim .. lim+len) of the same oriented
+// read (SeedAligner::instantiateSeq, aligner_seed.cpp:301-314), so the kernel gets that
+// read's prefix in place: seeds of one read orientation share one pointer, which
+// MultiSeedAlignerHip::add copies once.  Returns false on a device error (the caller's
+// `throw 1`).
 template<class Params, class Data>
 bool search_all_seeds(MultiSeedAlignerHip& gpu, const Params* paramVec, Data* dataVec, size_t n, bool doExtend) {
 	gpu.clear();
-	std::vector<uint8_t> buf;
 	for(size_t i = 0; i < n; i++) {
 		const Params& p = paramVec[i];
 		const char* left = nullptr;
 		uint8_t lim = 0;
 		p.sr->get_rel_offs(p.fw, (uint8_t)p.sr->idx2off(p.seedoffidx), left, lim);
-		buf.assign((size_t)lim + p.cs.seq_len, 0);
-		for(int k = 0; k < lim; k++) buf[(size_t)k] = (uint8_t)left[k - (lim - 1)];   // read[0 .. seed_off)
-		for(int k = 0; k < p.cs.seq_len; k++) buf[(size_t)lim + (size_t)k] = (uint8_t)p.cs.seq[k];
-		gpu.add(buf.data(), buf.size(), /*seed_off*/ lim, /*seed_len*/ (size_t)p.cs.n_seed_steps);
+		const char* read = lim ? left - (lim - 1) : left;          // the oriented read's first character
+		if(read + lim != p.cs.seq) return false;                   // not the layout above
+		gpu.add(reinterpret_cast<const uint8_t*>(read), (size_t)lim + p.cs.seq_len, /*seed_off*/ lim,
+		        /*seed_len*/ (size_t)p.cs.n_seed_steps);
 	}
 	if(!gpu.searchAllSeedsDoAll(doExtend)) return false;
 	for(size_t i = 0; i < n; i++) {
 		const bt2x_seed_out& o = gpu.data((uint32_t)i);
 		Data& d = dataVec[i];
+		// searchSeedBi's per-seed reset (aligner_seed.cpp:849): the seed key (SAKey) the
+		// caller's seed cache is keyed on is set here, not by the search itself
+		d.resetData(paramVec[i].cs.seq, paramVec[i].cs.seq_len);
 		d.bwt.topf = o.topf;                 // BwtTopBotFw (valid when need_reporting)
 		d.bwt.botf = o.botf;
 		d.nlex = o.nlex;

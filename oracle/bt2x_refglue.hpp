@@ -8,6 +8,8 @@
 // SwAligner::initRead/initRef/align/nextAlignment and aligner_sw.h's done()) call these.
 #pragma once
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <unordered_map>
@@ -19,6 +21,12 @@ namespace bt2x_refglue {
 
 // defined after the reference's TU (they read its globals bt2index and multiseed_sc)
 bt2x::Device& device();
+
+// BT2X_GLUE_TRACE=1: one stderr line per patched call (debugging the drop-in)
+inline bool trace() {
+	static const bool t = std::getenv("BT2X_GLUE_TRACE") != nullptr;
+	return t;
+}
 
 inline std::mutex& gpu_mutex() {
 	static std::mutex m;

@@ -19,7 +19,11 @@ repository; the only output is the binary in oracle/_ref/ (git-ignored).
   SwAligner::nextAlignment                aligner_sw.cpp:252-375
   SwAligner::done                         aligner_sw.h:322-325
 
-    python3 oracle/ref_glue_build.py [--ref /root/reference] [--i16]
+With --cpu the binary links oracle/bt2x_abi_oracle.cpp (the C-ABI answered by the CPU
+oracle) instead of libbt2x.so, so the CPU suite runs the same glue; BT2X_GLUE_TRACE=1 at run
+time prints one line per patched call.
+
+    python3 oracle/ref_glue_build.py [--ref /root/reference] [--i16] [--cpu] [--only seeds|sw]
 """
 from __future__ import annotations
 
@@ -63,6 +67,11 @@ PATCHES = [
 	std::lock_guard<std::mutex> g_(bt2x_refglue::gpu_mutex());
 	static bt2x::MultiSeedAlignerHip* gpu_ = new bt2x::MultiSeedAlignerHip(bt2x_refglue::device());
 	if(!bt2x::glue::search_all_seeds(*gpu_, _paramVec, _dataVec, _bufVec_filled, doExtend)) throw 1;
+	if(bt2x_refglue::trace())
+		for(size_t i_ = 0; i_ < _bufVec_filled; i_++)
+			fprintf(stderr, "GLUE seed %zu fw=%d off=%d topf=%llu botf=%llu nlex=%u rep=%d\n", i_, (int)_paramVec[i_].fw,
+			        (int)_paramVec[i_].sr->idx2off(_paramVec[i_].seedoffidx), (unsigned long long)_dataVec[i_].bwt.topf,
+			        (unsigned long long)_dataVec[i_].bwt.botf, (unsigned)_dataVec[i_].nlex, (int)_dataVec[i_].need_reporting);
 }'''),
     (r"bool\s+SwAligner::initRead\s*\(", None, r'''{
 	rdfw_ = &rdfw; rdrc_ = &rdrc; qufw_ = &qufw; qurc_ = &qurc; rdlen_ = rdlen; sc_ = &sc;
@@ -75,6 +84,9 @@ PATCHES = [
 	s_.refidx = (size_t)refidx; s_.reflen = (int64_t)reflen;
 	fw_ = fw;
 	initedRef_ = s_.swa.initRef(fw, (size_t)refidx, rect, refs, (int64_t)reflen, (int64_t)minsc, enable8, extend, upto, nsUpto);
+	if(bt2x_refglue::trace())
+		fprintf(stderr, "GLUE initRef fw=%d ref=%zu rect=[%lld,%lld] minsc=%lld ok=%d\n", (int)fw, (size_t)refidx,
+		        (long long)rect.refl, (long long)rect.refr, (long long)minsc, (int)initedRef_);
 	return initedRef_;
 }'''),
     (r"bool\s+SwAligner::align\s*\(", None, r'''{
@@ -82,6 +94,7 @@ PATCHES = [
 	int64_t b_ = 0;
 	const bool ok_ = bt2x_refglue::sw(this).swa.align(b_);
 	best = (TAlScore)b_;
+	if(bt2x_refglue::trace()) fprintf(stderr, "GLUE align ok=%d best=%lld\n", (int)ok_, (long long)b_);
 	return ok_;
 }'''),
     (r"bool\s+SwAligner::nextAlignment\s*\(", None, r'''{
@@ -89,6 +102,9 @@ PATCHES = [
 	bt2x::AlnView v_;
 	const bool ok_ = s_.swa.nextAlignment(v_, (int64_t)minsc, rnd);
 	bt2x::glue::to_swresult(v_, ok_, res, s_.refidx, s_.reflen, rdlen_);
+	if(bt2x_refglue::trace())
+		fprintf(stderr, "GLUE next ok=%d score=%lld refoff=%lld fw=%d ned=%zu\n", (int)ok_, (long long)v_.score,
+		        (long long)v_.refoff, (int)v_.fw, (size_t)v_.edits.size());
 	return ok_;
 }'''),
 ]
@@ -149,12 +165,19 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--i16", action="store_true", help="the -DENABLE_I16 build")
+    ap.add_argument("--cpu", action="store_true",
+                    help="link oracle/bt2x_abi_oracle.cpp (the C-ABI answered by the CPU oracle) instead of "
+                         "libbt2x.so, so the patched aligner runs in the CPU test suite")
+    ap.add_argument("--only", choices=["seeds", "sw"], default=None,
+                    help="apply only the seed-search or only the SwAligner patch (bisecting a mismatch)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    out = a.out or os.path.join(HERE, "_ref", "bowtie2-align-l-bt2x" + ("-i16" if a.i16 else ""))
+    out = a.out or os.path.join(HERE, "_ref", "bowtie2-align-l-bt2x" + ("-i16" if a.i16 else "") +
+                                ("-cpu" if a.cpu else ""))
     os.makedirs(os.path.dirname(out), exist_ok=True)
     deps = [os.path.abspath(__file__), os.path.join(HERE, "bt2x_refglue.hpp")] + \
-        [os.path.join(ROOT, "include", h) for h in ("bt2x.h", "bt2x_shims.hpp", "bt2x_ref_glue.hpp")]
+        [os.path.join(ROOT, "include", h) for h in ("bt2x.h", "bt2x_shims.hpp", "bt2x_ref_glue.hpp")] + \
+        ([os.path.join(HERE, f) for f in ("bt2x_abi_oracle.cpp", "bt2x_oracle.c", "bt2x_oracle.h")] if a.cpu else [])
     if os.path.exists(out) and os.path.getmtime(out) > max(os.path.getmtime(d) for d in deps):
         return                                    # up to date (libbt2x.so is linked dynamically)
     cxx = os.environ.get("CXX", "g++")
@@ -169,19 +192,30 @@ def main() -> None:
                         "-I" + os.path.join(ROOT, "include"), "-I" + HERE, tu, "-o", ii], check=True)
         src = open(ii).read()
         for sig, sel, body in PATCHES:
+            if a.only and (a.only == "seeds") != ("searchAllSeeds" in sig):
+                continue
             src = replace_body(src, sig, sel, body)
         # SwAligner::done(), an inline member in the class body
-        c = re.search(r"class\s+SwAligner\s*\{", src)
-        if not c:
+        c = None if a.only == "seeds" else re.search(r"class\s+SwAligner\s*\{", src)
+        if not c and a.only != "seeds":
             raise SystemExit("ref_glue_build: class SwAligner not found")
-        src = replace_body(src, r"bool\s+done\s*\(", None, r'''{
+        if c:
+            src = replace_body(src, r"bool\s+done\s*\(", None, r'''{
 		return bt2x_refglue::sw(this).swa.done();
 	}''', start=c.end())
         with open(ii, "w") as f:
             f.write(src)
-        subprocess.run([cxx] + CXXFLAGS + ["-x", "c++", ii, "-o", out, "-L" + LIBDIR, "-lbt2x",
-                        "-Wl,-rpath,$ORIGIN/../../omp-bowtie2-prime_amd/bt2x", "-L/opt/rocm/lib",
-                        "-Wl,-rpath,/opt/rocm/lib", "-lpthread", "-lz"], check=True)
+        if a.cpu:
+            objs = [os.path.join(tmp, "abi.o"), os.path.join(tmp, "oracle.o")]
+            subprocess.run([cxx, "-O2", "-std=c++17", "-c", os.path.join(HERE, "bt2x_abi_oracle.cpp"), "-I" + HERE,
+                            "-o", objs[0]], check=True)
+            subprocess.run([os.environ.get("CC", "gcc"), "-O2", "-std=c11", "-ffp-contract=off", "-c",
+                            os.path.join(HERE, "bt2x_oracle.c"), "-o", objs[1]], check=True)
+            link = ["-x", "none"] + objs
+        else:
+            link = ["-L" + LIBDIR, "-lbt2x", "-Wl,-rpath,$ORIGIN/../../omp-bowtie2-prime_amd/bt2x", "-L/opt/rocm/lib",
+                    "-Wl,-rpath,/opt/rocm/lib"]
+        subprocess.run([cxx] + CXXFLAGS + ["-x", "c++", ii, "-o", out] + link + ["-lpthread", "-lz"], check=True)
         print(f"ref_glue_build: {out}", file=sys.stderr)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

@@ -55,15 +55,12 @@ DROPIN_SETS = [("e2e_rep", "rep", "rep_reads.fq", [], "u8"),
                ("e2e_rep_i16", "rep", "rep_reads.fq", ["--no-sse8"], "i16")]
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("name,idx,fq,opts,build", DROPIN_SETS, ids=[s[0] for s in DROPIN_SETS])
-def test_patched_reference_aligner_on_gpu(tmp_path, name, idx, fq, opts, build):
+def _run_patched(tmp_path, binary, name, idx, fq, opts):
     import lzma
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import golden_io as g
     from test_e2e import check_summary, sam_records
-    binary = PATCHED[build]
     if not os.access(binary, os.X_OK):
         pytest.skip("oracle/_ref/ has no patched reference build (needs /root/reference where it is built)")
     base = g.materialize_index(idx, str(tmp_path))
@@ -79,3 +76,18 @@ def test_patched_reference_aligner_on_gpu(tmp_path, name, idx, fq, opts, build):
     bad = [(a, b) for a, b in zip(got, exp) if a != b]
     assert len(got) == len(exp) and not bad, (len(got), len(exp), bad[:1])
     check_summary(b"\n".join(ln for ln in r.stderr.split(b"\n") if not ln.startswith(b"Timer:")), name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,idx,fq,opts,build", DROPIN_SETS, ids=[s[0] for s in DROPIN_SETS])
+def test_patched_reference_aligner_on_gpu(tmp_path, name, idx, fq, opts, build):
+    _run_patched(tmp_path, PATCHED[build], name, idx, fq, opts)
+
+
+@pytest.mark.parametrize("name,idx,fq,opts,build", DROPIN_SETS, ids=[s[0] for s in DROPIN_SETS])
+def test_patched_reference_glue_on_cpu(tmp_path, name, idx, fq, opts, build):
+    """The same patched aligner with the C-ABI answered by the CPU oracle
+    (oracle/bt2x_abi_oracle.cpp, oracle/ref_glue_build.py --cpu): the glue's hand-over of
+    the reference's seed batch and SwAligner state is checked in the CPU suite, so a glue
+    fault is told apart from a kernel fault."""
+    _run_patched(tmp_path, PATCHED[build] + "-cpu", name, idx, fq, opts)
