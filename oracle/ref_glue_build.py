@@ -8,7 +8,7 @@ against the stock reference's SAM).
 The reference is compiled as its Makefile does (one translation unit, bowtie2-align.cpp,
 with oracle/Makefile's REFDEFS), from /root/reference where it lies.  The patch is made on
 the *preprocessed* translation unit in a temporary directory outside the repository: the
-bodies of five member functions are replaced by the glue calls below (brace matching is
+bodies of six member functions are replaced by the glue calls below (brace matching is
 exact there: no #ifdef branches left).  Nothing of the reference is written into the
 repository; the only output is the binary in oracle/_ref/ (git-ignored).
 
