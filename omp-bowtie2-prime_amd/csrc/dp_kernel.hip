@@ -1199,19 +1199,29 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			uint32_t hp = 0, fp = 0, ep = 0, hlp = 0;      // previous step's packed H, F, E, hl
 			uint32_t tbacc = 0;
 			int lra = 0, lrb = 0;                           // H[R-1][j0], H[R-1][j0+1]
-#pragma unroll
+			// Row info of the current block (iw) and of the one above (iv); the next block's is
+			// read a block ahead, so no step waits on LDS (the executed blocks are contiguous:
+			// the band window [slo, shi]).
+			uint32_t cur_iw, cur_iv;
+			{
+				const int b0 = slo >> 2;
+				cur_iw = lds[(b0 < kRowWords ? b0 : kRowWords - 1) * 64 + lane];
+				cur_iv = lds[(b0 > 0 ? b0 - 1 : 0) * 64 + lane];
+			}
 			// the window is widened to whole 4-step blocks: a skipped block costs one scalar
 			// branch and a computed one none (the extra rows are outside every lane's band, or
 			// past its read: any values do)
+#pragma unroll
 			for(int b4 = 0; b4 < kSteps; b4 += 4) {
 			if(b4 >= slo && b4 <= shi) {                                 // wave-uniform
+			const int nb = (b4 >> 2) + 1;
+			const uint32_t nxt_iw = lds[(nb < kRowWords ? nb : kRowWords - 1) * 64 + lane];
 #pragma unroll
 			for(int st = b4; st < b4 + 4 && st < kSteps; st++) {
 				{
 				const int blk = st >> 2, r = st & 3;
 				// --- operands: low half = (row st, col j0), high half = (row st-1, col j0+1)
-				const uint32_t iw = lds[(blk < kRowWords ? blk : kRowWords - 1) * 64 + lane];
-				const uint32_t iv = lds[(blk > 0 ? blk - 1 : 0) * 64 + lane];
+				const uint32_t iw = cur_iw, iv = cur_iv;
 				uint32_t info = (st == 0) ? perm(0, iw, 0x0c0c0c00u)
 				              : (st == kRows) ? (perm(iw, 0, 0x0c070c0cu) | (kNone & 0xffu))
 				              : (r == 0) ? perm(iv, iw, 0x0c070c00u)
@@ -1314,6 +1324,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				hlp = hl; hp = h; fp = f; ep = e;
 				}
 			}
+			cur_iv = cur_iw; cur_iw = nxt_iw;
 			}
 			}
 			if(j0 < C) {
