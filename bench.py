@@ -396,7 +396,8 @@ def replay(args, base, fq, rdir, gpu):
                         counters[kk][k] = counters[kk].get(k, 0) + v
                 if kind == "round":
                     rs = ctx.last_round_stats()
-                    for k in ("reads", "jobs", "samples"):
+                    for k in ("reads", "jobs", "samples", "batches", "batch_draws", "serial_draws", "swap_draws",
+                              "kcyc_setup", "kcyc_batch", "kcyc_serial", "kcyc_rest"):
                         counters["round"][k] = counters["round"].get(k, 0) + rs[k]
                     counters["round"]["max_samples"] = max(counters["round"].get("max_samples", 0), rs["max_samples"])
 
@@ -755,6 +756,13 @@ def main():
                        "peak_rss_mib": peak, "summary": bdist.alignment_summary(tot).splitlines(),
                        "stats": stats, "gpu": kv_line(err, "BT2X_GPU"), "rusage_align": kv_line(err, "BT2X_RUSAGE_ALIGN")},
     }
+    # host CPU per read (rank 0's aligner process over its timed files): user + system time
+    # of all its threads, and the thread-seconds the run had (threads x t_align)
+    ru = line["end_to_end"]["rusage_align"]
+    if ru and met["nread"]:
+        cpu_s = float(ru.get("user", 0)) + float(ru.get("sys", 0))
+        line["end_to_end"]["host_cpu_us_per_read"] = round(cpu_s / met["nread"] * 1e6, 3)
+        line["end_to_end"]["host_thread_us_per_read"] = round(args.host_threads * t_align / met["nread"] * 1e6, 3)
     # ---- rank 0: kernels (replay) and, at N=1, the CPU baseline + parity
     if rank == 0 and not args.no_replay:
         rp = replay(args, base, warm[0] if warm else steps[0], rdir, gpu)

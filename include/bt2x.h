@@ -9,6 +9,7 @@
  *                                       forward .1/.2.bt2l pair into host arrays.
  *   bt2x_open / bt2x_close              one context per GPU; uploads the index arrays
  *                                       (Ebwt::_ebwt/_ftab/_eftab/_fchr, bt2_idx.h:2617-2639).
+ *   bt2x_open_shared                    a further context (own stream) over the same index.
  *   bt2x_seed_search                    MultiSeedAligner::searchAllSeedsDoAll(doExtend)
  *                                       (aligner_seed.cpp:674-725): exact backward search of
  *                                       every seed (searchSeedBi<8>, :820-957) and the
@@ -119,6 +120,11 @@ typedef struct bt2x_ctx bt2x_ctx;
 /* sc = NULL: defaults.  Penalties above 15 (--mp MX > 15 or --np > 15) are rejected
  * with BT2X_E_ARG: the u8 DP kernel packs a row's penalty into 4 bits. */
 int  bt2x_open(int hip_device, const bt2x_index_desc* idx, const bt2x_scoring* sc, bt2x_ctx** out);
+/* A second context on base's GPU that shares base's device index and scoring (nothing is
+ * uploaded) but has its own stream and buffers, so calls on the two contexts run
+ * concurrently on the device (the reference's worker threads each own their aligner
+ * objects over one shared Ebwt, bt2_search.cpp:2297-2888).  base must outlive it. */
+int  bt2x_open_shared(const bt2x_ctx* base, bt2x_ctx** out);
 void bt2x_close(bt2x_ctx* ctx);
 /* Last kernel's duration in ms (HIP events on the launching stream), by kernel id. */
 enum { BT2X_K_SEED = 0, BT2X_K_DP = 1, BT2X_K_RESOLVE = 2, BT2X_K_ROUND = 3, BT2X_K_COUNT = 4 };
@@ -141,8 +147,12 @@ typedef struct {
 } bt2x_counters;
 int bt2x_last_counters(const bt2x_ctx* ctx, int kernel, bt2x_counters* out);
 /* The last seed round's sampling work (bt2x_seed_round[_dev]): out[0] reads, out[1] reads
- * that sampled (RowSampler jobs), out[2] elements drawn, out[3] most elements one read drew. */
-int bt2x_last_round_stats(const bt2x_ctx* ctx, uint32_t out[4]);
+ * that sampled (RowSampler jobs), out[2] elements drawn, out[3] most elements one read drew;
+ * how the sampling kernel drew them: out[4] 64-draw batches, out[5] draws committed by a
+ * batch, out[6] draws taken one at a time, out[7] of out[5] from swap lists; out[8..11]
+ * the kernel's clock in units of 1024 cycles summed over jobs: setup, batch draws, serial
+ * draws, the rest. */
+int bt2x_last_round_stats(const bt2x_ctx* ctx, uint32_t out[12]);
 
 /* ------------------------------------------------------------ seed search */
 

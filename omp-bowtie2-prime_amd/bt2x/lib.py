@@ -24,6 +24,7 @@ FUNCS = {
     "bt2x_scoring_init": (None, [ctypes.POINTER(abi.Scoring)]),
     "bt2x_open": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(abi.IndexDesc),
                                  ctypes.POINTER(abi.Scoring), ctypes.POINTER(ctypes.c_void_p)]),
+    "bt2x_open_shared": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "bt2x_close": (None, [ctypes.c_void_p]),
     "bt2x_last_kernel_ms": (ctypes.c_double, [ctypes.c_void_p, ctypes.c_int]),
     "bt2x_last_counters": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(abi.Counters)]),
@@ -289,9 +290,11 @@ class Context:
 
     def last_round_stats(self) -> dict:
         """The last seed round's sampling work (bt2x_last_round_stats)."""
-        o = (ctypes.c_uint32 * 4)()
+        o = (ctypes.c_uint32 * 12)()
         check(load().bt2x_last_round_stats(self.h, o), "bt2x_last_round_stats")
-        return {"reads": o[0], "jobs": o[1], "samples": o[2], "max_samples": o[3]}
+        return {"reads": o[0], "jobs": o[1], "samples": o[2], "max_samples": o[3], "batches": o[4],
+                "batch_draws": o[5], "serial_draws": o[6], "swap_draws": o[7], "kcyc_setup": o[8],
+                "kcyc_batch": o[9], "kcyc_serial": o[10], "kcyc_rest": o[11]}
 
 
 def build_index(fasta: str, outbase: str, off_rate: int = 4, ftab_chars: int = 10) -> str:

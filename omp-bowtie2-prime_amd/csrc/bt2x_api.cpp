@@ -174,6 +174,7 @@ struct bt2x_ctx {
 	uint32_t* d_counters = nullptr;
 	uint64_t n_seed_last = 0, n_dp_last = 0, n_resolve_last = 0;
 	uint32_t n_round_last = 0;
+	bool shares_index = false;                 // bt2x_open_shared: the index arrays are the base's
 };
 
 bt2x_ctx::~bt2x_ctx() {
@@ -184,8 +185,10 @@ bt2x_ctx::~bt2x_ctx() {
 	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws,
 	                 &b_jobs, &b_ranges, &b_rcnt})
 		b->release();
-	for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen, (void*)d_stats,
-	               (void*)d_counters, (void*)d_queue, (void*)d_mmpen})
+	if(!shares_index)
+		for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen})
+			if(p) (void)hipFree(p);
+	for(void* p : {(void*)d_stats, (void*)d_counters, (void*)d_queue, (void*)d_mmpen})
 		if(p) (void)hipFree(p);
 	for(int k = 0; k < BT2X_K_COUNT; k++)
 		for(int j = 0; j < 2; j++) if(ev[k][j]) (void)hipEventDestroy(ev[k][j]);
@@ -335,6 +338,35 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	return BT2X_OK;
 }
 
+extern "C" int bt2x_open_shared(const bt2x_ctx* base, bt2x_ctx** out) {
+	if(!base || !out) return BT2X_E_ARG;
+	*out = nullptr;
+	std::unique_ptr<bt2x_ctx> c(new bt2x_ctx());
+	c->device = base->device;
+	c->shares_index = true;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	HIPCHK(hipEventCreateWithFlags(&c->sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+	for(int k = 0; k < BT2X_K_COUNT; k++) {
+		HIPCHK(hipEventCreate(&c->ev[k][0]));
+		HIPCHK(hipEventCreate(&c->ev[k][1]));
+	}
+	c->ix = base->ix;
+	c->sc = base->sc;
+	c->d_ebwt = base->d_ebwt; c->d_ftab = base->d_ftab; c->d_eftab = base->d_eftab; c->d_blk = base->d_blk;
+	c->d_sa = base->d_sa; c->d_text = base->d_text; c->d_offs = base->d_offs; c->d_rstarts = base->d_rstarts;
+	c->d_plen = base->d_plen;
+	c->npat = base->npat; c->exact_best = base->exact_best; c->ncu = base->ncu; c->chunk_groups = base->chunk_groups;
+	HIPCHK(hipMalloc(&c->d_mmpen, sizeof c->sc.mmpen));
+	HIPCHK(hipMemcpy(c->d_mmpen, c->sc.mmpen, sizeof c->sc.mmpen, hipMemcpyHostToDevice));
+	HIPCHK(hipMalloc((void**)&c->d_stats, 32 * sizeof(unsigned long long)));
+	HIPCHK(hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long)));
+	HIPCHK(hipMalloc((void**)&c->d_counters, 16 * sizeof(uint32_t)));
+	HIPCHK(hipMalloc((void**)&c->d_queue, 4 * sizeof(uint32_t)));
+	*out = c.release();
+	return BT2X_OK;
+}
+
 extern "C" void bt2x_close(bt2x_ctx* c) {
 	delete c;        // ~bt2x_ctx releases everything
 }
@@ -392,15 +424,16 @@ extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) 
 	return BT2X_OK;
 }
 
-extern "C" int bt2x_last_round_stats(const bt2x_ctx* c, uint32_t out[4]) {
+extern "C" int bt2x_last_round_stats(const bt2x_ctx* c, uint32_t out[12]) {
 	if(!c || !out) return BT2X_E_ARG;
-	out[0] = out[1] = out[2] = out[3] = 0;
+	for(int i = 0; i < 12; i++) out[i] = 0;
 	if(!c->b_rcnt.p) return BT2X_OK;
-	uint32_t cnt[8];
+	uint32_t cnt[16];
 	HIPCHK(hipSetDevice(c->device));
 	HIPCHK(hipStreamSynchronize(c->stream));
 	HIPCHK(hipMemcpy(cnt, c->b_rcnt.p, sizeof cnt, hipMemcpyDeviceToHost));
 	out[0] = c->n_round_last; out[1] = cnt[3]; out[2] = cnt[6]; out[3] = cnt[7];
+	for(int i = 0; i < 8; i++) out[4 + i] = cnt[8 + i];
 	return BT2X_OK;
 }
 
@@ -660,7 +693,7 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	   (rc = c->b_ws.ensure(bt2x_round_ws_bytes() * lanes)) ||
 	   (rc = c->b_jobs.ensure(bt2x_round_job_bytes() * job_cap)) ||
 	   (rc = c->b_ranges.ensure(bt2x_round_range_bytes() * range_cap)) ||
-	   (rc = c->b_rcnt.ensure(8 * sizeof(uint32_t)))) return rc;
+	   (rc = c->b_rcnt.ensure(16 * sizeof(uint32_t)))) return rc;
 	uint32_t* cnt = (uint32_t*)c->b_rcnt.p;
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_ROUND][0], s));
 	// 1. seed search (searchAllSeedsDoAll)
@@ -673,7 +706,7 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	c->n_seed_last = nseeds;
 	c->n_round_last = nreads;
 	// 2. finalize + rank + prioritize per read, then 3. place every row
-	HIPCHK(hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), s));
+	HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s));
 	HIPCHK(hipMemsetAsync(c->d_stats + 8, 0, 3 * sizeof(unsigned long long), s));
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][0], s));
 	RoundLaunch a;

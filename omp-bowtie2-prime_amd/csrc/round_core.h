@@ -58,7 +58,7 @@ struct Range {                                // a satpos2 entry (SATupleAndPos)
 	uint8_t nlex, fw;
 };
 
-struct R1N {                                  // Random1toN state; lists live in the arena
+struct alignas(4) R1N {                       // Random1toN state; lists live in the arena
 	uint16_t n, cur, thresh, list;            // list: arena offset of list_
 	uint8_t inited, swaplist, converted, pad;
 };
@@ -83,6 +83,7 @@ struct SampleWs {
 	R1N r1n[kMaxRanges];
 	uint16_t arena[kArena];
 	uint32_t hash[kHash];
+	uint32_t bkey[128], bmlo[128], bmhi[128]; // a batch's keys and the lanes that drew them (wave kernel)
 };
 
 // How sample() spreads its list work over the lanes that run one job together.  All
@@ -349,12 +350,17 @@ __host__ __device__ inline bool r1n_next(SampleWs& w, R1N& s, int ri, Rnd& rnd, 
 	return true;
 }
 
-// RowSampler over w.big[0 .. nb) (lensq = szsq = true) and one Random1toN per range:
-// emit(k, range, element) for each of the nsamples draws (on the leader lane).  The caller
-// fills w.big; false on workspace overflow.
-template<class C, class Emit>
-__host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, C& co,
-                                       Emit&& emit) {
+// sample()'s loop state between draws
+struct SampleState {
+	double mass;                              // RowSampler's total live mass
+	uint32_t nlive;                           // live ranges
+	uint32_t arenaTop;                        // swap-list storage used
+};
+
+// RowSampler::init over w.big[0 .. nb) (lensq = szsq = true) and a fresh Random1toN per
+// range; false if there are more ranges than the workspace holds.
+template<class C>
+__host__ __device__ inline bool sample_setup(uint32_t nb, SampleWs& w, C& co, SampleState& st) {
 	if(nb > (uint32_t)kMaxRanges) return false;
 	for(uint32_t k = co.lane(); k < (uint32_t)kHash; k += co.width()) w.hash[k] = 0;
 	for(uint32_t i = co.lane(); i < nb; i += co.width()) {
@@ -369,35 +375,54 @@ __host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd,
 	co.big_load(w, nb);
 	double mass = 0.0f;
 	for(uint32_t i = 0; i < nb; i++) mass += w.masses[i];
-	uint32_t nlive = nb;
+	st.mass = mass;
+	st.nlive = nb;
+	st.arenaTop = 0;
 	co.rs_init(w, nb);
-	co.rs_rebuild(w, nlive, 0);
-	uint32_t arenaTop = 0;
-	for(uint64_t k = 0; k < nsamples; k++) {
-		const double rd = rnd.nextFloat() * mass;
-		// the dart: first live range whose running mass exceeds it (else the last live one)
-		if(nlive == 0) return false;
-		const uint32_t bi = co.rs_dart(w, rd, nlive);
-		R1N s = co.r1n_get(w, bi);
-		const Range rg = co.big_get(w, bi);
-		if(!s.inited) {
-			const uint16_t n = (uint16_t)rg.size;                              // uint16_t element type
-			if(n == 0) return false;
-			s.inited = 1; s.n = n; s.cur = 0; s.converted = 0; s.swaplist = n < 128 ? 1 : 0;
-			const uint16_t t = (uint16_t)(0.10f * (float)n);
-			s.thresh = t > 16 ? t : 16;
-		}
-		uint16_t rr;
-		if(!r1n_next(w, s, (int)bi, rnd, arenaTop, rr, co)) return false;
-		co.r1n_set(w, bi, s);
-		if(s.n > 0 && s.cur >= s.n) {                                          // done(): finishedRange
-			mass -= w.masses[bi];
-			const uint32_t q = co.rs_remove(w, bi, nlive);
-			nlive--;
-			co.rs_rebuild(w, nlive, q);
-		}
-		if(co.leader()) emit(k, rg, rr);
+	co.rs_rebuild(w, st.nlive, 0);
+	return true;
+}
+
+// Draw k: one RowSampler dart and one Random1toN::next; emit(k, range, element) on the
+// leader lane.  False on workspace overflow.
+template<class C, class Emit>
+__host__ __device__ inline bool sample_step(uint64_t k, Rnd& rnd, SampleWs& w, C& co, SampleState& st, Emit&& emit) {
+	const double rd = rnd.nextFloat() * st.mass;
+	// the dart: first live range whose running mass exceeds it (else the last live one)
+	if(st.nlive == 0) return false;
+	const uint32_t bi = co.rs_dart(w, rd, st.nlive);
+	R1N s = co.r1n_get(w, bi);
+	const Range rg = co.big_get(w, bi);
+	if(!s.inited) {
+		const uint16_t n = (uint16_t)rg.size;                              // uint16_t element type
+		if(n == 0) return false;
+		s.inited = 1; s.n = n; s.cur = 0; s.converted = 0; s.swaplist = n < 128 ? 1 : 0;
+		const uint16_t t = (uint16_t)(0.10f * (float)n);
+		s.thresh = t > 16 ? t : 16;
 	}
+	uint16_t rr;
+	if(!r1n_next(w, s, (int)bi, rnd, st.arenaTop, rr, co)) return false;
+	co.r1n_set(w, bi, s);
+	if(s.n > 0 && s.cur >= s.n) {                                          // done(): finishedRange
+		st.mass -= w.masses[bi];
+		const uint32_t q = co.rs_remove(w, bi, st.nlive);
+		st.nlive--;
+		co.rs_rebuild(w, st.nlive, q);
+	}
+	if(co.leader()) emit(k, rg, rr);
+	return true;
+}
+
+// RowSampler over w.big[0 .. nb) and one Random1toN per range: emit(k, range, element)
+// for each of the nsamples draws (on the leader lane).  The caller fills w.big; false on
+// workspace overflow.
+template<class C, class Emit>
+__host__ __device__ inline bool sample(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, C& co,
+                                       Emit&& emit) {
+	SampleState st;
+	if(!sample_setup(nb, w, co, st)) return false;
+	for(uint64_t k = 0; k < nsamples; k++)
+		if(!sample_step(k, rnd, w, co, st, emit)) return false;
 	return true;
 }
 

@@ -115,29 +115,36 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 	// list positions l and l + 64
 	uint32_t lv0, lv1;
 	double m0, m1, p0, p1;
-	// Random1toN state of ranges l and l + 64 (n | cur << 16, thresh | list << 16, flags)
-	// and their fields (topf, size, rdoff | fw << 24)
-	uint32_t ra[3], rb[3];
+	// range fields of ranges l and l + 64 (topf, size, rdoff | fw << 24)
 	uint32_t ga[4], gb[4];
-	__device__ void r1n_reset(const SampleWs&, uint32_t) {
-		for(int i = 0; i < 3; i++) { ra[i] = 0; rb[i] = 0; }
+	// Random1toN state in LDS, w.r1n[] read and written as three 32-bit words (n | cur << 16,
+	// thresh | list << 16, inited | swaplist << 8 | converted << 16) so the speculative
+	// draws can merge their counts with atomicMax on word 0
+	__device__ static uint32_t* r1w(const SampleWs& w, uint32_t bi) {
+		return reinterpret_cast<uint32_t*>(const_cast<R1N*>(&w.r1n[bi]));
 	}
-	__device__ R1N r1n_get(const SampleWs&, uint32_t bi) const {
-		const uint32_t l = bi & 63;
-		const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ra[0] : rb[0]), (int)l);
-		const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ra[1] : rb[1]), (int)l);
-		const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)(bi < 64 ? ra[2] : rb[2]), (int)l);
+	__device__ void r1n_reset(const SampleWs& w, uint32_t nb) {
+		for(uint32_t i = threadIdx.x; i < nb; i += 64) { uint32_t* p = r1w(w, i); p[0] = 0; p[1] = 0; p[2] = 0; }
+		__syncthreads();
+	}
+	__device__ static R1N unpack(uint32_t w0, uint32_t w1, uint32_t w2) {
 		R1N r;
 		r.n = (uint16_t)w0; r.cur = (uint16_t)(w0 >> 16); r.thresh = (uint16_t)w1; r.list = (uint16_t)(w1 >> 16);
 		r.inited = (uint8_t)w2; r.swaplist = (uint8_t)(w2 >> 8); r.converted = (uint8_t)(w2 >> 16); r.pad = 0;
 		return r;
 	}
-	__device__ void r1n_set(const SampleWs&, uint32_t bi, const R1N& r) {
-		const uint32_t w0 = (uint32_t)r.n | ((uint32_t)r.cur << 16), w1 = (uint32_t)r.thresh | ((uint32_t)r.list << 16);
-		const uint32_t w2 = (uint32_t)r.inited | ((uint32_t)r.swaplist << 8) | ((uint32_t)r.converted << 16);
-		if(threadIdx.x == (bi & 63)) {
-			if(bi < 64) { ra[0] = w0; ra[1] = w1; ra[2] = w2; } else { rb[0] = w0; rb[1] = w1; rb[2] = w2; }
+	__device__ R1N r1n_get(const SampleWs& w, uint32_t bi) const {
+		const uint32_t* p = r1w(w, bi);
+		return unpack(p[0], p[1], p[2]);
+	}
+	__device__ void r1n_set(const SampleWs& w, uint32_t bi, const R1N& r) {
+		if(threadIdx.x == 0) {
+			uint32_t* p = r1w(w, bi);
+			p[0] = (uint32_t)r.n | ((uint32_t)r.cur << 16);
+			p[1] = (uint32_t)r.thresh | ((uint32_t)r.list << 16);
+			p[2] = (uint32_t)r.inited | ((uint32_t)r.swaplist << 8) | ((uint32_t)r.converted << 16);
 		}
+		__syncthreads();
 	}
 	__device__ void big_load(const SampleWs& w, uint32_t nb) {
 		const uint32_t l = threadIdx.x;
@@ -239,6 +246,186 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 	}
 };
 
+constexpr uint32_t kLcgA = 1664525u, kLcgC = 1013904223u;      // Rnd::nextU32's LCG
+
+// Draws k .. k+63 at once, one per lane, on the guess that each earlier draw of the batch
+// is a plain draw: two nextU32 (lane l starts 4l LCG steps on, jA/jC), a dart into a range
+// whose Random1toN is either in seen-list mode (an element neither seen before nor drawn by
+// an earlier lane, and no conversion to a swap list) or a swap list already laid out (and
+// not finished by this draw, and not touching a position an earlier draw of the batch
+// moved).  The lanes before the first draw that breaks the guess are exactly the serial
+// draws, so they commit together (seen-set inserts, swap-list exchanges, the ranges'
+// counts); that draw runs through the serial step (sample_step), which handles every case,
+// and the next batch starts after it.
+// stats: batches, draws committed by batches, serial draws, swap-list draws in batches;
+// clock64 cycles in setup, batch draws, serial draws, the rest (exchanges, output stores).
+template<class Put>
+__device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, WaveCoop& co, uint32_t jA,
+                            uint32_t jC, uint64_t stats[8], Put&& put) {
+	uint64_t t = clock64();
+	SampleState st;
+	if(!sample_setup(nb, w, co, st)) return false;
+	const uint32_t lane = threadIdx.x;
+	uint64_t k = 0;
+	{ const uint64_t t1 = clock64(); stats[4] += t1 - t; t = t1; }
+	while(k < nsamples) {
+		if(st.nlive == 0) return false;                            // as sample_step
+		const uint32_t act = nsamples - k < 64 ? (uint32_t)(nsamples - k) : 64u;
+		const uint32_t x0 = jA * rnd.last + jC;
+		const uint32_t x1 = kLcgA * x0 + kLcgC, x2 = kLcgA * x1 + kLcgC;
+		const double rd = (double)((float)((x1 >> 16) ^ x2) / (float)0xffffffffu) * st.mass;
+		// the dart (rs_dart's count of running sums <= rd, by bisection)
+		uint32_t lo = 0, hi = st.nlive;
+		while(lo < hi) {
+			const uint32_t mid = (lo + hi) >> 1;
+			if(rd < w.pre[mid]) hi = mid; else lo = mid + 1;
+		}
+		const uint32_t idx = lo < st.nlive ? lo : st.nlive - 1;
+		const uint32_t l0 = (uint32_t)__shfl((int)co.lv0, (int)(idx & 63)), l1 = (uint32_t)__shfl((int)co.lv1, (int)(idx & 63));
+		const uint32_t bi = idx < 64 ? l0 : l1;
+		const uint32_t* rw = WaveCoop::r1w(w, bi);
+		const R1N s = WaveCoop::unpack(rw[0], rw[1], rw[2]);
+		uint32_t n, cur0, thresh;
+		bool swap, ready;
+		if(s.inited) {
+			n = s.n; cur0 = s.cur; thresh = s.thresh; swap = s.swaplist != 0;
+			ready = swap && (cur0 > 0 || s.converted);            // the swap list is laid out
+		} else {
+			n = (uint16_t)w.big[bi].size; cur0 = 0; swap = n < 128; ready = false;
+			const uint16_t t = (uint16_t)(0.10f * (float)n);
+			thresh = t > 16 ? t : 16;
+		}
+		const uint32_t x3 = kLcgA * x2 + kLcgC, x4 = kLcgA * x3 + kLcgC;
+		const uint32_t u2 = (x3 >> 16) ^ x4;
+		const uint32_t rn = n ? u2 % n : 0;
+		const uint32_t key = ((bi << 16) | rn) + 1u;
+		// the batch's earlier draws from the same range (its count), one pass per distinct range
+		uint32_t cnt = 1;
+		for(uint64_t rem = __ballot(lane < act); rem;) {
+			const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bi, (int)((uint32_t)__ffsll((unsigned long long)rem) - 1));
+			const uint64_t m = __ballot(bi == b) & rem;
+			if(bi == b) cnt = (uint32_t)__popcll(m & ((1ull << lane) - 1ull)) + 1;
+			rem &= ~m;
+		}
+		const uint32_t cur1 = cur0 + cnt;                          // the range's count after this draw
+		bool reg = lane < act && n != 0 && cur1 < n;               // cur1 >= n: done(), the range leaves
+		uint32_t pos = 0;                                          // swap list: the drawn position
+		if(swap) {
+			reg = reg && ready;
+			pos = cur1 - 1 + (reg ? u2 % (n - (cur1 - 1)) : 0);
+		} else {
+			reg = reg && cur1 < thresh && !seen_has(w, key);       // cur1 >= thresh: conversion
+		}
+		// Inside the batch, from a 128-slot LDS table (key -> mask of the lanes that drew it):
+		// a seen-list draw of a key an earlier lane drew is a redraw (the serial step's); a
+		// swap-list draw reads what its range's earlier exchanges left.  With A the list at
+		// the batch start, lane L moves v_L to its drawn position r_L and takes the element at
+		// r_L: v_L = A[c_L] unless an earlier lane drew c_L (then that lane's v), the element
+		// = A[r_L] unless an earlier lane drew r_L (then the last such lane's v).  Cursor
+		// positions grow and drawn ones are >= them, so no other write reaches either.
+		const uint32_t ikey = swap ? ((bi << 16) | pos) + 1u : key;
+		w.bkey[lane] = 0; w.bkey[lane + 64] = 0;
+		w.bmlo[lane] = 0; w.bmlo[lane + 64] = 0; w.bmhi[lane] = 0; w.bmhi[lane + 64] = 0;
+		__syncthreads();
+		uint32_t bslot = 0;
+		if(reg) {
+			bslot = (ikey * 2654435761u) >> 25;
+			for(;;) {
+				const uint32_t old = atomicCAS(&w.bkey[bslot], 0u, ikey);
+				if(old == 0u || old == ikey) break;
+				bslot = (bslot + 1) & 127;
+			}
+		}
+		__syncthreads();
+		if(reg) atomicOr(lane < 32 ? &w.bmlo[bslot] : &w.bmhi[bslot], 1u << (lane & 31));
+		__syncthreads();
+		const uint64_t below = (1ull << lane) - 1ull;
+		uint64_t mine = 0;                                         // the lanes that drew our key
+		int pr = -1, pc = -1;                                      // last earlier lane drawing r_L / c_L
+		if(reg) {
+			mine = ((uint64_t)w.bmhi[bslot] << 32) | w.bmlo[bslot];
+			if(!swap) {
+				if(mine & below) reg = false;                      // a redraw
+			} else {
+				if(mine & below) pr = 63 - __clzll(mine & below);
+				const uint32_t ckey = ((bi << 16) | (cur1 - 1)) + 1u;
+				for(uint32_t h = (ckey * 2654435761u) >> 25;; h = (h + 1) & 127) {
+					const uint32_t v = w.bkey[h];
+					if(v == 0u) break;
+					if(v == ckey) {
+						const uint64_t mc = (((uint64_t)w.bmhi[h] << 32) | w.bmlo[h]) & below;
+						if(mc) pc = 63 - __clzll(mc);
+						break;
+					}
+				}
+			}
+		}
+		const uint64_t bad = __ballot(!reg) & (act == 64 ? ~0ull : ((1ull << act) - 1ull));
+		const uint32_t F = bad ? (uint32_t)__ffsll((unsigned long long)bad) - 1 : act;
+		const uint64_t com = F == 64 ? ~0ull : ((1ull << F) - 1ull);   // the committed lanes
+		bool full = false;
+		uint32_t out = rn;
+		const bool sw = lane < F && swap;
+		const uint32_t cpos = s.list + cur1 - 1, rpos = s.list + pos;   // swap lists: arena positions
+		uint32_t v = sw ? w.arena[cpos] : 0u, a0r = sw ? w.arena[rpos] : 0u;
+		if(lane < F) {
+			uint32_t* pw = WaveCoop::r1w(w, bi);
+			atomicMax(&pw[0], n | (cur1 << 16));
+			if(!swap) {
+				uint32_t h = (key * 2654435761u) >> 22;
+				full = true;
+				for(int probe = 0; probe < kHash; probe++, h = (h + 1) & (kHash - 1))
+					if(atomicCAS(&w.hash[h], 0u, key) == 0u) { full = false; break; }
+				pw[1] = thresh | ((uint32_t)s.list << 16);
+				pw[2] = 1u;                                        // inited, seen-list mode
+			}
+		}
+		{ const uint64_t t1 = clock64(); stats[5] += t1 - t; t = t1; }
+		const uint64_t swm = __ballot(sw);
+		if(swm) {
+			// v_L through the chain of earlier lanes that drew c_L (pointer jumping: after
+			// round i a lane points 2^i links up; a lane whose link is a root takes its v)
+			int p = sw ? pc : -1;
+			for(int it = 0; it < 6; it++) {
+				const int src = p >= 0 ? p : (int)lane;
+				const uint32_t vp = (uint32_t)__shfl((int)v, src);
+				const int pp = __shfl(p, src);
+				if(p >= 0) { if(pp < 0) { v = vp; p = -1; } else p = pp; }
+			}
+			const uint32_t vr = (uint32_t)__shfl((int)v, pr >= 0 ? pr : (int)lane);
+			if(sw) out = pr >= 0 ? vr : a0r;
+			// the exchanges' net effect: each drawn position ends with the last committed
+			// drawer's v, then each cursor position with its draw's element (a cursor position
+			// may be an earlier drawn one)
+			__syncthreads();
+			if(sw && 63 - __clzll(mine & com) == (int)lane) w.arena[rpos] = (uint16_t)v;
+			__syncthreads();
+			if(sw) w.arena[cpos] = (uint16_t)out;
+			__syncthreads();
+			stats[3] += (uint32_t)__popcll(swm);
+		}
+		if(lane < F) put(k + lane, w.big[bi], (uint16_t)out);
+		if(__ballot(full)) return false;
+		stats[0]++;
+		if(F) {
+			rnd.last = (uint32_t)__builtin_amdgcn_readlane((int)x4, (int)(F - 1));   // 4F steps on
+			rnd.lastOff = 0;
+			k += F;
+			stats[1] += F;
+		}
+		__syncthreads();
+		{ const uint64_t t1 = clock64(); stats[7] += t1 - t; t = t1; }
+		if(F < act) {
+			if(!sample_step(k, rnd, w, co, st, [&](uint64_t kk, const Range& rg, uint16_t elt) { put(kk, rg, elt); }))
+				return false;
+			k++;
+			stats[2]++;
+			{ const uint64_t t1 = clock64(); stats[6] += t1 - t; t = t1; }
+		}
+	}
+	return true;
+}
+
 // One wave per job, its workspace in LDS: the sampling loop is a chain of dependent
 // list/mass lookups, so it runs at LDS latency instead of HBM latency.  Jobs are taken
 // from a queue counter (counters[5]) so long and short jobs balance over the grid.
@@ -251,6 +438,9 @@ round_sample_kernel(RoundLaunch a) {
 	const Range* ranges = reinterpret_cast<const Range*>(a.ranges);
 	const uint32_t njobs = min(a.counters[3], a.job_cap);
 	const bool fits = a.counters[0] <= a.sat_cap && a.counters[1] <= a.row_cap;
+	// lane l's draw in a batch starts 4l LCG steps on: x -> jA * x + jC
+	uint32_t jA = 1, jC = 0;
+	for(uint32_t i = 0; i < 4 * threadIdx.x; i++) { jA *= kLcgA; jC = kLcgA * jC + kLcgC; }
 	for(;;) {
 		if(threadIdx.x == 0) qsh = atomicAdd(&a.counters[5], 1u);
 		__syncthreads();
@@ -262,7 +452,8 @@ round_sample_kernel(RoundLaunch a) {
 		for(uint32_t i = threadIdx.x; i < j.nb && i < (uint32_t)kMaxRanges; i += 64) w.big[i] = ranges[j.range0 + i];
 		__syncthreads();
 		Rnd rnd{j.rnd_last, j.rnd_lastoff};
-		const bool ok = sample(j.nb, j.nsamples, rnd, w, co, [&](uint64_t k, const Range& rg, uint16_t elt) {
+		uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+		const bool ok = sample_wave(j.nb, j.nsamples, rnd, w, co, jA, jC, stats, [&](uint64_t k, const Range& rg, uint16_t elt) {
 			if(!fits) return;
 			bt2x_sat s;
 			s.rdoff = rg.rdoff; s.rand_n = 1; s.fw = rg.fw; s.seedlen = (uint8_t)j.seedlen;
@@ -272,6 +463,8 @@ round_sample_kernel(RoundLaunch a) {
 			a.rows[j.elt_base + k] = ri;
 		});
 		if(threadIdx.x == 0) {
+			for(int i = 0; i < 4; i++) atomicAdd(&a.counters[8 + i], (uint32_t)stats[i]);
+			for(int i = 4; i < 8; i++) atomicAdd(&a.counters[8 + i], (uint32_t)(stats[i] >> 10));
 			bt2x_round_out& o = a.out[j.read];
 			o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
 			if(!ok) o.status = BT2X_ROUND_REDO;

@@ -509,9 +509,11 @@ void append_refname(std::string& o, const std::string& name) {   // SamConfig::p
 
 void append_seq(std::string& o, const std::vector<uint8_t>& s) {
 	if(s.empty()) { o.push_back('*'); return; }
-	const size_t b = o.size();
-	o.resize(b + s.size());
-	for(size_t i = 0; i < s.size(); i++) o[b + i] = "ACGTN"[s[i]];
+	const size_t b = o.size(), n = s.size();
+	o.resize(b + n);
+	char* d = &o[b];
+	const uint8_t* c = s.data();
+	for(size_t i = 0; i < n; i++) d[i] = "ACGTN"[c[i]];
 }
 
 // AlnSinkWrap::finishRead, unpaired branch (aln_sink.cpp:643-1384) -> one SAM record in
@@ -548,8 +550,9 @@ void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, 
 	thread_local std::vector<std::pair<int64_t, size_t>> buf;
 	buf.resize(sz);
 	for(size_t i = 0; i < sz; i++) buf[i] = {sk.rs[i].score, i};
-	std::stable_sort(buf.begin(), buf.end());
-	std::reverse(buf.begin(), buf.end());
+	// descending (score, index): the reverse of the stable ascending sort by score, and the
+	// pairs are distinct, so an unstable sort gives it without stable_sort's temporary buffer
+	std::sort(buf.begin(), buf.end(), std::greater<std::pair<int64_t, size_t>>());
 	auto shuffle = [&](size_t begin, size_t num) {
 		if(num < 2) return;
 		size_t left = num;
@@ -1045,6 +1048,21 @@ double now_s() {
 }
 }
 
+// A cohort's read contexts are cold when a pass over the cohort reaches them (its host
+// state is far larger than the caches): the loops below fetch a read's leading lines (and,
+// before a resume, its coroutine frame) a few reads ahead.  BT2X_HOST_PREFETCH=0: off.
+namespace {
+bool host_prefetch() {
+	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH"); return !(e && e[0] == '0'); }();
+	return on;
+}
+inline void prefetch_ctx(const ReadCtx* c, bool frame) {
+	for(int k = 0; k < 4; k++) __builtin_prefetch(reinterpret_cast<const char*>(c) + 64 * k);
+	if(frame)
+		for(int k = 0; k < 8; k++) __builtin_prefetch(c->frame_ + 64 * k);
+}
+}
+
 // ----- one launch: gather a cohort's waiting requests, run them, scatter the results
 
 // Classify the cohort's reads by pending request and fill the launch's input buffers
@@ -1064,8 +1082,10 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 		C.ws.clear(); C.wr.clear(); C.wd.clear(); C.wn.clear();
 		C.sbytes = C.nseed = C.nres = C.dbytes = C.nprob = C.rbytes = C.nbytes = C.nnseed = C.nexr = 0;
 		const long e = std::min(n, (ch + 1) * kChunk);
+		const bool pf = host_prefetch();
 		for(long i = ch * kChunk; i < e; i++) {
 			ReadCtx* c = cohort[(size_t)i];
+			if(pf && i + 4 < e) prefetch_ctx(cohort[(size_t)i + 4], false);
 			if(c->req == REQ_SEED) {
 				C.ws.push_back(c); C.sbytes += 2 * c->rd.length(); C.nseed += c->seed_in.size();
 			} else if(c->req == REQ_RESOLVE) {
@@ -1179,28 +1199,30 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 	L.t_gather = now_s() - tg;
 }
 
-// The launch's backend calls (on the GPU thread when pipelined).
+// The launch's backend calls (on the GPU thread when pipelined; launch 1 on the second
+// backend when there is one).
 void Aligner::execute(Launch& L) {
+	Backend& be = (be2_ && &L == &launch_[1]) ? *be2_ : be_;
 	L.t_seed = L.t_resolve = L.t_dp = L.t_round = 0;
 	if(!L.wn.empty()) {
 		const double t0 = now_s();
-		be_.seed_round(L.round_reads, L.round_seeds, L.round_in, L.round_exr, (uint32_t)p_.mxIter, L.round_out,
-		               L.round_sats, L.round_elts, L.round_exr_out);
+		be.seed_round(L.round_reads, L.round_seeds, L.round_in, L.round_exr, (uint32_t)p_.mxIter, L.round_out,
+		              L.round_sats, L.round_elts, L.round_exr_out);
 		L.t_round = now_s() - t0;
 	}
 	if(!L.ws.empty()) {
 		const double t0 = now_s();
-		be_.seed_search(L.seed_reads, L.seed_in, L.seed_out);
+		be.seed_search(L.seed_reads, L.seed_in, L.seed_out);
 		L.t_seed = now_s() - t0;
 	}
 	if(!L.wr.empty()) {
 		const double t0 = now_s();
-		be_.resolve(L.res_in, L.res_out);
+		be.resolve(L.res_in, L.res_out);
 		L.t_resolve = now_s() - t0;
 	}
 	if(!L.wd.empty()) {
 		const double t0 = now_s();
-		be_.dp_align(L.dp_reads, L.dp_quals, L.dp_refs, L.dp_in, L.dp_out, L.recs, L.edits);
+		be.dp_align(L.dp_reads, L.dp_quals, L.dp_refs, L.dp_in, L.dp_out, L.recs, L.edits);
 		L.t_dp = now_s() - t0;
 	}
 }
@@ -1228,8 +1250,10 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	const long nrun = (long)L.run.size();
 	const double t0 = now_s();
 	st.t_gather += L.t_gather;
+	const bool prefetch = host_prefetch();
 	pool().parallel_for(nrun, 64, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
+		if(prefetch && i + 3 < nrun) prefetch_ctx(L.run[(size_t)i + 3], true);
 		if(i < nwn) {
 			const bt2x_round_out& o = L.round_out[(size_t)i];
 			c->round_out = o;
@@ -1488,29 +1512,36 @@ Aligner::~Aligner() {
 void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, const std::function<void(uint64_t, std::string&)>& put) {
 	const long n = (long)act.size(), nch = (n + 1023) / 1024;
 	std::vector<RetireAcc> acc((size_t)nch);
+	// each chunk splits its reads into the ones still running and the finished ones (in
+	// order), so the serial part only concatenates the chunks' lists: a serial pass over
+	// the cohort's cold contexts cost ~2.5 ms per step
+	if(retire_keep_.size() < (size_t)nch) { retire_keep_.resize((size_t)nch); retire_fin_.resize((size_t)nch); }
+	const bool pf = host_prefetch();
 	pool().parallel_for(nch, 1, [&](long ch) {
 		RetireAcc& a = acc[(size_t)ch];
-		for(long i = ch * 1024; i < std::min(n, (ch + 1) * 1024); i++) {
+		std::vector<ReadCtx*>& keep = retire_keep_[(size_t)ch];
+		std::vector<ReadCtx*>& fin = retire_fin_[(size_t)ch];
+		keep.clear(); fin.clear();
+		const long e = std::min(n, (ch + 1) * 1024);
+		for(long i = ch * 1024; i < e; i++) {
 			ReadCtx* c = act[(size_t)i];
-			if(!c->done) continue;
+			if(pf && i + 4 < e) __builtin_prefetch(&act[(size_t)i + 4]->done);
+			if(!c->done) { keep.push_back(c); continue; }
 			c->task.h.destroy();
 			c->task.h = nullptr;
 			a.count(c);
 			if(!c->warn.empty()) std::fputs(c->warn.c_str(), stderr);
 			put(c->rd.rdid, c->sam);
+			c->done = false;
+			fin.push_back(c);
 		}
 	});
 	for(const RetireAcc& a : acc) a.into(st);
-	size_t w = 0;
-	for(ReadCtx* c : act) {
-		if(c->done) {
-			c->done = false;
-			free_.push_back(c);
-		} else {
-			act[w++] = c;
-		}
+	act.clear();
+	for(long ch = 0; ch < nch; ch++) {
+		act.insert(act.end(), retire_keep_[(size_t)ch].begin(), retire_keep_[(size_t)ch].end());
+		free_.insert(free_.end(), retire_fin_[(size_t)ch].begin(), retire_fin_[(size_t)ch].end());
 	}
-	act.resize(w);
 }
 
 namespace {
@@ -1623,8 +1654,10 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
 		writer.reserve(rdid + (uint64_t)nf);
 		st.t_alloc += now_s() - t0;
+		const bool pf = host_prefetch();
 		pool().parallel_for(nf, 64, [&](long i) {
 			ReadCtx* c = fresh[(size_t)i];
+			if(pf && i + 3 < nf) prefetch_ctx(fresh[(size_t)i + 3], true);
 			FastqReader::decode(src[i], c->rd, rdid + (uint64_t)i, p_.randSeed, rdid0 + rdid + (uint64_t)i);
 			c->task = align_read(c);
 			c->task.h.resume();
@@ -1656,39 +1689,43 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	} else {
 		// Two cohorts of up to slots/2 reads alternate: while the GPU thread runs one
 		// cohort's launches, the host threads resume the other with its previous results,
-		// retire and refill it, and gather its next launch.
+		// retire and refill it, and gather its next launch.  With a second backend each
+		// cohort has a GPU thread of its own, and a cohort's next launch starts as soon as it
+		// is gathered, alongside the other cohort's launch still on the GPU.
 		std::vector<ReadCtx*> co[2];
 		const size_t cap = slots / 2;
 		auto empty = [](const Launch& L) { return L.ws.empty() && L.wr.empty() && L.wd.empty() && L.wn.empty(); };
-		// A backend error on the GPU thread is carried over to this one and rethrown after
-		// the join; unwinding on either side joins the thread first (a joinable std::thread
-		// must not be destroyed).
-		std::exception_ptr gpu_err;
+		// A backend error on a GPU thread is carried over to this one and rethrown after the
+		// join; unwinding on either side joins the threads first (a joinable std::thread must
+		// not be destroyed).
+		std::exception_ptr gpu_err[2];
+		std::thread gpu[2];
+		struct Joiner { std::thread* t; ~Joiner() { for(int k = 0; k < 2; k++) if(t[k].joinable()) t[k].join(); } } joiner{gpu};
 		auto start = [&](int k) {
-			return std::thread([this, k, &gpu_err] {
-				try { execute(launch_[k]); } catch(...) { gpu_err = std::current_exception(); }
+			gpu[k] = std::thread([this, k, &gpu_err] {
+				try { execute(launch_[k]); } catch(...) { gpu_err[k] = std::current_exception(); }
 			});
 		};
-		std::thread gpu;
-		struct Joiner { std::thread& t; ~Joiner() { if(t.joinable()) t.join(); } } joiner{gpu};
-		auto join = [&] {
-			gpu.join();
-			if(gpu_err) std::rethrow_exception(gpu_err);
+		auto join = [&](int k) {
+			if(gpu[k].joinable()) gpu[k].join();
+			if(gpu_err[k]) std::rethrow_exception(gpu_err[k]);
 		};
+		const bool two = be2_ != nullptr;
 		int a = 0;
 		refill(co[0], cap);
 		gather(launch_[0], co[0]);
-		gpu = start(0);
+		start(0);
 		refill(co[1], cap);
 		gather(launch_[1], co[1]);
+		if(two) start(1);
 		while(true) {
-			// invariant: the GPU thread runs launch a (cohort a waits on it); launch b is
-			// gathered from cohort b
+			// invariant: launch a is on (or through) the GPU; launch b is gathered, and with one
+			// backend it starts once launch a is through
 			const double t0 = now_s();
-			join();
+			join(a);
 			st.t_wait += now_s() - t0;
 			const int b = 1 - a;
-			gpu = start(b);
+			if(!two) start(b);
 			const double t1 = now_s();
 			scatter_resume(launch_[a], st);
 			retire_write(co[a]);
@@ -1696,9 +1733,11 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			gather(launch_[a], co[a]);
 			st.t_step += now_s() - t1;
 			if(eof && co[a].empty() && co[b].empty() && empty(launch_[a]) && empty(launch_[b])) break;
+			if(two) start(a);
 			a = b;
 		}
-		join();
+		join(0);
+		join(1);
 	}
 	if(ahead_f.valid()) ahead_f.get();            // (a batch taken past the end: empty)
 	writer.finish();

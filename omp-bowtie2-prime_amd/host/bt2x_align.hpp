@@ -1057,6 +1057,9 @@ public:
 	~Aligner();
 	// run(): overlap one cohort's GPU launches with the host work of another (default on)
 	void set_pipeline(bool on) { pipeline_ = on; }
+	// pipelined: the second cohort's launches on their own backend (a second context with
+	// its own GPU stream), so the two cohorts' launches also overlap each other on the GPU
+	void set_second_backend(Backend* be) { be2_ = be; }
 	// seed rounds through bt2x_seed_round (default on; off: seed search, host ranking and
 	// prioritization, SA resolution as three requests)
 	void set_gpu_round(bool on) { gpu_round_ = on; }
@@ -1122,6 +1125,7 @@ private:
 	// pooled read contexts (kept across runs; released by the destructor)
 	std::vector<std::unique_ptr<ReadCtx>> ctxs_;
 	std::vector<ReadCtx*> free_;
+	std::vector<std::vector<ReadCtx*>> retire_keep_, retire_fin_;   // retire()'s per-chunk lists
 	// host threads for the parallel loops over reads
 	std::unique_ptr<WorkPool> pool_;
 	WorkPool& pool();
@@ -1129,6 +1133,7 @@ private:
 	const Params& p_;
 	const RefInfo& ref_;
 	Backend& be_;
+	Backend* be2_ = nullptr;
 };
 
 } // namespace host

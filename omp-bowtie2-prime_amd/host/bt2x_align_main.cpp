@@ -227,7 +227,7 @@ void usage() {
 	             "                  [-i FUNC] [--score-min FUNC] [--n-ceil FUNC] [--mp MX,MN] [--np N]\n"
 	             "                  [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N] [--no-sse8] [--i16-build]\n"
 	             "                  [--no-hd] [-p threads] [--slots N] [--device N] [--stats]\n"
-	             "                  [--shard i/N] [--warmup-files K] [--metrics]\n");
+	             "                  [--shard i/N] [--warmup-files K] [--metrics] [--no-pipeline] [--streams 1|2]\n");
 }
 
 } // namespace
@@ -239,6 +239,11 @@ int main(int argc, char** argv) {
 	int threads = 16, device = 0;
 	size_t slots = 1 << 17;
 	bool stats = false, pipeline = true, gpu_round = true, hd = true, metrics = false;
+	// --streams 2: the second cohort on a second context (bt2x_open_shared).  One is the
+	// default: the run is host-bound, and two contexts' concurrent launches each take longer
+	// (C3, one box: 2.05 vs 1.87 M reads/s).  BT2X_STREAMS sets the default (A/B runs).
+	int streams = 1;
+	if(const char* e = std::getenv("BT2X_STREAMS")) streams = std::atoi(e);
 	int shard = 0, nshards = 1, warm_files = 0;
 	std::string dump;
 	for(int i = 1; i < argc; i++) {
@@ -259,6 +264,7 @@ int main(int argc, char** argv) {
 		else if(a == "--stats") stats = true;
 		else if(a == "--dump") dump = val();
 		else if(a == "--no-pipeline") pipeline = false;
+		else if(a == "--streams") streams = std::atoi(val());
 		else if(a == "--no-gpu-round") gpu_round = false;
 		else if(a == "--no-hd") hd = false;
 		else if(a == "--metrics") metrics = true;
@@ -311,12 +317,25 @@ int main(int argc, char** argv) {
 		// not print: skip the kernels' exact-best pass (bt2x.h BT2X_OPT_EXACT_BEST)
 		bt2x::check(bt2x_set_option(dev.ctx(), BT2X_OPT_EXACT_BEST, 0), "bt2x_set_option");
 		HipBackend hip(dev.ctx());
+		// --streams 2 (pipelined): the second cohort's launches run on a second context over the
+		// same device index (its own stream), so the two cohorts' launches overlap on the GPU
+		// (--dump records one launch sequence on one context)
+		std::unique_ptr<bt2x_ctx, void (*)(bt2x_ctx*)> ctx2(nullptr, bt2x_close);
+		std::unique_ptr<HipBackend> hip2;
+		if(pipeline && streams >= 2 && dump.empty()) {
+			bt2x_ctx* c2 = nullptr;
+			bt2x::check(bt2x_open_shared(dev.ctx(), &c2), "bt2x_open_shared");
+			ctx2.reset(c2);
+			bt2x::check(bt2x_set_option(c2, BT2X_OPT_EXACT_BEST, 0), "bt2x_set_option");
+			hip2.reset(new HipBackend(c2));
+		}
 		set_host_allocator(PinnedCache::alloc, PinnedCache::release);   // launch buffers page-locked
 		std::unique_ptr<DumpBackend> dumper;
 		if(!dump.empty()) dumper.reset(new DumpBackend(hip, dump));
 		Backend& be = dumper ? static_cast<Backend&>(*dumper) : static_cast<Backend&>(hip);
 		Aligner al(p, ref, be);
 		al.set_pipeline(pipeline);
+		if(hip2) al.set_second_backend(hip2.get());
 		al.set_gpu_round(gpu_round);
 		al.set_header(hd);
 		pin.join();
@@ -378,7 +397,13 @@ int main(int argc, char** argv) {
 			             (unsigned long long)st.round_launches, (unsigned long long)st.rounds, st.t_round,
 			             (unsigned long long)st.dp_max_launch);
 		if(stats) {
-			const HipBackend::GpuStats& g = hip.gs;
+			HipBackend::GpuStats g = hip.gs;
+			if(hip2) {
+				const HipBackend::GpuStats& h = hip2->gs;
+				g.k_round_ms += h.k_round_ms; g.k_dp_ms += h.k_dp_ms; g.t_round_call += h.t_round_call;
+				g.t_dp_call += h.t_dp_call; g.round_h2d += h.round_h2d; g.round_d2h += h.round_d2h;
+				g.dp_h2d += h.dp_h2d; g.dp_d2h += h.dp_d2h; g.retries += h.retries;
+			}
 			std::fprintf(stderr, "BT2X_GPU k_round=%.4f t_round_call=%.4f round_h2d_mib=%.1f round_d2h_mib=%.1f "
 			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f retries=%llu\n", g.k_round_ms * 1e-3, g.t_round_call,
 			             g.round_h2d / 1048576.0, g.round_d2h / 1048576.0, g.k_dp_ms * 1e-3, g.t_dp_call,

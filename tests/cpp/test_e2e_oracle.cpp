@@ -172,7 +172,7 @@ int main(int argc, char** argv) {
 	size_t slots = 4096;
 	int threads = 4;
 	bool host_timing = false, pipeline = true, gpu_round = true, hd = true, metrics = false, host_windows = false;
-	int reps = 1, inject = 0, shard = 0, nshards = 1, warm_files = 0;
+	int reps = 1, inject = 0, shard = 0, nshards = 1, warm_files = 0, streams = 1;
 	std::string idx, fqs, outp;
 	std::vector<std::string> pos;
 	for(int i = 1; i < argc; i++) {
@@ -185,6 +185,7 @@ int main(int argc, char** argv) {
 		else if(a == "-S" && i + 1 < argc) outp = argv[++i];
 		else if(a == "--host-timing") host_timing = true;
 		else if(a == "--no-pipeline") pipeline = false;
+		else if(a == "--streams" && i + 1 < argc) streams = std::atoi(argv[++i]);
 		else if(a == "--no-gpu-round") gpu_round = false;
 		else if(a == "--no-hd") hd = false;
 		else if(a == "--host-windows") host_windows = true;
@@ -259,6 +260,11 @@ int main(int argc, char** argv) {
 	al.set_pipeline(pipeline);
 	al.set_gpu_round(gpu_round);
 	al.set_header(hd);
+	// --streams 2: the second cohort's launches on a backend of their own (bt2x-align's two
+	// contexts), so the two GPU threads run concurrently
+	OracleBackend be2(index.desc(), p.sc, host_windows ? nullptr : &ref);
+	be2.fail_at = inject;
+	if(streams >= 2) al.set_second_backend(&be2);
 	RunStats st;
 	uint64_t first_rdid = 0;
 	double t_align = 0;

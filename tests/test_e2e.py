@@ -51,7 +51,8 @@ SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
 # the DP kernel modes each set runs through on the GPU: the launcher's default
 # (lane-per-problem banded kernel above BT2X_DP_WAVE_MAX problems, wave per problem
 # below), and each kernel forced for every launch
-DP_MODES = {"default": None, "lane": "0", "wave": "1", "hostwin": "host", "handover": "handover", "parwave": "parwave"}
+DP_MODES = {"default": None, "lane": "0", "wave": "1", "hostwin": "host", "handover": "handover", "parwave": "parwave",
+            "stream2": "stream2"}
 MD5 = os.path.join(g.GOLDEN, "e2e_md5.json")
 SUMMARY = os.path.join(g.GOLDEN, "e2e_summary.json")
 
@@ -144,12 +145,19 @@ def test_host_driver_vs_reference_sam_three_requests(fixtures, name, idx, fq, op
     check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4", "--no-gpu-round"] + opts, name)
 
 
-@pytest.mark.parametrize("pipeline", [True, False])
-def test_host_driver_backend_error_exits_cleanly(fixtures, pipeline):
-    """A backend failure (a GPU call's bt2x::Error) on the pipelined GPU thread reaches the
+@pytest.mark.parametrize("name,idx,fq,opts", [SETS[1], SETS[4]], ids=[SETS[1][0], SETS[4][0]])
+def test_host_driver_two_backends(fixtures, name, idx, fq, opts):
+    """The same with the second cohort's launches on a backend of its own (bt2x-align's
+    second context, bt2x_open_shared): two GPU threads whose launches overlap."""
+    check([ORACLE_DRIVER, fixtures[idx], fixtures[fq], "--slots", "777", "-p", "4", "--streams", "2"] + opts, name)
+
+
+@pytest.mark.parametrize("mode", ["pipeline", "two", "serial"])
+def test_host_driver_backend_error_exits_cleanly(fixtures, mode):
+    """A backend failure (a GPU call's bt2x::Error) on a pipelined GPU thread reaches the
     caller as an exception: exit code 1 and the message, not std::terminate (SIGABRT)."""
     cmd = [ORACLE_DRIVER, fixtures["rep"], fixtures["rep_reads.fq"], "--slots", "400", "-p", "3",
-           "--inject-error", "3"] + ([] if pipeline else ["--no-pipeline"])
+           "--inject-error", "3"] + {"pipeline": [], "two": ["--streams", "2"], "serial": ["--no-pipeline"]}[mode]
     r = subprocess.run(cmd, capture_output=True, timeout=600)
     assert r.returncode == 1, (r.returncode, r.stderr[-500:])
     assert b"injected backend error" in r.stderr
@@ -192,9 +200,12 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     elif DP_MODES[mode] == "parwave":             # wave per problem, its parallel walk
         env["BT2X_DP_WAVE"] = "1"
         env["BT2X_DP_PARWALK"] = "2"
-    elif DP_MODES[mode] is not None:
+    elif DP_MODES[mode] not in (None, "stream2"):
         env["BT2X_DP_WAVE"] = DP_MODES[mode]
-    _, err = check([ALIGN, "-x", fixtures[idx], "-U", fixtures[fq], "--slots", "1000"] + opts, name, env=env)
+    # stream2: the two cohorts on two contexts (bt2x_open_shared); default: one context
+    env.pop("BT2X_STREAMS", None)
+    extra = ["--streams", "2"] if DP_MODES[mode] == "stream2" else []
+    _, err = check([ALIGN, "-x", fixtures[idx], "-U", fixtures[fq], "--slots", "1000"] + opts + extra, name, env=env)
     check_summary(err, name)
 
 
