@@ -752,6 +752,7 @@ def main():
                    "host_threads": args.host_threads, "host_threads_note": threads_note, "cpu_share": share,
                    "slots": args.slots, "key": workload_key(args)},
         "end_to_end": {"t_align_s": round(t_align, 3), "t_align_max_s": round(t_max, 3),
+                       "t_run_s": timed.get("t_run"), "t_return_s": timed.get("t_ret"),
                        "step_done_s": [round(t, 3) for t in t_files], "wall_incl_index_load_s": round(wall, 2),
                        "peak_rss_mib": peak, "summary": bdist.alignment_summary(tot).splitlines(),
                        "stats": stats, "gpu": kv_line(err, "BT2X_GPU"), "rusage_align": kv_line(err, "BT2X_RUSAGE_ALIGN")},

@@ -157,7 +157,7 @@ struct bt2x_ctx {
 	DevScoring sc{};
 	void* d_ebwt = nullptr; void* d_ftab = nullptr; void* d_eftab = nullptr; void* d_blk = nullptr;
 	void* d_sa = nullptr; void* d_text = nullptr;
-	void* d_offs = nullptr; void* d_rstarts = nullptr; void* d_plen = nullptr;
+	void* d_offs = nullptr; void* d_rstarts = nullptr; void* d_plen = nullptr; void* d_tfirst = nullptr;
 	DevBuf b_reads, b_quals, b_refs, b_in, b_out, b_recs, b_edits, b_dbg_dig, b_dbg_cand;
 	// seed round: host-variant staging, and the round's own scratch (seed results, rows
 	// to resolve, per-lane workspace)
@@ -186,7 +186,7 @@ bt2x_ctx::~bt2x_ctx() {
 	                 &b_jobs, &b_ranges, &b_rcnt})
 		b->release();
 	if(!shares_index)
-		for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen})
+		for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen, d_tfirst})
 			if(p) (void)hipFree(p);
 	for(void* p : {(void*)d_stats, (void*)d_counters, (void*)d_queue, (void*)d_mmpen})
 		if(p) (void)hipFree(p);
@@ -312,6 +312,18 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 		HIPCHK(hipMemcpy(c->d_plen, idx->plen, 8 * idx->npat, hipMemcpyHostToDevice));
 		c->ix.rstarts = (const uint64_t*)c->d_rstarts;
 		c->ix.plen = (const uint64_t*)c->d_plen;
+		// each text's first fragment (the window kernel's per-problem search starts there)
+		if(idx->nfrag < 0xffffffffULL) {
+			std::vector<uint32_t> tf(idx->npat + 1);
+			uint64_t k = 0;
+			for(uint64_t t = 0; t <= idx->npat; t++) {
+				while(k < idx->nfrag && idx->rstarts[3 * k + 1] < t) k++;
+				tf[t] = (uint32_t)k;
+			}
+			HIPCHK(hipMalloc(&c->d_tfirst, 4 * tf.size()));
+			HIPCHK(hipMemcpy(c->d_tfirst, tf.data(), 4 * tf.size(), hipMemcpyHostToDevice));
+			c->ix.tfirst = (const uint32_t*)c->d_tfirst;
+		}
 	} else {
 		c->ix.nfrag = 0;
 	}
@@ -355,7 +367,7 @@ extern "C" int bt2x_open_shared(const bt2x_ctx* base, bt2x_ctx** out) {
 	c->sc = base->sc;
 	c->d_ebwt = base->d_ebwt; c->d_ftab = base->d_ftab; c->d_eftab = base->d_eftab; c->d_blk = base->d_blk;
 	c->d_sa = base->d_sa; c->d_text = base->d_text; c->d_offs = base->d_offs; c->d_rstarts = base->d_rstarts;
-	c->d_plen = base->d_plen;
+	c->d_plen = base->d_plen; c->d_tfirst = base->d_tfirst;
 	c->npat = base->npat; c->exact_best = base->exact_best; c->ncu = base->ncu; c->chunk_groups = base->chunk_groups;
 	HIPCHK(hipMalloc(&c->d_mmpen, sizeof c->sc.mmpen));
 	HIPCHK(hipMemcpy(c->d_mmpen, c->sc.mmpen, sizeof c->sc.mmpen, hipMemcpyHostToDevice));

@@ -28,6 +28,8 @@ struct DevIndex {
 	const uint64_t* rstarts;  // 3 words per fragment (joined off, tidx, text off)
 	const uint64_t* plen;     // reference lengths
 	uint64_t nfrag;
+	const uint32_t* tfirst;   // text t's fragments are rstarts[tfirst[t] .. tfirst[t+1]) (npat+1
+	                          // entries; fragments are in joined = text order); or NULL
 };
 
 struct DevScoring {

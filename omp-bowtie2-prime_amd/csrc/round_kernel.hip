@@ -34,72 +34,98 @@ struct Job {                 // one read's sampling work
 	uint32_t pad;
 };
 
+// This lane's base in a block of the counter reserved for the whole wave (one atomic per
+// wave instead of one per lane: the prep kernel's counters are shared by every wave of the
+// launch, so per-lane atomics serialised at them).  Every lane of the wave must call it.
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t* ctr, uint32_t v) {
+	const uint32_t lane = threadIdx.x & 63u;
+	uint32_t x = v;                                            // inclusive scan
+	for(int d = 1; d < 64; d <<= 1) {
+		const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+		if(lane >= (uint32_t)d) x += y;
+	}
+	const uint32_t tot = (uint32_t)__shfl((int)x, 63);
+	uint32_t base = 0;
+	if(lane == 0 && tot) base = atomicAdd(ctr, tot);
+	base = (uint32_t)__shfl((int)base, 0);
+	return base + x - v;
+}
+
 __global__ void __launch_bounds__(64)
 round_prep_kernel(RoundLaunch a) {
 	const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
 	PrepWs& w = *reinterpret_cast<PrepWs*>(a.ws + (size_t)lane * sizeof(PrepWs));
 	Job* jobs = reinterpret_cast<Job*>(a.jobs);
 	Range* ranges = reinterpret_cast<Range*>(a.ranges);
-	for(uint32_t r = lane; r < a.n; r += gridDim.x * blockDim.x) {
-		const bt2x_round_in in = a.in[r];
-		Rnd rnd{in.rnd_last, in.rnd_lastoff};
-		Prep p = prep(in, a.seeds + in.seed0, a.seed_out + in.seed0, a.exr + in.exr0, a.maxelt, rnd, w);
+	const uint32_t stride = gridDim.x * blockDim.x;
+	// the wave walks the reads together (inactive lanes past the end), so the counters can
+	// be reserved per wave
+	for(uint32_t r0 = blockIdx.x * blockDim.x; r0 < a.n; r0 += stride) {
+		const uint32_t r = r0 + threadIdx.x;
+		const bool act = r < a.n;
+		Prep p{};
+		bt2x_round_in in{};
+		Rnd rnd{0, 0};
 		bt2x_round_out o;
+		if(act) {
+			in = a.in[r];
+			rnd = Rnd{in.rnd_last, in.rnd_lastoff};
+			p = prep(in, a.seeds + in.seed0, a.seed_out + in.seed0, a.exr + in.exr0, a.maxelt, rnd, w);
+		}
 		o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
 		o.num_elts = p.numElts; o.nonz = p.nonz; o.status = p.status;
 		o.sat0 = o.nsat = o.elt0 = o.nelt = o.exr0 = o.nexr = 0;
-		if(p.status == BT2X_ROUND_OK) {
-			const uint32_t L = in.seedlen;
-			const uint32_t nsat = p.nsmallSat + (uint32_t)p.nsamples, nelt = (uint32_t)(p.smallElts + p.nsamples);
-			uint32_t job = 0xffffffffu, range0 = 0;
-			const uint32_t nb = p.n2 - p.nsmall;
-			if(p.nsamples) {
-				job = atomicAdd(&a.counters[3], 1u);
-				range0 = atomicAdd(&a.counters[4], nb);
-				if(job >= a.job_cap || range0 + nb > a.range_cap) {
-					p.status = BT2X_ROUND_REDO;                  // hand the read back to the host
-					if(job < a.job_cap) {                         // an empty job keeps the queue dense
-						Job j = {};
-						j.read = r; j.rnd_last = rnd.last; j.rnd_lastoff = rnd.lastOff;
-						jobs[job] = j;
-					}
-				}
-			}
-			if(p.status == BT2X_ROUND_OK) {
-				o.nsat = nsat; o.nelt = nelt; o.nexr = p.nexnew;
-				o.sat0 = atomicAdd(&a.counters[0], nsat);
-				o.elt0 = atomicAdd(&a.counters[1], nelt);
-				o.exr0 = p.nexnew ? atomicAdd(&a.counters[2], p.nexnew) : 0;
-				if(o.sat0 + nsat <= a.sat_cap && o.elt0 + nelt <= a.row_cap) {
-					uint32_t e = o.elt0;
-					for(uint32_t i = 0; i < p.nsmallSat; i++) {
-						const Range& rg = w.r2[i];
-						bt2x_sat s;
-						s.rdoff = rg.rdoff; s.rand_n = (uint16_t)rg.size; s.fw = rg.fw; s.seedlen = (uint8_t)L;
-						a.sats[o.sat0 + i] = s;
-						for(uint32_t k = 0; k < (uint32_t)rg.size; k++) {
-							bt2x_resolve_in ri;
-							ri.row = rg.topf + k; ri.qlen = L; ri.pad = 0;
-							a.rows[e++] = ri;
-						}
-					}
-				}
-				if(o.exr0 + p.nexnew <= a.exr_cap)
-					for(uint32_t i = 0; i < p.nexnew; i++) a.exr_out[o.exr0 + i] = w.exnew[i];
-				if(p.nsamples) {
-					for(uint32_t i = 0; i < nb; i++) ranges[range0 + i] = w.r2[p.nsmall + i];
-					Job j;
-					j.read = r; j.nb = nb; j.range0 = range0;
-					j.sat_base = o.sat0 + p.nsmallSat; j.elt_base = (uint32_t)(o.elt0 + p.smallElts);
-					j.rnd_last = rnd.last; j.rnd_lastoff = rnd.lastOff;
-					j.nsamples = (uint32_t)p.nsamples; j.seedlen = L; j.pad = 0;
-					jobs[job] = j;
-				}
-			} else {
-				o.status = p.status;
+		const bool ok0 = act && p.status == BT2X_ROUND_OK;
+		const uint32_t L = in.seedlen;
+		const uint32_t nsat = p.nsmallSat + (uint32_t)p.nsamples, nelt = (uint32_t)(p.smallElts + p.nsamples);
+		const uint32_t nb = ok0 ? p.n2 - p.nsmall : 0;
+		const bool wantjob = ok0 && p.nsamples;
+		const uint32_t job = wave_alloc(&a.counters[3], wantjob ? 1u : 0u);
+		const uint32_t range0 = wave_alloc(&a.counters[4], wantjob ? nb : 0u);
+		if(wantjob && (job >= a.job_cap || range0 + nb > a.range_cap)) {
+			p.status = BT2X_ROUND_REDO;                            // hand the read back to the host
+			if(job < a.job_cap) {                                   // an empty job keeps the queue dense
+				Job j = {};
+				j.read = r; j.rnd_last = rnd.last; j.rnd_lastoff = rnd.lastOff;
+				jobs[job] = j;
 			}
 		}
-		a.out[r] = o;
+		const bool ok1 = ok0 && p.status == BT2X_ROUND_OK;
+		const uint32_t sat0 = wave_alloc(&a.counters[0], ok1 ? nsat : 0u);
+		const uint32_t elt0 = wave_alloc(&a.counters[1], ok1 ? nelt : 0u);
+		const uint32_t exr0 = wave_alloc(&a.counters[2], ok1 ? p.nexnew : 0u);
+		if(ok1) {
+			o.nsat = nsat; o.nelt = nelt; o.nexr = p.nexnew;
+			o.sat0 = sat0; o.elt0 = elt0; o.exr0 = p.nexnew ? exr0 : 0;
+			if(o.sat0 + nsat <= a.sat_cap && o.elt0 + nelt <= a.row_cap) {
+				uint32_t e = o.elt0;
+				for(uint32_t i = 0; i < p.nsmallSat; i++) {
+					const Range& rg = w.r2[i];
+					bt2x_sat s;
+					s.rdoff = rg.rdoff; s.rand_n = (uint16_t)rg.size; s.fw = rg.fw; s.seedlen = (uint8_t)L;
+					a.sats[o.sat0 + i] = s;
+					for(uint32_t k = 0; k < (uint32_t)rg.size; k++) {
+						bt2x_resolve_in ri;
+						ri.row = rg.topf + k; ri.qlen = L; ri.pad = 0;
+						a.rows[e++] = ri;
+					}
+				}
+			}
+			if(o.exr0 + p.nexnew <= a.exr_cap)
+				for(uint32_t i = 0; i < p.nexnew; i++) a.exr_out[o.exr0 + i] = w.exnew[i];
+			if(p.nsamples) {
+				for(uint32_t i = 0; i < nb; i++) ranges[range0 + i] = w.r2[p.nsmall + i];
+				Job j;
+				j.read = r; j.nb = nb; j.range0 = range0;
+				j.sat_base = o.sat0 + p.nsmallSat; j.elt_base = (uint32_t)(o.elt0 + p.smallElts);
+				j.rnd_last = rnd.last; j.rnd_lastoff = rnd.lastOff;
+				j.nsamples = (uint32_t)p.nsamples; j.seedlen = L; j.pad = 0;
+				jobs[job] = j;
+			}
+		} else if(ok0) {
+			o.status = p.status;
+		}
+		if(act) a.out[r] = o;
 	}
 }
 
@@ -109,6 +135,19 @@ __device__ __forceinline__ double readlane_f64(double v, uint32_t k) {
 	const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), (int)k);
 	return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+
+// The sampling kernel's workgroup is one wave, so its threads need no barrier: a wave's
+// LDS operations execute in issue order, and a compiler scheduling barrier keeps the
+// issue order.  (__syncthreads() would also fence the wave's global stores -- the outputs
+// it writes every batch -- and wait for them each time.)
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// BT2X_ROUND_CLOCK builds: per-phase clock64 sums in bt2x_last_round_stats out[8..11]
+#ifdef BT2X_ROUND_CLOCK
+#define ROUND_CLOCK(i) do { const uint64_t t1_ = clock64(); stats[i] += t1_ - t_; t_ = t1_; } while(0)
+#else
+#define ROUND_CLOCK(i) do {} while(0)
+#endif
 
 struct WaveCoop {                            // a one-wave workgroup runs one job
 	// RowSampler state in registers: live range ids, their masses and running sums of
@@ -125,7 +164,7 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 	}
 	__device__ void r1n_reset(const SampleWs& w, uint32_t nb) {
 		for(uint32_t i = threadIdx.x; i < nb; i += 64) { uint32_t* p = r1w(w, i); p[0] = 0; p[1] = 0; p[2] = 0; }
-		__syncthreads();
+		wave_sync();
 	}
 	__device__ static R1N unpack(uint32_t w0, uint32_t w1, uint32_t w2) {
 		R1N r;
@@ -144,7 +183,7 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 			p[1] = (uint32_t)r.thresh | ((uint32_t)r.list << 16);
 			p[2] = (uint32_t)r.inited | ((uint32_t)r.swaplist << 8) | ((uint32_t)r.converted << 16);
 		}
-		__syncthreads();
+		wave_sync();
 	}
 	__device__ void big_load(const SampleWs& w, uint32_t nb) {
 		const uint32_t l = threadIdx.x;
@@ -192,7 +231,7 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 	}
 	__device__ uint32_t lane() const { return threadIdx.x; }
 	__device__ uint32_t width() const { return 64; }
-	__device__ void sync() const { __syncthreads(); }
+	__device__ void sync() const { wave_sync(); }
 	__device__ uint64_t ballot(bool p) const { return __ballot(p); }
 	__device__ bool leader() const { return threadIdx.x == 0; }
 	__device__ void rs_init(SampleWs& w, uint32_t nb) {
@@ -200,7 +239,7 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 		lv0 = l; lv1 = l + 64;
 		m0 = l < nb ? w.masses[l] : 0.0; m1 = l + 64 < nb ? w.masses[l + 64] : 0.0;
 		w.mlive[l] = m0; w.mlive[l + 64] = m1;
-		__syncthreads();
+		wave_sync();
 	}
 	// the running sums in list order from position `from` (lane 0, the order SerialCoop
 	// sums in), then every lane takes its two
@@ -218,7 +257,7 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 			}
 			for(; k < nlive; k++) { sofar += w.mlive[k]; w.pre[k] = sofar; }
 		}
-		__syncthreads();
+		wave_sync();
 		p0 = w.pre[l]; p1 = w.pre[l + 64];
 	}
 	// the count of running sums <= rd is the bisection's upper bound
@@ -241,7 +280,7 @@ struct WaveCoop {                            // a one-wave workgroup runs one jo
 		if(l >= q) { lv0 = l == 63 ? h0 : nl0; m0 = l == 63 ? hm : nm0; }
 		if(l + 64 >= q) { lv1 = nl1; m1 = nm1; }
 		w.mlive[l] = m0; w.mlive[l + 64] = m1;
-		__syncthreads();
+		wave_sync();
 		return q;
 	}
 };
@@ -262,12 +301,45 @@ constexpr uint32_t kLcgA = 1664525u, kLcgC = 1013904223u;      // Rnd::nextU32's
 template<class Put>
 __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& w, WaveCoop& co, uint32_t jA,
                             uint32_t jC, uint64_t stats[8], Put&& put) {
-	uint64_t t = clock64();
+#ifdef BT2X_ROUND_CLOCK
+	uint64_t t_ = clock64();
+#endif
 	SampleState st;
 	if(!sample_setup(nb, w, co, st)) return false;
 	const uint32_t lane = threadIdx.x;
+	// Lay out the swap lists of the small ranges (2 <= n < 128) now instead of at their
+	// first draw: the list is the identity either way and its arena offset is never
+	// observed, and a laid-out list's first draw can join a batch.  Marked `converted`
+	// (r1n_next then takes the list as laid out; n = 1 keeps its draw-free first draw, so
+	// it stays lazy).  Only while half the arena suffices, so a job that fits the arena
+	// serially still fits.
+	{
+		uint32_t tot = 0;
+		for(uint32_t i = 0; i < nb; i++) {
+			const uint32_t n = (uint16_t)w.big[i].size;
+			if(n >= 2 && n < 128) tot += n;
+		}
+		if(tot && tot <= (uint32_t)kArena / 2) {
+			uint32_t base = 0;
+			for(uint32_t i = 0; i < nb; i++) {
+				const uint32_t n = (uint16_t)w.big[i].size;
+				if(n < 2 || n >= 128) continue;
+				for(uint32_t e = lane; e < n; e += 64) w.arena[base + e] = (uint16_t)e;
+				if(lane == 0) {
+					uint32_t* pw = WaveCoop::r1w(w, i);
+					const uint16_t t = (uint16_t)(0.10f * (float)n);
+					pw[0] = n;                                             // cur 0
+					pw[1] = (uint32_t)(t > 16 ? t : 16) | (base << 16);
+					pw[2] = 1u | (1u << 8) | (1u << 16);                   // inited, swaplist, converted
+				}
+				base += n;
+			}
+			st.arenaTop = base;
+			wave_sync();
+		}
+	}
 	uint64_t k = 0;
-	{ const uint64_t t1 = clock64(); stats[4] += t1 - t; t = t1; }
+	ROUND_CLOCK(4);
 	while(k < nsamples) {
 		if(st.nlive == 0) return false;                            // as sample_step
 		const uint32_t act = nsamples - k < 64 ? (uint32_t)(nsamples - k) : 64u;
@@ -308,7 +380,9 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 			rem &= ~m;
 		}
 		const uint32_t cur1 = cur0 + cnt;                          // the range's count after this draw
-		bool reg = lane < act && n != 0 && cur1 < n;               // cur1 >= n: done(), the range leaves
+		// a swap list's last element may be drawn in the batch (the range then leaves the
+		// sampler after the batch, which ends with that draw); a seen list converts first
+		bool reg = lane < act && n != 0 && (swap ? cur1 <= n : cur1 < n);
 		uint32_t pos = 0;                                          // swap list: the drawn position
 		if(swap) {
 			reg = reg && ready;
@@ -316,6 +390,7 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 		} else {
 			reg = reg && cur1 < thresh && !seen_has(w, key);       // cur1 >= thresh: conversion
 		}
+		const bool term = reg && swap && cur1 == n;                // done(): finishedRange after it
 		// Inside the batch, from a 128-slot LDS table (key -> mask of the lanes that drew it):
 		// a seen-list draw of a key an earlier lane drew is a redraw (the serial step's); a
 		// swap-list draw reads what its range's earlier exchanges left.  With A the list at
@@ -326,7 +401,7 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 		const uint32_t ikey = swap ? ((bi << 16) | pos) + 1u : key;
 		w.bkey[lane] = 0; w.bkey[lane + 64] = 0;
 		w.bmlo[lane] = 0; w.bmlo[lane + 64] = 0; w.bmhi[lane] = 0; w.bmhi[lane + 64] = 0;
-		__syncthreads();
+		wave_sync();
 		uint32_t bslot = 0;
 		if(reg) {
 			bslot = (ikey * 2654435761u) >> 25;
@@ -336,9 +411,9 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 				bslot = (bslot + 1) & 127;
 			}
 		}
-		__syncthreads();
+		wave_sync();
 		if(reg) atomicOr(lane < 32 ? &w.bmlo[bslot] : &w.bmhi[bslot], 1u << (lane & 31));
-		__syncthreads();
+		wave_sync();
 		const uint64_t below = (1ull << lane) - 1ull;
 		uint64_t mine = 0;                                         // the lanes that drew our key
 		int pr = -1, pc = -1;                                      // last earlier lane drawing r_L / c_L
@@ -361,7 +436,11 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 			}
 		}
 		const uint64_t bad = __ballot(!reg) & (act == 64 ? ~0ull : ((1ull << act) - 1ull));
-		const uint32_t F = bad ? (uint32_t)__ffsll((unsigned long long)bad) - 1 : act;
+		uint32_t F = bad ? (uint32_t)__ffsll((unsigned long long)bad) - 1 : act;
+		// the batch ends with the first draw that exhausts its range (if before F)
+		const uint64_t terms = __ballot(term) & (F == 64 ? ~0ull : ((1ull << F) - 1ull));
+		const uint32_t T = terms ? (uint32_t)__ffsll((unsigned long long)terms) - 1 : 64u;
+		if(T < F) F = T + 1;
 		const uint64_t com = F == 64 ? ~0ull : ((1ull << F) - 1ull);   // the committed lanes
 		bool full = false;
 		uint32_t out = rn;
@@ -380,7 +459,7 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 				pw[2] = 1u;                                        // inited, seen-list mode
 			}
 		}
-		{ const uint64_t t1 = clock64(); stats[5] += t1 - t; t = t1; }
+		ROUND_CLOCK(5);
 		const uint64_t swm = __ballot(sw);
 		if(swm) {
 			// v_L through the chain of earlier lanes that drew c_L (pointer jumping: after
@@ -397,11 +476,11 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 			// the exchanges' net effect: each drawn position ends with the last committed
 			// drawer's v, then each cursor position with its draw's element (a cursor position
 			// may be an earlier drawn one)
-			__syncthreads();
+			wave_sync();
 			if(sw && 63 - __clzll(mine & com) == (int)lane) w.arena[rpos] = (uint16_t)v;
-			__syncthreads();
+			wave_sync();
 			if(sw) w.arena[cpos] = (uint16_t)out;
-			__syncthreads();
+			wave_sync();
 			stats[3] += (uint32_t)__popcll(swm);
 		}
 		if(lane < F) put(k + lane, w.big[bi], (uint16_t)out);
@@ -413,14 +492,24 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 			k += F;
 			stats[1] += F;
 		}
-		__syncthreads();
-		{ const uint64_t t1 = clock64(); stats[7] += t1 - t; t = t1; }
+		if(T < 64 && T + 1 == F) {                                 // finishedRange (as sample_step)
+			wave_sync();
+			const uint32_t tb = (uint32_t)__builtin_amdgcn_readlane((int)bi, (int)T);
+			st.mass -= w.masses[tb];
+			const uint32_t q = co.rs_remove(w, tb, st.nlive);
+			st.nlive--;
+			co.rs_rebuild(w, st.nlive, q);
+			wave_sync();
+			continue;                                              // the next batch
+		}
+		wave_sync();
+		ROUND_CLOCK(7);
 		if(F < act) {
 			if(!sample_step(k, rnd, w, co, st, [&](uint64_t kk, const Range& rg, uint16_t elt) { put(kk, rg, elt); }))
 				return false;
 			k++;
 			stats[2]++;
-			{ const uint64_t t1 = clock64(); stats[6] += t1 - t; t = t1; }
+			ROUND_CLOCK(6);
 		}
 	}
 	return true;
@@ -441,18 +530,21 @@ round_sample_kernel(RoundLaunch a) {
 	// lane l's draw in a batch starts 4l LCG steps on: x -> jA * x + jC
 	uint32_t jA = 1, jC = 0;
 	for(uint32_t i = 0; i < 4 * threadIdx.x; i++) { jA *= kLcgA; jC = kLcgA * jC + kLcgC; }
+	// the wave's statistics, added to the launch's counters once at the end (per-job
+	// atomics on a handful of shared counters serialised across the grid)
+	uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	uint64_t nsamp = 0;
+	uint32_t maxsamp = 0;
+	// first job: the workgroup's own index; then from the queue counter (offset by the grid)
+	uint32_t q = blockIdx.x;
 	for(;;) {
-		if(threadIdx.x == 0) qsh = atomicAdd(&a.counters[5], 1u);
-		__syncthreads();
-		const uint32_t q = qsh;
-		__syncthreads();
 		if(q >= njobs) break;
 		const Job j = jobs[q];
-		if(threadIdx.x == 0) { atomicAdd(&a.counters[6], j.nsamples); atomicMax(&a.counters[7], j.nsamples); }
+		nsamp += j.nsamples;
+		maxsamp = max(maxsamp, j.nsamples);
 		for(uint32_t i = threadIdx.x; i < j.nb && i < (uint32_t)kMaxRanges; i += 64) w.big[i] = ranges[j.range0 + i];
-		__syncthreads();
+		wave_sync();
 		Rnd rnd{j.rnd_last, j.rnd_lastoff};
-		uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 		const bool ok = sample_wave(j.nb, j.nsamples, rnd, w, co, jA, jC, stats, [&](uint64_t k, const Range& rg, uint16_t elt) {
 			if(!fits) return;
 			bt2x_sat s;
@@ -463,13 +555,20 @@ round_sample_kernel(RoundLaunch a) {
 			a.rows[j.elt_base + k] = ri;
 		});
 		if(threadIdx.x == 0) {
-			for(int i = 0; i < 4; i++) atomicAdd(&a.counters[8 + i], (uint32_t)stats[i]);
-			for(int i = 4; i < 8; i++) atomicAdd(&a.counters[8 + i], (uint32_t)(stats[i] >> 10));
 			bt2x_round_out& o = a.out[j.read];
 			o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
 			if(!ok) o.status = BT2X_ROUND_REDO;
+			qsh = gridDim.x + atomicAdd(&a.counters[5], 1u);       // the next job
 		}
-		__syncthreads();
+		wave_sync();
+		q = qsh;
+		wave_sync();
+	}
+	if(threadIdx.x == 0) {
+		atomicAdd(&a.counters[6], (uint32_t)nsamp);
+		atomicMax(&a.counters[7], maxsamp);
+		for(int i = 0; i < 4; i++) atomicAdd(&a.counters[8 + i], (uint32_t)stats[i]);
+		for(int i = 4; i < 8; i++) atomicAdd(&a.counters[8 + i], (uint32_t)(stats[i] >> 10));
 	}
 }
 

@@ -52,7 +52,10 @@ __global__ void __launch_bounds__(256) window_kernel(DevIndex ix, const bt2x_dp_
 	if(p.flags & BT2X_DP_REF_TEXT) {
 		const uint64_t t = p.ref_off;
 		const int64_t nfrag = (int64_t)ix.nfrag;
-		const int64_t lo = frag_text_lb(ix.rstarts, nfrag, t), hi = frag_text_lb(ix.rstarts, nfrag, t + 1);
+		// text t's fragment range: from the per-text table (one load), else two searches
+		const bool tab = ix.tfirst && t < (uint64_t)0xffffffffu;
+		const int64_t lo = tab ? (int64_t)ix.tfirst[t] : frag_text_lb(ix.rstarts, nfrag, t);
+		const int64_t hi = tab ? (int64_t)ix.tfirst[t + 1] : frag_text_lb(ix.rstarts, nfrag, t + 1);
 		// one search per problem (every lane the same addresses: broadcast loads), then each
 		// column moves forward from the window start's fragment; a window rarely crosses one
 		// (per-column binary searches made this kernel a chain of dependent loads per column)

@@ -358,7 +358,9 @@ int main(int argc, char** argv) {
 		if(!out) { std::fprintf(stderr, "cannot open %s\n", outp.c_str()); return 1; }
 		std::vector<char> obuf(1 << 24);
 		std::setvbuf(out, obuf.data(), _IOFBF, obuf.size());
-		const RunStats st = al.run(reader, out, slots, threads);
+		double t_run = 0;
+		const RunStats st = al.run(reader, out, slots, threads, &t_run);
+		const double t_ret = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
 		if(out != stdout) std::fclose(out); else std::fflush(out);
 		const double t_align = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
 		struct rusage ru_end;
@@ -370,8 +372,9 @@ int main(int argc, char** argv) {
 			std::fprintf(stderr, "%s\n", line.c_str());
 			std::string tf;
 			for(double t : st.t_files) { char b[32]; std::snprintf(b, sizeof b, "%s%.4f", tf.empty() ? "" : ",", t); tf += b; }
-			std::fprintf(stderr, "BT2X_TIMED reads=%llu first_rdid=%llu t_align=%.4f t_files=%s\n",
-			             (unsigned long long)st.reads, (unsigned long long)reader.first_rdid(), t_align, tf.c_str());
+			std::fprintf(stderr, "BT2X_TIMED reads=%llu first_rdid=%llu t_align=%.4f t_files=%s t_run=%.4f t_ret=%.4f\n",
+			             (unsigned long long)st.reads, (unsigned long long)reader.first_rdid(), t_align, tf.c_str(), t_run,
+			             t_ret);
 		}
 		if(stats) {
 			// the whole process, then the alignment window alone

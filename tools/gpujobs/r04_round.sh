@@ -2,7 +2,7 @@
 # trace + stats of a short bench run (per-kernel durations of round_sample_kernel et al.)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 TAG=${TAG:-r04x}
-timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_round.py tests/test_e2e.py \
+timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests/test_round.py tests/test_e2e.py tests/test_gpu_parity.py \
   > gpurun_out/${TAG}_round_tests.log 2>&1
 rc=$?; echo "round/e2e tests rc=$rc"; tail -3 gpurun_out/${TAG}_round_tests.log
 [ $rc -eq 0 ] || exit $rc
