@@ -1149,8 +1149,15 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 		// DP: the read's two orientations (codes and qualities) once per read, one
 		// reference window per posed problem (BitPairReference::getStretch)
 		uint64_t dbo = C.db0, pko = C.pk0, rbo = C.rb0;
+		const bool pf = host_prefetch();
 		for(size_t k = 0; k < C.wd.size(); k++) {
 			ReadCtx* c = C.wd[k];
+			if(pf && k + 3 < C.wd.size()) {                   // the read's codes and qualities (4 buffers)
+				const Read& r3 = C.wd[k + 3]->rd;
+				__builtin_prefetch(r3.fw.data()); __builtin_prefetch(r3.rc.data());
+				__builtin_prefetch(r3.qual.data()); __builtin_prefetch(r3.qualRev.data());
+				__builtin_prefetch(C.wd[k + 3]->dps.data());
+			}
 			const size_t i = C.wd0 + k, len = c->rd.length();
 			L.wd[i] = c; L.qb[i] = dbo; L.pb[i] = pko;
 			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)dbo);
@@ -1178,6 +1185,11 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 		uint64_t nbo = C.nb0, nko = C.nk0, neo = C.ne0;
 		for(size_t k = 0; k < C.wn.size(); k++) {
 			ReadCtx* c = C.wn[k];
+			if(pf && k + 3 < C.wn.size()) {
+				const ReadCtx* c3 = C.wn[k + 3];
+				__builtin_prefetch(c3->rd.fw.data()); __builtin_prefetch(c3->rd.rc.data());
+				__builtin_prefetch(c3->seed_in.data());
+			}
 			const size_t i = C.wn0 + k, len = c->rd.length();
 			L.wn[i] = c;
 			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.round_reads.begin() + (long)nbo);
@@ -1253,7 +1265,15 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	const bool prefetch = host_prefetch();
 	pool().parallel_for(nrun, 64, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
-		if(prefetch && i + 3 < nrun) prefetch_ctx(L.run[(size_t)i + 3], true);
+		if(prefetch) {
+			if(i + 6 < nrun) prefetch_ctx(L.run[(size_t)i + 6], true);
+			if(i + 3 < nrun) {                                // the arenas the results are copied into
+				const ReadCtx* c3 = L.run[(size_t)i + 3];
+				__builtin_prefetch(c3->elts.data(), 1); __builtin_prefetch(c3->sats.data(), 1);
+				__builtin_prefetch(c3->recs.data() + c3->recs.size(), 1);
+				__builtin_prefetch(c3->edits.data() + c3->edits.size(), 1);
+			}
+		}
 		if(i < nwn) {
 			const bt2x_round_out& o = L.round_out[(size_t)i];
 			c->round_out = o;
@@ -1657,7 +1677,13 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		const bool pf = host_prefetch();
 		pool().parallel_for(nf, 64, [&](long i) {
 			ReadCtx* c = fresh[(size_t)i];
-			if(pf && i + 3 < nf) prefetch_ctx(fresh[(size_t)i + 3], true);
+			if(pf && i + 6 < nf) prefetch_ctx(fresh[(size_t)i + 6], true);
+			if(pf && i + 3 < nf) {                             // the buffers decode writes
+				const Read& r3 = fresh[(size_t)i + 3]->rd;
+				__builtin_prefetch(r3.fw.data(), 1); __builtin_prefetch(r3.rc.data(), 1);
+				__builtin_prefetch(r3.qual.data(), 1); __builtin_prefetch(r3.qualRev.data(), 1);
+				__builtin_prefetch(r3.name.data(), 1);
+			}
 			FastqReader::decode(src[i], c->rd, rdid + (uint64_t)i, p_.randSeed, rdid0 + rdid + (uint64_t)i);
 			c->task = align_read(c);
 			c->task.h.resume();
