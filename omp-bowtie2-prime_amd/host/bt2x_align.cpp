@@ -1387,11 +1387,24 @@ private:
 // drains.
 class OrderedSamWriter {
 public:
-	explicit OrderedSamWriter(std::FILE* f) : f_(f) {
-		grow(1 << 16);
+	// `store`: the ring's strings, kept by the caller across runs, so the records' buffers
+	// are neither allocated again nor freed when the run ends (freeing a ring grown behind a
+	// lagging writer cost ~0.3 s at the end of a 10 M-read run)
+	OrderedSamWriter(std::FILE* f, std::vector<std::string>& store) : f_(f), store_(store) {
+		slot_.swap(store_);
+		size_t cap = 1 << 16;
+		while(cap < slot_.size()) cap *= 2;
+		if(slot_.size() != cap) slot_.resize(cap);
+		ready_.reset(new std::atomic<uint8_t>[cap]);
+		for(size_t i = 0; i < cap; i++) ready_[i].store(0, std::memory_order_relaxed);
+		cap_ = cap;
 		th_ = std::thread([this] { loop(); });
 	}
-	~OrderedSamWriter() { finish(); }
+	~OrderedSamWriter() {
+		finish();
+		for(std::string& r : slot_) r.clear();
+		store_.swap(slot_);
+	}
 	void reserve(uint64_t end) {                       // scheduler thread
 		if(end - base_.load(std::memory_order_acquire) <= cap_) return;
 		std::lock_guard<std::mutex> g(mu_);
@@ -1469,6 +1482,7 @@ private:
 		}
 	}
 	std::FILE* f_;
+	std::vector<std::string>& store_;
 	std::vector<std::string> slot_;
 	std::unique_ptr<std::atomic<uint8_t>[]> ready_;
 	size_t cap_ = 0;
@@ -1607,7 +1621,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	bool eof = false;
 	std::vector<FastqReader::Raw> raw;
 	std::vector<ReadCtx*> fresh;
-	OrderedSamWriter writer(out);
+	OrderedSamWriter writer(out, sam_ring_);
 	const auto put = [&writer](uint64_t id, std::string& rec) { writer.put(id, rec); };
 	if(slots < 2) slots = 2;
 	reserve_launch_buffers(pipeline_ ? slots / 2 : slots);

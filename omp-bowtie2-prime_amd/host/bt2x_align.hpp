@@ -1126,6 +1126,7 @@ private:
 	std::vector<std::unique_ptr<ReadCtx>> ctxs_;
 	std::vector<ReadCtx*> free_;
 	std::vector<std::vector<ReadCtx*>> retire_keep_, retire_fin_;   // retire()'s per-chunk lists
+	std::vector<std::string> sam_ring_;   // the SAM writer's ring of record buffers (kept across runs)
 	// host threads for the parallel loops over reads
 	std::unique_ptr<WorkPool> pool_;
 	WorkPool& pool();
