@@ -1,4 +1,4 @@
-"""Host-side DP problem framing: the arithmetic SwDriver::extendSeeds performs between a
+"""TEST HELPER (tests/ only; moved out of the product package in round 4). Host-side DP problem framing: the arithmetic SwDriver::extendSeeds performs between a
 resolved seed hit and SwAligner::initRef, vectorised with numpy.
 
   min score       Scoring scoreMin "L,-0.6,-0.6" (bt2_search.cpp:394, simple_func.h:90-112),
@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import abi
+from bt2x import abi
 
 _F32_C = float(np.float32(-0.6))
 _F32_L = float(np.float32(-0.6))

@@ -1,4 +1,4 @@
-"""Host-side seed instantiation: MultiSeedResults::instantiateSeeds / SeedAligner::
+"""TEST HELPER (tests/ only; moved out of the product package in round 4). Host-side seed instantiation: MultiSeedResults::instantiateSeeds / SeedAligner::
 prepareSeed + instantiateSeed (aligner_seed.cpp:321-447) and the per-read round offsets
 of bt2_search.cpp:2555-2578, producing the bt2x_seed_in batch the seed kernel consumes.
 
@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import abi
+from bt2x import abi
 
 SEED_LEN = 22
 N_ROUNDS = 2

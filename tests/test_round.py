@@ -87,7 +87,7 @@ def test_round_kernel_vs_reference_rank_golden(tmp_path):
     state after rankSeedHits equal the reference's."""
     import numpy as np
     from bt2x import abi, lib
-    from bt2x import seeds as bseeds
+    import seeds_ref as bseeds
     base = g.materialize_index("rep", str(tmp_path))
     case = g.SeedCase(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), os.path.join(g.GOLDEN, "seeds_rep.txt.xz"))
     reads = g.read_fastq(os.path.join(g.GOLDEN, "rep_reads.fq.xz"))

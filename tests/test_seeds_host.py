@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import golden_io as g
-from bt2x import seeds
+import seeds_ref as seeds
 
 
 @pytest.mark.parametrize("fq,gold", [("lambda_longreads.fq.xz", "seeds_lambda.txt.xz"),
