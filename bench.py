@@ -85,6 +85,11 @@ def parse(argv=None):
                     help="skip the configs C2 and C5 legs (rank 0 at N=1: E. coli 1M x 100 bp --no-sse8; 5M x 400 bp)")
     ap.add_argument("--c2-reads", type=int, default=1_000_000)
     ap.add_argument("--c5-reads", type=int, default=5_000_000)
+    ap.add_argument("--rep-leg", action="store_true",
+                    help="add a repeat-heavy sensitivity leg (rank 0, N=1): 50%% repeat families on a 200 Mbp "
+                         "synthetic genome, 1M x 150 bp reads, with the reference baseline and parity on 100k")
+    ap.add_argument("--rep-mb", type=float, default=200.0, help="the repeat-heavy leg's genome size")
+    ap.add_argument("--rep-reads", type=int, default=1_000_000, help="the repeat-heavy leg's timed reads")
     ap.add_argument("--cpu-index", action="store_true",
                     help="index the genome with the host builder (bt2x_build_index) instead of the GPU suffix sort")
     return ap.parse_args(argv)
@@ -604,6 +609,58 @@ def ref_baseline(args, binary, base, fqs, rdir, n, extra, tag):
                       f"{share}-CPU share, one run; alignment time = wall - wall of a 1-read run"}, sam
 
 
+def rep_leg(args, rdir):
+    """A repeat-heavy sensitivity leg: hg38 is ~50% repeats, the C3 stand-in 5%, so the walk
+    tail and the DP work per read are understated there.  200 Mbp, 8 chromosomes, 50% of
+    it copies of 8 repeat families (~2% divergence), 1M x 150 bp reads, --dpad 12."""
+    import simdata as sd
+    from bt2x import lib
+    mb = getattr(args, "rep_mb", 200.0)
+    chroms = sd.gen_genome(int(mb * 1e6), nchrom=8, seed=7, repeat_frac=0.5)
+    codes, starts = sd.concat_genome(chroms)
+    base = os.path.join(args.workdir, f"rep50_{mb:g}M")
+    if not all(os.path.exists(f"{base}.{k}.bt2l") for k in "1234"):
+        fa = base + ".fa"
+        sd.write_fasta(fa, chroms)
+        if getattr(args, "cpu_index", False):
+            lib.build_index(fa, base + ".tmp")
+        else:
+            import torch
+            import gpu_sa
+            sa, bwt, keys = gpu_sa.suffix_array(codes[codes < 4], device="cuda")
+            lib.build_index_sa(fa, base + ".tmp", sa, bwt=bwt, keys=keys)
+            del sa, bwt, keys
+            torch.cuda.empty_cache()
+        for k in "1234":
+            os.replace(f"{base}.tmp.{k}.bt2l", f"{base}.{k}.bt2l")
+        os.unlink(fa)
+    files = []
+    nr = getattr(args, "rep_reads", 1_000_000)
+    nw = max(1, nr // 10)
+    for k, (n, seed) in enumerate(((nw, 31), (nr, 37))):
+        path = os.path.join(rdir, f"rep50_{k}_{n}_R150.fq")
+        if not os.path.exists(path):
+            reads, quals = sd.sim_reads_fast(codes, starts, n, 150, seed)
+            sd.write_fastq_fixed(path + ".tmp", reads, quals, first_id=0 if k == 0 else nw)
+            os.replace(path + ".tmp", path)
+        files.append(path)
+    t, met, stats, out, peak = timed_align(args, base, files, 1, rdir, "rep50", ["--dpad", str(args.dpad)])
+    leg = {"workload": f"repeat-heavy sensitivity: {nr} x 150 bp SE reads vs a seeded {mb:g} Mbp synthetic genome with "
+                       "50% repeat families (C3's stand-in has 5%), --dpad 12, FASTQ -> SAM",
+           "value": round(met["nread"] / t / 1e6, 4), "unit": "M reads/s", "t_align_s": round(t, 3),
+           "reads": met["nread"], "aligned": met["nunp_uni"] + met["nunp_rep"], "repetitive": met["nunp_rep"],
+           "dps_per_read": round(float(stats.get("dps", 0)) / max(1, met["nread"]), 3), "stats": stats,
+           "peak_rss_mib": peak}
+    if not args.no_cpu and os.access(REF_ALIGN, os.X_OK):
+        cb, rsam = ref_baseline(args, REF_ALIGN, base, files[1:], rdir, min(nr, 100_000), ["--dpad", str(args.dpad)],
+                                "rep50")
+        leg["cpu_baseline"] = cb
+        leg["parity"] = parity(out, rsam, cb["sample_reads"])
+        leg["gpu_vs_cpu"] = round(leg["value"] / cb["value"], 2) if cb["value"] else None
+    os.unlink(out)
+    return leg
+
+
 def extra_legs(args, c3_base, rdir):
     """BASELINE.json's other single-GPU configs, beside the C3 headline (rank 0, N=1):
     C2 -- the E. coli stand-in (4.64 Mbp, simdata.ecoli_genome), 1M x 100 bp reads,
@@ -793,6 +850,8 @@ def main():
         os.unlink(out_sam)
     if rank == 0 and world == 1 and not args.no_legs:
         line["configs_other"] = extra_legs(args, base, rdir)
+    if rank == 0 and world == 1 and getattr(args, "rep_leg", False):
+        line.setdefault("configs_other", {})["C3_rep50"] = rep_leg(args, rdir)
     if dist:
         dist.barrier()
     if rank == 0:

@@ -106,3 +106,19 @@ def test_bench_one_rank_with_config_legs_on_cpu(tmp_path):
     if os.access(os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l"), os.X_OK):
         assert line["parity"]["records_differ"] == 0 and line["parity"]["sample_reads"] == 300
         assert legs["C2"]["parity"]["records_differ"] == 0 and legs["C5"]["parity"]["records_differ"] == 0
+
+
+def test_bench_repeat_leg_on_cpu(tmp_path):
+    """The optional repeat-heavy sensitivity leg (--rep-leg) at toy size through the host
+    driver over the CPU oracle: a rate, the DP work per read field (bt2x-align --stats), and (where the reference binary is
+    built) its baseline and 0 differing records."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", BT2X_BENCH_DIR=str(tmp_path / "work"))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--reads", "400",
+           "--genome-mb", "0.25", "--replay-reads", "200", "--slots", "512", "--host-threads", "2", "--no-replay",
+           "--cpu-index", "--aligner", ORACLE_DRIVER, "--no-legs", "--no-cpu", "--rep-leg", "--rep-mb", "0.3",
+           "--rep-reads", "1500"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    leg = line["configs_other"]["C3_rep50"]
+    assert leg["reads"] == 1500 and leg["value"] > 0 and leg["aligned"] > 1000 and "dps_per_read" in leg
