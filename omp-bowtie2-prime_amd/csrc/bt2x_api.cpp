@@ -529,7 +529,7 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	// (BT2X_DP_HEAVY=0: never); read per launch (tests switch it)
 	{
 		const char* hv = getenv("BT2X_DP_HEAVY");
-		a.heavy = hv ? (uint32_t)atol(hv) : 896u;
+		a.heavy = hv ? (uint32_t)atol(hv) : 800u;
 		if(a.heavy && !d_debug) {
 			if((rc = c->b_heavy.ensure(sizeof(uint32_t) * ((size_t)n + 1)))) return rc;
 			a.heavy_list = (uint32_t*)c->b_heavy.p;
