@@ -368,7 +368,7 @@ def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, pa
     i16: the share of BT2X_DP_I16 problems (all, or mixed into u8 launches; the 16-bit lane
     kernels, including minimum scores below -254).  heavy: BT2X_DP_HEAVY, the walk-step budget
     past which the lane kernel drops a problem for the wave kernel to redo (0: never; 1 and 2:
-    nearly every successful problem, mid-walk; default 896).  parwalk: BT2X_DP_PARWALK, the
+    nearly every successful problem, mid-walk; default 800).  parwalk: BT2X_DP_PARWALK, the
     wave kernel's nextAlignment sequence on all lanes (walk_wave_par; default: for the walks
     handed over, 2: the small-launch mode too, 0: lane 0 everywhere)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
