@@ -88,6 +88,8 @@ def parse(argv=None):
     ap.add_argument("--rep-leg", action="store_true",
                     help="add a repeat-heavy sensitivity leg (rank 0, N=1): 50%% repeat families on a 200 Mbp "
                          "synthetic genome, 1M x 150 bp reads, with the reference baseline and parity on 100k")
+    ap.add_argument("--align-extra", default=os.environ.get("BT2X_ALIGN_EXTRA", ""),
+                    help="extra bt2x-align options for the timed run and the replay recording (experiments)")
     ap.add_argument("--rep-mb", type=float, default=200.0, help="the repeat-heavy leg's genome size")
     ap.add_argument("--rep-reads", type=int, default=1_000_000, help="the repeat-heavy leg's timed reads")
     ap.add_argument("--cpu-index", action="store_true",
@@ -319,7 +321,7 @@ def replay(args, base, fq, rdir, gpu):
     # replayed launches have the shapes the end-to-end run launches
     run_aligner(args, [ALIGN, "-x", base, "-U", fq, "-S", os.devnull, "--dpad", str(args.dpad), "-p",
                        str(args.host_threads), "--slots", str(args.replay_slots or max(1, args.slots // 2)), "--dump", ddir,
-                       "--no-pipeline"],
+                       "--no-pipeline"] + getattr(args, "align_extra", "").replace(",", " ").split(),
                 os.path.join(rdir, "dump.err"), "launch recording")
     launches = load_dumps(ddir)
     shutil.rmtree(ddir, ignore_errors=True)
@@ -766,6 +768,12 @@ def main():
     del chroms, codes
     rdir = os.path.join(workdir, f"rank{rank}")
 
+    # the inputs and the index were just written: flush them to disk now, so the timed run
+    # does not share the box with the page cache's writeback of ~15 GB (first runs on a
+    # fresh box were up to ~20 % slower than later runs of the same files)
+    t_sync = time.perf_counter()
+    os.sync()
+    mark(f"inputs synced to disk in {time.perf_counter() - t_sync:.1f} s")
     # ---- timed: the aligner over the step files (warmup files first, untimed)
     # every rank writes its SAM to the node's disk when all of them fit (the same choice at
     # every N, so the per-GPU work does not change with N); else /dev/null everywhere
@@ -777,7 +785,7 @@ def main():
         out_sam = os.devnull
     cmd = [args.aligner, "-x", base, "-U", ",".join(warm + steps), "-S", out_sam, "--dpad", str(args.dpad),
            "--device", str(gpu), "-p", str(args.host_threads), "--slots", str(args.slots),
-           "--warmup-files", str(len(warm)), "--metrics", "--stats"]
+           "--warmup-files", str(len(warm)), "--metrics", "--stats"] + args.align_extra.replace(",", " ").split()
     if dist:
         dist.barrier()
     err, wall, peak = run_aligner(args, cmd, os.path.join(rdir, "align.err"), "timed run")
