@@ -126,6 +126,9 @@ int  bt2x_open(int hip_device, const bt2x_index_desc* idx, const bt2x_scoring* s
  * objects over one shared Ebwt, bt2_search.cpp:2297-2888).  base must outlive it. */
 int  bt2x_open_shared(const bt2x_ctx* base, bt2x_ctx** out);
 void bt2x_close(bt2x_ctx* ctx);
+/* NUMA node of the host socket the GPU hangs off (sysfs numa_node of its PCI device), or
+ * -1 if unknown: a host driver keeps its threads and memory there (bt2x-align does). */
+int  bt2x_device_numa_node(int hip_device);
 /* Last kernel's duration in ms (HIP events on the launching stream), by kernel id. */
 enum { BT2X_K_SEED = 0, BT2X_K_DP = 1, BT2X_K_RESOLVE = 2, BT2X_K_ROUND = 3, BT2X_K_COUNT = 4 };
 double bt2x_last_kernel_ms(const bt2x_ctx* ctx, int kernel);

@@ -25,6 +25,7 @@ FUNCS = {
     "bt2x_open": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(abi.IndexDesc),
                                  ctypes.POINTER(abi.Scoring), ctypes.POINTER(ctypes.c_void_p)]),
     "bt2x_open_shared": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "bt2x_device_numa_node": (ctypes.c_int, [ctypes.c_int]),
     "bt2x_close": (None, [ctypes.c_void_p]),
     "bt2x_last_kernel_ms": (ctypes.c_double, [ctypes.c_void_p, ctypes.c_int]),
     "bt2x_last_counters": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(abi.Counters)]),

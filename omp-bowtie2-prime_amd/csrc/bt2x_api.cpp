@@ -379,6 +379,19 @@ extern "C" int bt2x_open_shared(const bt2x_ctx* base, bt2x_ctx** out) {
 	return BT2X_OK;
 }
 
+extern "C" int bt2x_device_numa_node(int device) {
+	char bus[64] = {0};
+	if(hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, device) != hipSuccess) return -1;
+	for(char* p = bus; *p; p++) if(*p >= 'A' && *p <= 'F') *p = (char)(*p - 'A' + 'a');
+	const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+	FILE* f = std::fopen(path.c_str(), "r");
+	if(!f) return -1;
+	int node = -1;
+	if(std::fscanf(f, "%d", &node) != 1) node = -1;
+	std::fclose(f);
+	return node;
+}
+
 extern "C" void bt2x_close(bt2x_ctx* c) {
 	delete c;        // ~bt2x_ctx releases everything
 }
