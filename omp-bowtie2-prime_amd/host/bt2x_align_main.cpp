@@ -379,6 +379,9 @@ int main(int argc, char** argv) {
 			if(!null) throw std::runtime_error("cannot open /dev/null");
 			al.run(wr, null, slots, threads);
 			std::fclose(null);
+			// BT2X_GPU, like BT2X_TIMED, covers the timed files only
+			hip.gs = HipBackend::GpuStats{};
+			if(hip2) hip2->gs = HipBackend::GpuStats{};
 		}
 		// unnamed reads of the timed files are numbered after the warmup files' records, as in
 		// one run over the whole -U list
