@@ -150,12 +150,16 @@ typedef struct {
 } bt2x_counters;
 int bt2x_last_counters(const bt2x_ctx* ctx, int kernel, bt2x_counters* out);
 /* The last seed round's sampling work (bt2x_seed_round[_dev]): out[0] reads, out[1] reads
- * that sampled (RowSampler jobs), out[2] elements drawn, out[3] most elements one read drew;
- * how the sampling kernel drew them: out[4] 64-draw batches, out[5] draws committed by a
- * batch, out[6] draws taken one at a time, out[7] of out[5] from swap lists; out[8..11]
- * the kernel's clock in units of 1024 cycles summed over jobs: setup, batch draws, serial
- * draws, the rest. */
-int bt2x_last_round_stats(const bt2x_ctx* ctx, uint32_t out[12]);
+ * that sampled (RowSampler jobs), out[2] elements drawn, out[3] most elements one read drew.
+ * Writes exactly these 4 words (the abi-1 contract). */
+int bt2x_last_round_stats(const bt2x_ctx* ctx, uint32_t out[4]);
+/* The same words followed by how the sampling kernel drew them: out[4] 64-draw batches,
+ * out[5] draws committed by a batch, out[6] draws taken one at a time, out[7] of out[5] from
+ * swap lists; out[8..11] the kernel's clock in units of 1024 cycles summed over jobs
+ * (BT2X_ROUND_CLOCK builds; else 0): setup, batch draws, serial draws, the rest.  Writes
+ * min(n, BT2X_ROUND_STATS_N) words; returns that count (or a negative BT2X_E_*). */
+#define BT2X_ROUND_STATS_N 12
+int bt2x_last_round_stats_ex(const bt2x_ctx* ctx, uint32_t* out, uint32_t n);
 
 /* ------------------------------------------------------------ seed search */
 

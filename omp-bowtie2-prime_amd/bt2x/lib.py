@@ -65,6 +65,7 @@ FUNCS = {
     "bt2x_version": (ctypes.c_char_p, []),
     "bt2x_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
     "bt2x_last_round_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "bt2x_last_round_stats_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "bt2x_host_free": (None, [ctypes.c_void_p]),
     "bt2x_suffix_array": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
     "bt2x_build_index": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
@@ -290,9 +291,10 @@ class Context:
         return c.as_dict()
 
     def last_round_stats(self) -> dict:
-        """The last seed round's sampling work (bt2x_last_round_stats)."""
+        """The last seed round's sampling work (bt2x_last_round_stats_ex)."""
         o = (ctypes.c_uint32 * 12)()
-        check(load().bt2x_last_round_stats(self.h, o), "bt2x_last_round_stats")
+        rc = load().bt2x_last_round_stats_ex(self.h, o, 12)
+        check(min(rc, 0), "bt2x_last_round_stats_ex")
         return {"reads": o[0], "jobs": o[1], "samples": o[2], "max_samples": o[3], "batches": o[4],
                 "batch_draws": o[5], "serial_draws": o[6], "swap_draws": o[7], "kcyc_setup": o[8],
                 "kcyc_batch": o[9], "kcyc_serial": o[10], "kcyc_rest": o[11]}

@@ -127,7 +127,7 @@ extern "C" void bt2x_host_free(void* p) {
 	if(p) (void)hipHostFree(p);
 }
 
-extern "C" const char* bt2x_version(void) { return "bt2x 0.1 (gfx950; abi 1)"; }
+extern "C" const char* bt2x_version(void) { return "bt2x 0.2 (gfx950; abi 1.1)"; }
 
 // -------------------------------------------------------------------- context
 struct DevBuf {
@@ -305,6 +305,7 @@ extern "C" int bt2x_open(int device, const bt2x_index_desc* idx, const bt2x_scor
 	// full SA was built (the resolve kernel then walks LF to it, as GroupWalk does)
 	c->ix.offs = nullptr; c->ix.rstarts = nullptr; c->ix.plen = nullptr; c->ix.nfrag = idx->nfrag;
 	c->npat = idx->npat;
+	c->ix.npat = idx->npat;
 	if(idx->nfrag && idx->rstarts && idx->plen && idx->npat) {
 		HIPCHK(hipMalloc(&c->d_rstarts, 24 * idx->nfrag));
 		HIPCHK(hipMemcpy(c->d_rstarts, idx->rstarts, 24 * idx->nfrag, hipMemcpyHostToDevice));
@@ -449,17 +450,26 @@ extern "C" int bt2x_last_counters(const bt2x_ctx* c, int k, bt2x_counters* out) 
 	return BT2X_OK;
 }
 
-extern "C" int bt2x_last_round_stats(const bt2x_ctx* c, uint32_t out[12]) {
-	if(!c || !out) return BT2X_E_ARG;
-	for(int i = 0; i < 12; i++) out[i] = 0;
-	if(!c->b_rcnt.p) return BT2X_OK;
-	uint32_t cnt[16];
-	HIPCHK(hipSetDevice(c->device));
-	HIPCHK(hipStreamSynchronize(c->stream));
-	HIPCHK(hipMemcpy(cnt, c->b_rcnt.p, sizeof cnt, hipMemcpyDeviceToHost));
-	out[0] = c->n_round_last; out[1] = cnt[3]; out[2] = cnt[6]; out[3] = cnt[7];
-	for(int i = 0; i < 8; i++) out[4 + i] = cnt[8 + i];
-	return BT2X_OK;
+extern "C" int bt2x_last_round_stats_ex(const bt2x_ctx* c, uint32_t* out, uint32_t n) {
+	if(!c || (!out && n)) return BT2X_E_ARG;
+	uint32_t all[BT2X_ROUND_STATS_N] = {};
+	if(c->b_rcnt.p) {
+		uint32_t cnt[16];
+		HIPCHK(hipSetDevice(c->device));
+		HIPCHK(hipStreamSynchronize(c->stream));
+		HIPCHK(hipMemcpy(cnt, c->b_rcnt.p, sizeof cnt, hipMemcpyDeviceToHost));
+		all[0] = c->n_round_last; all[1] = cnt[3]; all[2] = cnt[6]; all[3] = cnt[7];
+		for(int i = 0; i < 8; i++) all[4 + i] = cnt[8 + i];
+	}
+	const uint32_t k = n < BT2X_ROUND_STATS_N ? n : BT2X_ROUND_STATS_N;
+	for(uint32_t i = 0; i < k; i++) out[i] = all[i];
+	return (int)k;
+}
+
+extern "C" int bt2x_last_round_stats(const bt2x_ctx* c, uint32_t out[4]) {
+	if(!out) return BT2X_E_ARG;
+	const int r = bt2x_last_round_stats_ex(c, out, 4);
+	return r < 0 ? r : BT2X_OK;
 }
 
 // ------------------------------------------------------------- seed search

@@ -30,7 +30,13 @@ struct DevIndex {
 	uint64_t nfrag;
 	const uint32_t* tfirst;   // text t's fragments are rstarts[tfirst[t] .. tfirst[t+1]) (npat+1
 	                          // entries; fragments are in joined = text order); or NULL
+	uint64_t npat;            // number of texts (tfirst has npat + 1 entries)
 };
+
+// Internal dp_in flag (never set by callers; bt2x.h uses bits 0-1): the window kernel
+// could not cut the problem's BT2X_DP_REF_TEXT window (no resident text, or a text id out
+// of range), so the DP kernels refuse it (status -1, counters[3]) instead of reading it.
+constexpr uint8_t kDpBadWindow = 0x80u;
 
 struct DevScoring {
 	int32_t rdo, rde, rfo, rfe;   // read/ref gap open (const+linear) and extend (linear)

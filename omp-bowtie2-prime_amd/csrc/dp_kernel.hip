@@ -759,6 +759,15 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 	for(uint32_t k = blockIdx.x; k < nwork; k += gridDim.x) {
 		const uint32_t pi = kMode == 1 ? a.fail_list[k] : kMode == 2 ? a.heavy_list[1 + k] : k;
 		const bt2x_dp_in p = a.in[pi];
+		if(kMode == 0 && (p.flags & kDpBadWindow)) {             // refused (window_kernel)
+			if(lane == 0) {
+				bt2x_dp_out o;
+				o.nrec = 0; o.rec_off = 0; o.status = -1; o.best = 0; o.ncand = 0;
+				a.out[pi] = o;
+				atomicAdd(&a.counters[3], 1u);
+			}
+			continue;
+		}
 		const int R = p.rdlen, C = p.ncol;
 		const bool i16 = (p.flags & BT2X_DP_I16) != 0;
 		const uint32_t top = i16 ? 0xffffu : 0xffu;
@@ -1054,8 +1063,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		else { p.read_off = p.qual_off = p.ref_off = 0; p.refl = 0; p.rdlen = 0; p.ncol = 0;
 		       p.minsc = 0; p.nceil = 0; p.triml = p.corel = p.corer = 0; p.fw = 1; p.flags = 0; }
 		const bool i16 = kWide && (p.flags & BT2X_DP_I16);
-		// an i16 problem in a u8 launch (bt2x_dp_align_dev without BT2X_DPL_I16): refused
-		const bool refused = !kWide && active && (p.flags & BT2X_DP_I16);
+		// an i16 problem in a u8 launch (bt2x_dp_align_dev without BT2X_DPL_I16), or one whose
+		// named window could not be cut (window_kernel): refused
+		const bool refused = active && ((!kWide && (p.flags & BT2X_DP_I16)) || (p.flags & kDpBadWindow));
 		const int R = p.rdlen, C = p.ncol;
 		const int top = i16 ? 0xffff : 0xff;            // score 0 (H of row -1)
 		// wave-uniform bounds in SGPRs: every per-step guard below is a scalar branch

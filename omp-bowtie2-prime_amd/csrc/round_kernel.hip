@@ -136,11 +136,18 @@ __device__ __forceinline__ double readlane_f64(double v, uint32_t k) {
 	return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-// The sampling kernel's workgroup is one wave, so its threads need no barrier: a wave's
-// LDS operations execute in issue order, and a compiler scheduling barrier keeps the
-// issue order.  (__syncthreads() would also fence the wave's global stores -- the outputs
-// it writes every batch -- and wait for them each time.)
-__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+// The sampling kernel's workgroup is one wave, so its threads need no workgroup barrier:
+// a wave's LDS operations execute in issue order.  The wave barrier alone only orders
+// instruction scheduling (LLVM marks it as touching no memory), so wavefront-scope
+// release/acquire fences around it tell the compiler that LDS written before it is read
+// after it (no reordering or forwarding of those accesses across it).  At wavefront scope
+// they emit no s_waitcnt on global stores, which __syncthreads() would (the outputs it
+// writes every batch would be waited for each time).
+__device__ __forceinline__ void wave_sync() {
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // BT2X_ROUND_CLOCK builds: per-phase clock64 sums in bt2x_last_round_stats out[8..11]
 #ifdef BT2X_ROUND_CLOCK
@@ -311,15 +318,23 @@ __device__ bool sample_wave(uint32_t nb, uint64_t nsamples, Rnd& rnd, SampleWs& 
 	// first draw: the list is the identity either way and its arena offset is never
 	// observed, and a laid-out list's first draw can join a batch.  Marked `converted`
 	// (r1n_next then takes the list as laid out; n = 1 keeps its draw-free first draw, so
-	// it stays lazy).  Only while half the arena suffices, so a job that fits the arena
-	// serially still fits.
+	// it stays lazy).  Only when the arena holds every list the job could ever build: the
+	// small ranges' lists plus, for each seen-list range (n >= 128) whose conversion
+	// threshold the job's draws can reach, its swap list of the n - thresh unseen elements
+	// (r1n_next).  Then neither the serial path nor this one can overflow, and a job that
+	// might overflow keeps the serial (lazy) layout exactly.
 	{
-		uint32_t tot = 0;
+		uint32_t tot = 0, need = 0;
 		for(uint32_t i = 0; i < nb; i++) {
 			const uint32_t n = (uint16_t)w.big[i].size;
 			if(n >= 2 && n < 128) tot += n;
+			else if(n >= 128) {
+				const uint16_t t = (uint16_t)(0.10f * (float)n);
+				const uint32_t thresh = t > 16 ? t : 16;
+				if(thresh <= nsamples) need += n - thresh;
+			}
 		}
-		if(tot && tot <= (uint32_t)kArena / 2) {
+		if(tot && tot + need <= (uint32_t)kArena) {
 			uint32_t base = 0;
 			for(uint32_t i = 0; i < nb; i++) {
 				const uint32_t n = (uint16_t)w.big[i].size;

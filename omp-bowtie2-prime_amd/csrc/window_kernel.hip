@@ -49,11 +49,18 @@ __global__ void __launch_bounds__(256) window_kernel(DevIndex ix, const bt2x_dp_
 	bt2x_dp_in p = in[i];
 	uint8_t* w = win + (size_t)i * BT2X_MAX_COLS;
 	const uint32_t ncol = p.ncol;
-	if(p.flags & BT2X_DP_REF_TEXT) {
+	const bool named = (p.flags & BT2X_DP_REF_TEXT) != 0;
+	if(named && (!ix.text || !ix.rstarts || p.ref_off >= ix.npat)) {
+		// a window the context cannot cut (a launch without BT2X_DPL_REF_TEXT on a context
+		// with no resident text, or a text id out of range): N columns, and the DP kernels
+		// refuse the problem
+		for(uint32_t c = lane; c < ncol; c += 64u) w[c] = 4;
+		p.flags |= kDpBadWindow;
+	} else if(named) {
 		const uint64_t t = p.ref_off;
 		const int64_t nfrag = (int64_t)ix.nfrag;
 		// text t's fragment range: from the per-text table (one load), else two searches
-		const bool tab = ix.tfirst && t < (uint64_t)0xffffffffu;
+		const bool tab = ix.tfirst != nullptr;             // t < npat (checked above)
 		const int64_t lo = tab ? (int64_t)ix.tfirst[t] : frag_text_lb(ix.rstarts, nfrag, t);
 		const int64_t hi = tab ? (int64_t)ix.tfirst[t + 1] : frag_text_lb(ix.rstarts, nfrag, t + 1);
 		// one search per problem (every lane the same addresses: broadcast loads), then each

@@ -226,22 +226,25 @@ private:
 // first-touch places their memory there): the box's CPU share is a quota over both sockets'
 // CPUs, and threads drifting across sockets reached the read contexts remotely -- runs of
 // the same input alternated between ~6.3 and ~8.5 us of CPU per read.  BT2X_NUMA=0 keeps
-// the inherited mask; BT2X_NUMA=<node+1> picks a node.
-void pin_to_gpu_node(int device) {
+// the inherited mask; BT2X_NUMA=<node+1> picks a node.  The mask narrows only when the node
+// holds at least as many allowed CPUs as the run's worker threads (-p): a cpuset split
+// across sockets, or ranks sharing one node, would otherwise be squeezed onto fewer CPUs
+// than threads.  Returns the decision for the BT2X_STATS line.
+std::string pin_to_gpu_node(int device, int threads) {
 	const char* e = std::getenv("BT2X_NUMA");
-	if(e && e[0] == '0') return;
+	if(e && e[0] == '0') return "off";
 	int node = e ? std::atoi(e) - 1 : bt2x_device_numa_node(device);
-	if(node < 0) return;
+	if(node < 0) return "nonode";
 	char path[96];
 	std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
 	std::FILE* f = std::fopen(path, "r");
-	if(!f) return;
+	if(!f) return "nonode";
 	char buf[4096] = {0};
 	const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
 	std::fclose(f);
 	buf[n] = 0;
 	cpu_set_t cur, want;
-	if(sched_getaffinity(0, sizeof cur, &cur) != 0) return;
+	if(sched_getaffinity(0, sizeof cur, &cur) != 0) return "noaffinity";
 	CPU_ZERO(&want);
 	for(char* p = buf; *p && *p != '\n';) {                 // "0-63,128-191"
 		char* q = nullptr;
@@ -251,7 +254,13 @@ void pin_to_gpu_node(int device) {
 		for(long c = a; c <= b && c < CPU_SETSIZE; c++) if(CPU_ISSET(c, &cur)) CPU_SET(c, &want);
 		p = (*q == ',') ? q + 1 : q;
 	}
-	if(CPU_COUNT(&want) >= 4) sched_setaffinity(0, sizeof want, &want);
+	const int have = CPU_COUNT(&want);
+	char note[64];
+	if(have >= 4 && have >= threads && sched_setaffinity(0, sizeof want, &want) == 0)
+		std::snprintf(note, sizeof note, "node%d:%d", node, have);
+	else
+		std::snprintf(note, sizeof note, "kept(node%d:%d<%d)", node, have, threads);
+	return note;
 }
 
 void usage() {
@@ -324,7 +333,7 @@ int main(int argc, char** argv) {
 		fq = mate1;
 	}
 	if(idx.empty() || fq.empty()) { usage(); return 1; }
-	pin_to_gpu_node(device);
+	const std::string numa = pin_to_gpu_node(device, threads);
 	const std::vector<std::string> files = split_list(fq);
 	if(warm_files < 0 || (size_t)warm_files >= files.size()) {
 		std::fprintf(stderr, "--warmup-files must leave at least one -U file to time\n");
@@ -429,7 +438,7 @@ int main(int argc, char** argv) {
 			std::fprintf(stderr, "BT2X_STATS reads=%llu t_align=%.4f seed_launches=%llu seeds=%llu t_seed=%.4f "
 			             "resolve_launches=%llu resolves=%llu t_resolve=%.4f dp_launches=%llu dps=%llu t_dp=%.4f "
 			             "t_host=%.4f t_io=%.4f dps_used=%llu tight_recs=%llu t_backend=%.4f t_step=%.4f t_wait=%.4f t_gather=%.4f t_retire=%.4f "
-			             "round_launches=%llu rounds=%llu t_round=%.4f dp_max_launch=%llu\n", (unsigned long long)st.reads, t_align,
+			             "round_launches=%llu rounds=%llu t_round=%.4f dp_max_launch=%llu numa=%s\n", (unsigned long long)st.reads, t_align,
 			             (unsigned long long)st.seed_launches, (unsigned long long)st.seeds, st.t_seed,
 			             (unsigned long long)st.resolve_launches, (unsigned long long)st.resolves, st.t_resolve,
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io, (unsigned long long)st.dps_used,

@@ -248,3 +248,46 @@ def test_shards_and_warmup_number_unnamed_reads_globally(tmp_path):
                        capture_output=True, timeout=600, check=True)
     assert int(bdist.parse_metrics(r.stderr.decode())["timed"]["first_rdid"]) == 250
     assert r.stdout == b"".join(ln + b"\n" for ln in whole.splitlines()[250:])
+
+
+ALIGN = os.path.join(ROOT, "omp-bowtie2-prime_amd", "bt2x", "bt2x-align")
+
+
+@pytest.mark.gpu
+def test_gpu_two_rank_sharded_alignment(tmp_path):
+    """Config C4's sharded product path on the MI355X: python -m bt2x.dist under
+    torch.distributed.run with two ranks, each running bt2x-align (libbt2x.so kernels) on its
+    shard of the stream; both ranks on device 0 (HIP_VISIBLE_DEVICES=0,0: rank_device gives
+    each rank '0'; the launcher and bt2x.dist itself never touch the GPU).  -1/-2 take the
+    mate-1 files as unpaired reads.  The concatenated SAM equals the reference's
+    e2e_rep records, the summary printed from the gloo-summed ReportingMetrics equals the
+    reference's (bt2_search.cpp:2867-2869's merge, across processes), and BT2X_DIST names 2
+    ranks."""
+    import json
+    import lzma
+    import golden_io as g
+    from test_e2e import sam_records, split_stderr
+    base = g.materialize_index("rep", str(tmp_path / "idx"))
+    m1, m2 = tmp_path / "rep_reads.fq", tmp_path / "m2.fq"
+    with lzma.open(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), "rb") as f:
+        m1.write_bytes(f.read())
+    m2.write_bytes(m1.read_bytes())
+    out = tmp_path / "dist.sam"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", HIP_VISIBLE_DEVICES="0,0",
+               PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "omp-bowtie2-prime_amd"), os.environ.get("PYTHONPATH", "")]))
+    env.pop("ROCR_VISIBLE_DEVICES", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "bt2x.dist", "--aligner", ALIGN, "--",
+           "-x", base, "-1", str(m1), "-2", str(m2), "--slots", "1000", "-p", "4", "-S", str(out)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    with lzma.open(os.path.join(g.GOLDEN, "e2e_rep.sam.xz"), "rb") as f:
+        exp = sam_records(f.read())
+    got = sam_records(out.read_bytes())
+    bad = sum(1 for a, b in zip(got, exp) if a != b)
+    assert len(got) == len(exp) and bad == 0, f"{bad} of {len(exp)} records differ ({len(got)} records)"
+    with open(os.path.join(g.GOLDEN, "e2e_summary.json")) as f:
+        ref = json.load(f)["sets"]["e2e_rep"]["summary"]
+    assert split_stderr(r.stderr)[1] == split_stderr(ref)[1]
+    assert "BT2X_DIST ranks=2 reads=3560" in r.stderr
+    assert not list(tmp_path.glob("dist.sam.part*"))
