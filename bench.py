@@ -85,9 +85,14 @@ def parse(argv=None):
                     help="skip the configs C2 and C5 legs (rank 0 at N=1: E. coli 1M x 100 bp --no-sse8; 5M x 400 bp)")
     ap.add_argument("--c2-reads", type=int, default=1_000_000)
     ap.add_argument("--c5-reads", type=int, default=5_000_000)
-    ap.add_argument("--rep-leg", action="store_true",
-                    help="add a repeat-heavy sensitivity leg (rank 0, N=1): 50%% repeat families on a 200 Mbp "
+    ap.add_argument("--runs", type=int, default=3,
+                    help="timed runs of bt2x-align over the same index and files; value = the median run")
+    ap.add_argument("--rep-leg", action="store_true", default=True,
+                    help="the repeat-heavy leg C3_rep50 (rank 0, N=1; default on): 50%% repeat families on a 200 Mbp "
                          "synthetic genome, 1M x 150 bp reads, with the reference baseline and parity on 100k")
+    ap.add_argument("--no-rep-leg", dest="rep_leg", action="store_false")
+    ap.add_argument("--leg-replay-reads", type=int, default=1 << 18,
+                    help="reads whose GPU launches are replayed for the C2 / C3_rep50 legs' DP rooflines")
     ap.add_argument("--align-extra", default=os.environ.get("BT2X_ALIGN_EXTRA", ""),
                     help="extra bt2x-align options for the timed run and the replay recording (experiments)")
     ap.add_argument("--rep-mb", type=float, default=200.0, help="the repeat-heavy leg's genome size")
@@ -122,6 +127,8 @@ def mark(msg):
 
 
 def workload_key(args) -> str:
+    if getattr(args, "leg_key", None):          # the C2 / C3_rep50 legs' replays
+        return f"{args.leg_key}|replay{args.replay_reads}|inflight{args.replay_slots or max(1, args.slots // 2)}"
     return (f"c3|synthetic{args.genome_mb:g}Mbp_s{args.genome_seed}|reads{args.reads}|R{args.read_len}|"
             f"dpad{args.dpad}|replay{args.replay_reads}|inflight{args.replay_slots or max(1, args.slots // 2)}")
 
@@ -308,18 +315,22 @@ def load_dumps(ddir):
     return out
 
 
-def replay(args, base, fq, rdir, gpu):
-    """Record the GPU launches bt2x-align makes for the reads of `fq` (whole file in flight),
-    replay them from HBM and time each launch with HIP events on the launch stream."""
+def replay(args, base, fq, rdir, gpu, n=None, opts=None):
+    """Record the GPU launches bt2x-align makes for the reads of `fq` (a cohort of the timed
+    run's size in flight), replay them from HBM and time each launch with HIP events on the
+    launch stream.  opts: the aligner options of the workload (default --dpad)."""
     import torch
     from bt2x import abi, lib
-    n = int(os.path.basename(fq).split("_")[1])
+    if n is None:
+        n = int(os.path.basename(fq).split("_")[1])
+    if opts is None:
+        opts = ["--dpad", str(args.dpad)]
     ddir = os.path.join(rdir, "dump")
     shutil.rmtree(ddir, ignore_errors=True)
     os.makedirs(ddir)
     # one cohort of the timed run's size in flight (--slots / 2, its pipeline's cohorts): the
     # replayed launches have the shapes the end-to-end run launches
-    run_aligner(args, [ALIGN, "-x", base, "-U", fq, "-S", os.devnull, "--dpad", str(args.dpad), "-p",
+    run_aligner(args, [ALIGN, "-x", base, "-U", fq, "-S", os.devnull] + opts + ["-p",
                        str(args.host_threads), "--slots", str(args.replay_slots or max(1, args.slots // 2)), "--dump", ddir,
                        "--no-pipeline"] + getattr(args, "align_extra", "").replace(",", " ").split(),
                 os.path.join(rdir, "dump.err"), "launch recording")
@@ -434,9 +445,9 @@ def replay(args, base, fq, rdir, gpu):
     return {"reads": n, "elapsed": elapsed, "kms": kms, "ctr": ctr, "nl": nl, "units": units}
 
 
-def roofline(args, rp):
-    """SURVEY §8(d)'s algorithmic bytes per launch of the dominant kernel / its average
-    launch time (HIP events), with the kernel's own bytes beside it."""
+def roofline(args, rp, kernel=None):
+    """SURVEY §8(d)'s algorithmic bytes per launch of the dominant kernel (or `kernel`) / its
+    average launch time (HIP events), with the kernel's own bytes beside it."""
     R = args.read_len
     cs, cr, cd = rp["ctr"]["seed"], rp["ctr"]["resolve"], rp["ctr"]["dp"]
     kms, nl = rp["kms"], rp["nl"]
@@ -446,7 +457,7 @@ def roofline(args, rp):
     res_bytes = cr.get("alg_bytes", 0)
     dp_bytes = 3 * cd.get("dp_cells", 0) + cd.get("dp_cols", 0) + rp["units"]["dp"] * 10 * ((R + 15) // 16) * 16
     kern = {"seed": (kms["seed"], fm_bytes), "resolve": (kms["resolve"], res_bytes), "dp": (kms["dp"], dp_bytes)}
-    dom = max(kern, key=lambda k: kern[k][0])
+    dom = kernel or max(kern, key=lambda k: kern[k][0])
     ms, alg = kern[dom]
     ach = alg / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     own = {"seed": cs.get("alg_bytes", 0), "resolve": cr.get("alg_bytes", 0), "dp": cd.get("alg_bytes", 0)}[dom]
@@ -611,7 +622,27 @@ def ref_baseline(args, binary, base, fqs, rdir, n, extra, tag):
                       f"{share}-CPU share, one run; alignment time = wall - wall of a 1-read run"}, sam
 
 
-def rep_leg(args, rdir):
+def leg_roofline(args, base, srcs, rdir, gpu, tag, opts, read_len, leg_key):
+    """The DP kernel's roofline on a leg's own workload: the GPU launches bt2x-align makes for
+    the first --leg-replay-reads reads of the leg's timed files, recorded with a cohort of
+    the timed run's size in flight and replayed from HBM (as the headline's `roofline`)."""
+    n = getattr(args, "leg_replay_reads", 0)
+    if n <= 0 or args.no_replay:
+        return None
+    fq = os.path.join(rdir, f"{tag}_replay.fq")
+    m = head_fastq(srcs, fq, n)
+    wargs = argparse.Namespace(**vars(args))
+    wargs.replay_reads, wargs.read_len, wargs.leg_key, wargs.replay_slots = m, read_len, leg_key, 0
+    rp = replay(wargs, base, fq, rdir, gpu, n=m, opts=opts)
+    os.unlink(fq)
+    roof, kern = roofline(wargs, rp, kernel="dp")
+    return {"roofline": roof,
+            "kernels": {k: kern[k] for k in ("seed_ms", "resolve_ms", "dp_ms", "dp_alg_bytes", "launches", "units",
+                                             "counters_dp", "replay_reads", "replay_steps", "replay_reads_per_s", "what")},
+            "workload_key": workload_key(wargs)}
+
+
+def rep_leg(args, rdir, gpu=0):
     """A repeat-heavy sensitivity leg: hg38 is ~50% repeats, the C3 stand-in 5%, so the walk
     tail and the DP work per read are understated there.  200 Mbp, 8 chromosomes, 50% of
     it copies of 8 repeat families (~2% divergence), 1M x 150 bp reads, --dpad 12."""
@@ -646,13 +677,17 @@ def rep_leg(args, rdir):
             sd.write_fastq_fixed(path + ".tmp", reads, quals, first_id=0 if k == 0 else nw)
             os.replace(path + ".tmp", path)
         files.append(path)
-    t, met, stats, out, peak = timed_align(args, base, files, 1, rdir, "rep50", ["--dpad", str(args.dpad)])
+    t, met, stats, out, peak = timed_align(args, base, files, 1, rdir, "rep50", ["--dpad", str(args.dpad), "--device", str(gpu)])
     leg = {"workload": f"repeat-heavy sensitivity: {nr} x 150 bp SE reads vs a seeded {mb:g} Mbp synthetic genome with "
                        "50% repeat families (C3's stand-in has 5%), --dpad 12, FASTQ -> SAM",
            "value": round(met["nread"] / t / 1e6, 4), "unit": "M reads/s", "t_align_s": round(t, 3),
            "reads": met["nread"], "aligned": met["nunp_uni"] + met["nunp_rep"], "repetitive": met["nunp_rep"],
            "dps_per_read": round(float(stats.get("dps", 0)) / max(1, met["nread"]), 3), "stats": stats,
            "peak_rss_mib": peak}
+    lr = leg_roofline(args, base, files[1:], rdir, gpu, "rep50", ["--dpad", str(args.dpad)], 150,
+                      f"c3rep50|synthetic{mb:g}Mbp_s7|R150|dpad{args.dpad}")
+    if lr:
+        leg.update(lr)
     if not args.no_cpu and os.access(REF_ALIGN, os.X_OK):
         cb, rsam = ref_baseline(args, REF_ALIGN, base, files[1:], rdir, min(nr, 100_000), ["--dpad", str(args.dpad)],
                                 "rep50")
@@ -663,7 +698,7 @@ def rep_leg(args, rdir):
     return leg
 
 
-def extra_legs(args, c3_base, rdir):
+def extra_legs(args, c3_base, rdir, gpu=0):
     """BASELINE.json's other single-GPU configs, beside the C3 headline (rank 0, N=1):
     C2 -- the E. coli stand-in (4.64 Mbp, simdata.ecoli_genome), 1M x 100 bp reads,
           --no-sse8: the i16 DP kernel end to end (the reference's -DENABLE_I16 build beside
@@ -689,11 +724,26 @@ def extra_legs(args, c3_base, rdir):
             sd.write_fastq_fixed(path + ".tmp", reads, quals, first_id=0 if k == 0 else args.c2_reads // 10)
             os.replace(path + ".tmp", path)
         files.append(path)
-    t, met, stats, out, peak = timed_align(args, base, files, 1, rdir, "c2", ["--no-sse8"])
+    t, met, stats, out, peak = timed_align(args, base, files, 1, rdir, "c2", ["--no-sse8", "--device", str(gpu)])
     leg = {"workload": f"C2 stand-in: {args.c2_reads} x 100 bp SE reads vs the seeded 4.64 Mbp E. coli stand-in, "
                        "--no-sse8 (the i16 DP kernel; the reference's -DENABLE_I16 build), FASTQ -> SAM",
            "value": round(met["nread"] / t / 1e6, 4), "unit": "M reads/s", "t_align_s": round(t, 3),
            "reads": met["nread"], "aligned": met["nunp_uni"] + met["nunp_rep"], "stats": stats, "peak_rss_mib": peak}
+    # the i16 fill's roofline: SURVEY 8(d)'s bytes count 3 B per cell for the reference's u8
+    # matrix; its i16 kernel keeps 16-bit E/F/H, 6 B per cell (roofline_i16)
+    lr = leg_roofline(args, base, files[1:], rdir, gpu, "c2", ["--no-sse8"], 100, "c2|ecoli4.64Mbp_s11|R100|nosse8")
+    if lr:
+        r = lr["roofline"]
+        cd = lr["kernels"]["counters_dp"]
+        b16 = 6 * cd.get("dp_cells", 0) + cd.get("dp_cols", 0) + lr["kernels"]["units"]["dp"] * 20 * ((100 + 15) // 16) * 16
+        L = max(r["launches_per_step"], 1)
+        ms = lr["kernels"]["dp_ms"]
+        lr["roofline_i16"] = {"bound": "hbm", "kernel": "dp", "alg_bytes": int(b16 / L),
+                              "achieved": round(b16 / (ms / 1e3) / 1e9, 2) if ms > 0 else 0.0, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(b16 / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if ms > 0 else 0.0,
+                              "what": "SURVEY 8(d) i16 bytes: 6*R*C (16-bit E/F/H) + C + 20*ceil(R/16)*16 (16-bit "
+                                      "query profile) per problem, over the same replayed launches as `roofline`"}
+        leg.update(lr)
     ref16 = os.path.join(ROOT, "oracle", "_ref", "bowtie2-align-l-i16")
     if not args.no_cpu and os.access(ref16, os.X_OK):
         cb, rsam = ref_baseline(args, ref16, base, files[1:], rdir, 200_000, ["--no-sse8"], "c2")
@@ -747,6 +797,32 @@ def host_threads(args, share: int, world: int) -> tuple[int, str]:
     return t, note
 
 
+def reap_children() -> list:
+    """Terminate and wait for every process this bench started that is still alive (none
+    should be: each aligner / reference run is waited for), so nothing outlives bench.py;
+    returns what was found."""
+    try:
+        import psutil
+    except ImportError:
+        return []
+    kids = psutil.Process().children(recursive=True)
+    found = []
+    for c in kids:
+        try:
+            found.append(f"{c.pid}:{c.name()}")
+            c.terminate()
+        except psutil.Error:
+            pass
+    _, alive = psutil.wait_procs(kids, timeout=5)
+    for c in alive:
+        try:
+            c.kill()
+        except psutil.Error:
+            pass
+    psutil.wait_procs(alive, timeout=5)
+    return found
+
+
 # ------------------------------------------------------------------------ main
 
 def main():
@@ -786,21 +862,42 @@ def main():
     cmd = [args.aligner, "-x", base, "-U", ",".join(warm + steps), "-S", out_sam, "--dpad", str(args.dpad),
            "--device", str(gpu), "-p", str(args.host_threads), "--slots", str(args.slots),
            "--warmup-files", str(len(warm)), "--metrics", "--stats"] + args.align_extra.replace(",", " ").split()
-    if dist:
-        dist.barrier()
-    err, wall, peak = run_aligner(args, cmd, os.path.join(rdir, "align.err"), "timed run")
-    if dist:
-        dist.barrier()
-    timed = kv_line(err, "BT2X_TIMED")
+    # args.runs timed runs over the same index and files (separate processes); value = the
+    # median run's (by the max over ranks of its timed wall time); every run is listed
+    runs = []
+    for k in range(max(1, args.runs)):
+        if dist:
+            dist.barrier()
+        err, wall, peak = run_aligner(args, cmd, os.path.join(rdir, f"align{k}.err"), f"timed run {k + 1}/{args.runs}")
+        if dist:
+            dist.barrier()
+        timed = kv_line(err, "BT2X_TIMED")
+        met = bdist.parse_metrics(err)["metrics"]
+        t_align = float(timed["t_align"])
+        if met["nread"] != args.reads:
+            raise SystemExit(f"timed run aligned {met['nread']} reads, expected {args.reads}")
+        tot = bdist.sum_counters(met, dist)
+        t_max = bdist.max_over_ranks(t_align, dist)
+        runs.append({"err": err, "wall": wall, "peak": peak, "timed": timed, "met": met, "tot": tot,
+                     "t_align": t_align, "t_max": t_max})
+    order = sorted(range(len(runs)), key=lambda k: runs[k]["t_max"])
+    med = runs[order[len(order) // 2]]
+    err, wall, peak, timed, met, tot, t_align, t_max = (med[k] for k in ("err", "wall", "peak", "timed", "met", "tot",
+                                                                         "t_align", "t_max"))
     stats = kv_line(err, "BT2X_STATS")
-    met = bdist.parse_metrics(err)["metrics"]
-    t_align = float(timed["t_align"])
-    if met["nread"] != args.reads:
-        raise SystemExit(f"timed run aligned {met['nread']} reads, expected {args.reads}")
-    tot = bdist.sum_counters(met, dist)
-    t_max = bdist.max_over_ranks(t_align, dist)
     value = tot["nread"] / t_max / 1e6
     t_files = [float(x) for x in str(timed.get("t_files", "")).split(",") if x]
+
+    def run_entry(r):
+        ru = kv_line(r["err"], "BT2X_RUSAGE_ALIGN")
+        e = {"value": round(r["tot"]["nread"] / r["t_max"] / 1e6, 4), "t_align_s": round(r["t_align"], 3),
+             "t_align_max_s": round(r["t_max"], 3), "peak_rss_mib": r["peak"]}
+        if ru and r["met"]["nread"]:
+            e["host_cpu_us_per_read"] = round((float(ru.get("user", 0)) + float(ru.get("sys", 0))) / r["met"]["nread"] * 1e6, 3)
+        g = kv_line(r["err"], "BT2X_GPU")
+        if g:
+            e["k_dp_s"], e["k_round_s"] = g.get("k_dp"), g.get("k_round")
+        return e
 
     line = {
         "metric": "M reads/s aligned (150 bp SE vs hg38) at 1/2/4/8 MI355X; % HBM-roofline",
@@ -816,7 +913,10 @@ def main():
                    "reads_per_gpu": args.reads, "read_len": args.read_len, "parallelism": f"dp{world} (read shards)",
                    "host_threads": args.host_threads, "host_threads_note": threads_note, "cpu_share": share,
                    "slots": args.slots, "key": workload_key(args)},
-        "end_to_end": {"t_align_s": round(t_align, 3), "t_align_max_s": round(t_max, 3),
+        "end_to_end": {"runs": [run_entry(r) for r in runs],
+                       "value_is": f"the median of {len(runs)} timed runs (separate bt2x-align processes, same index "
+                                   "and files); the fields below are that run's",
+                       "t_align_s": round(t_align, 3), "t_align_max_s": round(t_max, 3),
                        "t_run_s": timed.get("t_run"), "t_return_s": timed.get("t_ret"),
                        "step_done_s": [round(t, 3) for t in t_files], "wall_incl_index_load_s": round(wall, 2),
                        "peak_rss_mib": peak, "summary": bdist.alignment_summary(tot).splitlines(),
@@ -857,9 +957,10 @@ def main():
     if out_sam != os.devnull and os.path.exists(out_sam):
         os.unlink(out_sam)
     if rank == 0 and world == 1 and not args.no_legs:
-        line["configs_other"] = extra_legs(args, base, rdir)
+        line["configs_other"] = extra_legs(args, base, rdir, gpu)
     if rank == 0 and world == 1 and getattr(args, "rep_leg", False):
-        line.setdefault("configs_other", {})["C3_rep50"] = rep_leg(args, rdir)
+        line.setdefault("configs_other", {})["C3_rep50"] = rep_leg(args, rdir, gpu)
+    line["end_to_end"]["reaped_at_exit"] = reap_children()
     if dist:
         dist.barrier()
     if rank == 0:

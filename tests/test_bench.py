@@ -73,7 +73,7 @@ def test_bench_two_ranks_on_cpu(tmp_path):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--reads", str(reads), "--genome-mb", "0.25",
            "--replay-reads", "200", "--slots", "512", "--host-threads", "2", "--no-replay", "--no-cpu",
-           "--cpu-index", "--aligner", ORACLE_DRIVER]
+           "--cpu-index", "--aligner", ORACLE_DRIVER, "--runs", "2"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -85,6 +85,10 @@ def test_bench_two_ranks_on_cpu(tmp_path):
     assert abs(line["value"] - 2 * reads / e["t_align_max_s"] / 1e6) < 1e-3
     assert e["t_align_max_s"] >= e["t_align_s"] > 0
     assert line["config"]["host_threads"] == 2
+    # two timed runs, each over both ranks; value is the median (here: the slower) run's
+    assert len(e["runs"]) == 2 and all(x["value"] > 0 for x in e["runs"])
+    assert any(abs(x["t_align_max_s"] - e["t_align_max_s"]) < 1e-3 for x in e["runs"])
+    assert e["reaped_at_exit"] == []
 
 
 def test_bench_one_rank_with_config_legs_on_cpu(tmp_path):
@@ -96,7 +100,7 @@ def test_bench_one_rank_with_config_legs_on_cpu(tmp_path):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--reads", "600",
            "--genome-mb", "0.25", "--replay-reads", "200", "--slots", "512", "--host-threads", "2", "--no-replay",
            "--cpu-index", "--aligner", ORACLE_DRIVER, "--c2-reads", "1500", "--c5-reads", "1000",
-           "--cpu-sample", "300", "--cpu-sample-1t", "100"]
+           "--cpu-sample", "300", "--cpu-sample-1t", "100", "--no-rep-leg", "--runs", "1"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=1200)
     assert r.returncode == 0, r.stderr[-4000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
