@@ -260,18 +260,32 @@ __device__ __forceinline__ uint32_t publish_edbuf(const DpLaunch& a, const uint3
 	return eo;
 }
 
-// SwAligner::nextAlignment until done() for problem pi (lane gl of the group whose fill
-// output starts at gslot): its candidates in order, each not already reportedThrough
-// backtraced over the fill's traceback bytes; records and edits staged per lane.
+// Byte address of cell (row, col) in a traceback layout of G problems per group and PW
+// dwords per column pair (tb_addr is G = 64, PW = kPairWords): problem slot tbl.
+template<int G, int PW>
+__device__ __forceinline__ size_t tb_addr_g(int row, int col, int tbl) {
+	const int st = row + (col & 1);
+	return ((((size_t)(col >> 1) * PW + (st >> 1)) * G + tbl) << 2) + ((st & 1) << 1) + (col & 1);
+}
+
+// SwAligner::nextAlignment until done() for problem pi: its candidates in order (cands,
+// [k * 64 + lane]), each not already reportedThrough backtraced over the fill's traceback
+// bytes (layout tb_addr_g<G, PW>, problem slot tbl, from dirbase); records and edits
+// staged per lane.
+template<int G, int PW>
 __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t* mmpen, const DpLaunch& a, uint32_t pi,
-                                             int lane, uint8_t* gslot, uint32_t* stage_ed,
+                                             int lane, int tbl, const uint8_t* dirbase, uint32_t dirbytes,
+                                             const uint8_t* cands, uint32_t* stage_ed,
                                              bt2x_aln_rec* stage_rec, unsigned long long& st_bt, bool refN,
                                              unsigned long long* pw = nullptr) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 	const uint32_t gl = (uint32_t)lane;
+	// the layout's move offsets (see kDiag1Even): one step pair up is -4G bytes
+	constexpr int kD1E = -(PW * 4 * G) + 1;        // (r, 2p) -> (r-1, 2p-1)
+	constexpr int kD1O = -(4 * G + 1);             // (r, 2p+1) -> (r-1, 2p)
+	constexpr int kD2 = kD1O + kD1E;               // two diagonal moves
 	const __amdgpu_buffer_rsrc_t dirsrc =
-		__builtin_amdgcn_make_buffer_rsrc(gslot + kDirOff, 0, (int)(kDirBytesLane * 64u), 0x00020000);
-	const uint8_t* cands = gslot + kCandOff;
+		__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(dirbase), 0, (int)dirbytes, 0x00020000);
 	bt2x_dp_out o = a.out[pi];
 	if(o.status > 0 && o.ncand > 0 && a.ablate != 1) {
 		const bt2x_dp_in p = a.in[pi];
@@ -302,13 +316,13 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 #define BT2X_RING_LOAD(A0, A1, A2, A3, A4, A5, A6, A7, BO, COL)                                          \
 		{                                                                                         \
 			const uint32_t bo_ = (BO);                                                            \
-			const int d1_ = ((COL) & 1) ? -257 : kDiag1Even;                                      \
+			const int d1_ = ((COL) & 1) ? kD1O : kD1E;                                      \
 			A0 = tb_load(dirsrc, bo_);                      A1 = tb_load(dirsrc, bo_ + d1_);      \
-			A2 = tb_load(dirsrc, bo_ + kDiag2);             A3 = tb_load(dirsrc, bo_ + kDiag2 + d1_); \
-			A4 = tb_load(dirsrc, bo_ + 2 * kDiag2);         A5 = tb_load(dirsrc, bo_ + 2 * kDiag2 + d1_); \
-			A6 = tb_load(dirsrc, bo_ + 3 * kDiag2);         A7 = tb_load(dirsrc, bo_ + 3 * kDiag2 + d1_); \
+			A2 = tb_load(dirsrc, bo_ + kD2);             A3 = tb_load(dirsrc, bo_ + kD2 + d1_); \
+			A4 = tb_load(dirsrc, bo_ + 2 * kD2);         A5 = tb_load(dirsrc, bo_ + 2 * kD2 + d1_); \
+			A6 = tb_load(dirsrc, bo_ + 3 * kD2);         A7 = tb_load(dirsrc, bo_ + 3 * kD2 + d1_); \
 		}
-		BT2X_RING_LOAD(n0, n1, n2, n3, n4, n5, n6, n7, (uint32_t)tb_addr(row0, c_next, gl), c_next)
+		BT2X_RING_LOAD(n0, n1, n2, n3, n4, n5, n6, n7, ((uint32_t)tb_addr_g<G, PW>(row0, c_next, tbl)), c_next)
 		int c_next2 = ncand > 1 ? cands[64 + gl] : 0;
 		uint32_t cmask = 0;                                    // last attempt's marks on the next ring
 		// stage_ed doubles as the reference's per-read edit buffer (SwResult::alres.ned_,
@@ -331,7 +345,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 				if(ndone < ncand) {
 					c_next = c_next2;
 					dnx = c_next - row0;
-					BT2X_RING_LOAD(n0, n1, n2, n3, n4, n5, n6, n7, (uint32_t)tb_addr(row0, c_next, gl), c_next)
+					BT2X_RING_LOAD(n0, n1, n2, n3, n4, n5, n6, n7, ((uint32_t)tb_addr_g<G, PW>(row0, c_next, tbl)), c_next)
 					if(ndone + 1 < ncand) c_next2 = cands[(size_t)(ndone + 1) * 64 + gl];
 				}
 				cmask = 0;
@@ -353,12 +367,12 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 				// attempt never revisits its own cells and earlier attempts' marks were stored
 				// before these loads (or are patched in from cmask), so a ring byte is the byte
 				// the reference reads.
-				uint32_t bo = (uint32_t)tb_addr(row, col, gl);
+				uint32_t bo = (uint32_t)tb_addr_g<G, PW>(row, col, tbl);
 				bool fin = false;
 #define BT2X_WALK_STEP(T0, T1, T2, T3, T4, T5, T6, T7)                                                        \
 				{                                                                                     \
 					const uint32_t ctb = T0;                                                          \
-					uint32_t nbo = bo + 4 * kDiag2;  /* the next ring load; finished lanes: harmless */ \
+					uint32_t nbo = bo + 4 * kD2;  /* the next ring load; finished lanes: harmless */ \
 					if(fin) {}                                                                        \
 					else if(++steps > budget) { ok = false; fin = true; aborted = true; }             \
 					else if(st_bt++, ctb & TB_MARK) { ok = false; fin = true; }  /* reportedThrough */ \
@@ -381,9 +395,9 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 							const int nct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);          \
 							/* byte-offset deltas of the moves (tb_addr's pair/step layout) */        \
 							const int st = row + (col & 1);                                           \
-							const int dU = (st & 1) ? -2 : -254;                                      \
-							const int dL = (col & 1) ? ((row & 1) ? -255 : -3)                        \
-							                         : ((row & 1) ? kDiag1Even + 254 : kDiag1Even + 2); \
+							const int dU = (st & 1) ? -2 : -(4 * G - 2);                              \
+							const int dL = (col & 1) ? ((row & 1) ? -(4 * G - 1) : -3)                \
+							                         : ((row & 1) ? kD1E + 4 * G - 2 : kD1E + 2);     \
 							const uint32_t cbo = bo;                                                  \
 							const int crow = row, ccol = col;                                         \
 							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;                \
@@ -402,14 +416,14 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 								gaps++;                                                               \
 							}                                                                         \
 							if(isD) {                                                                 \
-								bo = cbo + ((ccol & 1) ? -257 : kDiag1Even);                          \
+								bo = cbo + ((ccol & 1) ? kD1O : kD1E);                          \
 							} else {                                                                  \
 								bo = cbo + (isF ? dU : dL);                                           \
-								const int d1 = (col & 1) ? -257 : kDiag1Even;                         \
+								const int d1 = (col & 1) ? kD1O : kD1E;                         \
 								T1 = tb_load(dirsrc, bo);                  T2 = tb_load(dirsrc, bo + d1); \
-								T3 = tb_load(dirsrc, bo + kDiag2);         T4 = tb_load(dirsrc, bo + kDiag2 + d1); \
-								T5 = tb_load(dirsrc, bo + 2 * kDiag2);     T6 = tb_load(dirsrc, bo + 2 * kDiag2 + d1); \
-								T7 = tb_load(dirsrc, bo + 3 * kDiag2);     nbo = bo + 3 * kDiag2 + d1;    \
+								T3 = tb_load(dirsrc, bo + kD2);         T4 = tb_load(dirsrc, bo + kD2 + d1); \
+								T5 = tb_load(dirsrc, bo + 2 * kD2);     T6 = tb_load(dirsrc, bo + 2 * kD2 + d1); \
+								T7 = tb_load(dirsrc, bo + 3 * kD2);     nbo = bo + 3 * kD2 + d1;    \
 							}                                                                         \
 							__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)cbo, 0, 0); /* setReportedThrough */ \
 						}                                                                             \
@@ -1446,8 +1460,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			uint8_t* wslot = gslot + kGroupBytes;
 			const unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 			const unsigned long long bt0 = st_bt;
-			walk_problem(sc, pen_lds, a, pi, lane, gslot, reinterpret_cast<uint32_t*>(wslot + kEditOff),
-			             reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, a.prof ? pw : nullptr);
+			walk_problem<64, kPairWords>(sc, pen_lds, a, pi, lane, lane, gslot + kDirOff, kDirBytesLane * 64u, gslot + kCandOff,
+			                             reinterpret_cast<uint32_t*>(wslot + kEditOff), reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff),
+			                             st_bt, refN != 0, a.prof ? pw : nullptr);
 			if(a.prof) {
 				const unsigned long long t2 = __builtin_amdgcn_s_memtime();
 				t_fill += t1 - t0; t_walk += t2 - t1; ngrp++;
@@ -1488,6 +1503,384 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 	}
 }
 
+// ------------------------------------------------------------- duo fill (two lanes per problem)
+// At cohort launch sizes a launch holds about one 64-problem group per SIMD, so the lane
+// kernel's launch lasts one lane's dependent chain: ~the band's rows (~94 at 150 bp,
+// --dpad 12) of steps per column pair.  Here each problem has two lanes (even lane A, odd
+// lane B; 32 problems per wave) that split the band along a diagonal, so a wave sweeps
+// about half the steps per column pair and a launch has twice the waves (two per SIMD,
+// whose VALU streams interleave).
+//  * Column pair p's band rows [s0, e] (s0 = max(2p - wdh, 0)) split at b = s0 + K: A
+//    computes rows [s0, b] of pair p (its step b: the high half, row b-1 of column 2p+1,
+//    is exact; the low half is not, and B overwrites that byte), B rows [b, e] one
+//    iteration later (iteration i: A pair i, B pair i-1).  K (a multiple of 4, ~half the
+//    band) is B's slot offset: B keeps row r in register / LDS slot r - K, so both lanes'
+//    windows are the same ~K slots and the wave's step code (fully unrolled by slot, as in
+//    dp_fill_kernel) serves both.
+//  * The split moves down 2 rows per pair, so the halves depend on each other every pair:
+//    T1 (A -> B): B's first step needs the step before it, A's outputs (packed H, F, E and
+//      hl) at slot (s0 & ~3) + K - 1, the last step of a block; B starts at the block-aligned
+//      slot, recomputing up to 2 of A's rows exactly from them.
+//    T2 (B -> A): A's rows b, b+1 of the next pair need their left neighbours (H, E of
+//      column 2p+1) from B, computed at B's second and third steps: B's state dword after
+//      them goes to A (DPP), which splices it in before it reads them.
+//    Both are wave-uniform events at blocks known per iteration (one scalar test per
+//    block).  A's garbage cells below b (and its garbage low half at b) are overwritten by
+//    B's later stores of the same bytes; B's stores of rows it recomputes are exact; cells
+//    outside the band obey dp_fill_kernel's rule (computed values <= true values).
+//  * Traceback: tb_addr_g<32, kDuoPW> with one spare pair in front (B's pair -1 in the
+//    first iteration) and kDuoPW >= (161 + K) / 2 dword rows per pair (B's slots past its
+//    window write rows below the matrix, never above another pair).
+//  * Last rows, candidates and the walk run on the A lanes (walk_problem<32, kDuoPW>);
+//    the owner of row R-1 of each pair (A if R-1 < b, else B) supplies its last-row bytes.
+constexpr int kDuoG = 32;                                   // problems per wave
+constexpr int kDuoKMax = 80;                                // largest slot offset of B
+constexpr int kDuoPW = (kSteps + kDuoKMax + 1) / 2;       // dword rows per column pair
+constexpr int kDuoPairs = kCols / 2 + 2;                    // pairs -1 .. kCols / 2
+constexpr uint32_t kDuoPairBytes = (uint32_t)kDuoPW * kDuoG * 4;
+constexpr uint32_t kDuoDirBytes = (uint32_t)kDuoPairs * kDuoPairBytes;
+constexpr size_t kDuoLastRowOff = kDuoDirBytes;                        // [col * 64 + lane]
+constexpr size_t kDuoCandOff = kDuoLastRowOff + (size_t)kCols * 64;    // [k * 64 + lane]
+constexpr size_t kDuoGroupBytes = kDuoCandOff + (size_t)kCandBytesLane * 64;
+static_assert(kDuoGroupBytes <= kGroupBytes, "the duo layout fits a fused slot");
+
+// quad_perm DPP within lane pairs: odd lane l gets lane l-1's value, even lane l gets l+1's
+__device__ __forceinline__ uint32_t from_even(uint32_t v) {
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t from_odd(uint32_t v) {
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xf, 0xf, false);
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
+	__shared__ uint32_t lds[(kCols / 4) * 64];        // row info during the fill, then candidate keys
+	__shared__ uint32_t pen4[64];
+	const uint8_t* pen_lds = reinterpret_cast<const uint8_t*>(pen4);
+	const int lane = threadIdx.x;
+	const bool isB = (lane & 1) != 0;
+	const int q = lane >> 1;                           // problem slot in the group
+	pen4[lane] = reinterpret_cast<const uint32_t*>(a.mmpen)[lane];
+	__syncthreads();
+	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0, st_comp = 0;
+	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
+	const uint32_t one2 = opaque(0x00010001u);
+	for(uint32_t grp = blockIdx.x; (uint64_t)grp * kDuoG < nprob; grp += gridDim.x) {
+		uint8_t* gslot = a.scratch + (size_t)blockIdx.x * (kGroupBytes + kWalkSlotBytes);
+		uint8_t* lastrow = gslot + kDuoLastRowOff;
+		uint8_t* cands = gslot + kDuoCandOff;
+		const uint32_t pi = grp * kDuoG + (uint32_t)q;
+		const bool active = pi < nprob;
+		bt2x_dp_in p;
+		if(active) p = a.in[pi];
+		else { p.read_off = p.qual_off = p.ref_off = 0; p.refl = 0; p.rdlen = 0; p.ncol = 0;
+		       p.minsc = 0; p.nceil = 0; p.triml = p.corel = p.corer = 0; p.fw = 1; p.flags = 0; }
+		const bool refused = active && ((p.flags & BT2X_DP_I16) || (p.flags & kDpBadWindow));
+		const int R = p.rdlen, C = p.ncol;
+		constexpr int top = 0xff;
+		const int Rmax = __builtin_amdgcn_readfirstlane(wave_max(R));
+		const int Cmax = __builtin_amdgcn_readfirstlane(wave_max(C));
+		const uint8_t* rd = a.reads + p.read_off;
+		const uint8_t* qu = a.quals + p.qual_off;
+		const uint8_t* rf = a.refs + p.ref_off;
+		const int thr = (int)p.minsc + top;
+		// the exact band (dp_fill_kernel): pair j0's rows [j0 - wdhi, j0 + wdlo]
+		int wdhi, wdlo;
+		{
+			const int mo = imax(1, rdo < rfo ? rdo : rfo);
+			int me = rde < rfe ? rde : rfe;
+			me = me < mo ? me : mo;
+			const int budget = -(int)p.minsc;
+			int G = (me <= 0) ? (1 << 16) : (budget < mo ? 0 : 1 + (budget - mo) / me);
+			G = G > (1 << 16) ? (1 << 16) : G;
+			constexpr int kBandMargin = 2;
+			const int dh = active ? (C - R) + G + kBandMargin : -(1 << 20);
+			const int dl = active ? G + kBandMargin + 2 : -(1 << 20);
+			wdhi = __builtin_amdgcn_readfirstlane(wave_max(dh));
+			wdlo = __builtin_amdgcn_readfirstlane(wave_max(dl));
+			wdhi = wdhi > 4 * kRows ? 4 * kRows : wdhi;
+			wdlo = wdlo > 4 * kRows ? 4 * kRows : wdlo;
+		}
+		const int wdh = wdhi + (wdhi & 1);             // even: every window start 2p - wdh is even
+		int K = ((wdh + wdlo - 2) / 2 + 2) & ~3;       // balances A's K + 1 rows and B's
+		K = K < 8 ? 8 : (K > kDuoKMax ? kDuoKMax : K);
+		K = __builtin_amdgcn_readfirstlane(K);
+		const int rowoff = isB ? K : 0;                // this lane's slot s holds row s + rowoff
+		// ------------- row info per slot (rows >= R: N, barred), as dp_fill_kernel
+		const uint32_t kNone = row_info(7, true, npen);
+		auto rinfo = [&](int i, uint32_t rb, uint32_t qb) -> uint32_t {
+			if(i >= R) return kNone;
+			int qq = (int)qb - 33;
+			qq = qq < 0 ? 0 : qq;
+			const bool gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
+			return rb > 3 ? row_info(7, gbar, npen) : row_info((int)rb, gbar, pen_lds[qq]);
+		};
+		const ByteStr rds = byte_str(rd, R > 0 ? R : 1), qus = byte_str(qu, R > 0 ? R : 1);
+		const int w4off = rowoff >> 2;
+#pragma unroll
+		for(int c16 = 0; c16 < kRows / 16; c16++) {
+			if(c16 * 16 < Rmax) {                                     // wave-uniform
+				uint32_t rw[4], qw[4];
+#pragma unroll
+				for(int k = 0; k < 4; k++) {
+					rw[k] = bs_bytes4(rds, 4 * c16 + k + w4off); qw[k] = bs_bytes4(qus, 4 * c16 + k + w4off);
+				}
+#pragma unroll
+				for(int k = 0; k < 4; k++) {
+					uint32_t w = 0;
+#pragma unroll
+					for(int r = 0; r < 4; r++) {
+						const int i = 16 * c16 + 4 * k + r + rowoff;
+						w |= rinfo(i, (rw[k] >> (8 * r)) & 0xffu, (qw[k] >> (8 * r)) & 0xffu) << (8 * r);
+					}
+					lds[(4 * c16 + k) * 64 + lane] = w;
+				}
+			} else {
+#pragma unroll
+				for(int k = 0; k < 4; k++) lds[(4 * c16 + k) * 64 + lane] = kNone * 0x01010101u;
+			}
+		}
+		// B's first step at slot 0 (early pairs) computes row K-1 of the high column: its info
+		const uint32_t info_m1 = (isB && K - 1 < R) ? rinfo(K - 1, rd[K - 1], qu[K - 1]) : 0u;
+		// ------------- fill
+		uint32_t Hs[kRowWords], Es[kRowWords];
+#pragma unroll
+		for(int b = 0; b < kRowWords; b++) { Hs[b] = 0; Es[b] = 0; }
+		int lrmax = 0, ncand = 0;
+		const int rl0 = active ? R - rowoff : (1 << 20);            // slot of row R (row R-1 at rl - 1)
+		const int Rmin = __builtin_amdgcn_readfirstlane(-wave_max(-rl0));
+		const uint32_t rdo2 = (uint32_t)rdo * 0x10001u, rde2 = (uint32_t)rde * 0x10001u;
+		const uint32_t rfo2 = (uint32_t)rfo * 0x10001u, rfe2 = (uint32_t)rfe * 0x10001u;
+		const uint32_t npen2 = (uint32_t)npen * 0x10001u;
+		const int npairs = (Cmax + 1) >> 1;
+		const __amdgpu_buffer_rsrc_t dirsrc = __builtin_amdgcn_make_buffer_rsrc(gslot, 0, (int)kDuoDirBytes, 0x00020000);
+		// pair p is stored at (p + 1) pair strides; the per-step scalar offset carries pair
+		// pp - 1 (B's) and the step's dword row, the lane offset A's extra pair or B's K / 2 rows
+		const uint32_t voff = (uint32_t)q * 4u + (isB ? (uint32_t)(K / 2) * (kDuoG * 4u) : kDuoPairBytes);
+		const uint32_t* rfw = reinterpret_cast<const uint32_t*>(rf);
+		const int lastw = ((C > 0 ? C : 1) - 1) >> 2;
+		uint32_t cw0 = 0, cw1 = 0, cw2 = 0, cw3 = 0;
+		uint32_t refN = 0;
+		uint32_t t1h = 0, t1f = 0, t1e = 0, t1hl = 0;                 // T1 (B lanes after the DPP)
+		uint32_t t2h = 0, t2e = 0;                                     // T2 (A lanes)
+		for(int pp = 0; pp <= npairs; pp++) {
+			const int pl = pp - (isB ? 1 : 0);                        // this lane's pair
+			const int j0 = 2 * pl;
+			// wave-uniform windows: A's pair pp rows [s0A, s0A + K], B's pair pp-1 slots [s0B, endB]
+			const bool hasA = pp < npairs, hasB = pp > 0;
+			const int s0A = imax(2 * pp - wdh, 0), s0B = imax(2 * pp - 2 - wdh, 0);
+			const int endA = hasA ? min(s0A + K, Rmax) : -1;
+			const int endB = hasB ? min(2 * pp - 2 + wdlo, Rmax) - K : -1;
+			int slo = (hasB ? s0B : s0A) & ~3;
+			int shi = imax(endA, endB) | 3;
+			shi = shi > kSteps - 1 ? kSteps - 1 : shi;
+			const int kT1 = hasA ? ((s0A & ~3) + K) / 4 - 1 : -1;     // A's step before B's next start
+			const int kT2 = hasB ? (s0B + 2) >> 2 : -1;                 // B's rows b, b+1 done
+			const int kP = hasB ? ((s0B + K) >> 2) - 1 : -1;            // patch A's rows b, b+1 after it
+			uint64_t ev = 0;
+			if(kT1 >= 0 && kT1 < 64) ev |= 1ull << kT1;
+			if(kT2 >= 0 && kT2 < 64) ev |= 1ull << kT2;
+			if(kP >= 0 && kP < 64) ev |= 1ull << kP;
+			const uint32_t t2sel = (s0B & 2) ? 0xffff0000u : 0x0000ffffu;   // the patched half
+			if(active && hasA && !isB) st_comp += 2u * (unsigned)imax(0, endA - s0A);
+			if(active && hasB && isB) st_comp += 2u * (unsigned)imax(0, endB - s0B + 1);
+			int rmin = Rmin, rl = rl0;
+			// opaque per pair (dp_fill_kernel): keeps the per-step guards and last-row compares from
+			// being hoisted out of the pair loop as precomputed lane masks (SGPR spills)
+			asm volatile("" : "+s"(rmin), "+s"(slo), "+s"(shi), "+s"(ev), "+v"(rl));
+			asm volatile("" ::: "memory");
+			// this lane's reference columns: 16 per load at every eighth pair of its own
+			if((pl & 7) == 0) {
+				const int w0 = pl >> 1;
+				cw0 = rfw[min(w0, lastw)]; cw1 = rfw[min(w0 + 1, lastw)];
+				cw2 = rfw[min(w0 + 2, lastw)]; cw3 = rfw[min(w0 + 3, lastw)];
+				asm volatile("" : "+v"(cw0), "+v"(cw1), "+v"(cw2), "+v"(cw3));
+			}
+			const uint32_t wsel = (pl & 4) ? ((pl & 2) ? cw3 : cw2) : ((pl & 2) ? cw1 : cw0);
+			const uint32_t wsh = (uint32_t)(pl & 1) * 16u;
+			const int ca = (j0 >= 0 && j0 < C) ? (int)((wsel >> wsh) & 0xffu) : 4;
+			const int cb = (j0 >= 0 && j0 + 1 < C) ? (int)((wsel >> (wsh + 8u)) & 0xffu) : 4;
+			const uint32_t refc2 = (uint32_t)ca | ((uint32_t)cb << 16);
+			const uint32_t coln = (ca > 3 ? 0x0000ffffu : 0u) | (cb > 3 ? 0xffff0000u : 0u);
+			refN |= ((ca > 3) & (j0 >= 0) & (j0 < C)) | ((cb > 3) & (j0 >= 0) & (j0 + 1 < C));
+			const uint32_t sbase = (uint32_t)pp * kDuoPairBytes;
+			// the step before the window: dead above for A, T1 for B
+			uint32_t hp = isB ? t1h : 0u, fp = isB ? t1f : 0u, ep = isB ? t1e : 0u, hlp = isB ? t1hl : 0u;
+			uint32_t tbacc = 0;
+			int lra = 0, lrb = 0;
+			uint32_t cur_iw, cur_iv;
+			{
+				const int b0 = slo >> 2;
+				cur_iw = lds[(b0 < kRowWords ? b0 : kRowWords - 1) * 64 + lane];
+				cur_iv = lds[(b0 > 0 ? b0 - 1 : 0) * 64 + lane];
+			}
+#pragma unroll
+			for(int b4 = 0; b4 < kSteps; b4 += 4) {
+			if(b4 >= slo && b4 <= shi) {                                 // wave-uniform
+			const int nb = (b4 >> 2) + 1;
+			const uint32_t nxt_iw = lds[(nb < kRowWords ? nb : kRowWords - 1) * 64 + lane];
+#pragma unroll
+			for(int st = b4; st < b4 + 4 && st < kSteps; st++) {
+				{
+				const int blk = st >> 2, r = st & 3;
+				const uint32_t iw = cur_iw, iv = cur_iv;
+				// slot 0 is row 0 for A, row K for B (whose high half is row K - 1)
+				uint32_t info = (st == 0) ? (perm(0, iw, 0x0c0c0c00u) | (info_m1 << 16))
+				              : (st == kRows) ? (perm(iw, 0, 0x0c070c0cu) | (kNone & 0xffu))
+				              : (r == 0) ? perm(iv, iw, 0x0c070c00u)
+				                         : perm(0, iw, 0x0c000c00u | ((uint32_t)(r - 1) << 16) | (uint32_t)r);
+				const uint32_t hsw = st < kRows ? Hs[blk] : 0u, esw = st < kRows ? Es[blk] : 0u;
+				uint32_t hl = perm(hp, hsw, 0x0c040c00u | (uint32_t)r);
+				uint32_t el = perm(ep, esw, 0x0c040c00u | (uint32_t)r);
+				uint32_t hdiag = hlp;
+				if(st == 0 && !isB) {                   // A's row 0: row -1 is the top (start anywhere)
+					hl = perm(0, hsw, 0x0c0c0c00u) | 0x00ff0000u;
+					el = perm(0, esw, 0x0c0c0c00u);
+					hdiag = 0x000000ffu;
+				}
+				const uint32_t xrc = (info ^ refc2) & 0x00070007u;
+				uint32_t pen = pmin(pshr(info, 4), xrc << 8);
+				pen = (pen & ~coln) | (npen2 & coln);
+				const uint32_t gbm = info & 0x00080008u;
+				const uint32_t d = psubs(hdiag, pen);
+				// row 0 has no F (A only: low half at slot 0, high half at slot 1)
+				const uint32_t r0 = (st == 0 && !isB) ? 0x00000100u : (st == 1 && !isB) ? 0x01000000u : 0u;
+				const uint32_t rdoe = (gbm << 5) + rdo2, rfoe = (gbm << 5) + (rfo2 + r0), rfee = (gbm << 5) + (rfe2 + r0);
+				const uint32_t hl_o = psubs(hl, rdoe), el_e = psubs(el, rde2);
+				const uint32_t hu_o = psubs(hp, rfoe), fu_e = psubs(fp, rfee);
+				const uint32_t e = pmax(hl_o, el_e);
+				const uint32_t f = pmax(hu_o, fu_e);
+				const uint32_t h = pmax(pmax(d, e), f);
+				uint32_t tb = pmin(xrc, one2);                        // TB_MM
+				tb = (tb << 1) | pne(hl_o, e, one2);                   // TB_EONE
+				tb = (tb << 1) | pne(hu_o, f, one2);                   // TB_FONE
+				tb = (tb << 1) | pne(f, h, one2);                      // TB_FNE
+				tb = (tb << 1) | pne(d, h, one2);                      // TB_DNE
+				if(st + 1 >= rmin) {                         // wave-uniform
+					lra = (st == rl - 1) ? (int)(h & 0xffu) : lra;
+					lrb = (st == rl) ? (int)((h >> 16) & 0xffu) : lrb;
+				}
+				if(st >= 1) {
+					const int pb = (st - 1) >> 2, pr = (st - 1) & 3;
+					const uint32_t selh = (0x03020100u & ~(0xffu << (8 * pr))) | (6u << (8 * pr));
+					Hs[pb] = perm(h, Hs[pb], selh);
+					Es[pb] = perm(e, Es[pb], selh);
+				}
+				if(st & 1) {
+					__builtin_amdgcn_raw_buffer_store_b32(perm(tb, tbacc, 0x06040200u), dirsrc, (int)voff,
+					                                      (int)(sbase + (uint32_t)(st >> 1) * (kDuoG * 4u)), 0);
+				} else {
+					tbacc = tb;
+					if(st == shi)
+						__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, (int)voff,
+						                                      (int)(sbase + (uint32_t)(st >> 1) * (kDuoG * 4u)), 0);
+				}
+				hlp = hl; hp = h; fp = f; ep = e;
+				}
+			}
+			cur_iv = cur_iw; cur_iw = nxt_iw;
+			// the halves' hand-offs at this block (wave-uniform)
+			const int bk = b4 >> 2;
+			if((ev >> bk) & 1ull) {
+				if(bk == kT1) { t1h = hp; t1f = fp; t1e = ep; t1hl = hlp; }   // its last step's outputs
+				if(bk == kT2) {                     // B's dword of slots s0B, s0B + 1 (rows b, b+1)
+					const bool prev = (s0B & 2) != 0 && bk >= 1;
+					const uint32_t xh = prev ? Hs[bk >= 1 ? bk - 1 : 0] : Hs[bk];
+					const uint32_t xe = prev ? Es[bk >= 1 ? bk - 1 : 0] : Es[bk];
+					t2h = from_odd(xh); t2e = from_odd(xe);
+				}
+				if(bk == kP && bk + 1 < kRowWords) {   // A: rows b, b+1 of column 2pp-1 from B
+					const uint32_t mh = (Hs[bk + 1] & ~t2sel) | (t2h & t2sel);
+					const uint32_t me = (Es[bk + 1] & ~t2sel) | (t2e & t2sel);
+					Hs[bk + 1] = isB ? Hs[bk + 1] : mh;
+					Es[bk + 1] = isB ? Es[bk + 1] : me;
+				}
+			}
+			}
+			}
+			// T1 to the B lanes for their next window
+			t1h = from_even(t1h); t1f = from_even(t1f); t1e = from_even(t1e); t1hl = from_even(t1hl);
+			// last rows: the owner of row R-1 of a pair supplies both of its columns (A if
+			// R-1 < b, else B; B's come over to its A lane)
+			const bool ownA = !isB && hasA && (R - 1 < s0A + K);
+			const bool ownB = isB && hasB && (R - 1 >= s0B + K);
+			const int xa = (int)from_odd((uint32_t)lra), xb = (int)from_odd((uint32_t)lrb);
+			const bool xown = from_odd(ownB ? 1u : 0u) != 0;
+			if(!isB && active) {
+				const int jA = 2 * pp, jB = 2 * pp - 2;
+				if(ownA) {
+					if(jA < C) { lastrow[(size_t)jA * 64 + lane] = (uint8_t)lra; lrmax = imax(lrmax, lra); ncand += (lra >= thr); }
+					if(jA + 1 < C) { lastrow[(size_t)(jA + 1) * 64 + lane] = (uint8_t)lrb; lrmax = imax(lrmax, lrb); ncand += (lrb >= thr); }
+				}
+				if(xown) {
+					if(jB >= 0 && jB < C) { lastrow[(size_t)jB * 64 + lane] = (uint8_t)xa; lrmax = imax(lrmax, xa); ncand += (xa >= thr); }
+					if(jB >= 0 && jB + 1 < C) { lastrow[(size_t)(jB + 1) * 64 + lane] = (uint8_t)xb; lrmax = imax(lrmax, xb); ncand += (xb >= thr); }
+				}
+			}
+		}
+		if(!active || isB) continue;                   // A lanes: the verdict, candidates, the walk
+		st_cells += (unsigned long long)R * C;
+		st_cols += C;
+		bt2x_dp_out o;
+		o.nrec = 0; o.rec_off = 0;
+		int status = 0, best = 0;
+		dp_verdict(false, lrmax, p.minsc, ncand, status, best);
+		if(refused) { status = -1; best = 0; atomicAdd(&a.counters[3], 1u); }
+		o.status = status; o.best = best; o.ncand = status > 0 ? (uint16_t)ncand : (uint16_t)0;
+		if(status <= 0) {
+			a.out[pi] = o;
+			if(status == 0 && a.fail_list) a.fail_list[atomicAdd(&a.counters[2], 1u)] = pi;
+			continue;
+		}
+		// candidate order (DpBtCandidate: score desc, col desc), as dp_fill_kernel's u8 path
+		const int nw = (Cmax + 3) >> 2;
+		a.out[pi] = o;
+		for(int qw = 0; qw < nw; qw++) {
+			uint32_t w4 = 0;
+			for(int r = 0; r < 4; r++) {
+				const int j = qw * 4 + r;
+				if(j < C) w4 |= (uint32_t)lastrow[(size_t)j * 64 + lane] << (8 * r);
+			}
+			lds[qw * 64 + lane] = w4;
+		}
+		int cur_key = 0xffff;
+		for(int k = 0; k < ncand; k++) {
+			const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
+			uint32_t best2 = 0;
+#pragma unroll 2
+			for(int qw = 0; qw < nw; qw++) {
+				const uint32_t w4 = lds[qw * 64 + lane];
+				const uint32_t cq = (uint32_t)qw * 0x40004u + 0x10000u;
+				const uint32_t ka = perm(cq, w4, 0x01060004u);
+				const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);
+				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
+				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
+			}
+			const int bk2 = (int)max(best2 & 0xffffu, best2 >> 16);
+			cur_key = bk2;
+			cands[(size_t)k * 64 + lane] = (uint8_t)(bk2 & 0xff);
+		}
+		uint8_t* wslot = gslot + kGroupBytes;
+		walk_problem<kDuoG, kDuoPW>(sc, pen_lds, a, pi, lane, q, gslot + kDuoPairBytes, kDuoDirBytes - kDuoPairBytes,
+		                                cands, reinterpret_cast<uint32_t*>(wslot + kEditOff),
+		                                reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, nullptr);
+	}
+	if(a.stats) {
+		for(int d = 32; d > 0; d >>= 1) {
+			st_cells += __shfl_xor(st_cells, d);
+			st_cols += __shfl_xor(st_cols, d);
+			st_bt += __shfl_xor(st_bt, d);
+			st_comp += __shfl_xor(st_comp, d);
+		}
+		if(lane == 0) {
+			atomicAdd(&a.stats[0], st_cells);
+			atomicAdd(&a.stats[1], st_cols);
+			atomicAdd(&a.stats[2], st_bt);
+			atomicAdd(&a.stats[3], st_comp);
+		}
+	}
+}
+
 // ------------------------------------------------------------------ walk kernel
 // SwAligner::nextAlignment until done(): per problem, its candidates in order, each
 // not already reportedThrough backtraced over the fill's traceback bytes.  Low VGPR use
@@ -1505,7 +1898,9 @@ dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		const uint32_t q = grp * 64 + lane;
 		if(q < nprob) {
 			const uint32_t pi = base + q;
-			walk_problem(sc, a.mmpen, a, pi, lane, a.scratch + (size_t)grp * kGroupBytes, stage_ed, stage_rec, st_bt, true);
+			uint8_t* gs = a.scratch + (size_t)grp * kGroupBytes;
+			walk_problem<64, kPairWords>(sc, a.mmpen, a, pi, lane, lane, gs + kDirOff, kDirBytesLane * 64u, gs + kCandOff,
+			                             stage_ed, stage_rec, st_bt, true);
 		}
 	}
 	if(a.stats) {
@@ -1528,7 +1923,7 @@ namespace {
 struct DpOccupancy {
 	int fused[2][2];                // [debug][wide]
 	int fill[2][2];                 // split-mode fill kernels
-	int walk, wave;
+	int walk, wave, duo;
 	DpOccupancy() {
 		fused[0][0] = blocks_per_cu((const void*)dp_fill_kernel<false, true, false>);
 		fused[1][0] = blocks_per_cu((const void*)dp_fill_kernel<true, true, false>);
@@ -1540,6 +1935,7 @@ struct DpOccupancy {
 		fill[1][1] = blocks_per_cu((const void*)dp_fill_kernel<true, false, true>);
 		walk = blocks_per_cu((const void*)dp_walk_kernel);
 		wave = blocks_per_cu((const void*)dp_wave_kernel<1>);
+		duo = blocks_per_cu((const void*)dp_duo_kernel);
 	}
 };
 const DpOccupancy& occupancy() { static const DpOccupancy o; return o; }
@@ -1561,6 +1957,13 @@ bool dp_split_mode() {
 int dp_parwalk() {
 	const char* e = getenv("BT2X_DP_PARWALK");
 	return e ? (e[0] - '0') : 1;
+}
+
+// The two-lanes-per-problem fill (dp_duo_kernel) for banded u8 launches: BT2X_DP_DUO=0 keeps
+// dp_fill_kernel.  Read per launch (tests switch it).
+bool dp_duo() {
+	const char* e = getenv("BT2X_DP_DUO");
+	return !(e && e[0] == '0');
 }
 
 uint32_t dp_wave_max() {                        // read per launch (tests switch modes)
@@ -1585,6 +1988,7 @@ size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups) {
 	if(!dp_split_mode()) {
 		int nb = 0;
 		for(int d = 0; d < 2; d++) for(int w = 0; w < 2; w++) nb = max(nb, o.fused[d][w]);
+		nb = max(nb, o.duo);
 		return (size_t)ncu * nb * (kGroupBytes + kWalkSlotBytes);
 	}
 	return (size_t)chunk_groups * kGroupBytes + (size_t)ncu * o.walk * kWalkSlotBytes;
@@ -1609,7 +2013,12 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		else hipLaunchKernelGGL((dp_wave_kernel<0, false>), dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
-	if(!dp_split_mode()) {
+	if(!dbg && !wide && a0.band && !dp_split_mode() && dp_duo()) {
+		const uint32_t groups = (a0.n + kDuoG - 1) / kDuoG;
+		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.duo;
+		if(fb > groups) fb = groups;
+		hipLaunchKernelGGL(dp_duo_kernel, dim3(fb), dim3(64), 0, s, sc, a, a0.n);
+	} else if(!dp_split_mode()) {
 		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.fused[dbg ? 1 : 0][wide ? 1 : 0];
 		if(fb > groups_all) fb = groups_all;
 		if(dbg) launch_fill<true, true>(wide, fb, s, sc, a, 0u, a0.n);

@@ -444,7 +444,7 @@ int main(int argc, char** argv) {
 			             (unsigned long long)st.dp_launches, (unsigned long long)st.dps, st.t_dp, st.t_host, st.t_io, (unsigned long long)st.dps_used,
 			             (unsigned long long)st.tight_recs, st.t_backend, st.t_step, st.t_wait, st.t_gather, st.t_retire,
 			             (unsigned long long)st.round_launches, (unsigned long long)st.rounds, st.t_round,
-			             (unsigned long long)st.dp_max_launch);
+			             (unsigned long long)st.dp_max_launch, numa.c_str());
 		if(stats) {
 			HipBackend::GpuStats g = hip.gs;
 			if(hip2) {

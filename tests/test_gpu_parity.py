@@ -144,7 +144,10 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff", "nbuf"]
     # (and every successful walk handed to the wave kernel's parallel walk; the wave mode
     # with the parallel walk)
-    for wave, env in (("0", {}), ("1", {}), ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"})):
+    # (the u8 lane launches run the two-lanes-per-problem fill, dp_duo_kernel, unless
+    # BT2X_DP_DUO=0 keeps dp_fill_kernel)
+    for wave, env in (("0", {}), ("1", {}), ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"}),
+                      ("0", {"BT2X_DP_DUO": "0"}), ("0", {"BT2X_DP_DUO": "0", "BT2X_DP_HEAVY": "1"})):
         os.environ["BT2X_DP_WAVE"] = wave
         os.environ.update(env)
         try:
@@ -351,17 +354,19 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=True):
                                           eedits[rb["edit_off"]: rb["edit_off"] + rb["nedit"]])
 
 
-@pytest.mark.parametrize("debug,wave,band,i16,heavy,parwalk", [
-    (False, "0", "1", 0.0, None, None), (False, "0", "0", 0.0, None, None),
-    (False, "1", "1", 0.0, None, None), (True, "0", "1", 0.0, None, None),
-    (False, "0", "1", 1.0, None, None), (False, "1", "1", 1.0, None, None),
-    (True, "0", "1", 1.0, None, None), (False, "0", "1", 0.3, None, None),
-    (True, "0", "1", 0.3, None, None),
-    (False, "0", "1", 0.0, "0", None), (False, "0", "1", 0.0, "1", None),
-    (False, "0", "1", 0.3, "1", None), (False, "0", "0", 1.0, "2", None),
-    (False, "0", "1", 0.0, "1", "0"), (False, "1", "1", 0.0, None, "2"), (False, "1", "1", 1.0, None, "2"),
-    (False, "1", "1", 0.3, None, "2")])
-def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, parwalk, monkeypatch):
+@pytest.mark.parametrize("debug,wave,band,i16,heavy,parwalk,duo", [
+    (False, "0", "1", 0.0, None, None, None), (False, "0", "0", 0.0, None, None, None),
+    (False, "1", "1", 0.0, None, None, None), (True, "0", "1", 0.0, None, None, None),
+    (False, "0", "1", 1.0, None, None, None), (False, "1", "1", 1.0, None, None, None),
+    (True, "0", "1", 1.0, None, None, None), (False, "0", "1", 0.3, None, None, None),
+    (True, "0", "1", 0.3, None, None, None),
+    (False, "0", "1", 0.0, "0", None, None), (False, "0", "1", 0.0, "1", None, None),
+    (False, "0", "1", 0.3, "1", None, None), (False, "0", "0", 1.0, "2", None, None),
+    (False, "0", "1", 0.0, "1", "0", None), (False, "1", "1", 0.0, None, "2", None), (False, "1", "1", 1.0, None, "2", None),
+    (False, "1", "1", 0.3, None, "2", None),
+    (False, "0", "1", 0.0, None, None, "0"), (False, "0", "1", 0.0, "0", None, "0"), (False, "0", "1", 0.0, "1", None, "0"),
+    (False, "0", "1", 0.0, "2", None, None)])
+def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, parwalk, duo, monkeypatch):
     """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
     wave-per-problem mode) and debug kernels on random shapes/penalty thresholds at the ABI
     limits vs the oracle: statuses, bests, candidates, every nextAlignment record and edit.
@@ -370,9 +375,13 @@ def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, pa
     past which the lane kernel drops a problem for the wave kernel to redo (0: never; 1 and 2:
     nearly every successful problem, mid-walk; default 800).  parwalk: BT2X_DP_PARWALK, the
     wave kernel's nextAlignment sequence on all lanes (walk_wave_par; default: for the walks
-    handed over, 2: the small-launch mode too, 0: lane 0 everywhere)."""
+    handed over, 2: the small-launch mode too, 0: lane 0 everywhere).  duo: BT2X_DP_DUO, the
+    banded u8 lane launches on two lanes per problem (dp_duo_kernel, default) or one (0:
+    dp_fill_kernel)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     monkeypatch.setenv("BT2X_DP_BAND", band)
+    if duo is not None:
+        monkeypatch.setenv("BT2X_DP_DUO", duo)
     if heavy is not None:
         monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
     if parwalk is not None:
@@ -409,9 +418,11 @@ def test_dp_exact_best_option(ctxs, monkeypatch):
 
 
 @pytest.mark.parametrize("gold", ["dp_rep_dpad12.txt.xz", "dp_rep_i16.txt.xz", "dp_rep_i16_mix.txt.xz"])
-@pytest.mark.parametrize("wave,heavy,parwalk", [("0", None, None), ("1", None, None), ("0", "1", None),
-                                                ("1", None, "2"), ("0", "1", "0")])
-def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, gold, monkeypatch):
+@pytest.mark.parametrize("wave,heavy,parwalk,duo", [("0", None, None, None), ("1", None, None, None),
+                                                    ("0", "1", None, None), ("1", None, "2", None),
+                                                    ("0", "1", "0", None), ("0", None, None, "0"),
+                                                    ("0", "1", None, "0")])
+def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, duo, gold, monkeypatch):
     """The production (non-debug) kernel, in both modes and with walks handed to the wave
     kernel (its parallel walk, and lane 0's), reproduces the reference records of the golden
     set (oracle-checked, then against the golden itself)."""
@@ -420,6 +431,8 @@ def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, gold, monkey
         monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
     if parwalk is not None:
         monkeypatch.setenv("BT2X_DP_PARWALK", parwalk)
+    if duo is not None:
+        monkeypatch.setenv("BT2X_DP_DUO", duo)
     case = g.DpCase(os.path.join(g.GOLDEN, gold))
     ctx = ctxs["rep"][0]
     out, recs, edits = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
