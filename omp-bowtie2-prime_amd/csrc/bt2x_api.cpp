@@ -560,7 +560,7 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 		}
 	}
 	static const bool prof = [] { const char* e = getenv("BT2X_DP_PROF"); return e && e[0] == '1'; }();
-	if(prof) { a.prof = c->d_stats + 16; HIPCHK(hipMemsetAsync(a.prof, 0, 11 * sizeof(unsigned long long), s)); }
+	if(prof) { a.prof = c->d_stats + 16; HIPCHK(hipMemsetAsync(a.prof, 0, 14 * sizeof(unsigned long long), s)); }
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][0], s));
 	// every problem's window goes to a BT2X_MAX_COLS-byte slot (cut from the index for
 	// BT2X_DP_REF_TEXT problems, copied from d_refs for the others): the fill kernel reads
@@ -575,7 +575,7 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	rc = bt2x_launch_dp(c->sc, a, s);
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_DP][1], s));
 	if(prof) {                                   // development: where a lane-kernel wave's time goes
-		unsigned long long pv[11];
+		unsigned long long pv[14];
 		HIPCHK(hipStreamSynchronize(s));
 		HIPCHK(hipMemcpy(pv, a.prof, sizeof pv, hipMemcpyDeviceToHost));
 		float ms = 0;
@@ -584,8 +584,9 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 		if(a.heavy_list) HIPCHK(hipMemcpy(&nheavy, a.heavy_list, sizeof nheavy, hipMemcpyDeviceToHost));
 		std::fprintf(stderr, "BT2X_DP_PROF n=%u ms=%.3f groups=%llu fill_cyc=%llu walk_cyc=%llu walk_steps=%llu cand_iters=%llu "
 		             "max_wave_cyc=%llu max_fill_cyc=%llu max_walk_cyc=%llu heavy=%u lane_work_sum=%llu "
-		             "wave_lane_max_sum=%llu lane_max=%llu\n",
-		             n, ms, pv[4], pv[0], pv[1], pv[2], pv[3], pv[5], pv[6], pv[7], nheavy, pv[8], pv[9], pv[10]);
+		             "wave_lane_max_sum=%llu lane_max=%llu pro_cyc=%llu pair_cyc=%llu cand_cyc=%llu\n",
+		             n, ms, pv[4], pv[0], pv[1], pv[2], pv[3], pv[5], pv[6], pv[7], nheavy, pv[8], pv[9], pv[10], pv[11],
+		             pv[12], pv[13]);
 	}
 	c->ev_valid[BT2X_K_DP] = true;
 	c->n_dp_last = n;

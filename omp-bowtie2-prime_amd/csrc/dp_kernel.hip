@@ -44,6 +44,7 @@ constexpr uint32_t kLastRowBytesLane = 512;                        // u16 per co
 constexpr uint32_t kCandBytesLane = kCols;                         // sorted candidate columns
 constexpr uint32_t kEditStage = 400;                               // >= R + C + 2
 constexpr uint32_t kRecStage = kCols + 8;                          // >= ncand + 1
+constexpr int kMoveLogWords = (kRows + kCols + 15) / 16;           // an attempt's moves, 2 bits each
 // Group region: the fill's output for 64 problems (all regions lane-interleaved).
 constexpr size_t kDirOff = 0;
 constexpr size_t kLastRowOff = kDirOff + (size_t)kDirBytesLane * 64;
@@ -277,7 +278,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
                                              int lane, int tbl, const uint8_t* dirbase, uint32_t dirbytes,
                                              const uint8_t* cands, uint32_t* stage_ed,
                                              bt2x_aln_rec* stage_rec, unsigned long long& st_bt, bool refN,
-                                             unsigned long long* pw = nullptr) {
+                                             uint32_t* mlog, unsigned long long* pw = nullptr) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 	const uint32_t gl = (uint32_t)lane;
 	// the layout's move offsets (see kDiag1Even): one step pair up is -4G bytes
@@ -369,6 +370,17 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 				// the reference reads.
 				uint32_t bo = (uint32_t)tb_addr_g<G, PW>(row, col, tbl);
 				bool fin = false;
+				// The step loop issues loads only.  Its moves go to a log in LDS (2 bits each:
+				// diagonal, diagonal mismatch, up = reference gap, left = read gap; mlog[w * 64 +
+				// lane] holds moves 16w .. 16w + 15) and the attempt's marks (setReportedThrough)
+				// and edits are written from it after the attempt: vmcnt counts loads and stores
+				// in issue order, so a store in the chain made every later step wait for the
+				// store's completion, not only for its own load.  The attempt never revisits its
+				// own cells, and the next candidate's ring (loaded before these marks) is patched
+				// from cmask, so every byte the reference reads is the one read here.
+				uint32_t macc = 0;                                 // the log's current word
+				int nm = 0;                                        // moves logged
+				bool end0 = false;                                 // the path reached row 0
 #define BT2X_WALK_STEP(T0, T1, T2, T3, T4, T5, T6, T7)                                                        \
 				{                                                                                     \
 					const uint32_t ctb = T0;                                                          \
@@ -380,9 +392,9 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 						const int diag = col - row + (int)p.triml;                                    \
 						over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);   \
 						if(row == 0) {                                                                \
-							__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)bo, 0, 0); \
 							if(col == dnx && row0 < 8) cmask |= 1u << row0;                           \
 							tb_end = ctb;                                                             \
+							end0 = true;                                                              \
 							fin = true;                                                               \
 						} else {                                                                      \
 							/* the reference's fixed priority over the cell's flags (u8.cpp:843-990): \
@@ -402,13 +414,12 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 							const int crow = row, ccol = col;                                         \
 							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;                \
 							if(ccol - crow == dnx && row0 - crow < 8) cmask |= 1u << (row0 - crow);   \
-							/* the move's edit, characters (and a mismatch's penalty) resolved after  \
-							   the walk (resolve_edits): no read/reference loads in the chain */      \
-							if(!isD || (ctb & TB_MM)) {                                               \
-								stage_ed[(size_t)ne * 64 + lane] =                                    \
-									isD ? pend_edit(crow, EDIT_MM, ccol)                              \
-									    : isF ? pend_edit(crow, EDIT_REF_GAP, ccol) : pend_edit(crow + 1, EDIT_READ_GAP, ccol); \
-								ne++;                                                                 \
+							/* the move, logged (its edit and mark are written after the attempt) */  \
+							{                                                                         \
+								const uint32_t mv = isD ? ((ctb & TB_MM) ? 1u : 0u) : isF ? 2u : 3u;  \
+								macc |= mv << (2 * (nm & 15));                                        \
+								if((nm & 15) == 15) { mlog[(size_t)(nm >> 4) * 64 + lane] = macc; macc = 0; } \
+								nm++;                                                                 \
 							}                                                                         \
 							if(!isD) {                                                                \
 								const bool open = nct == 2;                                           \
@@ -424,8 +435,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 								T3 = tb_load(dirsrc, bo + kD2);         T4 = tb_load(dirsrc, bo + kD2 + d1); \
 								T5 = tb_load(dirsrc, bo + 2 * kD2);     T6 = tb_load(dirsrc, bo + 2 * kD2 + d1); \
 								T7 = tb_load(dirsrc, bo + 3 * kD2);     nbo = bo + 3 * kD2 + d1;    \
-							}                                                                         \
-							__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)cbo, 0, 0); /* setReportedThrough */ \
+								}                                                                         \
 						}                                                                             \
 					}                                                                                 \
 					/* one unconditional def per step: a load under a divergent branch would be \
@@ -448,7 +458,29 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 				}
 #undef BT2X_WALK_STEP
 #undef BT2X_RING_LOAD
-				if(aborted) break;
+if(aborted) break;
+// the attempt's marks and edits, from its move log (the reference's order: an
+// edit per move that records one, in walk order)
+if(nm & 15) mlog[(size_t)(nm >> 4) * 64 + lane] = macc;
+{
+	int r = row0, c = col0;
+	uint32_t b = (uint32_t)tb_addr_g<G, PW>(r, c, tbl), w = 0;
+	for(int k = 0; k < nm; k++) {
+		if((k & 15) == 0) w = mlog[(size_t)(k >> 4) * 64 + lane];
+		const uint32_t mv = (w >> (2 * (k & 15))) & 3u;
+		__builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)b, 0, 0);   // setReportedThrough
+		if(mv != 0) {
+			stage_ed[(size_t)ne * 64 + lane] = mv == 1 ? pend_edit(r, EDIT_MM, c)
+			                                 : mv == 2 ? pend_edit(r, EDIT_REF_GAP, c)
+			                                           : pend_edit(r + 1, EDIT_READ_GAP, c);
+			ne++;
+		}
+		if(mv <= 1) { b += (c & 1) ? kD1O : kD1E; r--; c--; }
+		else if(mv == 2) { b += ((r + (c & 1)) & 1) ? -2 : -(4 * G - 2); r--; }
+		else { b += (c & 1) ? ((r & 1) ? -(4 * G - 1) : -3) : ((r & 1) ? kD1E + 4 * G - 2 : kD1E + 2); c--; }
+	}
+	if(end0) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)TB_MARK, dirsrc, (int)b, 0, 0);
+}
 				if(!ok || !over_core) { hi = max(hi, ne); continue; }
 				if(tb_end & TB_MM) {                     // the final (row 0) cell
 					stage_ed[(size_t)ne * 64 + lane] = pend_edit(row, EDIT_MM, col);
@@ -1061,6 +1093,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 
 	unsigned long long pw[2] = {0, 0}, t_fill = 0, t_walk = 0, ngrp = 0;     // BT2X_DP_PROF
 	unsigned long long mx_fill = 0, mx_walk = 0, mylen_sum = 0, mylen_max = 0;
+	unsigned long long t_pro = 0, t_pair = 0, t_cand = 0;
 	const unsigned long long t_start = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
 		const unsigned long long t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -1128,6 +1161,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				for(int k = 0; k < 4; k++) lds[(4 * c16 + k) * 64 + lane] = kNone * 0x01010101u;
 			}
 		}
+		const unsigned long long tA = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 		// ------------- fill: two columns per sweep, per-row state in VGPRs ------------
 		// H and E of the previous column: u8 4 rows per dword (40 + 40 dwords for 160
 		// rows), wide 2 rows per dword (80 + 80).
@@ -1315,7 +1349,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 					}
 				}
 				// last row of each column (per-lane R; only in the wave's R range)
-				if(st + 1 >= rmin) {                         // wave-uniform
+				// wave-uniform; cold (a few steps per column pair): the common path falls
+				// through, a taken branch per step would stall the wave's instruction fetch
+				if(__builtin_expect(st + 1 >= rmin, 0)) {
 					lra = (st == rl - 1) ? (int)(h & (kWide ? 0xffffu : 0xffu)) : lra;
 					lrb = (st == rl) ? (int)((h >> 16) & (kWide ? 0xffffu : 0xffu)) : lrb;
 				}
@@ -1341,7 +1377,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 					                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
 				} else {
 					tbacc = tb;
-					if(st == shi)
+					if(__builtin_expect(st == shi, 0))
 						__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, lane * 4,
 						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
 				}
@@ -1364,6 +1400,8 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				ncand += (lrb >= thr);
 			}
 		}
+		const unsigned long long tB = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+		if(a.prof) { t_pro += tA - t0; t_pair += tB - tA; }
 		if(!active) continue;
 		st_cells += (unsigned long long)R * C;
 		st_cols += C;
@@ -1459,10 +1497,11 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		if(kFused) {
 			uint8_t* wslot = gslot + kGroupBytes;
 			const unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+			if(a.prof) t_cand += t1 - tB;
 			const unsigned long long bt0 = st_bt;
 			walk_problem<64, kPairWords>(sc, pen_lds, a, pi, lane, lane, gslot + kDirOff, kDirBytesLane * 64u, gslot + kCandOff,
 			                             reinterpret_cast<uint32_t*>(wslot + kEditOff), reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff),
-			                             st_bt, refN != 0, a.prof ? pw : nullptr);
+			                             st_bt, refN != 0, lds, a.prof ? pw : nullptr);
 			if(a.prof) {
 				const unsigned long long t2 = __builtin_amdgcn_s_memtime();
 				t_fill += t1 - t0; t_walk += t2 - t1; ngrp++;
@@ -1485,6 +1524,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			atomicMax(&a.prof[5], __builtin_amdgcn_s_memtime() - t_start);
 			atomicMax(&a.prof[6], mx_fill); atomicMax(&a.prof[7], mx_walk);
 			atomicAdd(&a.prof[8], ls); atomicAdd(&a.prof[9], lm); atomicMax(&a.prof[10], lm);
+			atomicAdd(&a.prof[11], t_pro); atomicAdd(&a.prof[12], t_pair); atomicAdd(&a.prof[13], t_cand);
 		}
 	}
 	if(a.stats) {
@@ -1565,7 +1605,10 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0, st_comp = 0;
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 	const uint32_t one2 = opaque(0x00010001u);
+	unsigned long long t_fill = 0, t_walk = 0, ngrp = 0, mx_fill = 0, mx_walk = 0;     // BT2X_DP_PROF
+	const unsigned long long t_start = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 	for(uint32_t grp = blockIdx.x; (uint64_t)grp * kDuoG < nprob; grp += gridDim.x) {
+		const unsigned long long t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
 		uint8_t* gslot = a.scratch + (size_t)blockIdx.x * (kGroupBytes + kWalkSlotBytes);
 		uint8_t* lastrow = gslot + kDuoLastRowOff;
 		uint8_t* cands = gslot + kDuoCandOff;
@@ -1756,7 +1799,9 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 				tb = (tb << 1) | pne(hu_o, f, one2);                   // TB_FONE
 				tb = (tb << 1) | pne(f, h, one2);                      // TB_FNE
 				tb = (tb << 1) | pne(d, h, one2);                      // TB_DNE
-				if(st + 1 >= rmin) {                         // wave-uniform
+				// wave-uniform; cold (a few steps per column pair): the common path falls
+				// through, a taken branch per step would stall the wave's instruction fetch
+				if(__builtin_expect(st + 1 >= rmin, 0)) {
 					lra = (st == rl - 1) ? (int)(h & 0xffu) : lra;
 					lrb = (st == rl) ? (int)((h >> 16) & 0xffu) : lrb;
 				}
@@ -1771,7 +1816,7 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 					                                      (int)(sbase + (uint32_t)(st >> 1) * (kDuoG * 4u)), 0);
 				} else {
 					tbacc = tb;
-					if(st == shi)
+					if(__builtin_expect(st == shi, 0))
 						__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, (int)voff,
 						                                      (int)(sbase + (uint32_t)(st >> 1) * (kDuoG * 4u)), 0);
 				}
@@ -1781,7 +1826,7 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 			cur_iv = cur_iw; cur_iw = nxt_iw;
 			// the halves' hand-offs at this block (wave-uniform)
 			const int bk = b4 >> 2;
-			if((ev >> bk) & 1ull) {
+			if(__builtin_expect((ev >> bk) & 1ull, 0)) {
 				if(bk == kT1) { t1h = hp; t1f = fp; t1e = ep; t1hl = hlp; }   // its last step's outputs
 				if(bk == kT2) {                     // B's dword of slots s0B, s0B + 1 (rows b, b+1)
 					const bool prev = (s0B & 2) != 0 && bk >= 1;
@@ -1818,6 +1863,8 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 				}
 			}
 		}
+		const unsigned long long t1 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+		if(a.prof) { t_fill += t1 - t0; mx_fill = max(mx_fill, t1 - t0); ngrp++; }
 		if(!active || isB) continue;                   // A lanes: the verdict, candidates, the walk
 		st_cells += (unsigned long long)R * C;
 		st_cols += C;
@@ -1863,7 +1910,13 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 		uint8_t* wslot = gslot + kGroupBytes;
 		walk_problem<kDuoG, kDuoPW>(sc, pen_lds, a, pi, lane, q, gslot + kDuoPairBytes, kDuoDirBytes - kDuoPairBytes,
 		                                cands, reinterpret_cast<uint32_t*>(wslot + kEditOff),
-		                                reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, nullptr);
+		                                reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, lds, nullptr);
+		if(a.prof) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); t_walk += t2 - t1; mx_walk = max(mx_walk, t2 - t1); }
+	}
+	if(a.prof && lane == 0) {
+		atomicAdd(&a.prof[0], t_fill); atomicAdd(&a.prof[1], t_walk); atomicAdd(&a.prof[4], ngrp);
+		atomicMax(&a.prof[5], __builtin_amdgcn_s_memtime() - t_start);
+		atomicMax(&a.prof[6], mx_fill); atomicMax(&a.prof[7], mx_walk);
 	}
 	if(a.stats) {
 		for(int d = 32; d > 0; d >>= 1) {
@@ -1887,6 +1940,7 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 // keeps many waves resident to hide the walk's dependent load chain.
 __global__ void __launch_bounds__(64)
 dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
+	__shared__ uint32_t mlog[kMoveLogWords * 64];             // walk_problem's move logs
 	const int lane = threadIdx.x;
 	uint8_t* wslot = a.walk_scratch + (size_t)blockIdx.x * kWalkSlotBytes;
 	uint32_t* stage_ed = reinterpret_cast<uint32_t*>(wslot + kEditOff);
@@ -1900,7 +1954,7 @@ dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			const uint32_t pi = base + q;
 			uint8_t* gs = a.scratch + (size_t)grp * kGroupBytes;
 			walk_problem<64, kPairWords>(sc, a.mmpen, a, pi, lane, lane, gs + kDirOff, kDirBytesLane * 64u, gs + kCandOff,
-			                             stage_ed, stage_rec, st_bt, true);
+			                             stage_ed, stage_rec, st_bt, true, mlog);
 		}
 	}
 	if(a.stats) {
@@ -1959,11 +2013,17 @@ int dp_parwalk() {
 	return e ? (e[0] - '0') : 1;
 }
 
-// The two-lanes-per-problem fill (dp_duo_kernel) for banded u8 launches: BT2X_DP_DUO=0 keeps
-// dp_fill_kernel.  Read per launch (tests switch it).
-bool dp_duo() {
+// The two-lanes-per-problem fill (dp_duo_kernel) for banded u8 launches of at most
+// BT2X_DP_DUO_MAX problems (default 65536: about one 64-problem group per SIMD, where one
+// lane's chain is the launch's latency; larger launches fill the SIMDs with dp_fill_kernel's
+// waves, and the duo kernel's extra steps would cost throughput).  BT2X_DP_DUO=0: never,
+// =1: always.  Read per launch (tests switch it).
+bool dp_duo(uint32_t n) {
 	const char* e = getenv("BT2X_DP_DUO");
-	return !(e && e[0] == '0');
+	if(e && e[0] == '0') return false;
+	if(e && e[0] == '1') return true;
+	const char* x = getenv("BT2X_DP_DUO_MAX");
+	return n <= (x ? (uint32_t)atoll(x) : 65536u);
 }
 
 uint32_t dp_wave_max() {                        // read per launch (tests switch modes)
@@ -2013,7 +2073,7 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		else hipLaunchKernelGGL((dp_wave_kernel<0, false>), dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
-	if(!dbg && !wide && a0.band && !dp_split_mode() && dp_duo()) {
+	if(!dbg && !wide && a0.band && !dp_split_mode() && dp_duo(a0.n)) {
 		const uint32_t groups = (a0.n + kDuoG - 1) / kDuoG;
 		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.duo;
 		if(fb > groups) fb = groups;

@@ -560,11 +560,26 @@ struct Read {
 	size_t length() const { return fw.size(); }
 };
 
-// genRandSeed (pat.cpp:45-88)
+// genRandSeed (pat.cpp:45-88).  The xors are order-free, so the code and quality terms are
+// folded 16 / 4 positions at a time (the shifts repeat with that period).
 inline uint32_t gen_rand_seed(const Read& r, uint32_t seed) {
 	uint32_t rseed = (seed + 101) * 59 * 61 * 67 * 71 * 73 * 79 * 83;
-	for(size_t i = 0; i < r.fw.size(); i++) rseed ^= ((uint32_t)r.fw[i] << ((i & 15) << 1));
-	for(size_t i = 0; i < r.fw.size(); i++) rseed ^= (uint32_t)((int)(signed char)r.qual[i] << ((i & 3) << 3));
+	const size_t n = r.fw.size();
+	const uint8_t* fw = r.fw.data();
+	const signed char* qu = reinterpret_cast<const signed char*>(r.qual.data());
+	size_t i = 0;
+	for(; i + 16 <= n; i += 16) {
+		uint32_t x = 0;
+		for(int k = 0; k < 16; k++) x ^= (uint32_t)fw[i + k] << (2 * k);
+		rseed ^= x;
+	}
+	for(; i < n; i++) rseed ^= ((uint32_t)fw[i] << ((i & 15) << 1));
+	for(i = 0; i + 4 <= n; i += 4) {
+		uint32_t x = 0;
+		for(int k = 0; k < 4; k++) x ^= (uint32_t)((int)qu[i + k] << (8 * k));
+		rseed ^= x;
+	}
+	for(; i < n; i++) rseed ^= (uint32_t)((int)qu[i] << ((i & 3) << 3));
 	for(size_t i = 0; i < r.name.size(); i++) {
 		const int p = (int)(signed char)r.name[i];
 		if(p == '/') break;
@@ -640,13 +655,32 @@ public:
 		size_t L = 0;
 		uint32_t nN = 0;
 		const unsigned char* sq = reinterpret_cast<const unsigned char*>(raw.l[1]);
-		for(size_t i = 0; i < n1; i++) {
-			const unsigned char c = sq[i] == '.' ? (unsigned char)'N' : sq[i];
-			const uint8_t code = kAsc2Dna[c];
-			const unsigned alpha = (unsigned)((c | 32u) - 'a') < 26u;
-			fw[L] = code;
-			nN += (code > 3) & alpha;
-			L += alpha;
+		// a line of letters only (the common case): codes by arithmetic on the ASCII value in
+		// a branch-free loop the compiler vectorizes (kAsc2Dna's values: A/C/G/T either case
+		// 0-3, every other letter 4); anything else ('.', skipped characters) the general loop
+		{
+			unsigned bad = 0;
+			uint32_t nn = 0;
+			for(size_t i = 0; i < n1; i++) {
+				const unsigned c = sq[i], u = c & 0xdfu;
+				bad |= (unsigned)((u - 'A') > 25u);
+				const unsigned t = (c >> 1) & 3u;                 // A 0, C 1, T 2, G 3
+				const bool acgt = (u == 'A') | (u == 'C') | (u == 'G') | (u == 'T');
+				fw[i] = acgt ? (uint8_t)(t ^ (t >> 1)) : (uint8_t)4;
+				nn += acgt ? 0u : 1u;
+			}
+			if(!bad) { L = n1; nN = nn; }
+		}
+		if(L != n1 || n1 == 0) {
+			L = 0; nN = 0;
+			for(size_t i = 0; i < n1; i++) {
+				const unsigned char c = sq[i] == '.' ? (unsigned char)'N' : sq[i];
+				const uint8_t code = kAsc2Dna[c];
+				const unsigned alpha = (unsigned)((c | 32u) - 'a') < 26u;
+				fw[L] = code;
+				nN += (code > 3) & alpha;
+				L += alpha;
+			}
 		}
 		r.fw.resize(L);
 		r.nN = nN;

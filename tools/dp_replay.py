@@ -94,6 +94,7 @@ def main():
         return ms
 
     for cfg in args.configs:
+        cfg = cfg.strip('"\'')                        # "" from a shell word: the default
         env = dict(kv.split("=", 1) for kv in cfg.split(",") if kv)
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
