@@ -383,13 +383,28 @@ typedef struct {
 
 /* One element of a seed round (bt2x_seed_round): the reference coordinate of
  * bt2x_resolve_out without the joined offset and the text length (the caller's
- * plen[tidx]), 16 bytes across PCIe instead of 32.  tidx = BT2X_NO_TIDX (toff = 0): the
- * row lies in no fragment. */
+ * plen[tidx]), packed into 8 bytes across PCIe instead of 32:
+ *   bits  0..38  textoff (offset into reference tidx)
+ *   bit  39      straddled (the hit runs past its fragment's end)
+ *   bits 40..63  tidx; 0xffffff = BT2X_NO_TIDX (toff = 0): the row lies in no fragment
+ * so a seed round needs fewer than 2^24 - 1 references (BT2X_E_ARG otherwise) and texts
+ * shorter than 2^39.  Read them with bt2x_elt_toff / _tidx / _straddled. */
 typedef struct {
-	uint64_t toff;           /* textoff: offset into reference tidx                      */
-	uint32_t tidx;
-	uint32_t straddled;      /* 1 if the hit runs past its fragment's end                 */
+	uint64_t v;
 } bt2x_elt;
+#define BT2X_ELT_TIDX_NONE 0xffffffu
+static inline uint64_t bt2x_elt_toff(bt2x_elt e) { return e.v & ((1ull << 39) - 1); }
+static inline uint32_t bt2x_elt_straddled(bt2x_elt e) { return (uint32_t)(e.v >> 39) & 1u; }
+static inline uint32_t bt2x_elt_tidx(bt2x_elt e) {
+	const uint32_t t = (uint32_t)(e.v >> 40);
+	return t == BT2X_ELT_TIDX_NONE ? BT2X_NO_TIDX : t;
+}
+static inline bt2x_elt bt2x_elt_pack(uint64_t toff, uint32_t tidx, uint32_t straddled) {
+	bt2x_elt e;
+	e.v = (toff & ((1ull << 39) - 1)) | ((uint64_t)(straddled & 1u) << 39) |
+	      ((uint64_t)(tidx == BT2X_NO_TIDX ? BT2X_ELT_TIDX_NONE : tidx & BT2X_ELT_TIDX_NONE) << 40);
+	return e;
+}
 
 /* With the resident full suffix array this is one 4-byte lookup per element; without
  * it (texts of 2^32 rows or more, BT2X_FULL_SA=0) the kernel walks LF to the SA sample

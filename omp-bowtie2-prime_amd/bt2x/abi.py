@@ -31,7 +31,7 @@ RESOLVE_IN = np.dtype([("row", "<u8"), ("qlen", "<u4"), ("pad", "<u4")], align=T
 RESOLVE_OUT = np.dtype([("joff", "<u8"), ("toff", "<u8"), ("tlen", "<u8"), ("tidx", "<u4"),
                         ("straddled", "<u4")], align=True)
 NO_TIDX = 0xFFFFFFFF
-ELT = np.dtype([("toff", "<u8"), ("tidx", "<u4"), ("straddled", "<u4")], align=True)   # bt2x_elt
+ELT = np.dtype([("v", "<u8")])   # bt2x_elt: toff bits 0-38, straddled bit 39, tidx bits 40-63
 ROUND_IN = np.dtype([("read_off", "<u8"), ("seed0", "<u8"), ("rnd_last", "<u4"), ("rnd_lastoff", "<i4"),
                      ("exr0", "<u4"), ("nexr", "<u2"), ("nseeds", "<u2"), ("num_offs", "<u2"),
                      ("rdlen", "<u2"), ("interval", "<u2"), ("offset", "<u2"), ("seedlen", "<u2"),

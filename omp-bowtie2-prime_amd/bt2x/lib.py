@@ -14,7 +14,7 @@ import numpy as np
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbt2x.so")
+LIB_PATH = os.environ.get("BT2X_LIB") or os.path.join(HERE, "libbt2x.so")   # BT2X_LIB: a development build
 _LIB = None
 
 FUNCS = {

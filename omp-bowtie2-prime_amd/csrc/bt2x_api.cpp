@@ -127,7 +127,7 @@ extern "C" void bt2x_host_free(void* p) {
 	if(p) (void)hipHostFree(p);
 }
 
-extern "C" const char* bt2x_version(void) { return "bt2x 0.2 (gfx950; abi 1.1)"; }
+extern "C" const char* bt2x_version(void) { return "bt2x 0.2 (gfx950; abi 1.2)"; }
 
 // -------------------------------------------------------------------- context
 struct DevBuf {
@@ -717,6 +717,7 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
                                    uint32_t exr_cap, uint32_t* d_used, void* stream) {
 	if(!c || !d_used) return BT2X_E_ARG;
 	if(!c->ix.sa && !c->ix.offs) return BT2X_E_ARG;        // index loaded without load_offs
+	if(c->npat >= BT2X_ELT_TIDX_NONE || c->ix.len >= (1ull << 39)) return BT2X_E_ARG;   // bt2x_elt's fields
 	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
 	HIPCHK(hipSetDevice(c->device));
 	int rc;

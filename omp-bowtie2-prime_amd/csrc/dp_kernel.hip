@@ -45,6 +45,10 @@ constexpr uint32_t kCandBytesLane = kCols;                         // sorted can
 constexpr uint32_t kEditStage = 400;                               // >= R + C + 2
 constexpr uint32_t kRecStage = kCols + 8;                          // >= ncand + 1
 constexpr int kMoveLogWords = (kRows + kCols + 15) / 16;           // an attempt's moves, 2 bits each
+#ifndef BT2X_WALK_BATCH
+#define BT2X_WALK_BATCH 32
+#endif
+constexpr int kWalkBatch = BT2X_WALK_BATCH;                        // walk bytes fetched per round trip (8, 16 or 32)
 // Group region: the fill's output for 64 problems (all regions lane-interleaved).
 constexpr size_t kDirOff = 0;
 constexpr size_t kLastRowOff = kDirOff + (size_t)kDirBytesLane * 64;
@@ -73,6 +77,15 @@ constexpr int kDiag1Even = -(kPairWords * 256) + 1;
 constexpr int kDiag2 = -257 + kDiag1Even;
 __device__ __forceinline__ uint32_t tb_load(__amdgpu_buffer_rsrc_t src, uint32_t off) {
 	return __builtin_amdgcn_raw_buffer_load_b8(src, (int)off, 0, 0);   // out of range: 0
+}
+// s_waitcnt vmcnt(0), expcnt and lgkmcnt left alone (gfx9 encoding: vmcnt bits 3:0 and
+// 15:14, expcnt 6:4, lgkmcnt 11:8)
+constexpr int kWaitVm0 = 0x0f70;
+// The byte at off in the low 8 bits of an (unaligned) dword load, the bits above it the
+// following bytes: for loop-carried registers, which the compiler would otherwise keep as
+// 8-bit values and re-extend with copies that wait for the loads.  Users test low bits only.
+__device__ __forceinline__ uint32_t tb_load4(__amdgpu_buffer_rsrc_t src, uint32_t off) {
+	return __builtin_amdgcn_raw_buffer_load_b32(src, (int)off, 0, 0);
 }
 
 // 1 in the lowest active lane, else 0 (summed over lanes: wave iterations)
@@ -268,6 +281,17 @@ __device__ __forceinline__ size_t tb_addr_g(int row, int col, int tbl) {
 	const int st = row + (col & 1);
 	return ((((size_t)(col >> 1) * PW + (st >> 1)) * G + tbl) << 2) + ((st & 1) << 1) + (col & 1);
 }
+// The same in 32 bits (a traceback region is far below 4 GiB): the walk's hot path, where
+// a 64-bit multiply-add's register pair can alias a ring register and wait for its load.
+template<int G, int PW>
+__device__ __forceinline__ uint32_t tb_off_g(int row, int col, int tbl) {
+	const uint32_t st = (uint32_t)(row + (col & 1));
+	// (the multiply in asm: the compiler would form the multiply-add as v_mad_u64_u32,
+	// whose 64-bit addend pair can take a ring register and so wait for its load)
+	uint32_t pr;
+	asm("v_mul_u32_u24 %0, %1, %2" : "=v"(pr) : "v"((uint32_t)(col >> 1)), "v"((uint32_t)PW));
+	return ((pr + (st >> 1)) * G + (uint32_t)tbl) * 4u + ((st & 1u) << 1) + ((uint32_t)col & 1u);
+}
 
 // SwAligner::nextAlignment until done() for problem pi: its candidates in order (cands,
 // [k * 64 + lane]), each not already reportedThrough backtraced over the fill's traceback
@@ -278,7 +302,7 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
                                              int lane, int tbl, const uint8_t* dirbase, uint32_t dirbytes,
                                              const uint8_t* cands, uint32_t* stage_ed,
                                              bt2x_aln_rec* stage_rec, unsigned long long& st_bt, bool refN,
-                                             uint32_t* mlog, unsigned long long* pw = nullptr) {
+                                             uint32_t* mlog, bool prof, unsigned long long& pw_steps, unsigned long long& pw_iters) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe;
 	const uint32_t gl = (uint32_t)lane;
 	// the layout's move offsets (see kDiag1Even): one step pair up is -4G bytes
@@ -318,10 +342,10 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 		{                                                                                         \
 			const uint32_t bo_ = (BO);                                                            \
 			const int d1_ = ((COL) & 1) ? kD1O : kD1E;                                      \
-			A0 = tb_load(dirsrc, bo_);                      A1 = tb_load(dirsrc, bo_ + d1_);      \
-			A2 = tb_load(dirsrc, bo_ + kD2);             A3 = tb_load(dirsrc, bo_ + kD2 + d1_); \
-			A4 = tb_load(dirsrc, bo_ + 2 * kD2);         A5 = tb_load(dirsrc, bo_ + 2 * kD2 + d1_); \
-			A6 = tb_load(dirsrc, bo_ + 3 * kD2);         A7 = tb_load(dirsrc, bo_ + 3 * kD2 + d1_); \
+			A0 = tb_load4(dirsrc, bo_);                      A1 = tb_load4(dirsrc, bo_ + d1_);      \
+			A2 = tb_load4(dirsrc, bo_ + kD2);             A3 = tb_load4(dirsrc, bo_ + kD2 + d1_); \
+			A4 = tb_load4(dirsrc, bo_ + 2 * kD2);         A5 = tb_load4(dirsrc, bo_ + 2 * kD2 + d1_); \
+			A6 = tb_load4(dirsrc, bo_ + 3 * kD2);         A7 = tb_load4(dirsrc, bo_ + 3 * kD2 + d1_); \
 		}
 		BT2X_RING_LOAD(n0, n1, n2, n3, n4, n5, n6, n7, ((uint32_t)tb_addr_g<G, PW>(row0, c_next, tbl)), c_next)
 		int c_next2 = ncand > 1 ? cands[64 + gl] : 0;
@@ -333,7 +357,11 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 			int ntries = 0, hi = 0;
 			bool found = false;
 			while(ndone < ncand) {
-				if(pw) pw[1] += first_active(lane);       // development counters (BT2X_DP_PROF)
+				if(prof) pw_iters += first_active(lane);    // development counters (BT2X_DP_PROF)
+				// Drain the last attempt's stores (its marks and edits) before this one's loads:
+				// with stores and loads both pending, the compiler treats vmcnt as out of order
+				// and would wait for vmcnt(0) at every step of the walk's ring below
+				__builtin_amdgcn_s_waitcnt(kWaitVm0);
 				const int col0 = c_next;
 				const uint32_t M = TB_MARK;
 				uint32_t q0 = n0 | ((cmask & 1u) ? M : 0u), q1 = n1 | ((cmask & 2u) ? M : 0u);
@@ -362,91 +390,113 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 				// last: a chain of cache-missing loads (the fill's bytes left L2 long ago).  Most
 				// moves are diagonal (all of them in the bottom gap-barrier rows, which hold no E
 				// or F), so the bytes of the next seven cells down the current diagonal are kept
-				// in flight: a ring of registers (q0..q7, rotated by unrolling the step kLook
-				// times, never moved -- a move would wait for the load) refilled one cell per
-				// diagonal step, and reloaded from the new cell after a gap move.  The current
-				// attempt never revisits its own cells and earlier attempts' marks were stored
-				// before these loads (or are patched in from cmask), so a ring byte is the byte
-				// the reference reads.
-				uint32_t bo = (uint32_t)tb_addr_g<G, PW>(row, col, tbl);
-				bool fin = false;
+				// in flight: a ring of registers (q0..q7, rotated by unrolling the step, never
+				// moved -- a move would wait for the load) refilled one cell per diagonal step,
+				// and reloaded from the new cell after a gap move.  The loads are dwords (the byte
+				// in bits 0-7): 8-bit values carried around the loop get re-extended by copies
+				// that wait for them.  The current attempt never revisits its own cells and
+				// earlier attempts' marks were stored before these loads (or are patched in from
+				// cmask), so a ring byte is the byte the reference reads.
+				uint32_t bo = tb_off_g<G, PW>(row, col, tbl);
+				uint32_t fin = 0, okw = 1, abw = 0;               // 0/1 (see BT2X_WALK_STEP)
 				// The step loop issues loads only.  Its moves go to a log in LDS (2 bits each:
 				// diagonal, diagonal mismatch, up = reference gap, left = read gap; mlog[w * 64 +
 				// lane] holds moves 16w .. 16w + 15) and the attempt's marks (setReportedThrough)
 				// and edits are written from it after the attempt: vmcnt counts loads and stores
 				// in issue order, so a store in the chain made every later step wait for the
-				// store's completion, not only for its own load.  The attempt never revisits its
-				// own cells, and the next candidate's ring (loaded before these marks) is patched
-				// from cmask, so every byte the reference reads is the one read here.
+				// store's completion, not only for its own load.
 				uint32_t macc = 0;                                 // the log's current word
+				int nvis = 0;                                      // cells checked (stats)
+				// Per diagonal, not per cell: a diagonal move keeps col - row, so whether the path
+				// is over the core diagonals and whether it runs down the next candidate's
+				// diagonal (cmask) change only with a gap move.
+				uint32_t on_next = col0 - row0 == dnx ? 1u : 0u;
+				uint32_t ocw = (col0 - row0 + (int)p.triml >= 0) & (col0 - row0 + (int)p.triml >= (int)p.corel) &
+				               (col0 - row0 + (int)p.triml <= (int)p.corer);
 				int nm = 0;                                        // moves logged
-				bool end0 = false;                                 // the path reached row 0
+				uint32_t end0 = 0;                                 // the path reached row 0
+// The step in integer arithmetic on 0/1 values (0u - b: a mask): as booleans the
+// conditions live in lane masks, and their nested ifs cost more scalar mask bookkeeping
+// than the work they guard.  Only the gap move, rare across a wave, is a branch.  The log
+// word is stored every step (unchanged when the lane did not move), so the last partial
+// word needs no flush.
 #define BT2X_WALK_STEP(T0, T1, T2, T3, T4, T5, T6, T7)                                                        \
 				{                                                                                     \
-					const uint32_t ctb = T0;                                                          \
-					uint32_t nbo = bo + 4 * kD2;  /* the next ring load; finished lanes: harmless */ \
-					if(fin) {}                                                                        \
-					else if(++steps > budget) { ok = false; fin = true; aborted = true; }             \
-					else if(st_bt++, ctb & TB_MARK) { ok = false; fin = true; }  /* reportedThrough */ \
-					else {                                                                            \
-						const int diag = col - row + (int)p.triml;                                    \
-						over_core |= (diag >= 0) & (diag >= (int)p.corel) & (diag <= (int)p.corer);   \
-						if(row == 0) {                                                                \
-							if(col == dnx && row0 < 8) cmask |= 1u << row0;                           \
-							tb_end = ctb;                                                             \
-							end0 = true;                                                              \
-							fin = true;                                                               \
-						} else {                                                                      \
-							/* the reference's fixed priority over the cell's flags (u8.cpp:843-990): \
-							   H: diag > F (H-up / F-up) > E (H-left / E-left); E/F prefer the open */ \
-							const uint32_t dne = ctb & TB_DNE, fne = (ctb >> 1) & 1u;                 \
-							const uint32_t fext = (ctb >> 2) & 1u, eext = (ctb >> 3) & 1u;            \
-							const bool inH = ct == 2;                                                 \
-							const bool isD = inH && !dne;                                             \
-							const bool isF = (ct == 1) || (inH && dne && !fne);                       \
-							const int nct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);          \
-							/* byte-offset deltas of the moves (tb_addr's pair/step layout) */        \
-							const int st = row + (col & 1);                                           \
-							const int dU = (st & 1) ? -2 : -(4 * G - 2);                              \
-							const int dL = (col & 1) ? ((row & 1) ? -(4 * G - 1) : -3)                \
-							                         : ((row & 1) ? kD1E + 4 * G - 2 : kD1E + 2);     \
-							const uint32_t cbo = bo;                                                  \
-							const int crow = row, ccol = col;                                         \
-							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;                \
-							if(ccol - crow == dnx && row0 - crow < 8) cmask |= 1u << (row0 - crow);   \
-							/* the move, logged (its edit and mark are written after the attempt) */  \
-							{                                                                         \
-								const uint32_t mv = isD ? ((ctb & TB_MM) ? 1u : 0u) : isF ? 2u : 3u;  \
-								macc |= mv << (2 * (nm & 15));                                        \
-								if((nm & 15) == 15) { mlog[(size_t)(nm >> 4) * 64 + lane] = macc; macc = 0; } \
-								nm++;                                                                 \
-							}                                                                         \
-							if(!isD) {                                                                \
-								const bool open = nct == 2;                                           \
-								bscore -= isF ? (open ? rfo : rfe) : (open ? rdo : rde);              \
-								gaps++;                                                               \
-							}                                                                         \
-							if(isD) {                                                                 \
-								bo = cbo + ((ccol & 1) ? kD1O : kD1E);                          \
-							} else {                                                                  \
-								bo = cbo + (isF ? dU : dL);                                           \
-								const int d1 = (col & 1) ? kD1O : kD1E;                         \
-								T1 = tb_load(dirsrc, bo);                  T2 = tb_load(dirsrc, bo + d1); \
-								T3 = tb_load(dirsrc, bo + kD2);         T4 = tb_load(dirsrc, bo + kD2 + d1); \
-								T5 = tb_load(dirsrc, bo + 2 * kD2);     T6 = tb_load(dirsrc, bo + 2 * kD2 + d1); \
-								T7 = tb_load(dirsrc, bo + 3 * kD2);     nbo = bo + 3 * kD2 + d1;    \
-								}                                                                         \
-						}                                                                             \
+					const uint32_t c = T0;                        /* the cell's byte in bits 0-7 */   \
+					const uint32_t go = 1u - fin;                                                     \
+					const uint32_t over = go & ((uint32_t)(budget - 1 - steps) >> 31); /* ++steps > budget */ \
+					steps += (int)go;                                                                 \
+					const uint32_t chk = go & (over ^ 1u);                                            \
+					nvis += (int)chk;                                                                 \
+					const uint32_t live = chk & (((c >> 7) & 1u) ^ 1u);  /* not reportedThrough */   \
+					const uint32_t mk = chk ^ live;                                                   \
+					const uint32_t z = (uint32_t)(row - 1) >> 31;  /* row == 0 */                     \
+					const uint32_t up = (uint32_t)(row0 - row);                                       \
+					cmask |= (live & on_next & ((up - 8u) >> 31)) << (up & 31u);                      \
+					const uint32_t at0 = live & z;                                                    \
+					tb_end |= c & (0u - at0);                                                         \
+					end0 |= at0;                                                                      \
+					const uint32_t mvg = live & (z ^ 1u);                                             \
+					/* the reference's fixed priority over the cell's flags (u8.cpp:843-990): H: \
+					   diag > F (H-up / F-up) > E (H-left / E-left); E/F prefer the open */       \
+					const uint32_t inH = (uint32_t)ct >> 1, inF = (uint32_t)ct & 1u;                  \
+					const uint32_t dne = c & 1u, fne = (c >> 1) & 1u;                                 \
+					const uint32_t isD = inH & (dne ^ 1u);                                            \
+					const uint32_t isF = inF | (inH & dne & (fne ^ 1u));                              \
+					const uint32_t isE = 1u - isD - isF;                                              \
+					const uint32_t nct = (2u & (0u - isD)) | ((2u - ((c >> 2) & 1u)) & (0u - isF)) | ((2u - 2u * ((c >> 3) & 1u)) & (0u - isE)); \
+					const uint32_t ccol = (uint32_t)col;                                              \
+					row -= (int)(mvg & (isD | isF));                                                  \
+					col -= (int)(mvg & (isD | isE));                                                  \
+					ct = (int)(((uint32_t)ct & ~(0u - mvg)) | (nct & (0u - mvg)));                    \
+					/* the move, logged (its edit and mark are written after the attempt) */      \
+					const uint32_t code = (((c >> 4) & 1u) & (0u - isD)) | (2u & (0u - isF)) | (3u & (0u - isE)); \
+					macc |= (code & (0u - mvg)) << (2u * ((uint32_t)nm & 15u));                        \
+					mlog[(size_t)(nm >> 4) * 64 + lane] = macc;                                       \
+					macc &= 0u - (1u - (mvg & (((uint32_t)nm & 15u) == 15u ? 1u : 0u)));             \
+					nm += (int)mvg;                                                                   \
+					const uint32_t gp = mvg & (isD ^ 1u);                                             \
+					{                                                                                 \
+						const uint32_t om = 0u - (nct >> 1), fm = 0u - isF;   /* open, F: masks */    \
+						const uint32_t pf = ((uint32_t)rfo & om) | ((uint32_t)rfe & ~om);              \
+						const uint32_t pe = ((uint32_t)rdo & om) | ((uint32_t)rde & ~om);              \
+						bscore -= (int)(((pf & fm) | (pe & ~fm)) & (0u - gp));                        \
 					}                                                                                 \
-					/* one unconditional def per step: a load under a divergent branch would be \
-					   merged by a register copy, which waits for it */                          \
-					T0 = tb_load(dirsrc, nbo);                                                        \
+					gaps += (int)gp;                                                                  \
+					okw &= (over | mk) ^ 1u;                                                          \
+					abw |= over;                                                                      \
+					fin |= over | mk | at0;                                                           \
+					uint32_t nbo = bo + 4 * kD2;  /* the next ring load; finished lanes: harmless */ \
+					/* a diagonal move: the ring's next cell */                                   \
+					bo += (uint32_t)((ccol & 1u) ? kD1O : kD1E) & (0u - (mvg & isD));                 \
+					if(gp) {                                                                          \
+						bo = tb_off_g<G, PW>(row, col, tbl);                                          \
+						const int d1 = (col & 1) ? kD1O : kD1E;                                       \
+						const int dg = col - row + (int)p.triml;                                      \
+						ocw |= (dg >= 0) & (dg >= (int)p.corel) & (dg <= (int)p.corer);               \
+						on_next = (col - row == dnx) ? 1u : 0u;                                       \
+						T1 = tb_load4(dirsrc, bo);                  T2 = tb_load4(dirsrc, bo + d1);    \
+						T3 = tb_load4(dirsrc, bo + kD2);         T4 = tb_load4(dirsrc, bo + kD2 + d1); \
+						T5 = tb_load4(dirsrc, bo + 2 * kD2);     T6 = tb_load4(dirsrc, bo + 2 * kD2 + d1); \
+						T7 = tb_load4(dirsrc, bo + 3 * kD2);     T0 = tb_load4(dirsrc, bo + 3 * kD2 + d1); \
+					} else {                                                                          \
+						T0 = tb_load4(dirsrc, nbo);                                                   \
+					}                                                                                 \
 				}
 				// lanes that finish idle to the end of the wave's step: the exits are wave-uniform
 				// (no divergent loop exits, whose joins would copy -- and so wait for -- the
-				// ring registers)
+				// ring registers).  Sixteen steps per pass: the compiler waits for every load at
+				// the top of the loop (it does not carry the ring's order across the back edge).
 				while(true) {
-					if(pw) pw[0] += first_active(lane);
+					if(prof) pw_steps += first_active(lane);
+					BT2X_WALK_STEP(q0, q1, q2, q3, q4, q5, q6, q7) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q1, q2, q3, q4, q5, q6, q7, q0) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q2, q3, q4, q5, q6, q7, q0, q1) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q3, q4, q5, q6, q7, q0, q1, q2) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q4, q5, q6, q7, q0, q1, q2, q3) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q5, q6, q7, q0, q1, q2, q3, q4) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q6, q7, q0, q1, q2, q3, q4, q5) if(wave_none(!fin)) break;
+					BT2X_WALK_STEP(q7, q0, q1, q2, q3, q4, q5, q6) if(wave_none(!fin)) break;
 					BT2X_WALK_STEP(q0, q1, q2, q3, q4, q5, q6, q7) if(wave_none(!fin)) break;
 					BT2X_WALK_STEP(q1, q2, q3, q4, q5, q6, q7, q0) if(wave_none(!fin)) break;
 					BT2X_WALK_STEP(q2, q3, q4, q5, q6, q7, q0, q1) if(wave_none(!fin)) break;
@@ -458,10 +508,11 @@ __device__ __forceinline__ void walk_problem(const DevScoring& sc, const uint8_t
 				}
 #undef BT2X_WALK_STEP
 #undef BT2X_RING_LOAD
+				st_bt += (unsigned long long)nvis;
+				ok = okw != 0; aborted = aborted || abw != 0; over_core = ocw != 0;
 if(aborted) break;
 // the attempt's marks and edits, from its move log (the reference's order: an
 // edit per move that records one, in walk order)
-if(nm & 15) mlog[(size_t)(nm >> 4) * 64 + lane] = macc;
 {
 	int r = row0, c = col0;
 	uint32_t b = (uint32_t)tb_addr_g<G, PW>(r, c, tbl), w = 0;
@@ -1091,7 +1142,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 	const uint32_t one2 = opaque(0x00010001u);
 
-	unsigned long long pw[2] = {0, 0}, t_fill = 0, t_walk = 0, ngrp = 0;     // BT2X_DP_PROF
+	unsigned long long pw_steps = 0, pw_iters = 0, t_fill = 0, t_walk = 0, ngrp = 0;     // BT2X_DP_PROF
 	unsigned long long mx_fill = 0, mx_walk = 0, mylen_sum = 0, mylen_max = 0;
 	unsigned long long t_pro = 0, t_pair = 0, t_cand = 0;
 	const unsigned long long t_start = a.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -1501,7 +1552,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			const unsigned long long bt0 = st_bt;
 			walk_problem<64, kPairWords>(sc, pen_lds, a, pi, lane, lane, gslot + kDirOff, kDirBytesLane * 64u, gslot + kCandOff,
 			                             reinterpret_cast<uint32_t*>(wslot + kEditOff), reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff),
-			                             st_bt, refN != 0, lds, a.prof ? pw : nullptr);
+			                             st_bt, refN != 0, lds, a.prof != 0, pw_steps, pw_iters);
 			if(a.prof) {
 				const unsigned long long t2 = __builtin_amdgcn_s_memtime();
 				t_fill += t1 - t0; t_walk += t2 - t1; ngrp++;
@@ -1513,7 +1564,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		}
 	}
 	if(a.prof) {
-		unsigned long long w0 = pw[0], w1 = pw[1], ls = mylen_sum, lm = mylen_max;
+		unsigned long long w0 = pw_steps, w1 = pw_iters, ls = mylen_sum, lm = mylen_max;
 		for(int d = 32; d > 0; d >>= 1) {
 			w0 += __shfl_xor(w0, d); w1 += __shfl_xor(w1, d); ls += __shfl_xor(ls, d);
 			const unsigned long long o = __shfl_xor(lm, d); lm = lm > o ? lm : o;
@@ -1603,6 +1654,7 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 	pen4[lane] = reinterpret_cast<const uint32_t*>(a.mmpen)[lane];
 	__syncthreads();
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0, st_comp = 0;
+	unsigned long long st_dummy0 = 0, st_dummy1 = 0;                 // walk_problem's profiling counters (unused)
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 	const uint32_t one2 = opaque(0x00010001u);
 	unsigned long long t_fill = 0, t_walk = 0, ngrp = 0, mx_fill = 0, mx_walk = 0;     // BT2X_DP_PROF
@@ -1910,7 +1962,7 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 		uint8_t* wslot = gslot + kGroupBytes;
 		walk_problem<kDuoG, kDuoPW>(sc, pen_lds, a, pi, lane, q, gslot + kDuoPairBytes, kDuoDirBytes - kDuoPairBytes,
 		                                cands, reinterpret_cast<uint32_t*>(wslot + kEditOff),
-		                                reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, lds, nullptr);
+		                                reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff), st_bt, refN != 0, lds, false, st_dummy0, st_dummy1);
 		if(a.prof) { const unsigned long long t2 = __builtin_amdgcn_s_memtime(); t_walk += t2 - t1; mx_walk = max(mx_walk, t2 - t1); }
 	}
 	if(a.prof && lane == 0) {
@@ -1946,6 +1998,7 @@ dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 	uint32_t* stage_ed = reinterpret_cast<uint32_t*>(wslot + kEditOff);
 	bt2x_aln_rec* stage_rec = reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff);
 	unsigned long long st_bt = 0;
+	unsigned long long st_dummy0 = 0, st_dummy1 = 0;
 	// one wave per 64-problem group, lane = problem: the lanes' main walks follow nearly
 	// the same diagonal, so their loads of the lane-interleaved bytes share lines
 	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
@@ -1954,7 +2007,7 @@ dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			const uint32_t pi = base + q;
 			uint8_t* gs = a.scratch + (size_t)grp * kGroupBytes;
 			walk_problem<64, kPairWords>(sc, a.mmpen, a, pi, lane, lane, gs + kDirOff, kDirBytesLane * 64u, gs + kCandOff,
-			                             stage_ed, stage_rec, st_bt, true, mlog);
+			                             stage_ed, stage_rec, st_bt, true, mlog, false, st_dummy0, st_dummy1);
 		}
 	}
 	if(a.stats) {

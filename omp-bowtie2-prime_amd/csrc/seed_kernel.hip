@@ -675,11 +675,13 @@ sa_resolve_kernel(DevIndex ix, const bt2x_resolve_in* __restrict__ in, uint32_t 
 
 // The same over a count that lives in HBM (written by the kernel that produced the
 // elements), grid-stride; at most cap elements.  Out: bt2x_resolve_out, or the seed
-// round's 16-byte bt2x_elt.
+// round's 8-byte bt2x_elt.
 __device__ __forceinline__ void put_elt(bt2x_resolve_out* out, uint32_t i, const bt2x_resolve_out& o) { out[i] = o; }
 __device__ __forceinline__ void put_elt(bt2x_elt* out, uint32_t i, const bt2x_resolve_out& o) {
+	// bt2x_elt_pack's layout (bt2x.h): toff bits 0-38, straddled bit 39, tidx bits 40-63
+	const uint64_t t = o.tidx == BT2X_NO_TIDX ? BT2X_ELT_TIDX_NONE : (o.tidx & BT2X_ELT_TIDX_NONE);
 	bt2x_elt e;
-	e.toff = o.toff; e.tidx = o.tidx; e.straddled = o.straddled;
+	e.v = (o.toff & ((1ull << 39) - 1)) | ((uint64_t)(o.straddled & 1u) << 39) | (t << 40);
 	out[i] = e;
 }
 

@@ -670,9 +670,10 @@ int ExtendWalk::next(int64_t minsc, DpKey& k) {
 		neltLeft_--;
 		// (no fragment: tidx, toff and tlen stay 0, the caller's initial values,
 		// aligner_sw_driver.cpp:392)
-		const bool none = wr.tidx == BT2X_NO_TIDX;
-		const int64_t tidx = none ? 0 : (int64_t)wr.tidx;
-		const int64_t toff = (int64_t)wr.toff, tlen = none ? 0 : (int64_t)plen_[wr.tidx];
+		const uint32_t wt = bt2x_elt_tidx(wr);
+		const bool none = wt == BT2X_NO_TIDX;
+		const int64_t tidx = none ? 0 : (int64_t)wt;
+		const int64_t toff = (int64_t)bt2x_elt_toff(wr), tlen = none ? 0 : (int64_t)plen_[wt];
 		const int64_t refoff = toff - (int64_t)rdoff;
 		const Coord refcoord(tidx, refoff, fw);
 		if(seen_->locusPresent(refcoord)) { prm_->nRedundants++; continue; }
@@ -1295,7 +1296,7 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 			c->elts.resize((size_t)(L.rk[r + 1] - L.rk[r]));
 			for(size_t k = 0; k < c->elts.size(); k++) {
 				const bt2x_resolve_out& o = L.res_out[L.rk[r] + k];
-				c->elts[k] = bt2x_elt{o.toff, o.tidx, o.straddled};
+				c->elts[k] = bt2x_elt_pack(o.toff, o.tidx, o.straddled);
 			}
 		} else {
 			const long r = i - nws - nwr;

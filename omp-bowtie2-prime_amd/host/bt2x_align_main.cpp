@@ -29,6 +29,7 @@
 #include <string>
 #include <vector>
 
+#include <csignal>
 #include <sched.h>
 #include <sys/resource.h>
 
@@ -379,7 +380,8 @@ int main(int argc, char** argv) {
 		Aligner al(p, ref, be);
 		al.set_pipeline(pipeline);
 		if(hip2) al.set_second_backend(hip2.get());
-		al.set_gpu_round(gpu_round);
+		// bt2x_elt holds fewer than 2^24 - 1 reference indices: beyond that, the three-request round
+		al.set_gpu_round(gpu_round && ref.nrefs() < BT2X_ELT_TIDX_NONE);
 		al.set_header(hd);
 		pin.join();
 		if(warm_files > 0) {                           // untimed: first launches, page faults, pools
@@ -405,7 +407,12 @@ int main(int argc, char** argv) {
 		std::vector<char> obuf(1 << 24);
 		std::setvbuf(out, obuf.data(), _IOFBF, obuf.size());
 		double t_run = 0;
+		// development: bt2x-align-prof (tools/sprof.c linked in) with SPROF_WAIT=1 samples the
+		// timed run only; SIGUSR2 toggles its sampling
+		const bool sprof = std::getenv("SPROF_WAIT") != nullptr;
+		if(sprof) std::raise(SIGUSR2);
 		const RunStats st = al.run(reader, out, slots, threads, &t_run);
+		if(sprof) std::raise(SIGUSR2);
 		const double t_ret = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
 		if(out != stdout) std::fclose(out); else std::fflush(out);
 		const double t_align = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();

@@ -105,7 +105,7 @@ public:
 		HostVec<bt2x_resolve_out> ro;
 		resolve(HostVec<bt2x_resolve_in>(rows.begin(), rows.end()), ro);
 		elts.resize(ro.size());
-		for(size_t k = 0; k < ro.size(); k++) elts[k] = bt2x_elt{ro[k].toff, ro[k].tidx, ro[k].straddled};
+		for(size_t k = 0; k < ro.size(); k++) elts[k] = bt2x_elt_pack(ro[k].toff, ro[k].tidx, ro[k].straddled);
 	}
 private:
 	const bt2x_index_desc& idx_;

@@ -230,8 +230,8 @@ int main(int argc, char** argv) {
 					if(!hr.empty() && bt2x_resolve(dev.ctx(), hr.data(), (uint32_t)hr.size(), 0, ho.data()) != BT2X_OK) return 1;
 					bool eq = ho.size() == out[r].nelt;
 					for(size_t k = 0; eq && k < ho.size(); k++)
-						eq = ho[k].toff == elts[out[r].elt0 + k].toff && ho[k].tidx == elts[out[r].elt0 + k].tidx &&
-						     ho[k].straddled == elts[out[r].elt0 + k].straddled;
+						eq = ho[k].toff == bt2x_elt_toff(elts[out[r].elt0 + k]) && ho[k].tidx == bt2x_elt_tidx(elts[out[r].elt0 + k]) &&
+						     ho[k].straddled == bt2x_elt_straddled(elts[out[r].elt0 + k]);
 					b.rows = eq ? a.rows : std::vector<uint64_t>{};
 				}
 				std::string why;
