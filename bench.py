@@ -922,6 +922,12 @@ def main():
                        "peak_rss_mib": peak, "summary": bdist.alignment_summary(tot).splitlines(),
                        "stats": stats, "gpu": kv_line(err, "BT2X_GPU"), "rusage_align": kv_line(err, "BT2X_RUSAGE_ALIGN")},
     }
+    # bytes over PCIe in the timed run (every BT2X_GPU *_h2d_mib / *_d2h_mib field: rounds,
+    # DP requests, read-store uploads)
+    g = line["end_to_end"]["gpu"] or {}
+    mib = [float(v) for k, v in g.items() if k.endswith("_h2d_mib") or k.endswith("_d2h_mib")]
+    if mib:
+        line["end_to_end"]["pcie_gb"] = round(sum(mib) / 1024.0, 2)
     # host CPU per read (rank 0's aligner process over its timed files): user + system time
     # of all its threads, and the thread-seconds the run had (threads x t_align)
     ru = line["end_to_end"]["rusage_align"]

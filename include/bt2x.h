@@ -292,7 +292,8 @@ typedef struct {
 } bt2x_dp_debug;
 
 /* Arena capacities are caller-given; on BT2X_E_OVERFLOW *nrec_used / *nedit_used hold
- * the required sizes and the call may be repeated with larger arenas. */
+ * the required sizes and the call may be repeated with larger arenas.  reads == quals ==
+ * NULL: read_off and qual_off index the read store (bt2x_store_reads, below). */
 int bt2x_dp_align(bt2x_ctx* ctx,
                   const uint8_t* reads, uint64_t reads_bytes,
                   const uint8_t* quals, uint64_t quals_bytes,
@@ -328,6 +329,30 @@ int bt2x_dp_align_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const uint8_t* d_qu
                       bt2x_dp_out* d_out, bt2x_aln_rec* d_recs, uint32_t rec_cap,
                       uint32_t* d_edits, uint32_t edit_cap, uint32_t* d_counters,
                       bt2x_dp_debug* d_debug, uint32_t launch_flags, void* stream);
+
+/* ------------------------------------------------------------- read store */
+
+/* A device-resident copy of the reads in flight: a read's codes and qualities cross PCIe
+ * once instead of with every seed round and DP request that needs them (the reference
+ * hands SwAligner::initRead the same Read object for every DP, aligner_sw.cpp:59).  The
+ * store is BT2X_STORE_SLOT_BYTES per slot; slot s holds, from byte s * SLOT_BYTES on, the
+ * read's patFw codes (0-4), its patRc codes, its Phred+33 qualities and the reversed
+ * qualities, rdlen bytes each and in that order.  bt2x_store_reads writes n reads into
+ * their slots: read i's patFw codes at packed[in[i].off], its qualities right after them
+ * (2 * len bytes); the GPU derives patRc and the reversed qualities.  bt2x_seed_round and
+ * bt2x_dp_align called with reads == NULL (and quals == NULL) then take read_off and
+ * qual_off as offsets into the store.  The store grows to the largest slot written and
+ * keeps its contents; calls on the context's stream stay in order. */
+#define BT2X_STORE_SLOT_BYTES 1024u
+#define BT2X_STORE_MAX_LEN 256u
+typedef struct {
+	uint64_t off;            /* packed[off .. +len): patFw codes; [off+len .. +len): quals */
+	uint32_t slot;
+	uint16_t len;            /* 1..BT2X_STORE_MAX_LEN */
+	uint16_t pad;
+} bt2x_store_in;
+int bt2x_store_reads(bt2x_ctx* ctx, const uint8_t* packed, uint64_t packed_bytes, const bt2x_store_in* in,
+                     uint32_t n);
 
 /* Context options.  BT2X_OPT_EXACT_BEST (default 1): bt2x_dp_align reports the exact
  * best of failed problems (one extra unbanded pass over them); 0 when the caller never
@@ -444,7 +469,9 @@ typedef struct {
 	uint16_t interval;       /* msIval(rdlen)                                             */
 	uint16_t offset;         /* this round's offset: interval * round / nrounds           */
 	uint16_t seedlen;        /* multiseedLen clipped to rdlen                              */
-	uint16_t pad[3];
+	uint16_t seedflags;      /* seeds == NULL (below): 1 = no patFw seeds (--nofw), 2 = no
+	                            patRc seeds (--norc)                                        */
+	uint16_t pad[2];
 } bt2x_round_in;
 
 /* extendSeeds' exRange entry: a read span [off, off+len) of strand fw already covered by
@@ -459,13 +486,16 @@ typedef struct {
 
 /* One SATupleAndPos of the read's extension list, in prioritizeSATups order: rand_n BW
  * elements (the whole range when it has <= 5 elements, else one sampled element), seed
- * at read offset rdoff of strand fw. */
+ * of length seedlen at read offset rdoff of strand fw.  4 bytes: fw and seedlen share a
+ * byte (BT2X_SAT_FW / BT2X_SAT_LEN, BT2X_SAT_FWLEN to build it). */
 typedef struct {
-	uint32_t rdoff;
-	uint16_t rand_n;
-	uint8_t  fw;
-	uint8_t  seedlen;
+	uint16_t rdoff;
+	uint8_t  rand_n;
+	uint8_t  fwlen;          /* bit 7: fw; bits 0-6: seedlen */
 } bt2x_sat;
+#define BT2X_SAT_FW(s) ((uint32_t)(s).fwlen >> 7)
+#define BT2X_SAT_LEN(s) ((uint32_t)(s).fwlen & 0x7fu)
+#define BT2X_SAT_FWLEN(fw, len) ((uint8_t)(((fw) ? 0x80u : 0u) | ((uint32_t)(len) & 0x7fu)))
 
 enum { BT2X_ROUND_OK = 0, BT2X_ROUND_NO_HITS = 1, BT2X_ROUND_REDO = 2 };
 
@@ -486,7 +516,12 @@ typedef struct {
 
 /* maxelt: -D ... maxIters (prioritizeSATups' maxelt, 400 by default).  Output arenas are
  * caller-sized; BT2X_E_OVERFLOW reports the required sizes in used[0..2] (sats, elts,
- * exr_out) and the call may be repeated. */
+ * exr_out) and the call may be repeated.  reads == NULL: read_off (of in[] and seeds[])
+ * indexes the read store (bt2x_store_reads).  seeds == NULL: the GPU instantiates every
+ * read's seeds itself, as listed above (patFw seeds, then patRc seeds, each strand at
+ * depths i * interval + offset for i < num_offs, a seed over an N skipped, a strand off
+ * per seedflags), into seeds[seed0 .. +nseeds) of a context-owned array of nseeds entries:
+ * in[r].nseeds must be the count that gives (and the reads' seeds must not overlap). */
 int bt2x_seed_round(bt2x_ctx* ctx, const uint8_t* reads, uint64_t reads_bytes,
                     const bt2x_seed_in* seeds, uint32_t nseeds,
                     const bt2x_round_in* in, uint32_t nreads,
@@ -514,7 +549,8 @@ void  bt2x_host_free(void* p);
 
 const char* bt2x_version(void);
 /* sizeof of the ABI structs (seed_in, seed_out, dp_in, dp_out, aln_rec, scoring,
- * index_desc, counters), for binding self-checks; returns the count. */
+ * index_desc, counters, resolve_in, resolve_out, round_in, round_out, sat, exrange, elt,
+ * store_in), for binding self-checks; returns the count. */
 int bt2x_abi_sizes(uint32_t* out, int n);
 
 #ifdef __cplusplus

@@ -32,12 +32,14 @@ RESOLVE_OUT = np.dtype([("joff", "<u8"), ("toff", "<u8"), ("tlen", "<u8"), ("tid
                         ("straddled", "<u4")], align=True)
 NO_TIDX = 0xFFFFFFFF
 ELT = np.dtype([("v", "<u8")])   # bt2x_elt: toff bits 0-38, straddled bit 39, tidx bits 40-63
+STORE_IN = np.dtype([("off", "<u8"), ("slot", "<u4"), ("len", "<u2"), ("pad", "<u2")], align=True)   # bt2x_store_in
+STORE_SLOT_BYTES = 1024
 ROUND_IN = np.dtype([("read_off", "<u8"), ("seed0", "<u8"), ("rnd_last", "<u4"), ("rnd_lastoff", "<i4"),
                      ("exr0", "<u4"), ("nexr", "<u2"), ("nseeds", "<u2"), ("num_offs", "<u2"),
                      ("rdlen", "<u2"), ("interval", "<u2"), ("offset", "<u2"), ("seedlen", "<u2"),
-                     ("pad", "<u2", 3)], align=True)
+                     ("seedflags", "<u2"), ("pad", "<u2", 2)], align=True)
 EXRANGE = np.dtype([("sz", "<u8"), ("off", "<u4"), ("len", "<u2"), ("fw", "u1"), ("pad", "u1")], align=True)
-SAT = np.dtype([("rdoff", "<u4"), ("rand_n", "<u2"), ("fw", "u1"), ("seedlen", "u1")], align=True)
+SAT = np.dtype([("rdoff", "<u2"), ("rand_n", "u1"), ("fwlen", "u1")], align=True)   # fwlen: fw << 7 | seedlen
 ROUND_OUT = np.dtype([("rnd_last", "<u4"), ("rnd_lastoff", "<i4"), ("num_elts", "<u8"), ("nonz", "<u4"),
                       ("status", "<u4"), ("sat0", "<u4"), ("nsat", "<u4"), ("elt0", "<u4"), ("nelt", "<u4"),
                       ("exr0", "<u4"), ("nexr", "<u4")], align=True)

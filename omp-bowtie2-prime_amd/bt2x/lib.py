@@ -62,6 +62,8 @@ FUNCS = {
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                            ctypes.c_void_p]),
+    "bt2x_store_reads": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_uint32]),
     "bt2x_version": (ctypes.c_char_p, []),
     "bt2x_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
     "bt2x_last_round_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
@@ -172,9 +174,19 @@ class Context:
               "bt2x_seed_search_dev")
 
     # ----------------------------------------------------------------- DP
+    def store_reads(self, packed, inp):
+        """bt2x_store_reads: read i's patFw codes then its qualities at packed[inp[i].off]
+        into store slot inp[i].slot."""
+        packed = np.ascontiguousarray(packed, dtype=np.uint8)
+        inp = np.ascontiguousarray(inp, dtype=abi.STORE_IN)
+        check(load().bt2x_store_reads(self.h, abi.ptr(packed), packed.nbytes, abi.ptr(inp), len(inp)),
+              "bt2x_store_reads")
+
     def dp_align(self, reads, quals, refs, inp, debug=False, rec_cap=None, edit_cap=None):
-        reads = np.ascontiguousarray(reads, dtype=np.uint8)
-        quals = np.ascontiguousarray(quals, dtype=np.uint8)
+        """reads = quals = None: read_off / qual_off index the read store."""
+        store = reads is None and quals is None
+        reads = np.zeros(1, np.uint8) if store else np.ascontiguousarray(reads, dtype=np.uint8)
+        quals = np.zeros(1, np.uint8) if store else np.ascontiguousarray(quals, dtype=np.uint8)
         refs = np.ascontiguousarray(refs, dtype=np.uint8)
         inp = np.ascontiguousarray(inp, dtype=abi.DP_IN)
         n = len(inp)
@@ -187,13 +199,15 @@ class Context:
         dig = np.zeros((n, 3), dtype=np.uint64) if debug else None
         cands = np.zeros((n, abi.MAX_COLS), dtype=np.uint32) if debug else None
         dbg = abi.DpDebug(abi.ptr(dig).value, abi.ptr(cands).value) if debug else None
-        rc = load().bt2x_dp_align(self.h, abi.ptr(reads), reads.nbytes, abi.ptr(quals), quals.nbytes,
+        rc = load().bt2x_dp_align(self.h, None if store else abi.ptr(reads), reads.nbytes,
+                                  None if store else abi.ptr(quals), quals.nbytes,
                                   abi.ptr(refs), refs.nbytes, abi.ptr(inp), n, abi.ptr(out),
                                   abi.ptr(recs), rec_cap, ctypes.byref(nrec), abi.ptr(edits),
                                   edit_cap, ctypes.byref(nedit),
                                   ctypes.byref(dbg) if dbg is not None else None)
         if rc == abi.E_OVERFLOW:
-            return self.dp_align(reads, quals, refs, inp, debug, nrec.value + 64, nedit.value + 1024)
+            return self.dp_align(None if store else reads, None if store else quals, refs, inp, debug,
+                                 nrec.value + 64, nedit.value + 1024)
         check(rc, "bt2x_dp_align")
         return out, recs[: nrec.value], edits[: nedit.value], dig, cands
 
@@ -235,10 +249,13 @@ class Context:
     # ------------------------------------------------------------ seed round
     def seed_round(self, reads, seeds, inp, exr, maxelt, sat_cap=None, elt_cap=None, exr_cap=None):
         """bt2x_seed_round (host buffers) -> (round_out, sats, elts, exr_out); arenas grown
-        and the call repeated once on BT2X_E_OVERFLOW."""
+        and the call repeated once on BT2X_E_OVERFLOW.  seeds = None: the GPU instantiates
+        them (inp's seed0 / nseeds / seedflags)."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)
-        seeds = np.ascontiguousarray(seeds, dtype=abi.SEED_IN)
         inp = np.ascontiguousarray(inp, dtype=abi.ROUND_IN)
+        gen = seeds is None
+        nseeds = int((inp["seed0"] + inp["nseeds"]).max()) if gen and len(inp) else 0
+        seeds = np.zeros(0, dtype=abi.SEED_IN) if gen else np.ascontiguousarray(seeds, dtype=abi.SEED_IN)
         exr = np.ascontiguousarray(exr if len(exr) else np.zeros(0, dtype=abi.EXRANGE), dtype=abi.EXRANGE)
         n = len(inp)
         sat_cap = sat_cap or 16 * n + 1024
@@ -249,11 +266,12 @@ class Context:
         elts = np.zeros(elt_cap, dtype=abi.ELT)
         exro = np.zeros(exr_cap, dtype=abi.EXRANGE)
         used = (ctypes.c_uint32 * 3)()
-        rc = load().bt2x_seed_round(self.h, abi.ptr(reads), reads.nbytes, abi.ptr(seeds), len(seeds), abi.ptr(inp), n,
+        rc = load().bt2x_seed_round(self.h, abi.ptr(reads), reads.nbytes, None if gen else abi.ptr(seeds),
+                                    nseeds if gen else len(seeds), abi.ptr(inp), n,
                                     abi.ptr(exr), len(exr), maxelt, abi.ptr(out), abi.ptr(sats), sat_cap,
                                     abi.ptr(elts), elt_cap, abi.ptr(exro), exr_cap, used)
         if rc == abi.E_OVERFLOW:
-            return self.seed_round(reads, seeds, inp, exr, maxelt, max(sat_cap, used[0]), max(elt_cap, used[1]),
+            return self.seed_round(reads, None if gen else seeds, inp, exr, maxelt, max(sat_cap, used[0]), max(elt_cap, used[1]),
                                    max(exr_cap, used[2]))
         check(rc, "bt2x_seed_round")
         return out, sats[: used[0]], elts[: used[1]], exro[: used[2]]

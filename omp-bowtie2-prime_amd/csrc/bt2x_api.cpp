@@ -164,6 +164,10 @@ struct bt2x_ctx {
 	DevBuf b_rin, b_exr, b_rout, b_sats, b_elts, b_exro, b_used, b_sout, b_rows, b_ws, b_jobs, b_ranges, b_rcnt;
 	const uint32_t* d_resolve_n = nullptr;     // element count of the last round's resolve (HBM)
 	DevBuf scratch, b_fail, b_heavy, b_in2, b_win;         // + DP windows cut from the text (BT2X_DP_REF_TEXT)
+	// the read store (bt2x_store_reads) and its upload staging
+	uint8_t* d_store = nullptr;
+	uint64_t store_bytes = 0;
+	DevBuf b_pack, b_sin, b_gseeds;                         // + seeds instantiated on the GPU
 	uint64_t npat = 0;
 	bool exact_best = true;                    // BT2X_OPT_EXACT_BEST
 	int ncu = 0;
@@ -183,8 +187,9 @@ bt2x_ctx::~bt2x_ctx() {
 	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch, &b_fail, &b_heavy,
 	                 &b_in2, &b_win,
 	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws,
-	                 &b_jobs, &b_ranges, &b_rcnt})
+	                 &b_jobs, &b_ranges, &b_rcnt, &b_pack, &b_sin, &b_gseeds})
 		b->release();
+	if(d_store) (void)hipFree(d_store);
 	if(!shares_index)
 		for(void* p : {d_ebwt, d_ftab, d_eftab, d_blk, d_sa, d_text, d_offs, d_rstarts, d_plen, d_tfirst})
 			if(p) (void)hipFree(p);
@@ -608,7 +613,10 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
                              bt2x_aln_rec* recs, uint32_t rec_cap, uint32_t* nrec_used,
                              uint32_t* edits, uint32_t edit_cap, uint32_t* nedit_used,
                              bt2x_dp_debug* debug) {
-	if(!c || (n && (!reads || !quals || (!refs && refs_bytes) || !in || !out))) return BT2X_E_ARG;
+	// reads == quals == NULL: read_off / qual_off index the read store (bt2x_store_reads)
+	const bool from_store = !reads && !quals;
+	if(from_store) reads_bytes = quals_bytes = c ? c->store_bytes : 0;
+	if(!c || (n && ((!from_store && (!reads || !quals)) || (!refs && refs_bytes) || !in || !out))) return BT2X_E_ARG;
 	if(nrec_used) *nrec_used = 0;
 	if(nedit_used) *nedit_used = 0;
 	if(n == 0) return BT2X_OK;
@@ -629,7 +637,7 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
 	}
 	HIPCHK(hipSetDevice(c->device));
 	int rc;
-	if((rc = c->b_reads.ensure(reads_bytes)) || (rc = c->b_quals.ensure(quals_bytes)) ||
+	if((!from_store && ((rc = c->b_reads.ensure(reads_bytes)) || (rc = c->b_quals.ensure(quals_bytes)))) ||
 	   (rc = c->b_refs.ensure(refs_bytes ? refs_bytes : 1)) || (rc = c->b_in.ensure(sizeof(bt2x_dp_in) * n)) ||
 	   (rc = c->b_out.ensure(sizeof(bt2x_dp_out) * n)) ||
 	   (rc = c->b_recs.ensure(sizeof(bt2x_aln_rec) * (size_t)(rec_cap ? rec_cap : 1))) ||
@@ -643,11 +651,14 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
 		if((rc = c->b_dbg_cand.ensure(sizeof(uint32_t) * BT2X_MAX_COLS * n))) return rc;
 		dd.cands = (uint32_t*)c->b_dbg_cand.p;
 	}
-	HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
-	HIPCHK(hipMemcpyAsync(c->b_quals.p, quals, quals_bytes, hipMemcpyHostToDevice, c->stream));
+	if(!from_store) {
+		HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
+		HIPCHK(hipMemcpyAsync(c->b_quals.p, quals, quals_bytes, hipMemcpyHostToDevice, c->stream));
+	}
 	if(refs_bytes) HIPCHK(hipMemcpyAsync(c->b_refs.p, refs, refs_bytes, hipMemcpyHostToDevice, c->stream));
 	HIPCHK(hipMemcpyAsync(c->b_in.p, in, sizeof(bt2x_dp_in) * n, hipMemcpyHostToDevice, c->stream));
-	rc = bt2x_dp_align_dev(c, (const uint8_t*)c->b_reads.p, (const uint8_t*)c->b_quals.p,
+	rc = bt2x_dp_align_dev(c, from_store ? c->d_store : (const uint8_t*)c->b_reads.p,
+	                       from_store ? c->d_store : (const uint8_t*)c->b_quals.p,
 	                       (const uint8_t*)c->b_refs.p, (const bt2x_dp_in*)c->b_in.p, n,
 	                       (bt2x_dp_out*)c->b_out.p, (bt2x_aln_rec*)c->b_recs.p, rec_cap,
 	                       (uint32_t*)c->b_edits.p, edit_cap, c->d_counters,
@@ -677,7 +688,8 @@ extern "C" int bt2x_abi_sizes(uint32_t* out, int n) {
 	                      (uint32_t)sizeof(bt2x_index_desc), (uint32_t)sizeof(bt2x_counters),
 	                      (uint32_t)sizeof(bt2x_resolve_in), (uint32_t)sizeof(bt2x_resolve_out),
 	                      (uint32_t)sizeof(bt2x_round_in), (uint32_t)sizeof(bt2x_round_out),
-	                      (uint32_t)sizeof(bt2x_sat), (uint32_t)sizeof(bt2x_exrange), (uint32_t)sizeof(bt2x_elt)};
+	                      (uint32_t)sizeof(bt2x_sat), (uint32_t)sizeof(bt2x_exrange), (uint32_t)sizeof(bt2x_elt),
+	                      (uint32_t)sizeof(bt2x_store_in)};
 	const int m = (int)(sizeof s / sizeof s[0]);
 	for(int i = 0; i < n && i < m; i++) out[i] = s[i];
 	return m;
@@ -733,6 +745,12 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	   (rc = c->b_rcnt.ensure(16 * sizeof(uint32_t)))) return rc;
 	uint32_t* cnt = (uint32_t*)c->b_rcnt.p;
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_ROUND][0], s));
+	if(!d_seeds && nseeds) {                         // instantiateSeeds on the GPU
+		if((rc = c->b_gseeds.ensure(sizeof(bt2x_seed_in) * (size_t)nseeds)) ||
+		   (rc = bt2x_launch_seed_gen(d_reads, d_in, nreads, (bt2x_seed_in*)c->b_gseeds.p, nseeds, s)))
+			return rc;
+		d_seeds = (const bt2x_seed_in*)c->b_gseeds.p;
+	}
 	// 1. seed search (searchAllSeedsDoAll)
 	HIPCHK(hipMemsetAsync(c->d_stats, 0, 3 * sizeof(unsigned long long), s));
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_SEED][0], s));
@@ -774,10 +792,13 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
                                bt2x_elt* elts, uint32_t elt_cap,
                                bt2x_exrange* exr_out, uint32_t exr_cap,
                                uint32_t used[3]) {
-	if(!c || !used || (nreads && (!in || !out)) || (nseeds && (!reads || !seeds))) return BT2X_E_ARG;
+	// reads == NULL: read_off indexes the read store (bt2x_store_reads)
+	const bool from_store = !reads;
+	if(from_store) reads_bytes = c ? c->store_bytes : 0;
+	if(!c || !used || (nreads && (!in || !out))) return BT2X_E_ARG;
 	used[0] = used[1] = used[2] = 0;
 	if(nreads == 0) return BT2X_OK;
-	for(uint32_t i = 0; i < nseeds; i++)
+	for(uint32_t i = 0; i < nseeds && seeds; i++)
 		if(seeds[i].seed_len < 1 || seeds[i].seed_len > 32 || seeds[i].read_off + seeds[i].seed_off + seeds[i].seed_len > reads_bytes)
 			return BT2X_E_ARG;
 	for(uint32_t r = 0; r < nreads; r++) {
@@ -785,10 +806,13 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 		if(q.seed0 + q.nseeds > nseeds || (uint64_t)q.exr0 + q.nexr > nexr || q.interval == 0 || q.seedlen == 0 ||
 		   q.read_off + 2ull * q.rdlen > reads_bytes)
 			return BT2X_E_ARG;
+		// seeds instantiated on the GPU: every one inside the read
+		if(!seeds && (q.seedlen > 32 || q.seedlen > q.rdlen || (uint64_t)(q.num_offs ? q.num_offs - 1 : 0) * q.interval + q.offset + q.seedlen > q.rdlen))
+			return BT2X_E_ARG;
 	}
 	HIPCHK(hipSetDevice(c->device));
 	int rc;
-	if((rc = c->b_reads.ensure(reads_bytes ? reads_bytes : 1)) ||
+	if((!from_store && (rc = c->b_reads.ensure(reads_bytes ? reads_bytes : 1))) ||
 	   (rc = c->b_in.ensure(sizeof(bt2x_seed_in) * (size_t)(nseeds ? nseeds : 1))) ||
 	   (rc = c->b_rin.ensure(sizeof(bt2x_round_in) * nreads)) ||
 	   (rc = c->b_exr.ensure(sizeof(bt2x_exrange) * (size_t)(nexr ? nexr : 1))) ||
@@ -797,11 +821,11 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 	   (rc = c->b_elts.ensure(sizeof(bt2x_elt) * (size_t)(elt_cap ? elt_cap : 1))) ||
 	   (rc = c->b_exro.ensure(sizeof(bt2x_exrange) * (size_t)(exr_cap ? exr_cap : 1))) ||
 	   (rc = c->b_used.ensure(4 * sizeof(uint32_t)))) return rc;
-	if(reads_bytes) HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
-	if(nseeds) HIPCHK(hipMemcpyAsync(c->b_in.p, seeds, sizeof(bt2x_seed_in) * nseeds, hipMemcpyHostToDevice, c->stream));
+	if(reads_bytes && !from_store) HIPCHK(hipMemcpyAsync(c->b_reads.p, reads, reads_bytes, hipMemcpyHostToDevice, c->stream));
+	if(nseeds && seeds) HIPCHK(hipMemcpyAsync(c->b_in.p, seeds, sizeof(bt2x_seed_in) * nseeds, hipMemcpyHostToDevice, c->stream));
 	HIPCHK(hipMemcpyAsync(c->b_rin.p, in, sizeof(bt2x_round_in) * nreads, hipMemcpyHostToDevice, c->stream));
 	if(nexr) HIPCHK(hipMemcpyAsync(c->b_exr.p, exr, sizeof(bt2x_exrange) * nexr, hipMemcpyHostToDevice, c->stream));
-	rc = bt2x_seed_round_dev(c, (const uint8_t*)c->b_reads.p, (const bt2x_seed_in*)c->b_in.p, nseeds,
+	rc = bt2x_seed_round_dev(c, from_store ? c->d_store : (const uint8_t*)c->b_reads.p, seeds ? (const bt2x_seed_in*)c->b_in.p : nullptr, nseeds,
 	                         (const bt2x_round_in*)c->b_rin.p, nreads, (const bt2x_exrange*)c->b_exr.p, maxelt,
 	                         (bt2x_round_out*)c->b_rout.p, (bt2x_sat*)c->b_sats.p, sat_cap,
 	                         (bt2x_elt*)c->b_elts.p, elt_cap, (bt2x_exrange*)c->b_exro.p, exr_cap,
@@ -815,6 +839,39 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 	if(used[1]) HIPCHK(hipMemcpyAsync(elts, c->b_elts.p, sizeof(bt2x_elt) * used[1], hipMemcpyDeviceToHost, c->stream));
 	if(used[2]) HIPCHK(hipMemcpyAsync(exr_out, c->b_exro.p, sizeof(bt2x_exrange) * used[2], hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(stream_wait(c));
+	return BT2X_OK;
+}
+
+extern "C" int bt2x_store_reads(bt2x_ctx* c, const uint8_t* packed, uint64_t packed_bytes, const bt2x_store_in* in,
+                                uint32_t n) {
+	if(!c || (n && (!packed || !in))) return BT2X_E_ARG;
+	if(n == 0) return BT2X_OK;
+	uint32_t top = 0;
+	for(uint32_t i = 0; i < n; i++) {
+		if(in[i].len < 1 || in[i].len > BT2X_STORE_MAX_LEN || in[i].off + 2ull * in[i].len > packed_bytes) return BT2X_E_ARG;
+		top = std::max(top, in[i].slot);
+	}
+	HIPCHK(hipSetDevice(c->device));
+	const uint64_t need = ((uint64_t)top + 1) * BT2X_STORE_SLOT_BYTES;
+	if(need > c->store_bytes) {                      // grow, keeping the slots already written
+		const uint64_t want = std::max<uint64_t>(need + need / 4, (uint64_t)1 << 20);
+		void* p = nullptr;
+		if(hipMalloc(&p, want) != hipSuccess) return BT2X_E_NOMEM;
+		if(c->d_store) {
+			HIPCHK(hipMemcpyAsync(p, c->d_store, c->store_bytes, hipMemcpyDeviceToDevice, c->stream));
+			HIPCHK(hipStreamSynchronize(c->stream));
+			(void)hipFree(c->d_store);
+		}
+		c->d_store = (uint8_t*)p;
+		c->store_bytes = want;
+	}
+	int rc;
+	if((rc = c->b_pack.ensure(packed_bytes)) || (rc = c->b_sin.ensure(sizeof(bt2x_store_in) * n))) return rc;
+	HIPCHK(hipMemcpyAsync(c->b_pack.p, packed, packed_bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->b_sin.p, in, sizeof(bt2x_store_in) * n, hipMemcpyHostToDevice, c->stream));
+	if((rc = bt2x_launch_store((const uint8_t*)c->b_pack.p, (const bt2x_store_in*)c->b_sin.p, n, c->d_store, c->stream)))
+		return rc;
+	HIPCHK(stream_wait(c));                          // the caller may reuse `packed` on return
 	return BT2X_OK;
 }
 

@@ -53,6 +53,9 @@ int bt2x_build_sa(const DevIndex& ix, const uint64_t* d_offs, uint64_t noffs, ui
 int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed_in* d_in,
                      uint32_t n, int do_extend, bt2x_seed_out* d_out,
                      unsigned long long* d_ctr, int ncu, void* stream);
+// a seed round's seeds instantiated on the GPU (bt2x_seed_round with seeds == NULL)
+int bt2x_launch_seed_gen(const uint8_t* d_reads, const bt2x_round_in* d_in, uint32_t nreads, bt2x_seed_in* d_seeds,
+                         uint32_t nseeds, void* stream);
 
 int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_t n, int reject,
                         bt2x_resolve_out* d_out, unsigned long long* d_ctr, void* stream);
@@ -89,6 +92,9 @@ size_t bt2x_round_job_bytes();
 size_t bt2x_round_range_bytes();
 uint32_t bt2x_round_lanes(int ncu);
 int bt2x_launch_round(const RoundLaunch& a, void* stream);
+// read store (bt2x_store_reads): n packed reads into their BT2X_STORE_SLOT_BYTES slots
+int bt2x_launch_store(const uint8_t* d_packed, const bt2x_store_in* d_in, uint32_t n, uint8_t* d_store,
+                      void* stream);
 
 struct DpLaunch {
 	const uint8_t* reads; const uint8_t* quals; const uint8_t* refs;

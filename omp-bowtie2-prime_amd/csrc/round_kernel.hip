@@ -102,7 +102,7 @@ round_prep_kernel(RoundLaunch a) {
 				for(uint32_t i = 0; i < p.nsmallSat; i++) {
 					const Range& rg = w.r2[i];
 					bt2x_sat s;
-					s.rdoff = rg.rdoff; s.rand_n = (uint16_t)rg.size; s.fw = rg.fw; s.seedlen = (uint8_t)L;
+					s.rdoff = (uint16_t)rg.rdoff; s.rand_n = (uint8_t)rg.size; s.fwlen = BT2X_SAT_FWLEN(rg.fw, L);
 					a.sats[o.sat0 + i] = s;
 					for(uint32_t k = 0; k < (uint32_t)rg.size; k++) {
 						bt2x_resolve_in ri;
@@ -563,7 +563,7 @@ round_sample_kernel(RoundLaunch a) {
 		const bool ok = sample_wave(j.nb, j.nsamples, rnd, w, co, jA, jC, stats, [&](uint64_t k, const Range& rg, uint16_t elt) {
 			if(!fits) return;
 			bt2x_sat s;
-			s.rdoff = rg.rdoff; s.rand_n = 1; s.fw = rg.fw; s.seedlen = (uint8_t)j.seedlen;
+			s.rdoff = (uint16_t)rg.rdoff; s.rand_n = 1; s.fwlen = BT2X_SAT_FWLEN(rg.fw, j.seedlen);
 			a.sats[j.sat_base + k] = s;
 			bt2x_resolve_in ri;
 			ri.row = rg.topf + elt; ri.qlen = j.seedlen; ri.pad = 0;

@@ -93,7 +93,35 @@ __global__ void __launch_bounds__(256) window_kernel(DevIndex ix, const bt2x_dp_
 	}
 }
 
+// Read store (bt2x_store_reads): one wave per read; lane k takes bytes k, k + 64, ... of
+// the read: patFw and the qualities as sent, patRc (complement, N stays N) and the
+// reversed qualities mirrored (Read::constructRevComps / constructReverses, read.h).
+__global__ void __launch_bounds__(256) store_kernel(const uint8_t* __restrict__ packed,
+                                                   const bt2x_store_in* __restrict__ in, uint32_t n,
+                                                   uint8_t* __restrict__ store) {
+	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+	if(i >= n) return;
+	const bt2x_store_in q = in[i];
+	const uint32_t len = q.len;
+	const uint8_t* src = packed + q.off;
+	uint8_t* dst = store + (size_t)q.slot * BT2X_STORE_SLOT_BYTES;
+	for(uint32_t k = lane; k < len; k += 64u) {
+		const uint8_t c = src[k], ql = src[len + k];
+		dst[k] = c;
+		dst[2 * len - 1 - k] = c < 4 ? (uint8_t)(3 - c) : c;
+		dst[2 * len + k] = ql;
+		dst[4 * len - 1 - k] = ql;
+	}
+}
+
 } // namespace
+
+int bt2x_launch_store(const uint8_t* d_packed, const bt2x_store_in* d_in, uint32_t n, uint8_t* d_store,
+                      void* stream) {
+	if(n == 0) return BT2X_OK;
+	hipLaunchKernelGGL(store_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, d_packed, d_in, n, d_store);
+	return hipGetLastError() == hipSuccess ? BT2X_OK : BT2X_E_NODEVICE;
+}
 
 int bt2x_launch_windows(const DevIndex& ix, const bt2x_dp_in* d_in, uint32_t n, const uint8_t* d_refs,
                         bt2x_dp_in* d_out, uint8_t* d_win, void* stream) {

@@ -662,9 +662,9 @@ int ExtendWalk::next(int64_t minsc, DpKey& k) {
 		if(prm_->nExIters >= P.mxIter) return EXTEND_EXCEEDED_HARD_LIMIT;
 		prm_->nExIters++;
 		first_ = false;
-		const bool fw = sp.fw != 0;
+		const bool fw = BT2X_SAT_FW(sp) != 0;
 		uint32_t rdoff = sp.rdoff;
-		if(!fw) rdoff = (uint32_t)(rdlen_ - rdoff - sp.seedlen);
+		if(!fw) rdoff = (uint32_t)(rdlen_ - rdoff - BT2X_SAT_LEN(sp));
 		const uint16_t elt = rands_[i_].next(*rnd_);
 		const bt2x_elt& wr = (*res_)[(*firstRow_)[i_] + elt];
 		neltLeft_--;
@@ -774,7 +774,7 @@ void host_round(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_see
 	const size_t sat0 = sats.size();
 	auto emit = [&](const SatPos& sp, uint64_t first, uint32_t n) {
 		bt2x_sat st;
-		st.rdoff = sp.rdoff; st.rand_n = (uint16_t)n; st.fw = sp.fw ? 1 : 0; st.seedlen = (uint8_t)L;
+		st.rdoff = (uint16_t)sp.rdoff; st.rand_n = (uint8_t)n; st.fwlen = BT2X_SAT_FWLEN(sp.fw, L);
 		sats.push_back(st);
 		for(uint32_t e = 0; e < n; e++) {
 			bt2x_resolve_in ri;
@@ -893,6 +893,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		q.rnd_last = rnd.last; q.rnd_lastoff = rnd.lastOff;
 		q.nseeds = (uint16_t)c->seed_in.size(); q.num_offs = (uint16_t)nseeds; q.rdlen = (uint16_t)rdlen;
 		q.interval = (uint16_t)interval; q.offset = (uint16_t)offset; q.seedlen = (uint16_t)L;
+		q.seedflags = (uint16_t)((P.nofw ? 1 : 0) | (P.norc ? 2 : 0));
 		q.nexr = (uint16_t)c->exRange.size();
 		c->sats.clear(); c->exNew.clear();
 		bool redo = !gpu_round_;
@@ -1077,11 +1078,14 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 	const long nch = (n + kChunk - 1) / kChunk;
 	if((long)L.chunks.size() < nch) L.chunks.resize((size_t)nch);
 	const bool ref_index = be_.ref_from_index();
+	const bool store = be_.read_store();
+	const bool dseeds = be_.device_seeds();
 	PH_START();
 	pool().parallel_for(nch, 1, [&](long ch) {
 		Launch::Chunk& C = L.chunks[(size_t)ch];
 		C.ws.clear(); C.wr.clear(); C.wd.clear(); C.wn.clear();
 		C.sbytes = C.nseed = C.nres = C.dbytes = C.nprob = C.rbytes = C.nbytes = C.nnseed = C.nexr = 0;
+		C.pbytes = C.nput = 0;
 		const long e = std::min(n, (ch + 1) * kChunk);
 		const bool pf = host_prefetch();
 		for(long i = ch * kChunk; i < e; i++) {
@@ -1092,29 +1096,36 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			} else if(c->req == REQ_RESOLVE) {
 				C.wr.push_back(c); C.nres += c->res_in.size();
 			} else if(c->req == REQ_DP) {
-				C.wd.push_back(c); C.dbytes += 2 * c->rd.length(); C.nprob += c->dps.size();
+				C.wd.push_back(c); C.nprob += c->dps.size();
+				if(!store) C.dbytes += 2 * c->rd.length();
 				if(!ref_index) for(const DpWork& d : c->dps) C.rbytes += d.key.ncol;
 			} else if(c->req == REQ_ROUND) {
-				C.wn.push_back(c); C.nbytes += 2 * c->rd.length(); C.nnseed += c->seed_in.size();
+				C.wn.push_back(c); C.nnseed += c->seed_in.size();
+				if(!store) C.nbytes += 2 * c->rd.length();
 				C.nexr += c->exRange.size();
 			}
+			// a read a round or DP request brings to the store for the first time
+			c->put_now = store && !c->in_store && (c->req == REQ_DP || c->req == REQ_ROUND);
+			if(c->put_now) { C.pbytes += 2 * c->rd.length(); C.nput++; }
 		}
 	});
 	PH(10);
 	// chunk bases
 	uint64_t nws = 0, nwr = 0, nwd = 0, sb = 0, sk = 0, rk = 0, db = 0, pk = 0, rb = 0;
-	uint64_t nwn = 0, nb = 0, nk = 0, ne = 0;
+	uint64_t nwn = 0, nb = 0, nk = 0, ne = 0, ppb = 0, npt = 0;
 	for(long ch = 0; ch < nch; ch++) {
 		Launch::Chunk& C = L.chunks[(size_t)ch];
 		C.ws0 = nws; C.sb0 = sb; C.sk0 = sk; C.wr0 = nwr; C.rk0 = rk; C.wd0 = nwd; C.db0 = db; C.pk0 = pk; C.rb0 = rb;
-		C.wn0 = nwn; C.nb0 = nb; C.nk0 = nk; C.ne0 = ne;
+		C.wn0 = nwn; C.nb0 = nb; C.nk0 = nk; C.ne0 = ne; C.pb0 = ppb; C.np0 = npt;
+		ppb += C.pbytes; npt += C.nput;
 		nws += C.ws.size(); sb += C.sbytes; sk += C.nseed;
 		nwr += C.wr.size(); rk += C.nres;
 		nwd += C.wd.size(); db += C.dbytes; pk += C.nprob; rb += C.rbytes;
 		nwn += C.wn.size(); nb += C.nbytes; nk += C.nnseed; ne += C.nexr;
 	}
 	L.ws.resize(nws); L.wr.resize(nwr); L.wd.resize(nwd); L.wn.resize(nwn);
-	L.round_reads.resize(nb); L.round_seeds.resize(nk); L.round_in.resize(nwn); L.round_exr.resize(ne);
+	L.round_reads.resize(nb); L.round_seeds.resize(dseeds ? 0 : nk); L.round_in.resize(nwn); L.round_exr.resize(ne);
+	L.n_round_seeds = nk;
 	L.sr.resize(nws + 1); L.sk.resize(nws + 1); L.rk.resize(nwr + 1);
 	L.qb.resize(nwd + 1); L.pb.resize(nwd + 1); L.fb.resize(pk + 1);
 	L.sr[nws] = sb; L.sk[nws] = sk; L.rk[nwr] = rk; L.qb[nwd] = db; L.pb[nwd] = pk; L.fb[pk] = rb;
@@ -1122,8 +1133,24 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 	L.seed_reads.resize(sb); L.seed_in.resize(sk);
 	L.res_in.resize(rk);
 	L.dp_reads.resize(db); L.dp_quals.resize(db); L.dp_refs.resize(rb); L.dp_in.resize(pk);
+	L.store_packed.resize(ppb); L.store_in.resize(npt);
 	pool().parallel_for(nch, 1, [&](long ch) {
 		const Launch::Chunk& C = L.chunks[(size_t)ch];
+		// read-store puts: the read's patFw codes then its qualities (the GPU derives the
+		// reverse complement and the reversed qualities); rounds and DP requests run on
+		// rdlen <= BT2X_MAX_ROWS reads only, within BT2X_STORE_MAX_LEN
+		uint64_t ppo = C.pb0, pno = C.np0;
+		auto put = [&](ReadCtx* c) {
+			const size_t len = c->rd.length();
+			uint8_t* d = L.store_packed.data() + ppo;
+			std::memcpy(d, c->rd.fw.data(), len);
+			std::memcpy(d + len, c->rd.qual.data(), len);
+			bt2x_store_in si;
+			si.off = ppo; si.slot = c->slot; si.len = (uint16_t)len; si.pad = 0;
+			L.store_in[pno++] = si;
+			ppo += 2 * len;
+			c->in_store = true;
+		};
 		// seeds: patFw+patRc of each read, then its seeds with read_off rebased
 		uint64_t sbo = C.sb0, sko = C.sk0;
 		for(size_t k = 0; k < C.ws.size(); k++) {
@@ -1161,14 +1188,24 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			}
 			const size_t i = C.wd0 + k, len = c->rd.length();
 			L.wd[i] = c; L.qb[i] = dbo; L.pb[i] = pko;
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)dbo);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.dp_reads.begin() + (long)(dbo + len));
-			// (memcpy: char -> uint8_t through std::copy is a scalar byte loop)
-			std::memcpy(L.dp_quals.data() + dbo, c->rd.qual.data(), len);
-			std::memcpy(L.dp_quals.data() + dbo + len, c->rd.qualRev.data(), len);
+			if(!store) {
+				std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.dp_reads.begin() + (long)dbo);
+				std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.dp_reads.begin() + (long)(dbo + len));
+				// (memcpy: char -> uint8_t through std::copy is a scalar byte loop)
+				std::memcpy(L.dp_quals.data() + dbo, c->rd.qual.data(), len);
+				std::memcpy(L.dp_quals.data() + dbo + len, c->rd.qualRev.data(), len);
+			} else if(c->put_now) {
+				put(c);
+			}
+			const uint64_t sbase = (uint64_t)c->slot * BT2X_STORE_SLOT_BYTES;
 			for(const DpWork& d : c->dps) {
 				bt2x_dp_in q = d.in;
-				q.read_off = q.qual_off = dbo + (d.key.fw ? 0 : len);
+				if(store) {                              // store slot: patFw, patRc, qual, qualRev
+					q.read_off = sbase + (d.key.fw ? 0 : len);
+					q.qual_off = sbase + 2 * len + (d.key.fw ? 0 : len);
+				} else {
+					q.read_off = q.qual_off = dbo + (d.key.fw ? 0 : len);
+				}
 				L.fb[pko] = rbo;
 				if(ref_index) {                          // the backend cuts the window from the index
 					q.ref_off = (uint64_t)d.key.tidx;
@@ -1180,7 +1217,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 				}
 				L.dp_in[pko++] = q;
 			}
-			dbo += 2 * len;
+			if(!store) dbo += 2 * len;
 		}
 		// seed rounds: the read, its seeds rebased, its round header, its exRange entries
 		uint64_t nbo = C.nb0, nko = C.nk0, neo = C.ne0;
@@ -1193,19 +1230,29 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			}
 			const size_t i = C.wn0 + k, len = c->rd.length();
 			L.wn[i] = c;
-			std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.round_reads.begin() + (long)nbo);
-			std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.round_reads.begin() + (long)(nbo + len));
+			uint64_t roff = nbo;
+			if(!store) {
+				std::copy(c->rd.fw.begin(), c->rd.fw.end(), L.round_reads.begin() + (long)nbo);
+				std::copy(c->rd.rc.begin(), c->rd.rc.end(), L.round_reads.begin() + (long)(nbo + len));
+				nbo += 2 * len;
+			} else {
+				if(c->put_now) put(c);
+				roff = (uint64_t)c->slot * BT2X_STORE_SLOT_BYTES;
+			}
 			bt2x_round_in q = c->round_in;
-			q.read_off = nbo; q.seed0 = nko; q.exr0 = (uint32_t)neo; q.nexr = (uint16_t)c->exRange.size();
+			q.read_off = roff; q.seed0 = nko; q.exr0 = (uint32_t)neo; q.nexr = (uint16_t)c->exRange.size();
 			L.round_in[i] = q;
-			for(const bt2x_seed_in& q0 : c->seed_in) {
-				bt2x_seed_in sq = q0;
-				sq.read_off += nbo;
-				L.round_seeds[nko++] = sq;
+			if(dseeds) {
+				nko += c->seed_in.size();                // (instantiated again on the GPU, same order)
+			} else {
+				for(const bt2x_seed_in& q0 : c->seed_in) {
+					bt2x_seed_in sq = q0;
+					sq.read_off += roff;
+					L.round_seeds[nko++] = sq;
+				}
 			}
 			std::copy(c->exRange.begin(), c->exRange.end(), L.round_exr.begin() + (long)neo);
 			neo += c->exRange.size();
-			nbo += 2 * len;
 		}
 	});
 	PH(12);
@@ -1217,6 +1264,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 void Aligner::execute(Launch& L) {
 	Backend& be = (be2_ && &L == &launch_[1]) ? *be2_ : be_;
 	L.t_seed = L.t_resolve = L.t_dp = L.t_round = 0;
+	if(!L.store_in.empty()) be.store_put(L.store_packed, L.store_in);   // before the requests that read them
 	if(!L.wn.empty()) {
 		const double t0 = now_s();
 		be.seed_round(L.round_reads, L.round_seeds, L.round_in, L.round_exr, (uint32_t)p_.mxIter, L.round_out,
@@ -1245,7 +1293,7 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	const long nws = (long)L.ws.size(), nwr = (long)L.wr.size(), nwd = (long)L.wd.size(), nwn = (long)L.wn.size();
 	if(nwn) {
 		st.round_launches++; st.rounds += (uint64_t)nwn; st.t_round += L.t_round;
-		st.seeds += L.round_seeds.size();
+		st.seeds += L.n_round_seeds;
 		for(const bt2x_round_out& o : L.round_out) st.resolves += o.nelt;
 	}
 	if(nws) { st.seed_launches++; st.seeds += L.seed_in.size(); st.t_seed += L.t_seed; }
@@ -1528,6 +1576,7 @@ void Aligner::use_threads(int threads) {
 ReadCtx* Aligner::take_ctx() {
 	if(free_.empty()) {
 		ctxs_.emplace_back(new ReadCtx);
+		ctxs_.back()->slot = (uint32_t)(ctxs_.size() - 1);
 		return ctxs_.back().get();
 	}
 	ReadCtx* c = free_.back();
@@ -1595,7 +1644,8 @@ std::vector<size_t> Aligner::launch_buffer_bytes(const Params& p, size_t reads) 
 	return {z.nr * 320, z.nr * 24 * sizeof(bt2x_seed_in), z.nr * sizeof(bt2x_round_in), z.nr * 4 * sizeof(bt2x_exrange),
 	        z.nr * sizeof(bt2x_round_out), z.nr * 64 * sizeof(bt2x_sat), z.nr * 64 * sizeof(bt2x_elt),
 	        z.nr * 4 * sizeof(bt2x_exrange), z.nd * 320, z.nd * 320, z.np * 210, z.np * sizeof(bt2x_dp_in),
-	        z.np * sizeof(bt2x_dp_out), (z.np * 4 + 64) * sizeof(bt2x_aln_rec), (z.np * 48 + 256) * sizeof(uint32_t)};
+	        z.np * sizeof(bt2x_dp_out), (z.np * 4 + 64) * sizeof(bt2x_aln_rec), (z.np * 48 + 256) * sizeof(uint32_t),
+	        z.nd * 320, z.nd * sizeof(bt2x_store_in)};
 }
 
 void Aligner::reserve_launch_buffers(size_t reads) {
@@ -1606,6 +1656,7 @@ void Aligner::reserve_launch_buffers(size_t reads) {
 		L.round_elts.reserve(z.nr * 64); L.round_exr_out.reserve(z.nr * 4);
 		L.dp_reads.reserve(z.nd * 320); L.dp_quals.reserve(z.nd * 320); L.dp_refs.reserve(z.np * 210);
 		L.dp_in.reserve(z.np); L.dp_out.reserve(z.np); L.recs.reserve(z.np * 4 + 64); L.edits.reserve(z.np * 48 + 256);
+		L.store_packed.reserve(z.nd * 320); L.store_in.reserve(z.nd);
 	}
 }
 
@@ -1700,6 +1751,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 				__builtin_prefetch(r3.name.data(), 1);
 			}
 			FastqReader::decode(src[i], c->rd, rdid + (uint64_t)i, p_.randSeed, rdid0 + rdid + (uint64_t)i);
+			c->in_store = false;
 			c->task = align_read(c);
 			c->task.h.resume();
 		});
@@ -1810,6 +1862,7 @@ std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threa
 		ring.reserve(next);
 		const long nf = (long)fresh.size();
 		pool().parallel_for(nf, 64, [&](long i) {
+			fresh[i]->in_store = false;
 			fresh[i]->task = align_read(fresh[i]);
 			fresh[i]->task.h.resume();
 		});

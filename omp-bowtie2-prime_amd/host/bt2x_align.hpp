@@ -1018,6 +1018,10 @@ struct ReadCtx {
 	uint64_t ndp_used = 0;          // DP results the walk consumed (the rest were lookahead)
 	uint64_t ntight = 0;            // nextAlignment records consumed after -M tightened minsc
 	                                // within the same DP problem
+	// the backend's read store (Backend::read_store): this context's slot, whether the
+	// current read is in it, and whether the launch being gathered puts it there
+	uint32_t slot = 0;
+	bool in_store = false, put_now = false;
 	// the coroutine frame (ReadTask::promise_type::operator new)
 	static constexpr size_t kFrameBytes = 1536;     // align_read's frame is ~1.25 KiB
 	alignas(std::max_align_t) unsigned char frame_[kFrameBytes];
@@ -1054,6 +1058,15 @@ public:
 	// true: DP problems name their reference window (BT2X_DP_REF_TEXT: ref_off = tidx) and
 	// the backend cuts it from the index; false: the driver fills refs (RefInfo::stretch)
 	virtual bool ref_from_index() const { return false; }
+	// true: the backend keeps the reads in flight in a device-resident store
+	// (bt2x_store_reads): store_put uploads a launch's new reads (patFw codes then
+	// qualities, packed per in[i]) before its requests, and seed_round / dp_align then get
+	// empty reads (and quals) and read_off / qual_off index the store's slots
+	virtual bool read_store() const { return false; }
+	// true: seed_round gets no seeds (bt2x_seed_round with seeds == NULL: the GPU
+	// instantiates them, round_in's seed0 / nseeds / seedflags as the driver set them)
+	virtual bool device_seeds() const { return false; }
+	virtual void store_put(const HostVec<uint8_t>& packed, const HostVec<bt2x_store_in>& in) { (void)packed; (void)in; }
 };
 
 // -------------------------------------------------------------------- driver
@@ -1135,13 +1148,17 @@ private:
 		HostVec<bt2x_round_out> round_out;
 		HostVec<bt2x_sat> round_sats;
 		HostVec<bt2x_elt> round_elts;
+		uint64_t n_round_seeds = 0;                      // the round's seeds (sent or instantiated on the GPU)
+		HostVec<uint8_t> store_packed;                   // the launch's new reads for the read store
+		HostVec<bt2x_store_in> store_in;
 		double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_gather = 0;
 		// gather's per-chunk lists, sizes and bases
 		struct Chunk {
 			std::vector<ReadCtx*> ws, wr, wd, wn;
 			uint64_t sbytes = 0, nseed = 0, nres = 0, dbytes = 0, nprob = 0, rbytes = 0, nbytes = 0, nnseed = 0, nexr = 0;
+			uint64_t pbytes = 0, nput = 0;               // read-store puts
 			uint64_t ws0 = 0, sb0 = 0, sk0 = 0, wr0 = 0, rk0 = 0, wd0 = 0, db0 = 0, pk0 = 0, rb0 = 0;
-			uint64_t wn0 = 0, nb0 = 0, nk0 = 0, ne0 = 0;
+			uint64_t wn0 = 0, nb0 = 0, nk0 = 0, ne0 = 0, pb0 = 0, np0 = 0;
 		};
 		std::vector<Chunk> chunks;
 	};

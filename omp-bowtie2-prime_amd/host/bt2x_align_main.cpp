@@ -85,6 +85,16 @@ public:
 		uint32_t caps = 0;
 		bt2x::check(bt2x_capabilities(ctx, &caps), "bt2x_capabilities");
 		ref_text_ = (caps & BT2X_CAP_REF_TEXT) != 0 && !(std::getenv("BT2X_HOST_WINDOWS") && std::getenv("BT2X_HOST_WINDOWS")[0] == '1');
+		const char* st = std::getenv("BT2X_READ_STORE");          // 0: reads travel with every request
+		store_ = !(st && st[0] == '0');
+		const char* hs = std::getenv("BT2X_HOST_SEEDS");          // 1: the driver's seed lists are sent
+		dseeds_ = !(hs && hs[0] == '1');
+	}
+	bool read_store() const override { return store_; }
+	bool device_seeds() const override { return dseeds_; }
+	void store_put(const HostVec<uint8_t>& packed, const HostVec<bt2x_store_in>& in) override {
+		bt2x::check(bt2x_store_reads(ctx_, packed.data(), packed.size(), in.data(), (uint32_t)in.size()), "bt2x_store_reads");
+		gs.store_h2d += packed.size() + in.size() * sizeof(bt2x_store_in);
 	}
 	// DP windows cut on the GPU from the resident text (BT2X_DP_REF_TEXT), unless the
 	// context lacks it or BT2X_HOST_WINDOWS=1 asks for host-side windows
@@ -106,6 +116,8 @@ public:
 		const auto t0 = std::chrono::steady_clock::now();
 		const uint32_t n = (uint32_t)in.size();
 		out.resize(n);
+		uint32_t nseeds = 0;                             // the GPU-instantiated seeds' array
+		for(const bt2x_round_in& q : in) nseeds = std::max<uint32_t>(nseeds, (uint32_t)(q.seed0 + q.nseeds));
 		// arenas sized from the last launch's use per read (grown and retried on overflow)
 		uint32_t used[3] = {0, 0, 0};
 		// (at least the buffers' reserved capacity: a retry re-runs the whole round)
@@ -114,7 +126,10 @@ public:
 		                   (uint32_t)std::max<size_t>(4 * (size_t)n + 256, exr_out.capacity())};
 		for(int attempt = 0; attempt < 2; attempt++) {
 			sats.resize(cap[0]); elts.resize(cap[1]); exr_out.resize(cap[2]);
-			const int rc = bt2x_seed_round(ctx_, reads.data(), reads.size(), seeds.data(), (uint32_t)seeds.size(), in.data(),
+			// (empty reads: the read store; no seeds: instantiated on the GPU -- a DumpBackend
+			// over this one sends both)
+			const int rc = bt2x_seed_round(ctx_, reads.empty() ? nullptr : reads.data(), reads.size(),
+			                               seeds.empty() ? nullptr : seeds.data(), seeds.empty() ? nseeds : (uint32_t)seeds.size(), in.data(),
 			                               n, exr.data(), (uint32_t)exr.size(), maxelt, out.data(), sats.data(), cap[0],
 			                               elts.data(), cap[1], exr_out.data(), cap[2], used);
 			if(rc == BT2X_E_OVERFLOW && attempt == 0) {
@@ -150,7 +165,8 @@ public:
 			recs.resize(rec_cap);
 			edits.resize(edit_cap);
 			uint32_t nrec = 0, ned = 0;
-			const int rc = bt2x_dp_align(ctx_, reads.data(), reads.size(), quals.data(), quals.size(),
+			const int rc = bt2x_dp_align(ctx_, reads.empty() ? nullptr : reads.data(), reads.size(),
+			                             quals.empty() ? nullptr : quals.data(), quals.size(),
 			                             refs.data(), refs.size(), in.data(), n, out.data(), recs.data(), rec_cap,
 			                             &nrec, edits.data(), edit_cap, &ned, nullptr);
 			if(rc == BT2X_E_OVERFLOW && attempt == 0) { rec_cap = nrec; edit_cap = ned; gs.retries++; continue; }
@@ -166,11 +182,11 @@ public:
 	}
 	struct GpuStats {                      // kernel time and bytes over PCIe, per request kind
 		double k_round_ms = 0, k_dp_ms = 0, t_round_call = 0, t_dp_call = 0;
-		uint64_t round_h2d = 0, round_d2h = 0, dp_h2d = 0, dp_d2h = 0, retries = 0;
+		uint64_t round_h2d = 0, round_d2h = 0, dp_h2d = 0, dp_d2h = 0, store_h2d = 0, retries = 0;
 	} gs;
 private:
 	bt2x_ctx* ctx_;
-	bool ref_text_ = false;
+	bool ref_text_ = false, store_ = true, dseeds_ = true;
 	double sat_per_read_ = 16, elt_per_read_ = 64;
 };
 
@@ -458,12 +474,13 @@ int main(int argc, char** argv) {
 				const HipBackend::GpuStats& h = hip2->gs;
 				g.k_round_ms += h.k_round_ms; g.k_dp_ms += h.k_dp_ms; g.t_round_call += h.t_round_call;
 				g.t_dp_call += h.t_dp_call; g.round_h2d += h.round_h2d; g.round_d2h += h.round_d2h;
-				g.dp_h2d += h.dp_h2d; g.dp_d2h += h.dp_d2h; g.retries += h.retries;
+				g.dp_h2d += h.dp_h2d; g.dp_d2h += h.dp_d2h; g.store_h2d += h.store_h2d; g.retries += h.retries;
 			}
 			std::fprintf(stderr, "BT2X_GPU k_round=%.4f t_round_call=%.4f round_h2d_mib=%.1f round_d2h_mib=%.1f "
-			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f retries=%llu\n", g.k_round_ms * 1e-3, g.t_round_call,
-			             g.round_h2d / 1048576.0, g.round_d2h / 1048576.0, g.k_dp_ms * 1e-3, g.t_dp_call,
-			             g.dp_h2d / 1048576.0, g.dp_d2h / 1048576.0, (unsigned long long)g.retries);
+			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f store_h2d_mib=%.1f retries=%llu\n",
+			             g.k_round_ms * 1e-3, g.t_round_call, g.round_h2d / 1048576.0, g.round_d2h / 1048576.0, g.k_dp_ms * 1e-3,
+			             g.t_dp_call, g.dp_h2d / 1048576.0, g.dp_d2h / 1048576.0, g.store_h2d / 1048576.0,
+			             (unsigned long long)g.retries);
 		}
 	} catch(const std::exception& e) {
 		std::fprintf(stderr, "bt2x-align: %s\n", e.what());

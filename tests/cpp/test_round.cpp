@@ -78,7 +78,7 @@ Got run_core(const Case& c, uint32_t maxelt, CoreWs& w) {
 		for(uint32_t i = 0; i < p.nsmallSat; i++) {
 			const bt2x_round::Range& rg = w.p.r2[i];
 			bt2x_sat s;
-			s.rdoff = rg.rdoff; s.rand_n = (uint16_t)rg.size; s.fw = rg.fw; s.seedlen = (uint8_t)c.in.seedlen;
+			s.rdoff = (uint16_t)rg.rdoff; s.rand_n = (uint8_t)rg.size; s.fwlen = BT2X_SAT_FWLEN(rg.fw, c.in.seedlen);
 			g.sats.push_back(s);
 			for(uint32_t k = 0; k < (uint32_t)rg.size; k++) g.rows.push_back(rg.topf + k);
 		}
@@ -92,7 +92,7 @@ Got run_core(const Case& c, uint32_t maxelt, CoreWs& w) {
 			g.rows.resize(e0 + p.nsamples);
 			const bool ok = bt2x_round::sample(nb, p.nsamples, rnd, w.s, co, [&](uint64_t k, const bt2x_round::Range& rg, uint16_t elt) {
 				bt2x_sat s;
-				s.rdoff = rg.rdoff; s.rand_n = 1; s.fw = rg.fw; s.seedlen = (uint8_t)c.in.seedlen;
+				s.rdoff = (uint16_t)rg.rdoff; s.rand_n = 1; s.fwlen = BT2X_SAT_FWLEN(rg.fw, c.in.seedlen);
 				g.sats[s0 + k] = s;
 				g.rows[e0 + k] = rg.topf + elt;
 			});

@@ -52,7 +52,7 @@ SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
 # (lane-per-problem banded kernel above BT2X_DP_WAVE_MAX problems, wave per problem
 # below), and each kernel forced for every launch
 DP_MODES = {"default": None, "lane": "0", "wave": "1", "hostwin": "host", "handover": "handover", "parwave": "parwave",
-            "stream2": "stream2", "lane1": "lane1"}
+            "stream2": "stream2", "lane1": "lane1", "nostore": "nostore"}
 MD5 = os.path.join(g.GOLDEN, "e2e_md5.json")
 SUMMARY = os.path.join(g.GOLDEN, "e2e_summary.json")
 
@@ -177,6 +177,7 @@ GPU_CASES = [(s, m) for s in SETS for m in DP_MODES
              if m == "default" or (m in ("hostwin", "handover") and s[0] in ("e2e_rep", "e2e_rep_i16_mix"))
              or (m == "parwave" and s[0] in ("e2e_rep", "e2e_tandem", "e2e_tandem_i16", "e2e_rep_i16_mix"))
              or (m == "lane1" and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem"))
+             or (m in ("nostore", "stream2") and s[0] in ("e2e_rep", "e2e_rep_i16_mix"))
              or (m in ("lane", "wave") and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem", "e2e_rep_i16",
                                                     "e2e_tandem_i16", "e2e_rep_i16_mix"))]
 
@@ -194,6 +195,7 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     env.pop("BT2X_DP_HEAVY", None)
     env.pop("BT2X_DP_PARWALK", None)
     env.pop("BT2X_DP_DUO", None)
+    env.pop("BT2X_READ_STORE", None)
     if DP_MODES[mode] == "host":
         env["BT2X_HOST_WINDOWS"] = "1"          # DP windows cut on the host (RefInfo::stretch)
     elif DP_MODES[mode] == "handover":
@@ -205,6 +207,8 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     elif DP_MODES[mode] == "lane1":               # lane kernels, one lane per problem (dp_fill_kernel)
         env["BT2X_DP_WAVE"] = "0"
         env["BT2X_DP_DUO"] = "0"
+    elif DP_MODES[mode] == "nostore":             # reads sent with every request (no read store)
+        env["BT2X_READ_STORE"] = "0"
     elif DP_MODES[mode] not in (None, "stream2"):
         env["BT2X_DP_WAVE"] = DP_MODES[mode]
     # stream2: the two cohorts on two contexts (bt2x_open_shared); default: one context

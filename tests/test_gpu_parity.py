@@ -442,6 +442,35 @@ def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, duo, gold, m
     assert not bad, "\n".join(bad)
 
 
+def test_dp_from_read_store_matches_uploaded_reads(ctxs):
+    """bt2x_store_reads + bt2x_dp_align(reads = quals = NULL): every problem's read put in a
+    store slot (half of them as the reverse complement, so their rows come from the slot's
+    GPU-derived patRc and reversed qualities) gives the records of the ordinary call."""
+    case = g.DpCase(os.path.join(g.GOLDEN, "dp_rep_dpad12.txt.xz"))
+    ctx = ctxs["rep"][0]
+    ref = ctx.dp_align(case.reads, case.quals, case.refs, case.inp, debug=False)[:3]
+    inp = case.inp.copy()
+    packed, sin = [], np.zeros(len(inp), dtype=abi.STORE_IN)
+    off = 0
+    comp = np.array([3, 2, 1, 0, 4], np.uint8)
+    for i, p in enumerate(case.inp):
+        n = int(p["rdlen"])
+        rd = case.reads[int(p["read_off"]):int(p["read_off"]) + n]
+        qu = case.quals[int(p["qual_off"]):int(p["qual_off"]) + n]
+        rc = i % 2 == 1
+        fw, fq = (comp[rd[::-1]], qu[::-1]) if rc else (rd, qu)
+        packed += [fw, fq]
+        slot = 3 * i + 7                            # sparse slots: the store grows to the largest
+        sin[i] = (off, slot, n, 0)
+        off += 2 * n
+        base = slot * abi.STORE_SLOT_BYTES
+        inp[i]["read_off"] = base + (n if rc else 0)
+        inp[i]["qual_off"] = base + 2 * n + (n if rc else 0)
+    ctx.store_reads(np.concatenate(packed), sin)
+    got = ctx.dp_align(None, None, case.refs, inp, debug=False)[:3]
+    _compare_dp(*got, *ref, case.inp)                    # (record arena offsets come from atomics)
+
+
 def test_empty_batches(ctxs):
     ctx = ctxs["rep"][0]
     out = ctx.seed_search(np.zeros(16, np.uint8), np.zeros(0, dtype=abi.SEED_IN), do_extend=True)

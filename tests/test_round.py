@@ -141,7 +141,11 @@ def test_round_kernel_vs_reference_rank_golden(tmp_path):
     n = len(rin)
     ctx = lib.Context(lib.Index(base, load_offs=True))
     out = ctx.seed_round(case.reads, sin, rin, np.zeros(0, dtype=abi.EXRANGE), 0)[0]
+    # the same round with the seeds instantiated on the GPU (seeds == NULL): the golden's
+    # seed rows are the reference's instantiateSeeds list, so every output is the same
+    gen = ctx.seed_round(case.reads, None, rin, np.zeros(0, dtype=abi.EXRANGE), 0)[0]
     ctx.close()
+    np.testing.assert_array_equal(gen, out)
     bad, nk = [], 0
     for i, t in enumerate(exp):
         o = out[i]
