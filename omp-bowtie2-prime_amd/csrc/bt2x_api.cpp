@@ -3,6 +3,7 @@
 // seed search and DP goes through the gfx950 kernels, and without a HIP device
 // bt2x_open fails with BT2X_E_NODEVICE.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -206,11 +207,15 @@ namespace {
 // thread that shares the CPUs with the host's per-read work: the wait blocks on an event
 // (hipEventBlockingSync) instead of spinning in hipStreamSynchronize (BT2X_SPIN_WAIT=1
 // restores that).
+// BT2X_SPIN_WAIT=2: poll the event, sleeping 20 us between polls (the runtime's blocking
+// wait still spins a while before it sleeps).
 hipError_t stream_wait(bt2x_ctx* c) {
-	static const bool spin = [] { const char* e = getenv("BT2X_SPIN_WAIT"); return e && e[0] == '1'; }();
-	if(spin || !c->sync_ev) return hipStreamSynchronize(c->stream);
+	static const int spin = [] { const char* e = getenv("BT2X_SPIN_WAIT"); return e ? atoi(e) : 0; }();
+	if(spin == 1 || !c->sync_ev) return hipStreamSynchronize(c->stream);
 	hipError_t e = hipEventRecord(c->sync_ev, c->stream);
-	return e != hipSuccess ? e : hipEventSynchronize(c->sync_ev);
+	if(e != hipSuccess || spin != 2) return e != hipSuccess ? e : hipEventSynchronize(c->sync_ev);
+	while((e = hipEventQuery(c->sync_ev)) == hipErrorNotReady) usleep(20);
+	return e;
 }
 }
 

@@ -495,16 +495,20 @@ int64_t mapq_v2(const Params& p, size_t rdlen, int64_t best, bool hasSecbest, in
 	return ret;
 }
 
+// isspace in the C locale (the reference's): ' ', \t, \n, \v, \f, \r
+inline bool c_space(unsigned char ch) { return ch == ' ' || (ch >= '\t' && ch <= '\r'); }
+
 void append_name(std::string& o, const std::string& name) {   // SamConfig::printReadName
-	size_t n = std::min<size_t>(name.size(), 255);
-	for(size_t i = 0; i < n; i++) {
-		if(std::isspace((unsigned char)name[i])) break;
-		o.push_back(name[i]);
-	}
+	const size_t n = std::min<size_t>(name.size(), 255);
+	size_t k = 0;
+	while(k < n && !c_space((unsigned char)name[k])) k++;
+	o.append(name.data(), k);
 }
 
 void append_refname(std::string& o, const std::string& name) {   // SamConfig::printRefName
-	for(char ch : name) { if(std::isspace((unsigned char)ch)) break; o.push_back(ch); }
+	size_t k = 0;
+	while(k < name.size() && !c_space((unsigned char)name[k])) k++;
+	o.append(name.data(), k);
 }
 
 void append_seq(std::string& o, const std::vector<uint8_t>& s) {
@@ -865,33 +869,44 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		if(offset > 0 && (size_t)P.multiseedLen + offset > rdlen) break;
 		// instantiateSeeds (aligner_seed.cpp:411-447): fw seed i at depth, rc seed at rdlen-depth-L
 		const uint32_t nseeds = (rdlen - offset > L) ? 1 + (uint32_t)((rdlen - offset - L) / interval) : 1;
-		c->seed_in.clear();
-		for(int fwi = 0; fwi < 2; fwi++) {
-			const bool fw = fwi == 0;
-			if((fw && P.nofw) || (!fw && P.norc)) continue;
-			const std::vector<uint8_t>& s = fw ? rd.fw : rd.rc;
-			for(uint32_t i = 0; i < nseeds; i++) {
-				const uint32_t depth = i * interval + offset;
-				const uint32_t st = fw ? depth : (uint32_t)(rdlen - depth - L);
-				bool ok = true;
-				if(rd.nN) for(uint32_t k = 0; k < L; k++) if(s[st + k] > 3) { ok = false; break; }
-				if(!ok) continue;
-				bt2x_seed_in si;
-				std::memset(&si, 0, sizeof(si));
-				si.read_off = fw ? 0 : rdlen;
-				si.seed_off = (uint8_t)st;
-				si.seed_len = (uint8_t)L;
-				c->seed_in.push_back(si);
+		// the seed list; with the seeds instantiated on the GPU (and the round not handed
+		// back) only its length: every seed of an N-free read, else the ones clear of an N
+		auto instantiate = [&](bool list) {
+			c->seed_in.clear();
+			uint32_t nvalid = 0;
+			for(int fwi = 0; fwi < 2; fwi++) {
+				const bool fw = fwi == 0;
+				if((fw && P.nofw) || (!fw && P.norc)) continue;
+				if(!list && !rd.nN) { nvalid += nseeds; continue; }
+				const std::vector<uint8_t>& s = fw ? rd.fw : rd.rc;
+				for(uint32_t i = 0; i < nseeds; i++) {
+					const uint32_t depth = i * interval + offset;
+					const uint32_t st = fw ? depth : (uint32_t)(rdlen - depth - L);
+					bool ok = true;
+					if(rd.nN) for(uint32_t k = 0; k < L; k++) if(s[st + k] > 3) { ok = false; break; }
+					if(!ok) continue;
+					nvalid++;
+					if(!list) continue;
+					bt2x_seed_in si;
+					std::memset(&si, 0, sizeof(si));
+					si.read_off = fw ? 0 : rdlen;
+					si.seed_off = (uint8_t)st;
+					si.seed_len = (uint8_t)L;
+					c->seed_in.push_back(si);
+				}
 			}
-		}
+			return nvalid;
+		};
+		const bool gpu_seeds = gpu_round_ && dseeds_;
+		const uint32_t nvalid = instantiate(!gpu_seeds);
 		PH(1);
-		if(c->seed_in.empty()) break;                                // no seed, no hit: done
+		if(nvalid == 0) break;                                       // no seed, no hit: done
 		// the rest of the round up to extendSeeds: on the GPU (bt2x_seed_round), or for a
 		// read it hands back, as seed search + host_round + SA resolution
 		bt2x_round_in& q = c->round_in;
 		std::memset(&q, 0, sizeof q);
 		q.rnd_last = rnd.last; q.rnd_lastoff = rnd.lastOff;
-		q.nseeds = (uint16_t)c->seed_in.size(); q.num_offs = (uint16_t)nseeds; q.rdlen = (uint16_t)rdlen;
+		q.nseeds = (uint16_t)nvalid; q.num_offs = (uint16_t)nseeds; q.rdlen = (uint16_t)rdlen;
 		q.interval = (uint16_t)interval; q.offset = (uint16_t)offset; q.seedlen = (uint16_t)L;
 		q.seedflags = (uint16_t)((P.nofw ? 1 : 0) | (P.norc ? 2 : 0));
 		q.nexr = (uint16_t)c->exRange.size();
@@ -905,6 +920,7 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			else { rnd.last = c->round_out.rnd_last; rnd.lastOff = c->round_out.rnd_lastoff; }
 		}
 		if(redo) {
+			if(gpu_seeds) instantiate(true);                         // the host searches the seeds itself
 			co_await Awaiter{c, REQ_SEED};
 			PH_START();
 			q.read_off = 0;                                          // seeds: patFw at 0, patRc at rdlen
@@ -1100,7 +1116,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 				if(!store) C.dbytes += 2 * c->rd.length();
 				if(!ref_index) for(const DpWork& d : c->dps) C.rbytes += d.key.ncol;
 			} else if(c->req == REQ_ROUND) {
-				C.wn.push_back(c); C.nnseed += c->seed_in.size();
+				C.wn.push_back(c); C.nnseed += c->round_in.nseeds;
 				if(!store) C.nbytes += 2 * c->rd.length();
 				C.nexr += c->exRange.size();
 			}
@@ -1243,7 +1259,7 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			q.read_off = roff; q.seed0 = nko; q.exr0 = (uint32_t)neo; q.nexr = (uint16_t)c->exRange.size();
 			L.round_in[i] = q;
 			if(dseeds) {
-				nko += c->seed_in.size();                // (instantiated again on the GPU, same order)
+				nko += c->round_in.nseeds;               // (instantiated on the GPU)
 			} else {
 				for(const bt2x_seed_in& q0 : c->seed_in) {
 					bt2x_seed_in sq = q0;
@@ -1663,6 +1679,7 @@ void Aligner::reserve_launch_buffers(size_t reads) {
 RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads, double* t_run) {
 	RunStats st;
 	use_threads(threads);
+	dseeds_ = be_.device_seeds();
 	const double t_start = now_s();
 	if(header_on_) {
 		const std::string hdr = header();
@@ -1845,6 +1862,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threads, RunStats* stp) {
 	RunStats st;
 	use_threads(threads);
+	dseeds_ = be_.device_seeds();
 	std::vector<ReadCtx*> act, fresh;
 	OutRing ring;
 	std::string out;

@@ -1169,6 +1169,7 @@ private:
 	void scatter_resume(Launch& L, RunStats& st);
 	Launch launch_[2];
 	bool pipeline_ = true, gpu_round_ = true, header_on_ = true;
+	bool dseeds_ = false;              // be_.device_seeds(), read when a run starts
 	ReadCtx* take_ctx();
 	// put(id, record) takes a finished read's SAM record; it is called from the pool's
 	// threads, for distinct ids

@@ -145,7 +145,9 @@ def test_round_kernel_vs_reference_rank_golden(tmp_path):
     # seed rows are the reference's instantiateSeeds list, so every output is the same
     gen = ctx.seed_round(case.reads, None, rin, np.zeros(0, dtype=abi.EXRANGE), 0)[0]
     ctx.close()
-    np.testing.assert_array_equal(gen, out)
+    keep = [f for f in out.dtype.names if f not in ("sat0", "elt0", "exr0")]   # arena offsets: atomics
+    for f in keep:
+        np.testing.assert_array_equal(gen[f], out[f], err_msg=f)
     bad, nk = [], 0
     for i, t in enumerate(exp):
         o = out[i]

@@ -48,9 +48,15 @@ def main() -> None:
     ap.add_argument("--replays", type=int, default=0,
                     help="bench steps in the profiled run (warmup + steps): traffic is then reported per step "
                          "(all launches of the op in one replay), as bench.py times it")
+    ap.add_argument("--segment", type=int, default=-1,
+                    help="with legs on: keep only the K-th replay of bench.py's process (0: C3, 1: the C2 leg, "
+                         "2: the repeat-heavy leg), the replays being the dispatch runs separated by gaps of "
+                         "more than --gap-s seconds (the legs' aligner runs)")
+    ap.add_argument("--gap-s", type=float, default=2.0)
+    ap.add_argument("--out", default="", help="output directory (default: the repo's profiles/)")
     a = ap.parse_args()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = os.path.join(root, "profiles")
+    out = a.out or os.path.join(root, "profiles")
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(a.src, "prof_kt", "run_kernel_stats.csv"),
                 os.path.join(out, f"{a.tag}_kernel_stats.csv"))
@@ -69,7 +75,22 @@ def main() -> None:
                 t = int(r.get("Start_Timestamp") or r.get("Start_Time") or 0)
                 first[r[pid]] = min(first.get(r[pid], t), t)
             keep = max(first, key=first.get)
+            if a.segment >= 0:
+                # legs on: the aligner runs of the legs start after bench.py's first replay; bench.py
+                # is their parent, so the lowest process id
+                keep = min(first, key=lambda k: int(k))
             rows = [r for r in rows if r[pid] == keep]
+        if a.segment >= 0 and rows:
+            def ts(r):
+                return int(r.get("Start_Timestamp") or r.get("Start_Time") or 0)
+            rows.sort(key=ts)
+            seg, last = [[]], None
+            for r in rows:
+                if last is not None and ts(r) - last > a.gap_s * 1e9:
+                    seg.append([])
+                seg[-1].append(r)
+                last = ts(r)
+            rows = seg[a.segment] if a.segment < len(seg) else []
         return rows
 
     dur = defaultdict(lambda: defaultdict(list))
