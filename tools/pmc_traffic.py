@@ -22,7 +22,7 @@ from collections import defaultdict
 # logical op -> the kernels one call launches (per-launch figures are summed over them)
 KERNELS = {"seed": ("seed_init_kernel", "seed_kernel"), "resolve": ("sa_resolve_kernel",),
            "round": ("round_prep_kernel", "round_sample_kernel"),
-           "dp": ("dp_fill_kernel", "dp_walk_kernel", "dp_wave_kernel", "dp_kernel")}
+           "dp": ("dp_fill_kernel", "dp_duo_kernel", "dp_walk_kernel", "dp_wave_kernel", "dp_kernel")}
 
 
 def short(name: str) -> str | None:
