@@ -1074,6 +1074,10 @@ bool host_prefetch() {
 	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH"); return !(e && e[0] == '0'); }();
 	return on;
 }
+bool host_prefetch_read() {                     // BT2X_HOST_PREFETCH_READ=0: off
+	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH_READ"); return !(e && e[0] == '0'); }();
+	return on;
+}
 inline void prefetch_ctx(const ReadCtx* c, bool frame) {
 	for(int k = 0; k < 4; k++) __builtin_prefetch(reinterpret_cast<const char*>(c) + 64 * k);
 	if(frame)
@@ -1337,6 +1341,11 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 				__builtin_prefetch(c3->elts.data(), 1); __builtin_prefetch(c3->sats.data(), 1);
 				__builtin_prefetch(c3->recs.data() + c3->recs.size(), 1);
 				__builtin_prefetch(c3->edits.data() + c3->edits.size(), 1);
+				// the read itself (a resume that finishes the read formats its record)
+				if(host_prefetch_read()) {
+					__builtin_prefetch(c3->rd.name.data()); __builtin_prefetch(c3->rd.fw.data());
+					__builtin_prefetch(c3->rd.qual.data()); __builtin_prefetch(c3->sam.data(), 1);
+				}
 			}
 		}
 		if(i < nwn) {
