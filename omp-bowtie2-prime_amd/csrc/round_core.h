@@ -65,8 +65,8 @@ struct alignas(4) R1N {                       // Random1toN state; lists live in
 
 // prep()'s per-lane workspace
 struct PrepWs {
-	uint64_t htopf[2][kMaxOffs], hn[2][kMaxOffs];
-	uint8_t hnlex[2][kMaxOffs], hvalid[2][kMaxOffs], hsorted[2][kMaxOffs];
+	uint64_t htopf[2][kMaxOffs], hn[2][kMaxOffs];  // valid where prep()'s strand mask has the bit
+	uint8_t hnlex[2][kMaxOffs];               // the cache's nlex for the offset's range
 	uint16_t rankIdx[kMaxRanges];
 	uint8_t rankFw[kMaxRanges];
 	uint64_t cacheTop[kMaxRanges];
@@ -161,8 +161,10 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 	res.status = BT2X_ROUND_OK;
 	const uint32_t numOffs = in.num_offs, L = in.seedlen, interval = in.interval, offset = in.offset;
 	if(numOffs > (uint32_t)kMaxOffs) { res.status = BT2X_ROUND_REDO; return res; }
-	for(int s = 0; s < 2; s++)
-		for(uint32_t i = 0; i < numOffs; i++) { w.hvalid[s][i] = 0; w.hsorted[s][i] = 0; }
+	// per strand, one bit per seed offset: a hit was added (and not yet ranked) with a
+	// non-empty range.  Registers instead of the reference's per-offset flags, so the
+	// ranking below loads only the sizes of the offsets still in the running.
+	uint64_t live[2] = {0, 0};
 	// ---- searchAllSeedsFinalize: SeedResults::add + the per-read cache's first nlex
 	uint32_t ncache = 0;
 	for(uint32_t k = 0; k < in.nseeds; k++) {
@@ -174,16 +176,20 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 		const uint32_t idx = (depth - offset) / interval;
 		if(idx < numOffs) {                    // SeedResults::add ignores other offsets
 			const int s = fw ? 0 : 1;
-			w.htopf[s][idx] = d.topf; w.hn[s][idx] = d.botf - d.topf; w.hnlex[s][idx] = d.nlex; w.hvalid[s][idx] = 1;
+			w.htopf[s][idx] = d.topf; w.hn[s][idx] = d.botf - d.topf;
+			if(d.botf > d.topf) live[s] |= 1ull << idx; else live[s] &= ~(1ull << idx);
 			res.numElts += d.botf - d.topf;
 			res.nonz++;
 		}
+		uint8_t cnlex = d.nlex;
 		bool have = false;
-		for(uint32_t q = 0; q < ncache; q++) if(w.cacheTop[q] == d.topf) { have = true; break; }
+		for(uint32_t q = 0; q < ncache; q++) if(w.cacheTop[q] == d.topf) { have = true; cnlex = w.cacheNlex[q]; break; }
 		if(!have) {
 			if(ncache >= (uint32_t)kMaxRanges) { res.status = BT2X_ROUND_REDO; return res; }
 			w.cacheTop[ncache] = d.topf; w.cacheNlex[ncache] = d.nlex; ncache++;
 		}
+		// the first add of a range fixes its nlex, so the offset's value is final here
+		if(idx < numOffs) w.hnlex[fw ? 0 : 1][idx] = cnlex;
 	}
 	if(res.nonz == 0) { res.status = BT2X_ROUND_NO_HITS; return res; }
 	// ---- rankSeedHits (random strand order and start, smallest range first)
@@ -195,16 +201,21 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 		for(int fwi = 0; fwi <= 1; fwi++) {
 			const int fw = (fwi == (rb ? 1 : 0)) ? 1 : 0;
 			const int s = fw ? 0 : 1;
-			uint32_t i = rnd.nextU32() % numOffs;
-			for(uint32_t ii = 0; ii < numOffs; ii++) {
-				if(w.hvalid[s][i] && w.hn[s][i] > 0 && !w.hsorted[s][i] && w.hn[s][i] < minsz) {
-					minsz = w.hn[s][i]; minidx = i; minfw = fw;
+			const uint32_t i = rnd.nextU32() % numOffs;
+			// the offsets in scan order i, i+1, ..., numOffs-1, 0, ..., i-1 (first minimum wins)
+			const uint64_t lo = (1ull << i) - 1;
+			for(int part = 0; part < 2; part++) {
+				uint64_t m = part ? live[s] & lo : live[s] & ~lo;
+				while(m) {
+					const uint32_t b = (uint32_t)__builtin_ctzll(m);
+					m &= m - 1;
+					const uint64_t n = w.hn[s][b];
+					if(n < minsz) { minsz = n; minidx = b; minfw = fw; }
 				}
-				if(++i == numOffs) i = 0;
 			}
 		}
 		if(minsz == 0xffffffffu) { res.status = BT2X_ROUND_REDO; return res; }
-		w.hsorted[minfw ? 0 : 1][minidx] = 1;
+		live[minfw ? 0 : 1] &= ~(1ull << minidx);
 		w.rankIdx[r] = (uint16_t)minidx;
 		w.rankFw[r] = (uint8_t)minfw;
 	}
@@ -221,8 +232,7 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 		sp.rdoff = offidx * interval + offset;
 		sp.offidx = (uint16_t)offidx;
 		sp.fw = (uint8_t)fw;
-		sp.nlex = 0;
-		for(uint32_t q = 0; q < ncache; q++) if(w.cacheTop[q] == sp.topf) { sp.nlex = w.cacheNlex[q]; break; }
+		sp.nlex = w.hnlex[s][offidx];
 		if(sp.size == 0) continue;
 		bool skip = false;
 		for(uint32_t q = 0; q < in.nexr && !skip; q++) skip = exr_covers(exr[q], fw, sp.rdoff, L, sp.size);
