@@ -154,6 +154,21 @@ __host__ __device__ inline bool exr_covers(const bt2x_exrange& er, int fw, uint3
 	return er.fw == fw && er.off <= rdoff && (uint64_t)er.off + er.len >= (uint64_t)rdoff + L && size <= er.sz;
 }
 
+// The first q < n with at(q) true, else n.  The kernel runs one read per lane at about one
+// wave per SIMD, so it is bound by the latency of its workspace loads: these scans load four
+// entries before testing any (at() must be safe to call up to n rounded up to 4).
+template<class F>
+__host__ __device__ inline uint32_t find_first4(uint32_t n, const F& at) {
+	for(uint32_t q = 0; q < n; q += 4) {
+		const bool t0 = at(q), t1 = at(q + 1), t2 = at(q + 2), t3 = at(q + 3);
+		if(t0) return q;
+		if(t1) return q + 1 < n ? q + 1 : n;
+		if(t2) return q + 2 < n ? q + 2 : n;
+		if(t3) return q + 3 < n ? q + 3 : n;
+	}
+	return n;
+}
+
 // Finalize, rank and prioritize up to the sampling decision.
 __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout,
                                      const bt2x_exrange* exr, uint32_t maxelt, Rnd& rnd, PrepWs& w) {
@@ -167,10 +182,13 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 	uint64_t live[2] = {0, 0};
 	// ---- searchAllSeedsFinalize: SeedResults::add + the per-read cache's first nlex
 	uint32_t ncache = 0;
+	bt2x_seed_out dn = in.nseeds ? sout[0] : bt2x_seed_out{};
+	bt2x_seed_in sn = in.nseeds ? sin[0] : bt2x_seed_in{};
 	for(uint32_t k = 0; k < in.nseeds; k++) {
-		const bt2x_seed_out d = sout[k];
+		const bt2x_seed_out d = dn;                // the next seed's loads go out first
+		const bt2x_seed_in si = sn;
+		if(k + 1 < in.nseeds) { dn = sout[k + 1]; sn = sin[k + 1]; }
 		if(!d.need_reporting) continue;
-		const bt2x_seed_in si = sin[k];
 		const bool fw = si.read_off == in.read_off;
 		const uint32_t depth = fw ? si.seed_off : (uint32_t)in.rdlen - si.seed_off - L;
 		const uint32_t idx = (depth - offset) / interval;
@@ -182,9 +200,10 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 			res.nonz++;
 		}
 		uint8_t cnlex = d.nlex;
-		bool have = false;
-		for(uint32_t q = 0; q < ncache; q++) if(w.cacheTop[q] == d.topf) { have = true; cnlex = w.cacheNlex[q]; break; }
-		if(!have) {
+		const uint32_t qh = find_first4(ncache, [&](uint32_t q) { return w.cacheTop[q] == d.topf; });
+		const bool have = qh < ncache;
+		if(have) cnlex = w.cacheNlex[qh];
+		else {
 			if(ncache >= (uint32_t)kMaxRanges) { res.status = BT2X_ROUND_REDO; return res; }
 			w.cacheTop[ncache] = d.topf; w.cacheNlex[ncache] = d.nlex; ncache++;
 		}
@@ -206,11 +225,20 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 			const uint64_t lo = (1ull << i) - 1;
 			for(int part = 0; part < 2; part++) {
 				uint64_t m = part ? live[s] & lo : live[s] & ~lo;
-				while(m) {
-					const uint32_t b = (uint32_t)__builtin_ctzll(m);
+				while(m) {                     // four offsets a pass (repeats of b0 pad it)
+					const uint32_t b0 = (uint32_t)__builtin_ctzll(m);
 					m &= m - 1;
-					const uint64_t n = w.hn[s][b];
-					if(n < minsz) { minsz = n; minidx = b; minfw = fw; }
+					const uint32_t b1 = m ? (uint32_t)__builtin_ctzll(m) : b0;
+					m &= m - 1;
+					const uint32_t b2 = m ? (uint32_t)__builtin_ctzll(m) : b0;
+					m &= m - 1;
+					const uint32_t b3 = m ? (uint32_t)__builtin_ctzll(m) : b0;
+					m &= m - 1;
+					const uint64_t n0 = w.hn[s][b0], n1 = w.hn[s][b1], n2 = w.hn[s][b2], n3 = w.hn[s][b3];
+					if(n0 < minsz) { minsz = n0; minidx = b0; minfw = fw; }
+					if(n1 < minsz) { minsz = n1; minidx = b1; minfw = fw; }
+					if(n2 < minsz) { minsz = n2; minidx = b2; minfw = fw; }
+					if(n3 < minsz) { minsz = n3; minidx = b3; minfw = fw; }
 				}
 			}
 		}
@@ -237,7 +265,7 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 		bool skip = false;
 		for(uint32_t q = 0; q < in.nexr && !skip; q++) skip = exr_covers(exr[q], fw, sp.rdoff, L, sp.size);
 		for(uint32_t q = 0; q < res.nexnew && !skip; q++) skip = exr_covers(w.exnew[q], fw, sp.rdoff, L, sp.size);
-		for(uint32_t q = 0; q < n2 && !skip; q++) skip = w.r2[q].topf == sp.topf;
+		if(!skip) skip = find_first4(n2, [&](uint32_t q) { return w.r2[q].topf == sp.topf; }) < n2;
 		if(skip) continue;
 		nelt += sp.size;
 		w.r2[n2++] = sp;
