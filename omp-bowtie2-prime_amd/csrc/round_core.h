@@ -170,8 +170,12 @@ __host__ __device__ inline uint32_t find_first4(uint32_t n, const F& at) {
 }
 
 // Finalize, rank and prioritize up to the sampling decision.
+// hn32: the ranking's copy of the range sizes, entry (s, i) at hn32[(s * kMaxOffs + i) *
+// hstride], clamped to 0xffffffff (a size the ranking never picks); the kernel keeps it in
+// LDS, one column per lane.
 __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout,
-                                     const bt2x_exrange* exr, uint32_t maxelt, Rnd& rnd, PrepWs& w) {
+                                     const bt2x_exrange* exr, uint32_t maxelt, Rnd& rnd, PrepWs& w,
+                                     uint32_t* hn32, uint32_t hstride) {
 	Prep res = {};
 	res.status = BT2X_ROUND_OK;
 	const uint32_t numOffs = in.num_offs, L = in.seedlen, interval = in.interval, offset = in.offset;
@@ -195,6 +199,8 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 		if(idx < numOffs) {                    // SeedResults::add ignores other offsets
 			const int s = fw ? 0 : 1;
 			w.htopf[s][idx] = d.topf; w.hn[s][idx] = d.botf - d.topf;
+			const uint64_t n = d.botf - d.topf;
+			hn32[((uint32_t)s * kMaxOffs + idx) * hstride] = n < 0xffffffffull ? (uint32_t)n : 0xffffffffu;
 			if(d.botf > d.topf) live[s] |= 1ull << idx; else live[s] &= ~(1ull << idx);
 			res.numElts += d.botf - d.topf;
 			res.nonz++;
@@ -213,7 +219,7 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 	if(res.nonz == 0) { res.status = BT2X_ROUND_NO_HITS; return res; }
 	// ---- rankSeedHits (random strand order and start, smallest range first)
 	for(uint32_t r = 0; r < res.nonz; r++) {
-		uint64_t minsz = 0xffffffffu;
+		uint32_t minsz = 0xffffffffu;
 		uint32_t minidx = 0;
 		int minfw = 1;
 		const bool rb = rnd.nextBool();
@@ -234,7 +240,8 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 					m &= m - 1;
 					const uint32_t b3 = m ? (uint32_t)__builtin_ctzll(m) : b0;
 					m &= m - 1;
-					const uint64_t n0 = w.hn[s][b0], n1 = w.hn[s][b1], n2 = w.hn[s][b2], n3 = w.hn[s][b3];
+					const uint32_t* h = hn32 + (uint32_t)s * kMaxOffs * hstride;
+					const uint32_t n0 = h[b0 * hstride], n1 = h[b1 * hstride], n2 = h[b2 * hstride], n3 = h[b3 * hstride];
 					if(n0 < minsz) { minsz = n0; minidx = b0; minfw = fw; }
 					if(n1 < minsz) { minsz = n1; minidx = b1; minfw = fw; }
 					if(n2 < minsz) { minsz = n2; minidx = b2; minfw = fw; }
@@ -297,6 +304,13 @@ __host__ __device__ inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in
 		res.nsamples = top > added ? top - added : 0;
 	}
 	return res;
+}
+
+// host callers (tests/cpp/test_round.cpp): the ranking copy on the stack
+inline Prep prep(const bt2x_round_in& in, const bt2x_seed_in* sin, const bt2x_seed_out* sout,
+                 const bt2x_exrange* exr, uint32_t maxelt, Rnd& rnd, PrepWs& w) {
+	uint32_t hn32[2 * kMaxOffs];
+	return prep(in, sin, sout, exr, maxelt, rnd, w, hn32, 1);
 }
 
 __host__ __device__ inline bool seen_has(const SampleWs& w, uint32_t key) {       // key != 0

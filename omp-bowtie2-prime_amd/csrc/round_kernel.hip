@@ -58,6 +58,9 @@ round_prep_kernel(RoundLaunch a) {
 	Job* jobs = reinterpret_cast<Job*>(a.jobs);
 	Range* ranges = reinterpret_cast<Range*>(a.ranges);
 	const uint32_t stride = gridDim.x * blockDim.x;
+	// prep()'s ranking reads the range sizes once per offset still in the running and rank:
+	// in LDS, one column per lane (conflict-free), not in the lane's HBM workspace
+	__shared__ uint32_t hn32[2 * kMaxOffs * 64];
 	// the wave walks the reads together (inactive lanes past the end), so the counters can
 	// be reserved per wave
 	for(uint32_t r0 = blockIdx.x * blockDim.x; r0 < a.n; r0 += stride) {
@@ -70,7 +73,7 @@ round_prep_kernel(RoundLaunch a) {
 		if(act) {
 			in = a.in[r];
 			rnd = Rnd{in.rnd_last, in.rnd_lastoff};
-			p = prep(in, a.seeds + in.seed0, a.seed_out + in.seed0, a.exr + in.exr0, a.maxelt, rnd, w);
+			p = prep(in, a.seeds + in.seed0, a.seed_out + in.seed0, a.exr + in.exr0, a.maxelt, rnd, w, hn32 + threadIdx.x, 64);
 		}
 		o.rnd_last = rnd.last; o.rnd_lastoff = rnd.lastOff;
 		o.num_elts = p.numElts; o.nonz = p.nonz; o.status = p.status;
