@@ -24,7 +24,9 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
-
+#ifdef __AVX2__
+#include <immintrin.h>
+#endif
 
 #ifdef BT2X_PHASE_PROF
 // Development-only phase profiler of the per-read coroutine (-DBT2X_PHASE_PROF): TSC
@@ -517,7 +519,16 @@ void append_seq(std::string& o, const std::vector<uint8_t>& s) {
 	o.resize(b + n);
 	char* d = &o[b];
 	const uint8_t* c = s.data();
-	for(size_t i = 0; i < n; i++) d[i] = "ACGTN"[c[i]];
+	size_t i = 0;
+#ifdef __AVX2__
+	// codes 0-4 through a byte shuffle, 32 a step
+	const __m256i tab = _mm256_setr_epi8('A', 'C', 'G', 'T', 'N', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+	                                     'A', 'C', 'G', 'T', 'N', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0);
+	for(; i + 32 <= n; i += 32)
+		_mm256_storeu_si256(reinterpret_cast<__m256i*>(d + i),
+		                    _mm256_shuffle_epi8(tab, _mm256_loadu_si256(reinterpret_cast<const __m256i*>(c + i))));
+#endif
+	for(; i < n; i++) d[i] = "ACGTN"[c[i]];
 }
 
 // AlnSinkWrap::finishRead, unpaired branch (aln_sink.cpp:643-1384) -> one SAM record in
