@@ -866,6 +866,11 @@ def main():
     # median run's (by the max over ranks of its timed wall time); every run is listed
     runs = []
     for k in range(max(1, args.runs)):
+        # every run writes a new file: opening the last run's 4 GB SAM with O_TRUNC would drop
+        # its page cache inside the timed region, and ext4 flushes a file truncated that way
+        # when it is closed (auto_da_alloc): runs 2 and 3 were 0.5 s slower than run 1
+        if out_sam != os.devnull and os.path.exists(out_sam):
+            os.unlink(out_sam)
         if dist:
             dist.barrier()
         err, wall, peak = run_aligner(args, cmd, os.path.join(rdir, f"align{k}.err"), f"timed run {k + 1}/{args.runs}")
