@@ -36,8 +36,8 @@
 namespace {
 constexpr int kPhases = 16;
 const char* kPhaseName[kPhases] = {"init", "seeds", "rank", "prioritize", "resolve_in", "walk", "lookahead",
-                                   "records", "finish", "scatter", "g_pass1", "g_bases", "g_pass2", "prio_hits",
-                                   "prio_small", "n_samples"};
+                                   "records", "finish", "scatter", "g_pass1", "g_bases", "g_pass2", "walk_reset",
+                                   "memo", "spare"};
 struct PhaseAcc { uint64_t c[kPhases] = {}; uint64_t last = 0; PhaseAcc(); };
 std::mutex g_ph_mu;
 std::vector<PhaseAcc*> g_ph_all;
@@ -959,12 +959,14 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 			const int64_t perfectScore = 0;
 			c->walk.reset(P, c->sats, c->firstRow, c->elts, ref_.lens(), nelt_, rdlen);
 			c->walk.bind(&rnd, &prm, &c->seenDiags);
+			PH(13);
 			for(;;) {
 				DpKey key;
 				ret = c->walk.next(minsc, key);
+				PH(5);
 				if(ret != ExtendWalk::PROBLEM) break;
 				long mi = find_memo(c->memo, key);
-				PH(5);
+				PH(14);
 				if(mi < 0) {
 					// pose this problem and the ones the walk reaches next if each of them
 					// fails (a copy of the walk over copies of the state it advances)
