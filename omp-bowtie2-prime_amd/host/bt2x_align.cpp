@@ -1091,6 +1091,13 @@ bool host_prefetch_read() {                     // BT2X_HOST_PREFETCH_READ=0: of
 	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH_READ"); return !(e && e[0] == '0'); }();
 	return on;
 }
+// BT2X_HOST_PREFETCH_CTX=0: a resume prefetches only the context's first lines and the
+// arenas its results go to; else the whole context ahead and, three reads ahead, the
+// walk's per-read state (cold since the read's last resume a cohort ago)
+bool host_prefetch_full() {
+	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH_CTX"); return !(e && e[0] == '0'); }();
+	return on;
+}
 inline void prefetch_ctx(const ReadCtx* c, bool frame) {
 	for(int k = 0; k < 4; k++) __builtin_prefetch(reinterpret_cast<const char*>(c) + 64 * k);
 	if(frame)
@@ -1344,13 +1351,25 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	const long nrun = (long)L.run.size();
 	const double t0 = now_s();
 	st.t_gather += L.t_gather;
-	const bool prefetch = host_prefetch();
+	const bool prefetch = host_prefetch(), full = host_prefetch_full();
 	pool().parallel_for(nrun, 64, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
 		if(prefetch) {
-			if(i + 6 < nrun) prefetch_ctx(L.run[(size_t)i + 6], true);
+			if(i + 6 < nrun) {
+				const ReadCtx* c6 = L.run[(size_t)i + 6];
+				prefetch_ctx(c6, true);
+				if(full)
+					for(size_t k = 256; k < offsetof(ReadCtx, frame_); k += 64)
+						__builtin_prefetch(reinterpret_cast<const char*>(c6) + k);
+			}
 			if(i + 3 < nrun) {                                // the arenas the results are copied into
 				const ReadCtx* c3 = L.run[(size_t)i + 3];
+				if(full) {
+					c3->seenDiags.prefetch(); c3->walk.prefetch();
+					__builtin_prefetch(c3->firstRow.data()); __builtin_prefetch(c3->memo.data());
+					__builtin_prefetch(c3->dps.data()); __builtin_prefetch(c3->sink.rs.data());
+					__builtin_prefetch(c3->edbuf.data());
+				}
 				__builtin_prefetch(c3->elts.data(), 1); __builtin_prefetch(c3->sats.data(), 1);
 				__builtin_prefetch(c3->recs.data() + c3->recs.size(), 1);
 				__builtin_prefetch(c3->edits.data() + c3->edits.size(), 1);

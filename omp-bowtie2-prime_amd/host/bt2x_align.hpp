@@ -256,6 +256,7 @@ public:
 		tail_.push_back(i);
 		if(tail_.size() == 16) flush();
 	}
+	void prefetch() const { __builtin_prefetch(sorted_.data()); __builtin_prefetch(tail_.data(), 1); }
 	bool locusPresent(const Coord& c) const {
 		if(base_ && base_->locusPresent(c)) return true;
 		for(const Interval& iv : tail_) if(iv.contains(c)) return true;
@@ -927,6 +928,7 @@ public:
 		i_ = 0; first_ = true; inPass_ = false;
 	}
 	void bind(Rng* rnd, Prm* prm, SeenDiags* seen) { rnd_ = rnd; prm_ = prm; seen_ = seen; }
+	void prefetch() const { __builtin_prefetch(rands_.data(), 1); }
 	int next(int64_t minsc, DpKey& k);
 	// the DP of the last next() found no alignment; false: the fail streak ends the walk
 	bool failed() {
