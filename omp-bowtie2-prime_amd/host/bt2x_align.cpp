@@ -1098,10 +1098,24 @@ bool host_prefetch_full() {
 	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH_CTX"); return !(e && e[0] == '0'); }();
 	return on;
 }
+bool host_prefetch_frame() {                   // BT2X_HOST_PREFETCH_FRAME=0: off
+	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH_FRAME"); return !(e && e[0] == '0'); }();
+	return on;
+}
+bool host_prefetch_more() {                    // BT2X_HOST_PREFETCH_MORE=0: off
+	static const bool on = [] { const char* e = std::getenv("BT2X_HOST_PREFETCH_MORE"); return !(e && e[0] == '0'); }();
+	return on;
+}
 inline void prefetch_ctx(const ReadCtx* c, bool frame) {
 	for(int k = 0; k < 4; k++) __builtin_prefetch(reinterpret_cast<const char*>(c) + 64 * k);
 	if(frame)
 		for(int k = 0; k < 8; k++) __builtin_prefetch(c->frame_ + 64 * k);
+}
+// the context's members past the first lines (vector headers, walk and sink state)
+inline void prefetch_ctx_rest(const ReadCtx* c) {
+	for(size_t k = 256; k < offsetof(ReadCtx, frame_); k += 64) __builtin_prefetch(reinterpret_cast<const char*>(c) + k);
+	if(host_prefetch_frame())                  // the frame past the first 512 bytes
+		for(size_t k = 512; k < ReadCtx::kFrameBytes; k += 64) __builtin_prefetch(c->frame_ + k);
 }
 }
 
@@ -1351,16 +1365,14 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	const long nrun = (long)L.run.size();
 	const double t0 = now_s();
 	st.t_gather += L.t_gather;
-	const bool prefetch = host_prefetch(), full = host_prefetch_full();
+	const bool prefetch = host_prefetch(), full = host_prefetch_full(), more = host_prefetch_more();
 	pool().parallel_for(nrun, 64, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
 		if(prefetch) {
 			if(i + 6 < nrun) {
 				const ReadCtx* c6 = L.run[(size_t)i + 6];
 				prefetch_ctx(c6, true);
-				if(full)
-					for(size_t k = 256; k < offsetof(ReadCtx, frame_); k += 64)
-						__builtin_prefetch(reinterpret_cast<const char*>(c6) + k);
+				if(full) prefetch_ctx_rest(c6);
 			}
 			if(i + 3 < nrun) {                                // the arenas the results are copied into
 				const ReadCtx* c3 = L.run[(size_t)i + 3];
@@ -1369,6 +1381,11 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 					__builtin_prefetch(c3->firstRow.data()); __builtin_prefetch(c3->memo.data());
 					__builtin_prefetch(c3->dps.data()); __builtin_prefetch(c3->sink.rs.data());
 					__builtin_prefetch(c3->edbuf.data());
+					if(more) {                                  // the lookahead's copies, the other strand
+						c3->seen2.prefetch(); c3->ahead.prefetch();
+						__builtin_prefetch(c3->exRange.data());
+						__builtin_prefetch(c3->rd.rc.data()); __builtin_prefetch(c3->rd.qualRev.data());
+					}
 				}
 				__builtin_prefetch(c3->elts.data(), 1); __builtin_prefetch(c3->sats.data(), 1);
 				__builtin_prefetch(c3->recs.data() + c3->recs.size(), 1);
@@ -1798,10 +1815,13 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		for(long i = 0; i < nf; i++) fresh[(size_t)i] = take_ctx();
 		writer.reserve(rdid + (uint64_t)nf);
 		st.t_alloc += now_s() - t0;
-		const bool pf = host_prefetch();
+		const bool pf = host_prefetch(), pf_more = host_prefetch_more();
 		pool().parallel_for(nf, 64, [&](long i) {
 			ReadCtx* c = fresh[(size_t)i];
-			if(pf && i + 6 < nf) prefetch_ctx(fresh[(size_t)i + 6], true);
+			if(pf && i + 6 < nf) {
+				prefetch_ctx(fresh[(size_t)i + 6], true);
+				if(pf_more) prefetch_ctx_rest(fresh[(size_t)i + 6]);
+			}
 			if(pf && i + 3 < nf) {                             // the buffers decode writes
 				const Read& r3 = fresh[(size_t)i + 3]->rd;
 				__builtin_prefetch(r3.fw.data(), 1); __builtin_prefetch(r3.rc.data(), 1);

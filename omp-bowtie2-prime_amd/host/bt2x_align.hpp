@@ -985,23 +985,30 @@ struct Sink {
 // reference's per-slot objects (SwDriver, SeedResults, AlnSinkWrap, RandomSource).
 // Contexts are pooled: buffers keep their capacity from read to read.
 struct ReadCtx {
-	Read rd;
+	// what the scheduler's passes read of every read in a cohort first, so that the
+	// context's first four cache lines (prefetch_ctx) hold it and the read's buffer headers
 	int req = REQ_NONE;
+	// the backend's read store (Backend::read_store): this context's slot, whether the
+	// current read is in it, and whether the launch being gathered puts it there
+	uint32_t slot = 0;
+	bool in_store = false, put_now = false;
+	bool done = false;                   // finished, record not yet handed to the writer
+	std::vector<DpWork> dps;             // the problems posed by the current DP request
+	std::vector<bt2x_exrange> exRange, exNew;           // extendSeeds' exRange (both strands)
+	bt2x_round_in round_in;              // the GPU round's request
+	Read rd;
 	// request payloads (gathered / scattered by the scheduler)
 	std::vector<bt2x_seed_in> seed_in;   // read_off: 0 = patFw, rdlen = patRc
 	std::vector<bt2x_seed_out> seed_out;
 	std::vector<bt2x_resolve_in> res_in;
 	std::vector<bt2x_elt> elts;      // the round's elements (bt2x_seed_round, or converted resolves)
-	std::vector<DpWork> dps;             // the problems posed by the current DP request
 	// DP results of this read (memo by DpKey; records and edit images in arenas)
 	std::vector<DpMemo> memo;
 	std::vector<bt2x_aln_rec> recs;
 	std::vector<uint32_t> edits;
-	// seed round: the GPU round's request and results (or, for a REDO read, the host's)
-	bt2x_round_in round_in;
+	// seed round: the GPU round's results (or, for a REDO read, the host's)
 	bt2x_round_out round_out;
 	std::vector<bt2x_sat> sats;
-	std::vector<bt2x_exrange> exRange, exNew;           // extendSeeds' exRange (both strands)
 	RoundScratch rs;
 	std::vector<uint32_t> firstRow;
 	// extendSeeds state
@@ -1012,7 +1019,6 @@ struct ReadCtx {
 	std::vector<uint32_t> edbuf;         // SwDriver::resGap_.alres.ned_ storage
 	std::string sam;                     // the finished record
 	ReadTask task;
-	bool done = false;                   // finished, record not yet handed to the writer
 	// statistics for the run summary
 	bool aligned = false, repetitive = false;
 	std::string warn;               // the read's stderr warnings (printEEScoreMsg), written at retire
@@ -1020,10 +1026,6 @@ struct ReadCtx {
 	uint64_t ndp_used = 0;          // DP results the walk consumed (the rest were lookahead)
 	uint64_t ntight = 0;            // nextAlignment records consumed after -M tightened minsc
 	                                // within the same DP problem
-	// the backend's read store (Backend::read_store): this context's slot, whether the
-	// current read is in it, and whether the launch being gathered puts it there
-	uint32_t slot = 0;
-	bool in_store = false, put_now = false;
 	// the coroutine frame (ReadTask::promise_type::operator new)
 	static constexpr size_t kFrameBytes = 1536;     // align_read's frame is ~1.25 KiB
 	alignas(std::max_align_t) unsigned char frame_[kFrameBytes];
