@@ -1234,11 +1234,16 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 		const bool pf = host_prefetch();
 		for(size_t k = 0; k < C.wd.size(); k++) {
 			ReadCtx* c = C.wd[k];
-			if(pf && k + 3 < C.wd.size()) {                   // the read's codes and qualities (4 buffers)
-				const Read& r3 = C.wd[k + 3]->rd;
-				__builtin_prefetch(r3.fw.data()); __builtin_prefetch(r3.rc.data());
-				__builtin_prefetch(r3.qual.data()); __builtin_prefetch(r3.qualRev.data());
-				__builtin_prefetch(C.wd[k + 3]->dps.data());
+			if(pf && k + 3 < C.wd.size()) {                   // the read's codes and qualities
+				const ReadCtx* c3 = C.wd[k + 3];
+				const Read& r3 = c3->rd;
+				if(!store) {
+					__builtin_prefetch(r3.fw.data()); __builtin_prefetch(r3.rc.data());
+					__builtin_prefetch(r3.qual.data()); __builtin_prefetch(r3.qualRev.data());
+				} else if(c3->put_now) {
+					__builtin_prefetch(r3.fw.data()); __builtin_prefetch(r3.qual.data());
+				}
+				__builtin_prefetch(c3->dps.data());
 			}
 			const size_t i = C.wd0 + k, len = c->rd.length();
 			L.wd[i] = c; L.qb[i] = dbo; L.pb[i] = pko;
@@ -1279,8 +1284,10 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 			ReadCtx* c = C.wn[k];
 			if(pf && k + 3 < C.wn.size()) {
 				const ReadCtx* c3 = C.wn[k + 3];
-				__builtin_prefetch(c3->rd.fw.data()); __builtin_prefetch(c3->rd.rc.data());
-				__builtin_prefetch(c3->seed_in.data());
+				__builtin_prefetch(c3->rd.fw.data());
+				if(store) __builtin_prefetch(c3->rd.qual.data()); else __builtin_prefetch(c3->rd.rc.data());
+				if(!dseeds) __builtin_prefetch(c3->seed_in.data());
+				if(!c3->exRange.empty()) __builtin_prefetch(c3->exRange.data());
 			}
 			const size_t i = C.wn0 + k, len = c->rd.length();
 			L.wn[i] = c;
