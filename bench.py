@@ -784,7 +784,7 @@ def parity(ours_sam, ref_sam, n) -> dict:
 
 def host_threads(args, share: int, world: int) -> tuple[int, str]:
     """bt2x-align -p per rank: the node's CPU share split over the ranks.  One rank keeps
-    ~14 cores busy at the current host cost per read (6.3 us x 2.3 M reads/s),
+    ~14 cores busy at the current host cost per read (4.7 us x 3.1 M reads/s),
     so a share that leaves a rank fewer than kRankCores is reported (not silently raised)."""
     kRankCores = 14
     if args.host_threads > 0:
