@@ -1373,7 +1373,8 @@ void Aligner::scatter_resume(Launch& L, RunStats& st) {
 	const double t0 = now_s();
 	st.t_gather += L.t_gather;
 	const bool prefetch = host_prefetch(), full = host_prefetch_full(), more = host_prefetch_more();
-	pool().parallel_for(nrun, 64, [&](long i) {
+	static const long chunk = [] { const char* e = std::getenv("BT2X_SCATTER_CHUNK"); return e ? std::max(1L, std::atol(e)) : 64L; }();
+	pool().parallel_for(nrun, chunk, [&](long i) {
 		ReadCtx* c = L.run[(size_t)i];
 		if(prefetch) {
 			if(i + 6 < nrun) {
