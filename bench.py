@@ -87,10 +87,12 @@ def parse(argv=None):
     ap.add_argument("--c5-reads", type=int, default=5_000_000)
     ap.add_argument("--runs", type=int, default=3,
                     help="timed runs of bt2x-align over the same index and files; value = the median run")
-    ap.add_argument("--rep-leg", action="store_true", default=True,
-                    help="the repeat-heavy leg C3_rep50 (rank 0, N=1; default on): 50%% repeat families on a 200 Mbp "
-                         "synthetic genome, 1M x 150 bp reads, with the reference baseline and parity on 100k")
-    ap.add_argument("--no-rep-leg", dest="rep_leg", action="store_false")
+    # the repeat-heavy leg C3_rep50 (rank 0, N=1) is on by default: 50% repeat families on a
+    # 200 Mbp synthetic genome, 1M x 150 bp reads, with the reference baseline, parity on 100k
+    # and a replayed DP roofline; --no-rep-leg (or --no-legs) skips it
+    ap.add_argument("--rep-leg", action="store_true", default=True, help=argparse.SUPPRESS)
+    ap.add_argument("--no-rep-leg", dest="rep_leg", action="store_false",
+                    help="skip the repeat-heavy leg C3_rep50 (on by default at N=1)")
     ap.add_argument("--leg-replay-reads", type=int, default=1 << 18,
                     help="reads whose GPU launches are replayed for the C2 / C3_rep50 legs' DP rooflines")
     ap.add_argument("--align-extra", default=os.environ.get("BT2X_ALIGN_EXTRA", ""),
@@ -486,7 +488,9 @@ def roofline(args, rp, kernel=None):
                "what": f"the GPU launch sequence bt2x-align issues for replay_reads reads (one file; "
                        f"{args.replay_slots or max(1, args.slots // 2)} reads in flight"
                        f"{'' if args.replay_slots else ', a cohort of the timed run'}), replayed from HBM; "
-                       "kernel times from HIP events on the launch stream"}
+                       "kernel times from HIP events on the launch stream; the recording backend uploads "
+                       "each request's read bytes (no read store), so the DP kernels read the same bytes "
+                       "from a per-launch buffer instead of the store's slots"}
     return roof, kernels
 
 

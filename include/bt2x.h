@@ -36,7 +36,10 @@
 extern "C" {
 #endif
 
-#define BT2X_ABI_VERSION 2
+/* 3: bt2x_elt 8 B, bt2x_sat 4 B, bt2x_last_round_stats 4 words, bt2x_seed_round_dev's
+ * d_used 4 words.  bt2x_abi_version() returns the library's value: a binding compares it
+ * with the header it was written against before any other call. */
+#define BT2X_ABI_VERSION 3
 
 enum {
 	BT2X_OK = 0,
@@ -342,7 +345,10 @@ int bt2x_dp_align_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const uint8_t* d_qu
  * (2 * len bytes); the GPU derives patRc and the reversed qualities.  bt2x_seed_round and
  * bt2x_dp_align called with reads == NULL (and quals == NULL) then take read_off and
  * qual_off as offsets into the store.  The store grows to the largest slot written and
- * keeps its contents; calls on the context's stream stay in order. */
+ * keeps its contents; calls on the context's stream stay in order.  Requests are checked
+ * against the written extent ((highest slot put + 1) * SLOT_BYTES), not the allocation;
+ * a slot below it that was never put reads as N codes (4).  A slot's layout is tied to
+ * the len it was put with: offsets into it must use that rdlen. */
 #define BT2X_STORE_SLOT_BYTES 1024u
 #define BT2X_STORE_MAX_LEN 256u
 typedef struct {
@@ -521,7 +527,9 @@ typedef struct {
  * read's seeds itself, as listed above (patFw seeds, then patRc seeds, each strand at
  * depths i * interval + offset for i < num_offs, a seed over an N skipped, a strand off
  * per seedflags), into seeds[seed0 .. +nseeds) of a context-owned array of nseeds entries:
- * in[r].nseeds must be the count that gives (and the reads' seeds must not overlap). */
+ * in[r].nseeds must be the count that gives (and the reads' seeds must not overlap).  The
+ * library checks it on the GPU: when any read's count differs the call returns BT2X_E_ARG
+ * (its slots were filled with in-bounds stand-ins, so nothing stale was searched). */
 int bt2x_seed_round(bt2x_ctx* ctx, const uint8_t* reads, uint64_t reads_bytes,
                     const bt2x_seed_in* seeds, uint32_t nseeds,
                     const bt2x_round_in* in, uint32_t nreads,
@@ -531,7 +539,9 @@ int bt2x_seed_round(bt2x_ctx* ctx, const uint8_t* reads, uint64_t reads_bytes,
                     bt2x_elt* elts, uint32_t elt_cap,
                     bt2x_exrange* exr_out, uint32_t exr_cap,
                     uint32_t used[3]);
-/* Device-pointer variant (inputs resident in HBM; used: 3 x u32 in HBM).  Events:
+/* Device-pointer variant (inputs resident in HBM; d_used: 4 x u32 in HBM, [0..2] as used[]
+ * above and [3] the number of reads whose GPU-instantiated seed count differed from
+ * in[r].nseeds -- nonzero means the round's outputs are not to be used).  Events:
  * BT2X_K_SEED brackets the seed kernel, BT2X_K_RESOLVE the ranking + resolution,
  * BT2X_K_ROUND the whole round. */
 int bt2x_seed_round_dev(bt2x_ctx* ctx, const uint8_t* d_reads, const bt2x_seed_in* d_seeds, uint32_t nseeds,
@@ -548,6 +558,7 @@ void* bt2x_host_alloc(size_t bytes);
 void  bt2x_host_free(void* p);
 
 const char* bt2x_version(void);
+int bt2x_abi_version(void);      /* BT2X_ABI_VERSION the library was built with */
 /* sizeof of the ABI structs (seed_in, seed_out, dp_in, dp_out, aln_rec, scoring,
  * index_desc, counters, resolve_in, resolve_out, round_in, round_out, sat, exrange, elt,
  * store_in), for binding self-checks; returns the count. */

@@ -8,6 +8,8 @@ from __future__ import annotations
 import ctypes
 import numpy as np
 
+ABI_VERSION = 3             # BT2X_ABI_VERSION of the bt2x.h these mirrors follow
+
 SEED_IN = np.dtype([("read_off", "<u8"), ("seed_off", "u1"), ("seed_len", "u1"),
                     ("pad", "u1", 6)], align=True)
 SEED_OUT = np.dtype([("topf", "<u8"), ("botf", "<u8"), ("nlex", "u1"),

@@ -65,6 +65,7 @@ FUNCS = {
     "bt2x_store_reads": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_uint32]),
     "bt2x_version": (ctypes.c_char_p, []),
+    "bt2x_abi_version": (ctypes.c_int, []),
     "bt2x_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
     "bt2x_last_round_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "bt2x_last_round_stats_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
@@ -98,6 +99,9 @@ def load():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        v = L.bt2x_abi_version()
+        if v != abi.ABI_VERSION:      # a stale binding would misread the record arenas
+            raise Bt2xError(f"{LIB_PATH} has ABI version {v}, this binding follows {abi.ABI_VERSION}")
         _LIB = L
     return _LIB
 
@@ -279,7 +283,8 @@ class Context:
     def seed_round_dev(self, d_reads, d_seeds, nseeds, d_in, nreads, d_exr, maxelt, d_out, d_sats, sat_cap,
                        d_elts, elt_cap, d_exr_out, exr_cap, d_used, stream=0):
         """bt2x_seed_round_dev: seed search + ranking/prioritization + SA resolution of a
-        batch of reads, inputs resident in HBM."""
+        batch of reads, inputs resident in HBM.  d_used: 4 x u32 in HBM (arena use, then
+        the count of reads whose GPU-instantiated seeds differ from nseeds)."""
         check(load().bt2x_seed_round_dev(self.h, d_reads, d_seeds, nseeds, d_in, nreads, d_exr, maxelt, d_out,
                                          d_sats, sat_cap, d_elts, elt_cap, d_exr_out, exr_cap, d_used, stream),
               "bt2x_seed_round_dev")

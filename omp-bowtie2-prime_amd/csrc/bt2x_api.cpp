@@ -18,6 +18,12 @@
 #define HIPCHK(x) do { if((x) != hipSuccess) return BT2X_E_NODEVICE; } while(0)
 
 // ----------------------------------------------------------------- index load
+// The seed round's device counters (b_rcnt): 0-2 arena use (sats, elts, exRange out),
+// 3-7 sampling jobs/ranges/queue/draws, 8-15 sampling statistics, 16 the reads whose
+// GPU-instantiated seed count differs from in[r].nseeds (seed_gen_kernel).
+constexpr int kRoundCounters = 17;
+constexpr int kRoundSeedMismatch = 16;
+
 namespace {
 struct IndexOwner { std::vector<std::vector<uint8_t>> blocks; };
 
@@ -128,7 +134,8 @@ extern "C" void bt2x_host_free(void* p) {
 	if(p) (void)hipHostFree(p);
 }
 
-extern "C" const char* bt2x_version(void) { return "bt2x 0.2 (gfx950; abi 1.2)"; }
+extern "C" const char* bt2x_version(void) { return "bt2x 0.3 (gfx950; abi 3)"; }
+extern "C" int bt2x_abi_version(void) { return BT2X_ABI_VERSION; }
 
 // -------------------------------------------------------------------- context
 struct DevBuf {
@@ -167,7 +174,8 @@ struct bt2x_ctx {
 	DevBuf scratch, b_fail, b_heavy, b_in2, b_win;         // + DP windows cut from the text (BT2X_DP_REF_TEXT)
 	// the read store (bt2x_store_reads) and its upload staging
 	uint8_t* d_store = nullptr;
-	uint64_t store_bytes = 0;
+	uint64_t store_bytes = 0;   // allocated (with growth slack)
+	uint64_t store_hw = 0;      // (highest slot written + 1) * BT2X_STORE_SLOT_BYTES: requests are checked against it
 	DevBuf b_pack, b_sin, b_gseeds;                         // + seeds instantiated on the GPU
 	uint64_t npat = 0;
 	bool exact_best = true;                    // BT2X_OPT_EXACT_BEST
@@ -620,7 +628,7 @@ extern "C" int bt2x_dp_align(bt2x_ctx* c,
                              bt2x_dp_debug* debug) {
 	// reads == quals == NULL: read_off / qual_off index the read store (bt2x_store_reads)
 	const bool from_store = !reads && !quals;
-	if(from_store) reads_bytes = quals_bytes = c ? c->store_bytes : 0;
+	if(from_store) reads_bytes = quals_bytes = c ? c->store_hw : 0;
 	if(!c || (n && ((!from_store && (!reads || !quals)) || (!refs && refs_bytes) || !in || !out))) return BT2X_E_ARG;
 	if(nrec_used) *nrec_used = 0;
 	if(nedit_used) *nedit_used = 0;
@@ -747,12 +755,13 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	   (rc = c->b_ws.ensure(bt2x_round_ws_bytes() * lanes)) ||
 	   (rc = c->b_jobs.ensure(bt2x_round_job_bytes() * job_cap)) ||
 	   (rc = c->b_ranges.ensure(bt2x_round_range_bytes() * range_cap)) ||
-	   (rc = c->b_rcnt.ensure(16 * sizeof(uint32_t)))) return rc;
+	   (rc = c->b_rcnt.ensure(kRoundCounters * sizeof(uint32_t)))) return rc;
 	uint32_t* cnt = (uint32_t*)c->b_rcnt.p;
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_ROUND][0], s));
+	HIPCHK(hipMemsetAsync(cnt, 0, kRoundCounters * sizeof(uint32_t), s));
 	if(!d_seeds && nseeds) {                         // instantiateSeeds on the GPU
 		if((rc = c->b_gseeds.ensure(sizeof(bt2x_seed_in) * (size_t)nseeds)) ||
-		   (rc = bt2x_launch_seed_gen(d_reads, d_in, nreads, (bt2x_seed_in*)c->b_gseeds.p, nseeds, s)))
+		   (rc = bt2x_launch_seed_gen(d_reads, d_in, nreads, (bt2x_seed_in*)c->b_gseeds.p, nseeds, cnt + kRoundSeedMismatch, s)))
 			return rc;
 		d_seeds = (const bt2x_seed_in*)c->b_gseeds.p;
 	}
@@ -766,7 +775,6 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	c->n_seed_last = nseeds;
 	c->n_round_last = nreads;
 	// 2. finalize + rank + prioritize per read, then 3. place every row
-	HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s));
 	HIPCHK(hipMemsetAsync(c->d_stats + 8, 0, 3 * sizeof(unsigned long long), s));
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][0], s));
 	RoundLaunch a;
@@ -781,6 +789,7 @@ extern "C" int bt2x_seed_round_dev(bt2x_ctx* c, const uint8_t* d_reads, const bt
 	if((rc = bt2x_launch_resolve_dn(c->ix, a.rows, cnt + 1, elt_cap, 0, d_elts, c->d_stats + 8, c->ncu, s)))
 		return rc;
 	HIPCHK(hipMemcpyAsync(d_used, cnt, 3 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+	HIPCHK(hipMemcpyAsync(d_used + 3, cnt + kRoundSeedMismatch, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_RESOLVE][1], s));
 	HIPCHK(hipEventRecord(c->ev[BT2X_K_ROUND][1], s));
 	c->ev_valid[BT2X_K_RESOLVE] = c->ev_valid[BT2X_K_ROUND] = true;
@@ -799,7 +808,7 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
                                uint32_t used[3]) {
 	// reads == NULL: read_off indexes the read store (bt2x_store_reads)
 	const bool from_store = !reads;
-	if(from_store) reads_bytes = c ? c->store_bytes : 0;
+	if(from_store) reads_bytes = c ? c->store_hw : 0;
 	if(!c || !used || (nreads && (!in || !out))) return BT2X_E_ARG;
 	used[0] = used[1] = used[2] = 0;
 	if(nreads == 0) return BT2X_OK;
@@ -836,9 +845,12 @@ extern "C" int bt2x_seed_round(bt2x_ctx* c, const uint8_t* reads, uint64_t reads
 	                         (bt2x_elt*)c->b_elts.p, elt_cap, (bt2x_exrange*)c->b_exro.p, exr_cap,
 	                         (uint32_t*)c->b_used.p, c->stream);
 	if(rc) return rc;
-	HIPCHK(hipMemcpyAsync(used, c->b_used.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+	uint32_t u4[4] = {0, 0, 0, 0};
+	HIPCHK(hipMemcpyAsync(u4, c->b_used.p, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(hipMemcpyAsync(out, c->b_rout.p, sizeof(bt2x_round_out) * nreads, hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(stream_wait(c));
+	used[0] = u4[0]; used[1] = u4[1]; used[2] = u4[2];
+	if(u4[3]) return BT2X_E_ARG;                       // some in[r].nseeds != the seeds its read gives
 	if(used[0] > sat_cap || used[1] > elt_cap || used[2] > exr_cap) return BT2X_E_OVERFLOW;
 	if(used[0]) HIPCHK(hipMemcpyAsync(sats, c->b_sats.p, sizeof(bt2x_sat) * used[0], hipMemcpyDeviceToHost, c->stream));
 	if(used[1]) HIPCHK(hipMemcpyAsync(elts, c->b_elts.p, sizeof(bt2x_elt) * used[1], hipMemcpyDeviceToHost, c->stream));
@@ -862,6 +874,8 @@ extern "C" int bt2x_store_reads(bt2x_ctx* c, const uint8_t* packed, uint64_t pac
 		const uint64_t want = std::max<uint64_t>(need + need / 4, (uint64_t)1 << 20);
 		void* p = nullptr;
 		if(hipMalloc(&p, want) != hipSuccess) return BT2X_E_NOMEM;
+		// the new region reads as N codes until a read is put there
+		HIPCHK(hipMemsetAsync((uint8_t*)p + c->store_bytes, 4, want - c->store_bytes, c->stream));
 		if(c->d_store) {
 			HIPCHK(hipMemcpyAsync(p, c->d_store, c->store_bytes, hipMemcpyDeviceToDevice, c->stream));
 			HIPCHK(hipStreamSynchronize(c->stream));
@@ -870,6 +884,7 @@ extern "C" int bt2x_store_reads(bt2x_ctx* c, const uint8_t* packed, uint64_t pac
 		c->d_store = (uint8_t*)p;
 		c->store_bytes = want;
 	}
+	c->store_hw = std::max(c->store_hw, need);
 	int rc;
 	if((rc = c->b_pack.ensure(packed_bytes)) || (rc = c->b_sin.ensure(sizeof(bt2x_store_in) * n))) return rc;
 	HIPCHK(hipMemcpyAsync(c->b_pack.p, packed, packed_bytes, hipMemcpyHostToDevice, c->stream));

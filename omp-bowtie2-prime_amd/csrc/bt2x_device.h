@@ -55,7 +55,7 @@ int bt2x_launch_seed(const DevIndex& ix, const uint8_t* d_reads, const bt2x_seed
                      unsigned long long* d_ctr, int ncu, void* stream);
 // a seed round's seeds instantiated on the GPU (bt2x_seed_round with seeds == NULL)
 int bt2x_launch_seed_gen(const uint8_t* d_reads, const bt2x_round_in* d_in, uint32_t nreads, bt2x_seed_in* d_seeds,
-                         uint32_t nseeds, void* stream);
+                         uint32_t nseeds, uint32_t* d_bad, void* stream);
 
 int bt2x_launch_resolve(const DevIndex& ix, const bt2x_resolve_in* d_in, uint32_t n, int reject,
                         bt2x_resolve_out* d_out, unsigned long long* d_ctr, void* stream);

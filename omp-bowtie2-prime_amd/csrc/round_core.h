@@ -156,9 +156,16 @@ __host__ __device__ inline bool exr_covers(const bt2x_exrange& er, int fw, uint3
 
 // The first q < n with at(q) true, else n.  The kernel runs one read per lane at about one
 // wave per SIMD, so it is bound by the latency of its workspace loads: these scans load four
-// entries before testing any (at() must be safe to call up to n rounded up to 4).
+// entries before testing any (at() must be safe to call up to n rounded up to 4).  The host
+// build (host_round's twin, tests/cpp/test_round) scans exactly [0, n), so no entry past n
+// is read there and sanitizer / valgrind runs of the CPU build stay clean.
 template<class F>
 __host__ __device__ inline uint32_t find_first4(uint32_t n, const F& at) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+	for(uint32_t q = 0; q < n; q++)
+		if(at(q)) return q;
+	return n;
+#endif
 	for(uint32_t q = 0; q < n; q += 4) {
 		const bool t0 = at(q), t1 = at(q + 1), t2 = at(q + 2), t3 = at(q + 3);
 		if(t0) return q;

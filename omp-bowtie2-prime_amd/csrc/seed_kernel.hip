@@ -733,16 +733,22 @@ namespace {
 // MultiSeedResults::instantiateSeeds (aligner_seed.cpp:411-447) as the host driver runs it
 // (bt2x_align.cpp align_read): per strand (patFw, then patRc) the seeds at depth
 // i * interval + offset, i < num_offs -- a patRc seed at rdlen - depth - L -- skipping a
-// seed over an N.  One lane per read; never past the read's nseeds slots.
+// seed over an N.  One lane per read; never past the read's nseeds slots.  The caller's
+// nseeds is checked, not trusted: a read whose instantiated count differs bumps *bad (the
+// entry point then refuses the round), and every slot of [seed0, seed0 + nseeds) it leaves
+// unwritten gets an in-bounds stand-in (the read's first patFw seed position), so the seed
+// search never reads a stale or uninitialised entry.
 __global__ void __launch_bounds__(256) seed_gen_kernel(const uint8_t* __restrict__ reads,
                                                        const bt2x_round_in* __restrict__ in, uint32_t n,
-                                                       bt2x_seed_in* __restrict__ seeds, uint32_t cap) {
+                                                       bt2x_seed_in* __restrict__ seeds, uint32_t cap,
+                                                       uint32_t* __restrict__ bad) {
 	const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
 	if(r >= n) return;
 	const bt2x_round_in q = in[r];
 	const uint32_t L = q.seedlen, len = q.rdlen;
 	uint64_t k = q.seed0;
 	const uint64_t end = min((uint64_t)cap, q.seed0 + q.nseeds);
+	uint32_t made = 0;
 	for(int s = 0; s < 2; s++) {
 		if(q.seedflags & (1u << s)) continue;
 		const uint64_t ro = q.read_off + (s ? len : 0);
@@ -751,21 +757,30 @@ __global__ void __launch_bounds__(256) seed_gen_kernel(const uint8_t* __restrict
 			const uint32_t st = s ? len - depth - L : depth;
 			bool ok = true;
 			for(uint32_t j = 0; j < L; j++) ok &= reads[ro + st + j] <= 3;
-			if(!ok || k >= end) continue;
+			if(!ok) continue;
+			made++;
+			if(k >= end) continue;
 			bt2x_seed_in si;
 			si.read_off = ro; si.seed_off = (uint8_t)st; si.seed_len = (uint8_t)L;
 			for(int b = 0; b < 6; b++) si.pad[b] = 0;
 			seeds[k++] = si;
 		}
 	}
+	if(made != q.nseeds) atomicAdd(bad, 1u);
+	for(; k < end; k++) {
+		bt2x_seed_in si;
+		si.read_off = q.read_off; si.seed_off = 0; si.seed_len = (uint8_t)L;
+		for(int b = 0; b < 6; b++) si.pad[b] = 0;
+		seeds[k] = si;
+	}
 }
 } // namespace
 
 int bt2x_launch_seed_gen(const uint8_t* d_reads, const bt2x_round_in* d_in, uint32_t nreads, bt2x_seed_in* d_seeds,
-                         uint32_t nseeds, void* stream) {
+                         uint32_t nseeds, uint32_t* d_bad, void* stream) {
 	if(nreads == 0) return 0;
 	hipLaunchKernelGGL(seed_gen_kernel, dim3((nreads + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_reads, d_in, nreads,
-	                   d_seeds, nseeds);
+	                   d_seeds, nseeds, d_bad);
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }
 

@@ -76,17 +76,11 @@ def test_round_kernel_matches_host(sets):
         assert st["mismatches"] == 0 and st["cases"] > 1000, (name, st)
 
 
-@pytest.mark.gpu
-def test_round_kernel_vs_reference_rank_golden(tmp_path):
-    """bt2x_seed_round against the reference's own rankSeedHits (tests/golden/rank_rep.txt.xz,
-    oracle/refharness.cpp "rank": aligner_seed.h:1000-1061 with a RandomSource seeded per
-    (read, round)).  Every read and round of the rep fixture runs through the kernel with
-    the golden's seeds, the golden's RNG seed and maxelt 0 (prioritizeSATups then samples
-    nothing, so the returned RNG state is the state after ranking): NO_HITS exactly where the
-    reference found none, and SeedResults::nonzeroOffsets(), numElts() and the RandomSource
-    state after rankSeedHits equal the reference's."""
+def _rank_rounds(tmp_path):
+    """The rep fixture's (read, round) pairs as bt2x_round_in rows (the golden's seeds, RNG
+    seeds and round offsets), with the golden's seed rows and rank records."""
     import numpy as np
-    from bt2x import abi, lib
+    from bt2x import abi
     import seeds_ref as bseeds
     base = g.materialize_index("rep", str(tmp_path))
     case = g.SeedCase(os.path.join(g.GOLDEN, "rep_reads.fq.xz"), os.path.join(g.GOLDEN, "seeds_rep.txt.xz"))
@@ -138,6 +132,21 @@ def test_round_kernel_vs_reference_rank_golden(tmp_path):
         exp.append(t)
     rin = np.concatenate(rin)
     sin = case.inp[np.array(seed_sel, dtype=np.int64)]
+    return base, case, reads, rin, sin, exp
+
+
+@pytest.mark.gpu
+def test_round_kernel_vs_reference_rank_golden(tmp_path):
+    """bt2x_seed_round against the reference's own rankSeedHits (tests/golden/rank_rep.txt.xz,
+    oracle/refharness.cpp "rank": aligner_seed.h:1000-1061 with a RandomSource seeded per
+    (read, round)).  Every read and round of the rep fixture runs through the kernel with
+    the golden's seeds, the golden's RNG seed and maxelt 0 (prioritizeSATups then samples
+    nothing, so the returned RNG state is the state after ranking): NO_HITS exactly where the
+    reference found none, and SeedResults::nonzeroOffsets(), numElts() and the RandomSource
+    state after rankSeedHits equal the reference's."""
+    import numpy as np
+    from bt2x import abi, lib
+    base, case, reads, rin, sin, exp = _rank_rounds(tmp_path)
     n = len(rin)
     ctx = lib.Context(lib.Index(base, load_offs=True))
     out = ctx.seed_round(case.reads, sin, rin, np.zeros(0, dtype=abi.EXRANGE), 0)[0]
@@ -161,3 +170,38 @@ def test_round_kernel_vs_reference_rank_golden(tmp_path):
         if got != want:
             bad.append((t[:3], got, want))
     assert nk > 5000 and not bad, (len(bad), bad[:5])
+
+
+@pytest.mark.gpu
+def test_round_refuses_a_wrong_gpu_seed_count(tmp_path):
+    """bt2x_seed_round with seeds == NULL checks each in[r].nseeds against the seeds the GPU
+    instantiates (a seed over an N is skipped, so the count depends on the read's bytes):
+    a read containing an N with its count off by one either way makes the call return
+    BT2X_E_ARG, and the context still answers the correct call exactly afterwards."""
+    import numpy as np
+    from bt2x import abi, lib
+    base, case, reads, rin, sin, exp = _rank_rounds(tmp_path)
+    ctx = lib.Context(lib.Index(base, load_offs=True))
+    noexr = np.zeros(0, dtype=abi.EXRANGE)
+    ref = ctx.seed_round(case.reads, None, rin, noexr, 0)[0]
+    # a round of a read with an N inside a would-be seed window (fewer seeds than offsets)
+    sel = None
+    for i, r in enumerate(rin):
+        o = int(r["read_off"])
+        codes = case.reads[o: o + int(r["rdlen"])]
+        if (codes > 3).any() and 0 < int(r["nseeds"]) < 2 * int(r["num_offs"]):
+            sel = i
+            break
+    assert sel is not None, "the rep fixture has reads with N"
+    for delta in (1, -1):
+        bad = rin.copy()
+        bad["nseeds"][sel] += delta
+        # later reads' seeds move with the count, so the reads' seeds never overlap
+        bad["seed0"][sel + 1:] += delta
+        with pytest.raises(lib.Bt2xError) as e:
+            ctx.seed_round(case.reads, None, bad, noexr, 0)
+        assert e.value.code == abi.E_ARG
+    again = ctx.seed_round(case.reads, None, rin, noexr, 0)[0]
+    ctx.close()
+    for f in ("status", "nonz", "num_elts", "rnd_last", "nsat", "nelt", "nexr"):
+        np.testing.assert_array_equal(again[f], ref[f], err_msg=f)
