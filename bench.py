@@ -835,7 +835,19 @@ def main():
     rank, world, local = bdist.world()
     gpu = int(os.environ.get("BT2X_BENCH_DEVICE", local))
     share = cpu_share()
-    args.host_threads, threads_note = host_threads(args, share, world)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    args.host_threads, threads_note = host_threads(args, share, local_world)
+    # N > 1: every local rank its own CPUs inside its GPU's NUMA node (bt2x.dist), and no
+    # more threads than it has CPUs; N = 1 keeps the aligner's own NUMA-node pinning
+    cpu_set, cpu_note = None, ""
+    if local_world > 1:
+        devs = [gpu] * local_world if "BT2X_BENCH_DEVICE" in os.environ else list(range(local_world))
+        sets, cpu_note = bdist.local_cpu_sets(local_world, devs)
+        if sets[local]:
+            cpu_set = bdist.format_cpu_list(sets[local])
+            if args.host_threads > len(sets[local]):
+                args.host_threads = len(sets[local])
+                threads_note += f"; capped at the rank's {len(sets[local])} CPUs"
     workdir = args.workdir
     os.makedirs(workdir, exist_ok=True)
     # inputs first: the read generator forks, which must happen before the GPU is touched
@@ -866,6 +878,8 @@ def main():
     cmd = [args.aligner, "-x", base, "-U", ",".join(warm + steps), "-S", out_sam, "--dpad", str(args.dpad),
            "--device", str(gpu), "-p", str(args.host_threads), "--slots", str(args.slots),
            "--warmup-files", str(len(warm)), "--metrics", "--stats"] + args.align_extra.replace(",", " ").split()
+    if cpu_set:
+        cmd += ["--cpus", cpu_set]
     # args.runs timed runs over the same index and files (separate processes); value = the
     # median run's (by the max over ranks of its timed wall time); every run is listed
     runs = []
@@ -895,6 +909,12 @@ def main():
                                                                          "t_align", "t_max"))
     stats = kv_line(err, "BT2X_STATS")
     value = tot["nread"] / t_max / 1e6
+    # every rank's CPU affinity as its aligner reported it (BT2X_CPUS), in rank order
+    mine = next((ln.split(" ", 1)[1].strip() for ln in err.splitlines() if ln.startswith("BT2X_CPUS ")), None)
+    host_cpus = [mine]
+    if dist:
+        host_cpus = [None] * world
+        dist.all_gather_object(host_cpus, mine)
     t_files = [float(x) for x in str(timed.get("t_files", "")).split(",") if x]
 
     def run_entry(r):
@@ -921,6 +941,7 @@ def main():
                                f"step = one FASTQ file of {per} reads",
                    "reads_per_gpu": args.reads, "read_len": args.read_len, "parallelism": f"dp{world} (read shards)",
                    "host_threads": args.host_threads, "host_threads_note": threads_note, "cpu_share": share,
+                   "host_cpus": host_cpus, "host_cpus_note": cpu_note or "one rank: the aligner pins itself to its GPU's NUMA node",
                    "slots": args.slots, "key": workload_key(args)},
         "end_to_end": {"runs": [run_entry(r) for r in runs],
                        "value_is": f"the median of {len(runs)} timed runs (separate bt2x-align processes, same index "

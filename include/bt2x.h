@@ -81,7 +81,10 @@ typedef struct {
 /* Parse <base>.1.bt2l like Ebwt::readIntoMemory; with load_offs also <base>.2.bt2l (SA
  * sample) and <base>.4.bt2l (packed joined text).  Given both, bt2x_open rebuilds the
  * full suffix array in HBM (an MI355X-first choice: 4 B/row resident, so SA lookups
- * and unique-range seed extension need no LF walks). */
+ * and unique-range seed extension need no LF walks).  The arrays are read-only views of
+ * the files mapped into memory (no copies): processes of one node that load the same
+ * index share one host copy through the page cache, and the desc stays valid until
+ * bt2x_index_free. */
 int  bt2x_index_load(const char* basename, int load_offs, bt2x_index_desc* out);
 void bt2x_index_free(bt2x_index_desc* idx);
 

@@ -139,6 +139,152 @@ def rank_device(local_rank: int, env=None) -> str:
     return str(local_rank)
 
 
+# ------------------------------------------------------------- per-rank host CPUs
+#
+# One rank keeps ~14 host cores busy per MI355X, so on a node with 8 GPUs
+# the ranks must not share cores: each local rank gets a disjoint set of CPUs inside the
+# NUMA node of its GPU (the ranks on one node split that node's allowed CPUs into equal
+# contiguous slices), and runs cpu_share / ranks threads on it.  Everything here reads
+# sysfs only: the launcher never initialises the GPU.
+
+def cpu_quota() -> int:
+    """CPUs this process may keep busy: its affinity, capped by the cgroup's CPU quota (a
+    GPU box's affinity lists the whole machine but its quota grants a share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def parse_cpu_list(text: str) -> list[int]:
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11] (the kernel's cpulist format)."""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def format_cpu_list(cpus) -> str:
+    """[0, 1, 2, 3, 8] -> '0-3,8'."""
+    cpus = sorted(set(cpus))
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def node_cpus(node: int, sysfs: str = "/sys") -> list[int]:
+    try:
+        with open(os.path.join(sysfs, f"devices/system/node/node{node}/cpulist")) as f:
+            return parse_cpu_list(f.read())
+    except OSError:
+        return []
+
+
+def gpu_numa_nodes(sysfs: str = "/sys") -> list[int]:
+    """NUMA node of every GPU in HIP's device order (the KFD topology's GPU nodes in node
+    order, as ROCr enumerates its agents), from the PCI device's numa_node; -1 where
+    unknown.  [] without a KFD topology (no GPU driver, e.g. the CPU container)."""
+    root = os.path.join(sysfs, "class/kfd/kfd/topology/nodes")
+    try:
+        ids = sorted(int(n) for n in os.listdir(root) if n.isdigit())
+    except OSError:
+        return []
+    out = []
+    for n in ids:
+        props = {}
+        try:
+            with open(os.path.join(root, str(n), "properties")) as f:
+                for ln in f:
+                    k, _, v = ln.partition(" ")
+                    props[k] = v.strip()
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0") or 0) == 0:
+            continue                             # a CPU node
+        loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+        bdf = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+        node = -1
+        try:
+            with open(os.path.join(sysfs, "bus/pci/devices", bdf, "numa_node")) as f:
+                node = int(f.read().strip())
+        except (OSError, ValueError):
+            pass
+        out.append(node)
+    return out
+
+
+def core_keys(cpus, sysfs: str = "/sys") -> dict:
+    """cpu -> its physical core's first hardware thread (SMT siblings share a key)."""
+    out = {}
+    for c in cpus:
+        try:
+            with open(os.path.join(sysfs, f"devices/system/cpu/cpu{c}/topology/thread_siblings_list")) as f:
+                out[c] = min(parse_cpu_list(f.read()))
+        except (OSError, ValueError):
+            out[c] = c
+    return out
+
+
+def rank_cpu_sets(devices: list[int], allowed, gpu_nodes: list[int], node_lists: dict,
+                  core_of: dict | None = None) -> tuple[list, str]:
+    """Disjoint CPU sets for the local ranks whose GPUs are `devices` (HIP indices, one per
+    local rank): the ranks on one NUMA node split that node's `allowed` CPUs into equal
+    slices of whole physical cores (SMT siblings stay together: `core_of` maps a CPU to its
+    core), in local-rank order.  A rank whose GPU's node is unknown, or whose node has fewer
+    allowed CPUs than ranks on it, draws from all allowed CPUs not taken by a node split.
+    Returns (per-rank sorted CPU lists, a note)."""
+    core_of = core_of or {}
+    allowed = sorted(set(allowed), key=lambda c: (core_of.get(c, c), c))
+    nodes = [gpu_nodes[d] if 0 <= d < len(gpu_nodes) else -1 for d in devices]
+    groups: dict = {}
+    for r, nd in enumerate(nodes):
+        groups.setdefault(nd, []).append(r)
+    sets: list = [None] * len(devices)
+    taken: set = set()
+    notes = []
+    for nd, ranks in sorted(groups.items()):
+        inode = set(node_lists.get(nd, []))
+        pool = [c for c in allowed if c in inode] if nd >= 0 else []
+        if nd < 0 or len(pool) < len(ranks):
+            continue
+        share = len(pool) // len(ranks)
+        for i, r in enumerate(ranks):
+            sets[r] = sorted(pool[i * share:(i + 1) * share])
+            taken.update(sets[r])
+        notes.append(f"node{nd}: {len(ranks)} rank(s) x {share} CPUs")
+    rest = [r for r in range(len(devices)) if sets[r] is None]
+    if rest:
+        pool = [c for c in allowed if c not in taken]
+        share = len(pool) // len(rest) if pool else 0
+        for i, r in enumerate(rest):
+            sets[r] = sorted(pool[i * share:(i + 1) * share] if share else allowed)
+        notes.append(f"no NUMA split for rank(s) {rest}: " + (f"{share} CPUs each" if share else "all allowed CPUs"))
+    return sets, "; ".join(notes)
+
+
+def local_cpu_sets(local_world: int, devices: list[int] | None = None) -> tuple[list, str]:
+    """rank_cpu_sets for this node's local ranks (GPU k for local rank k unless `devices`
+    says otherwise), over this process's affinity and the machine's sysfs."""
+    devices = list(range(local_world)) if devices is None else devices
+    gn = gpu_numa_nodes()
+    lists = {nd: node_cpus(nd) for nd in set(gn) if nd >= 0}
+    allowed = os.sched_getaffinity(0)
+    return rank_cpu_sets(devices, allowed, gn, lists, core_keys(allowed))
+
+
 def aligner_messages(stderr: str) -> str:
     """An aligner's stderr minus its launcher-facing lines (BT2X_*) and its alignment
     summary: what a single run leaves for the user (per-read warnings)."""
@@ -203,6 +349,14 @@ def run_sharded(aligner: str, args: list[str], dist=None, set_device: bool = Tru
     cmd = [aligner] + args + ["-S", part, "--shard", f"{rank}/{world_size}", "--metrics"]
     if rank > 0:
         cmd.append("--no-hd")
+    # this rank's own CPUs inside its GPU's NUMA node (unless the caller chose them)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    if local_world > 1 and "--cpus" not in args:
+        sets, _ = local_cpu_sets(local_world)
+        if sets[local_rank]:
+            cmd += ["--cpus", format_cpu_list(sets[local_rank])]
+            if "-p" not in args:
+                cmd += ["-p", str(max(1, min(len(sets[local_rank]), cpu_quota() // local_world)))]
     env = dict(os.environ)
     if set_device:
         env["HIP_VISIBLE_DEVICES"] = rank_device(local_rank, env)

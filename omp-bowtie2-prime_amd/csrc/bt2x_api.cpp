@@ -3,6 +3,9 @@
 // seed search and DP goes through the gfx950 kernels, and without a HIP device
 // bt2x_open fails with BT2X_E_NODEVICE.
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -25,72 +28,111 @@ constexpr int kRoundCounters = 17;
 constexpr int kRoundSeedMismatch = 16;
 
 namespace {
-struct IndexOwner { std::vector<std::vector<uint8_t>> blocks; };
+// The host image of an index is the .bt2l files themselves, mapped read-only: the arrays
+// bt2x_index_desc points at are views into the mappings (no copies), so ranks of one node
+// that load the same index share its pages through the page cache -- one host copy per
+// node, not per GPU -- and the pages a run never reads after bt2x_open's upload (the BWT,
+// the SA sample; the packed text unless host-cut windows ask for it) stay unread.
+struct Mapping {
+	const uint8_t* p = nullptr;
+	size_t n = 0;
+};
+struct IndexOwner {
+	std::vector<Mapping> maps;
+	~IndexOwner() { for(const Mapping& m : maps) if(m.p && m.n) munmap(const_cast<uint8_t*>(m.p), m.n); }
+};
 
-bool read_exact(FILE* f, void* p, size_t n) { return n == 0 || fread(p, 1, n, f) == n; }
-
-template<typename T> T* take(IndexOwner* o, size_t n) {
-	o->blocks.emplace_back(n * sizeof(T) + 16);
-	return reinterpret_cast<T*>(o->blocks.back().data());
+// Map a whole file read-only (empty files map to an empty view).
+bool map_file(IndexOwner* o, const std::string& path, Mapping& m) {
+	const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+	if(fd < 0) return false;
+	struct stat st;
+	if(fstat(fd, &st) != 0) { close(fd); return false; }
+	m.n = (size_t)st.st_size;
+	m.p = nullptr;
+	if(m.n) {
+		void* v = mmap(nullptr, m.n, PROT_READ, MAP_PRIVATE, fd, 0);
+		if(v == MAP_FAILED) { close(fd); return false; }
+		m.p = (const uint8_t*)v;
+		o->maps.push_back(m);
+	}
+	close(fd);
+	return true;
 }
+
+// A bounds-checked cursor over a mapping: scalar fields are copied out, arrays are views.
+struct Cursor {
+	const Mapping& m;
+	size_t at = 0;
+	bool ok = true;
+	template<typename T> T get() {
+		T v{};
+		if(!ok || at + sizeof(T) > m.n) { ok = false; return v; }
+		std::memcpy(&v, m.p + at, sizeof(T));
+		at += sizeof(T);
+		return v;
+	}
+	template<typename T> const T* view(uint64_t count) {
+		const uint64_t bytes = count * sizeof(T);
+		if(!ok || count > m.n / (sizeof(T) ? sizeof(T) : 1) || at + bytes > m.n) { ok = false; return nullptr; }
+		const T* v = reinterpret_cast<const T*>(m.p + at);
+		at += bytes;
+		return v;
+	}
+};
 }
 
 // Ebwt::readIntoMemory (bt2_io.cpp:39-560) for the 64-bit (.bt2l) forward index.
 extern "C" int bt2x_index_load(const char* base, int load_offs, bt2x_index_desc* o) {
 	if(!base || !o) return BT2X_E_ARG;
 	std::memset(o, 0, sizeof(*o));
-	std::string p1 = std::string(base) + ".1.bt2l";
-	FILE* f = fopen(p1.c_str(), "rb");
-	if(!f) return BT2X_E_IO;
 	std::unique_ptr<IndexOwner> own(new IndexOwner());
-	uint32_t one = 0; uint64_t len = 0; int32_t lineRate, lps, offRate, ftabChars, flags;
-	bool ok = read_exact(f, &one, 4) && read_exact(f, &len, 8) && read_exact(f, &lineRate, 4) &&
-	          read_exact(f, &lps, 4) && read_exact(f, &offRate, 4) && read_exact(f, &ftabChars, 4) &&
-	          read_exact(f, &flags, 4);
+	Mapping m1;
+	if(!map_file(own.get(), std::string(base) + ".1.bt2l", m1)) return BT2X_E_IO;
+	Cursor c1{m1};
+	const uint32_t one = c1.get<uint32_t>();
+	const uint64_t len = c1.get<uint64_t>();
+	const int32_t lineRate = c1.get<int32_t>(), lps = c1.get<int32_t>(), offRate = c1.get<int32_t>();
+	const int32_t ftabChars = c1.get<int32_t>(), flags = c1.get<int32_t>();
+	(void)lps;
 	// only the fork's build is supported: little-endian, lineRate 7 (128-B sides)
-	if(!ok || one != 1 || lineRate != 7 || ftabChars < 1 || ftabChars > 16) { fclose(f); return BT2X_E_IO; }
-	uint64_t npat = 0, nfrag = 0;
-	ok = read_exact(f, &npat, 8);
-	uint64_t* plen = take<uint64_t>(own.get(), npat + 1);
-	ok = ok && read_exact(f, plen, 8 * npat) && read_exact(f, &nfrag, 8);
-	uint64_t* rstarts = take<uint64_t>(own.get(), 3 * nfrag + 1);
-	ok = ok && read_exact(f, rstarts, 24 * nfrag);
+	if(!c1.ok || one != 1 || lineRate != 7 || ftabChars < 1 || ftabChars > 16) return BT2X_E_IO;
+	const uint64_t npat = c1.get<uint64_t>();
+	const uint64_t* plen = c1.view<uint64_t>(npat);
+	const uint64_t nfrag = c1.get<uint64_t>();
+	const uint64_t* rstarts = c1.view<uint64_t>(nfrag <= m1.n / 24 ? 3 * nfrag : m1.n);     // (too many: fails)
 	const uint64_t sideSz = 1ULL << lineRate, sideBwtSz = sideSz - 32;    // EbwtParams::init
 	const uint64_t numSides = (len / 4 + 1 + sideBwtSz - 1) / sideBwtSz;
 	const uint64_t ebwtTot = numSides * sideSz;
-	uint8_t* ebwt = take<uint8_t>(own.get(), ebwtTot);
-	uint64_t zoff = 0;
-	ok = ok && read_exact(f, ebwt, ebwtTot) && read_exact(f, &zoff, 8) && read_exact(f, o->fchr, 40);
+	const uint8_t* ebwt = c1.view<uint8_t>(ebwtTot);
+	const uint64_t zoff = c1.get<uint64_t>();
+	if(const uint64_t* fc = c1.view<uint64_t>(5)) std::memcpy(o->fchr, fc, 40);
 	const uint64_t ftabLen = (1ULL << (2 * ftabChars)) + 1, eftabLen = 2ULL * ftabChars;
-	uint64_t* ftab = take<uint64_t>(own.get(), ftabLen);
-	uint64_t* eftab = take<uint64_t>(own.get(), eftabLen);
-	ok = ok && read_exact(f, ftab, 8 * ftabLen) && read_exact(f, eftab, 8 * eftabLen);
-	fclose(f);
-	if(!ok) return BT2X_E_IO;
+	const uint64_t* ftab = c1.view<uint64_t>(ftabLen);
+	const uint64_t* eftab = c1.view<uint64_t>(eftabLen);
+	if(!c1.ok) return BT2X_E_IO;
 	o->len = len; o->zoff = zoff; o->ftab_chars = ftabChars; o->off_rate = offRate;
 	o->line_rate = lineRate; o->flags = flags;
 	o->ebwt = ebwt; o->ebwt_bytes = ebwtTot;
 	o->ftab = ftab; o->ftab_len = ftabLen; o->eftab = eftab; o->eftab_len = eftabLen;
 	o->plen = plen; o->npat = npat; o->rstarts = rstarts; o->nfrag = nfrag;
 	if(load_offs) {
-		std::string p2 = std::string(base) + ".2.bt2l";
-		f = fopen(p2.c_str(), "rb");
-		if(!f) return BT2X_E_IO;
+		Mapping m2;
+		if(!map_file(own.get(), std::string(base) + ".2.bt2l", m2)) return BT2X_E_IO;
+		Cursor c2{m2};
+		if(offRate < 0 || offRate > 62) return BT2X_E_IO;
 		const uint64_t offsLen = (len + 1 + (1ULL << offRate) - 1) >> offRate;
-		uint64_t* offs = take<uint64_t>(own.get(), offsLen);
-		ok = read_exact(f, &one, 4) && read_exact(f, offs, 8 * offsLen);
-		fclose(f);
-		if(!ok) return BT2X_E_IO;
+		(void)c2.get<uint32_t>();                             // endianness word
+		const uint64_t* offs = c2.view<uint64_t>(offsLen);
+		if(!c2.ok) return BT2X_E_IO;
 		o->offs = offs; o->offs_len = offsLen;
 		// packed joined text (BitPairReference .4: the non-N bases, 4 per byte)
-		std::string p4 = std::string(base) + ".4.bt2l";
-		f = fopen(p4.c_str(), "rb");
-		if(f) {
+		Mapping m4;
+		if(map_file(own.get(), std::string(base) + ".4.bt2l", m4)) {
+			Cursor c4{m4};
 			const uint64_t tb = (len + 3) / 4;
-			uint8_t* t = take<uint8_t>(own.get(), tb + 16);
-			ok = read_exact(f, t, tb);
-			fclose(f);
-			if(!ok) return BT2X_E_IO;
+			const uint8_t* t = c4.view<uint8_t>(tb);
+			if(!c4.ok) return BT2X_E_IO;
 			o->text2 = t; o->text2_bytes = tb;
 		}
 	}

@@ -19,6 +19,7 @@
 #include <climits>
 
 #include <fcntl.h>
+#include <sched.h>
 #include <future>
 #include <malloc.h>
 #include <sys/mman.h>
@@ -244,6 +245,57 @@ FastqReader::~FastqReader() {
 		if(F.map) ::munmap((void*)F.map, F.len);
 		if(F.fd >= 0) ::close(F.fd);
 	}
+}
+
+// ------------------------------------------------------------------- CPU sets
+
+bool parse_cpu_list(const std::string& s, std::vector<int>& out) {
+	out.clear();
+	size_t i = 0;
+	while(i < s.size()) {
+		size_t j = i;
+		while(j < s.size() && std::isdigit((unsigned char)s[j])) j++;
+		if(j == i) return false;
+		const long a = std::atol(s.substr(i, j - i).c_str());
+		long b = a;
+		if(j < s.size() && s[j] == '-') {
+			size_t k = ++j;
+			while(j < s.size() && std::isdigit((unsigned char)s[j])) j++;
+			if(j == k) return false;
+			b = std::atol(s.substr(k, j - k).c_str());
+		}
+		if(b < a || b >= CPU_SETSIZE) return false;
+		for(long c = a; c <= b; c++) out.push_back((int)c);
+		if(j < s.size() && s[j] != ',') return false;
+		i = j + 1;
+	}
+	return !out.empty();
+}
+
+std::string affinity_list() {
+	cpu_set_t cur;
+	if(sched_getaffinity(0, sizeof cur, &cur) != 0) return "";
+	std::string out;
+	for(int c = 0; c < CPU_SETSIZE; c++) {
+		if(!CPU_ISSET(c, &cur)) continue;
+		int e = c;
+		while(e + 1 < CPU_SETSIZE && CPU_ISSET(e + 1, &cur)) e++;
+		if(!out.empty()) out += ',';
+		out += std::to_string(c);
+		if(e > c) out += '-' + std::to_string(e);
+		c = e;
+	}
+	return out;
+}
+
+void apply_cpu_list(const std::string& list) {
+	std::vector<int> cpus;
+	if(!parse_cpu_list(list, cpus)) throw std::runtime_error("--cpus: malformed CPU list '" + list + "'");
+	cpu_set_t want;
+	CPU_ZERO(&want);
+	for(int c : cpus) CPU_SET(c, &want);
+	if(sched_setaffinity(0, sizeof want, &want) != 0)
+		throw std::runtime_error("--cpus " + list + ": none of these CPUs may be used by this process");
 }
 
 // ------------------------------------------------------------------- RefInfo

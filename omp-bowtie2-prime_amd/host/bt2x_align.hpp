@@ -743,6 +743,16 @@ inline std::vector<std::string> split_list(const std::string& s) {
 	return out;
 }
 
+// A CPU list as the kernel prints it ("0-15,128-143"); false on a malformed list.
+bool parse_cpu_list(const std::string& s, std::vector<int>& out);
+// The process's CPU affinity as such a list.
+std::string affinity_list();
+// --cpus: run on exactly these CPUs (sched_setaffinity before any worker thread starts, so
+// the threads inherit the mask and first-touch places their memory on those CPUs' node).
+// The sharded launcher (bt2x.dist, bench.py) gives each rank of a node a disjoint set
+// inside its GPU's NUMA node.  Throws on a malformed list or one the process may not use.
+void apply_cpu_list(const std::string& list);
+
 // ------------------------------------------------------------------- reference
 
 // What the driver needs of the index besides the device copy: reference names and

@@ -286,7 +286,8 @@ void usage() {
 	             "                  [-i FUNC] [--score-min FUNC] [--n-ceil FUNC] [--mp MX,MN] [--np N]\n"
 	             "                  [--rdg O,E] [--rfg O,E] [--gbar N] [--seed N] [--no-sse8] [--i16-build]\n"
 	             "                  [--no-hd] [-p threads] [--slots N] [--device N] [--stats]\n"
-	             "                  [--shard i/N] [--warmup-files K] [--metrics] [--no-pipeline] [--streams 1|2]\n");
+	             "                  [--shard i/N] [--warmup-files K] [--metrics] [--no-pipeline] [--streams 1|2]\n"
+	             "                  [--cpus LIST]\n");
 }
 
 } // namespace
@@ -304,7 +305,7 @@ int main(int argc, char** argv) {
 	int streams = 1;
 	if(const char* e = std::getenv("BT2X_STREAMS")) streams = std::atoi(e);
 	int shard = 0, nshards = 1, warm_files = 0;
-	std::string dump;
+	std::string dump, cpus;
 	for(int i = 1; i < argc; i++) {
 		const std::string a = argv[i];
 		auto val = [&]() -> const char* {
@@ -328,6 +329,7 @@ int main(int argc, char** argv) {
 		else if(a == "--no-hd") hd = false;
 		else if(a == "--metrics") metrics = true;
 		else if(a == "--warmup-files") warm_files = std::atoi(val());
+		else if(a == "--cpus") cpus = val();
 		else if(a == "--shard") {
 			if(std::sscanf(val(), "%d/%d", &shard, &nshards) != 2 || nshards < 1 || shard < 0 || shard >= nshards) {
 				std::fprintf(stderr, "--shard takes i/N with 0 <= i < N\n");
@@ -350,7 +352,15 @@ int main(int argc, char** argv) {
 		fq = mate1;
 	}
 	if(idx.empty() || fq.empty()) { usage(); return 1; }
-	const std::string numa = pin_to_gpu_node(device, threads);
+	// --cpus (the sharded launcher's per-rank set) replaces the NUMA-node pinning
+	std::string numa;
+	if(!cpus.empty()) {
+		try { apply_cpu_list(cpus); } catch(const std::exception& e) { std::fprintf(stderr, "%s\n", e.what()); return 1; }
+		numa = "cpus";
+	} else {
+		numa = pin_to_gpu_node(device, threads);
+	}
+	std::fprintf(stderr, "BT2X_CPUS %s\n", affinity_list().c_str());
 	const std::vector<std::string> files = split_list(fq);
 	if(warm_files < 0 || (size_t)warm_files >= files.size()) {
 		std::fprintf(stderr, "--warmup-files must leave at least one -U file to time\n");

@@ -195,6 +195,10 @@ int main(int argc, char** argv) {
 		else if(a == "--device" && i + 1 < argc) ++i;
 		else if(a == "--stats") {}
 		else if(a == "--warmup-files" && i + 1 < argc) warm_files = std::atoi(argv[++i]);
+		else if(a == "--cpus" && i + 1 < argc) {               // bt2x-align's per-rank CPU set
+			try { apply_cpu_list(argv[++i]); } catch(const std::exception& e) { std::fprintf(stderr, "%s\n", e.what()); return 1; }
+			std::fprintf(stderr, "BT2X_CPUS %s\n", affinity_list().c_str());
+		}
 		else if(a == "--reps" && i + 1 < argc) reps = std::atoi(argv[++i]);
 		else if(a == "--inject-error" && i + 1 < argc) inject = std::atoi(argv[++i]);
 		else if(a == "--shard" && i + 1 < argc) {

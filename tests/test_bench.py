@@ -11,6 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "omp-bowtie2-prime_amd"))
 import bench  # noqa: E402
 
 ORACLE_DRIVER = os.path.join(ROOT, "tests", "cpp", "test_e2e_oracle")
@@ -89,6 +90,65 @@ def test_bench_two_ranks_on_cpu(tmp_path):
     assert len(e["runs"]) == 2 and all(x["value"] > 0 for x in e["runs"])
     assert any(abs(x["t_align_max_s"] - e["t_align_max_s"]) < 1e-3 for x in e["runs"])
     assert e["reaped_at_exit"] == []
+
+
+def test_bench_eight_ranks_on_cpu(tmp_path):
+    """bench.py --gpus 8 as the driver launches it on an 8-GPU node (torch.distributed.run,
+    gloo, one process per rank), the host driver over the CPU oracle as the aligner: the
+    counters sum to all ranks' reads, every rank ran on its own CPUs (the aligners report
+    their affinity; the sets are disjoint and inside this process's), the threads per rank
+    are the CPU share split 8 ways, and the note says when that leaves a rank host-bound."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", BT2X_BENCH_DIR=str(tmp_path / "work"))
+    reads = 600
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--steps", "2", "--warmup", "1", "--reads", str(reads), "--genome-mb", "0.25",
+           "--replay-reads", "200", "--slots", "512", "--no-replay", "--no-cpu",
+           "--cpu-index", "--aligner", ORACLE_DRIVER, "--runs", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8
+    e, cfg = line["end_to_end"], line["config"]
+    assert e["summary"][0] == f"{8 * reads} reads; of these:"
+    assert abs(line["value"] - 8 * reads / e["t_align_max_s"] / 1e6) < 1e-3
+    share = bench.cpu_share()
+    assert cfg["host_threads"] == max(1, share // 8)
+    assert cfg["host_threads_note"].startswith(f"{share}-CPU share / 8 rank(s)")
+    if share // 8 < 14:
+        assert "host-bound" in cfg["host_threads_note"]
+    from bt2x import dist as bdist
+    sets = [set(bdist.parse_cpu_list(c)) for c in cfg["host_cpus"]]
+    assert len(sets) == 8 and all(sets)
+    allowed = os.sched_getaffinity(0)
+    assert all(s <= allowed for s in sets)
+    for i in range(8):
+        for j in range(i + 1, 8):
+            assert not (sets[i] & sets[j]), (i, j, cfg["host_cpus"])
+    assert cfg["host_cpus_note"]
+
+
+def test_rank_cpu_sets_split_each_gpu_node():
+    """The per-rank CPU sets on an 8-GPU, 2-socket node: four ranks per socket, each a
+    disjoint slice of whole cores (SMT siblings together) of its GPU's NUMA node; a GPU
+    with no known node draws from the CPUs left over."""
+    from bt2x import dist as bdist
+    node = {0: list(range(0, 64)) + list(range(128, 192)), 1: list(range(64, 128)) + list(range(192, 256))}
+    core = {c: c % 128 for c in range(256)}
+    sets, note = bdist.rank_cpu_sets(list(range(8)), range(256), [0, 0, 0, 0, 1, 1, 1, 1], node, core)
+    assert [bdist.format_cpu_list(s) for s in sets] == [
+        "0-15,128-143", "16-31,144-159", "32-47,160-175", "48-63,176-191",
+        "64-79,192-207", "80-95,208-223", "96-111,224-239", "112-127,240-255"]
+    assert "node0: 4 rank(s) x 32 CPUs" in note
+    # a cgroup cpuset that leaves part of each node, and one GPU of unknown node
+    allowed = list(range(0, 32)) + list(range(64, 96))
+    sets, note = bdist.rank_cpu_sets([0, 1, 2], allowed, [0, 1, -1], node, core)
+    assert sets[0] == list(range(0, 32)) and sets[1] == list(range(64, 96)) and sets[2] == allowed
+    # (no CPU left over for the unknown-node rank: it shares the allowed set, and says so)
+    assert "no NUMA split" in note
+    assert bdist.parse_cpu_list("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
 
 
 def test_bench_one_rank_with_config_legs_on_cpu(tmp_path):

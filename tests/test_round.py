@@ -195,9 +195,9 @@ def test_round_refuses_a_wrong_gpu_seed_count(tmp_path):
     assert sel is not None, "the rep fixture has reads with N"
     for delta in (1, -1):
         bad = rin.copy()
-        bad["nseeds"][sel] += delta
+        bad["nseeds"][sel] = int(bad["nseeds"][sel]) + delta
         # later reads' seeds move with the count, so the reads' seeds never overlap
-        bad["seed0"][sel + 1:] += delta
+        bad["seed0"][sel + 1:] = (bad["seed0"][sel + 1:].astype(np.int64) + delta).astype(np.uint64)
         with pytest.raises(lib.Bt2xError) as e:
             ctx.seed_round(case.reads, None, bad, noexr, 0)
         assert e.value.code == abi.E_ARG
