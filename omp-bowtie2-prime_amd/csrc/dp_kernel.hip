@@ -1986,6 +1986,388 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 	}
 }
 
+// ------------------------------------------------------------ split fill (two waves per group)
+// At the timed run's cohort launch sizes a launch holds about one 64-problem group per SIMD,
+// and a group's fill is one wave's serial sweep of the band: the launch lasts that wave's
+// dependent chain, whatever the chip's idle VALU.  Here a group has two waves (a 128-thread
+// workgroup); both own all 64 problems (lane l = problem l) and split every column pair's
+// band window [slo, shi] at a block-aligned row b that moves down with the band:
+//  * wave A computes steps [slo, b] and owns rows < b (both columns); its step b is an
+//    extra step whose high half (row b-1 of the odd column) it needs for its own next pair
+//    (the low half, row b, is not its own and is discarded);
+//  * wave B computes steps [b, shi] and owns rows >= b.  Its first step needs the step
+//    before it -- A's packed H, F, E and hl after step b-1 of the same pair (T1) -- so B
+//    runs one pair behind A;
+//  * when b moves down (by 4 rows, every other pair), rows [b, b+4) change owner: A takes
+//    B's H/E state dword of that block after B's pair (T2) before it reaches that block.
+// So each wave sweeps about half the band per pair and the two halves overlap in time; no
+// cell is computed differently from dp_fill_kernel (the same step code, the same band, the
+// same dead zeros), and each traceback dword is stored once, by the owner of its two steps.
+// T1 and T2 go through two-slot LDS rings with workgroup-scope flags (a pair of waves of one
+// CU; the waits are short: A needs T2 only at the end of its pair, B waits for A's pair).
+// After the fill both waves combine their last-row maxima and candidate counts, and each
+// orders candidates and walks half of the group's problems (lanes 32w .. 32w+31).
+constexpr int kSplitW = 2;                                   // waves per group
+__device__ __forceinline__ void flag_wait(const int* f, int target) {
+	while(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void flag_set(int* f, int v, int lane) {
+	// every lane's LDS writes before it are complete (release at workgroup scope); one store
+	if(lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ void __launch_bounds__(64 * kSplitW) __attribute__((amdgpu_waves_per_eu(3)))
+dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
+	__shared__ uint32_t lds[(kCols / 4) * 64];         // row info during the fill, then keys / move logs
+	__shared__ uint32_t pen4[64];
+	__shared__ uint32_t t1buf[2][4][64];               // A -> B: h, f, e, hl after A's step b-1
+	__shared__ uint32_t t2buf[2][2][64];               // B -> A: H, E state dword of block b/4
+	__shared__ int xlr[2][64], xnc[2][64];             // per wave: last-row max, candidate count
+	__shared__ int flags[4];                           // t1_ready, t1_used, t2_ready
+	const uint8_t* pen_lds = reinterpret_cast<const uint8_t*>(pen4);
+	const int lane = threadIdx.x & 63;
+	const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // 0 = A, 1 = B
+	const bool isA = wv == 0;
+	if(isA) pen4[lane] = reinterpret_cast<const uint32_t*>(a.mmpen)[lane];
+	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0, st_comp = 0, st_d0 = 0, st_d1 = 0;
+	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
+	const uint32_t one2 = opaque(0x00010001u);
+	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
+		__syncthreads();                               // the last group's walks are done with lds
+		if(threadIdx.x < 4) flags[threadIdx.x] = 0;
+		uint8_t* gslot = a.scratch + (size_t)blockIdx.x * (kGroupBytes + kWalkSlotBytes);
+		uint32_t* dir = reinterpret_cast<uint32_t*>(gslot + kDirOff);
+		uint8_t* lastrow = gslot + kLastRowOff;
+		const uint32_t pi = grp * 64 + lane;
+		const bool active = grp * 64 + lane < nprob;
+		bt2x_dp_in p;
+		if(active) p = a.in[pi];
+		else { p.read_off = p.qual_off = p.ref_off = 0; p.refl = 0; p.rdlen = 0; p.ncol = 0;
+		       p.minsc = 0; p.nceil = 0; p.triml = p.corel = p.corer = 0; p.fw = 1; p.flags = 0; }
+		const bool refused = active && ((p.flags & BT2X_DP_I16) || (p.flags & kDpBadWindow));
+		const int R = p.rdlen, C = p.ncol;
+		constexpr int top = 0xff;
+		const int Rmax = __builtin_amdgcn_readfirstlane(wave_max(R));
+		const int Cmax = __builtin_amdgcn_readfirstlane(wave_max(C));
+		const uint8_t* rd = a.reads + p.read_off;
+		const uint8_t* qu = a.quals + p.qual_off;
+		const uint8_t* rf = a.refs + p.ref_off;
+		const int thr = (int)p.minsc + top;
+		// ------------- row info, as dp_fill_kernel: the two waves build alternate 16-row blocks
+		const uint32_t kNone = row_info(7, true, npen);
+		const ByteStr rds = byte_str(rd, R > 0 ? R : 1), qus = byte_str(qu, R > 0 ? R : 1);
+		__syncthreads();                               // pen4 (first group) and the flags are set
+#pragma unroll
+		for(int c16 = 0; c16 < kRows / 16; c16++) {
+			if((c16 & 1) != wv) continue;               // wave-uniform
+			if(c16 * 16 < Rmax) {
+				uint32_t rw[4], qw[4];
+#pragma unroll
+				for(int k = 0; k < 4; k++) { rw[k] = bs_bytes4(rds, 4 * c16 + k); qw[k] = bs_bytes4(qus, 4 * c16 + k); }
+#pragma unroll
+				for(int k = 0; k < 4; k++) {
+					uint32_t w = 0;
+#pragma unroll
+					for(int r = 0; r < 4; r++) {
+						const int i = 16 * c16 + 4 * k + r;
+						uint32_t bb = kNone;
+						if(i < R) {
+							int q = (int)((qw[k] >> (8 * r)) & 0xffu) - 33;
+							q = q < 0 ? 0 : q;
+							const bool gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
+							const int rc = (int)((rw[k] >> (8 * r)) & 0xffu);
+							bb = rc > 3 ? row_info(7, gbar, npen) : row_info(rc, gbar, pen_lds[q]);
+						}
+						w |= bb << (8 * r);
+					}
+					lds[(4 * c16 + k) * 64 + lane] = w;
+				}
+			} else {
+#pragma unroll
+				for(int k = 0; k < 4; k++) lds[(4 * c16 + k) * 64 + lane] = kNone * 0x01010101u;
+			}
+		}
+		__syncthreads();
+		// ------------- fill
+		uint32_t Hs[kRowWords], Es[kRowWords];
+#pragma unroll
+		for(int bb = 0; bb < kRowWords; bb++) { Hs[bb] = 0; Es[bb] = 0; }
+		int lrmax = 0, ncand = 0;
+		const int Rmin = __builtin_amdgcn_readfirstlane(-wave_max(-R));
+		const uint32_t rdo2 = (uint32_t)rdo * 0x10001u, rde2 = (uint32_t)rde * 0x10001u;
+		const uint32_t rfo2 = (uint32_t)rfo * 0x10001u, rfe2 = (uint32_t)rfe * 0x10001u;
+		const uint32_t npen2 = (uint32_t)npen * 0x10001u;
+		// the exact band (dp_fill_kernel): pair p's steps [2p - wdhi, 2p + wdlo]
+		int wdhi = 1 << 20, wdlo = 1 << 20;
+		if(a.band) {
+			const int mo = imax(1, rdo < rfo ? rdo : rfo);
+			int me = rde < rfe ? rde : rfe;
+			me = me < mo ? me : mo;
+			const int budget = -(int)p.minsc;
+			int G = (me <= 0) ? (1 << 16) : (budget < mo ? 0 : 1 + (budget - mo) / me);
+			G = G > (1 << 16) ? (1 << 16) : G;
+			constexpr int kBandMargin = 2;
+			const int dh = active ? (C - R) + G + kBandMargin : -(1 << 20);
+			const int dl = active ? G + kBandMargin + 2 : -(1 << 20);
+			wdhi = __builtin_amdgcn_readfirstlane(wave_max(dh));
+			wdlo = __builtin_amdgcn_readfirstlane(wave_max(dl));
+		}
+		// the split row at pair p: the middle of the band (block-aligned), kept inside the
+		// pair's window; both ends and the middle move down by at most 4 per pair
+		const int mid = (int)(((long)wdlo - (long)wdhi) / 2);
+		auto window = [&](int pp, int& slo, int& shi, int& b) {
+			const int j0 = 2 * pp;
+			slo = j0 - wdhi; shi = j0 + wdlo;
+			slo = slo < 0 ? 0 : (slo & ~3);
+			shi = (shi > Rmax ? Rmax : shi) | 3;
+			shi = shi > kSteps - 1 ? kSteps - 1 : shi;
+			const int bhi = (shi + 1) & ~3;
+			int m = j0 + mid;
+			m = m < 0 ? 0 : (m & ~3);
+			b = m < slo ? slo : (m > bhi ? bhi : m);
+		};
+		const int npairs = (Cmax + 1) >> 1;
+		const __amdgpu_buffer_rsrc_t dirsrc =
+			__builtin_amdgcn_make_buffer_rsrc(dir, 0, (int)(kDirBytesLane * 64u), 0x00020000);
+		const uint32_t* rfw = reinterpret_cast<const uint32_t*>(rf);
+		const int lastw = ((C > 0 ? C : 1) - 1) >> 2;
+		uint32_t cw0 = 0, cw1 = 0, cw2 = 0, cw3 = 0;
+		uint32_t refN = 0;
+		int bprev = 0, bexec_prev = 0;                    // the last pair's split; whether B ran it
+		for(int pp = 0; pp < npairs; pp++) {
+			const int j0 = 2 * pp;
+			int slo, shi, b;
+			window(pp, slo, shi, b);
+			const bool execA = b > slo, execB = b <= shi;
+			// this wave's steps: A [slo, b] (b: the extra step, not stored), B [b, shi]
+			int lo = isA ? slo : b, hi = isA ? (b <= shi ? b : shi) : shi;
+			const bool exec = isA ? execA : execB;
+			// T2: A takes rows [bprev, bprev + 4) from B when the split moved down past them
+			const int t2blk = (isA && exec && pp > 0 && b > bprev && bexec_prev) ? (bprev >> 2) : -1;
+			// B publishes its state dword of block b/4 for A's next pair, after the step that
+			// completes it (b + 4) or after its last step when that comes first
+			int nslo, nshi, nb;
+			window(pp + 1, nslo, nshi, nb);
+			const bool pub = !isA && execB && pp + 1 < npairs && nb > b;
+			const int pubblk = pub ? ((shi >= b + 4) ? (b >> 2) + 1 : (b >> 2)) : -1;
+			const int pubsrc = b >> 2;
+			if(active && exec) st_comp += 2u * (unsigned)(isA ? (b - slo) : (shi - b + 1));
+			int rmin = Rmin, rl = R;
+			asm volatile("" : "+s"(rmin), "+s"(lo), "+s"(hi), "+v"(rl));
+			asm volatile("" ::: "memory");
+			if((pp & 7) == 0) {
+				const int w0 = pp >> 1;
+				cw0 = rfw[min(w0, lastw)]; cw1 = rfw[min(w0 + 1, lastw)];
+				cw2 = rfw[min(w0 + 2, lastw)]; cw3 = rfw[min(w0 + 3, lastw)];
+				asm volatile("" : "+v"(cw0), "+v"(cw1), "+v"(cw2), "+v"(cw3));
+			}
+			const uint32_t wsel = (pp & 4) ? ((pp & 2) ? cw3 : cw2) : ((pp & 2) ? cw1 : cw0);
+			const uint32_t wsh = (uint32_t)(pp & 1) * 16u;
+			const int ca = (j0 < C) ? (int)((wsel >> wsh) & 0xffu) : 4;
+			const int cb = (j0 + 1 < C) ? (int)((wsel >> (wsh + 8u)) & 0xffu) : 4;
+			const uint32_t refc2 = (uint32_t)ca | ((uint32_t)cb << 16);
+			const uint32_t coln = (ca > 3 ? 0x0000ffffu : 0u) | (cb > 3 ? 0xffff0000u : 0u);
+			refN |= ((ca > 3) & (j0 < C)) | ((cb > 3) & (j0 + 1 < C));
+			const uint32_t pbase = (uint32_t)pp * kPairWords * 256u;
+			uint32_t hp = 0, fp = 0, ep = 0, hlp = 0;
+			if(!isA) {                                  // T1: A's outputs after step b-1
+				flag_wait(&flags[0], pp + 1);
+				if(execA) {
+					hp = t1buf[pp & 1][0][lane]; fp = t1buf[pp & 1][1][lane];
+					ep = t1buf[pp & 1][2][lane]; hlp = t1buf[pp & 1][3][lane];
+				}
+				flag_set(&flags[1], pp + 1, lane);
+			}
+			uint32_t t1h = 0, t1f = 0, t1e = 0, t1hl = 0;
+			uint32_t tbacc = 0;
+			int lra = 0, lrb = 0;
+			if(exec) {
+			uint32_t cur_iw, cur_iv;
+			{
+				const int b0 = lo >> 2;
+				cur_iw = lds[(b0 < kRowWords ? b0 : kRowWords - 1) * 64 + lane];
+				cur_iv = lds[(b0 > 0 ? b0 - 1 : 0) * 64 + lane];
+			}
+#pragma unroll
+			for(int b4 = 0; b4 < kSteps; b4 += 4) {
+			if(b4 >= (lo & ~3) && b4 <= hi) {                            // wave-uniform
+			const int nbk = (b4 >> 2) + 1;
+			const uint32_t nxt_iw = lds[(nbk < kRowWords ? nbk : kRowWords - 1) * 64 + lane];
+			if(__builtin_expect((b4 >> 2) == t2blk, 0)) {                // A: rows [bprev, bprev+4) from B
+				flag_wait(&flags[2], pp);
+				Hs[b4 >> 2 < kRowWords ? b4 >> 2 : kRowWords - 1] = t2buf[(pp - 1) & 1][0][lane];
+				Es[b4 >> 2 < kRowWords ? b4 >> 2 : kRowWords - 1] = t2buf[(pp - 1) & 1][1][lane];
+			}
+			const bool lastA = isA && execB && b4 == b;                 // A's extra step only
+#pragma unroll
+			for(int st = b4; st < b4 + 4 && st < kSteps; st++) {
+				if(st == b4 || !lastA) {
+				const int blk = st >> 2, r = st & 3;
+				const uint32_t iw = cur_iw, iv = cur_iv;
+				const uint32_t info = (st == 0) ? perm(0, iw, 0x0c0c0c00u)
+				                    : (st == kRows) ? (perm(iw, 0, 0x0c070c0cu) | (kNone & 0xffu))
+				                    : (r == 0) ? perm(iv, iw, 0x0c070c00u)
+				                               : perm(0, iw, 0x0c000c00u | ((uint32_t)(r - 1) << 16) | (uint32_t)r);
+				const uint32_t hsw = st < kRows ? Hs[blk] : 0u, esw = st < kRows ? Es[blk] : 0u;
+				const uint32_t hl = (st == 0) ? perm(0, hsw, 0x0c0c0c00u) | 0x00ff0000u
+				                              : perm(hp, hsw, 0x0c040c00u | (uint32_t)r);
+				const uint32_t el = (st == 0) ? perm(0, esw, 0x0c0c0c00u)
+				                              : perm(ep, esw, 0x0c040c00u | (uint32_t)r);
+				const uint32_t hdiag = (st == 0) ? 0x000000ffu : hlp;
+				const uint32_t xrc = (info ^ refc2) & 0x00070007u;
+				uint32_t pen = pmin(pshr(info, 4), xrc << 8);
+				pen = (pen & ~coln) | (npen2 & coln);
+				const uint32_t gbm = info & 0x00080008u;
+				const uint32_t d = psubs(hdiag, pen);
+				const uint32_t r0 = (st == 0) ? 0x00000100u : (st == 1) ? 0x01000000u : 0u;
+				const uint32_t rdoe = (gbm << 5) + rdo2, rfoe = (gbm << 5) + (rfo2 + r0), rfee = (gbm << 5) + (rfe2 + r0);
+				const uint32_t hl_o = psubs(hl, rdoe), el_e = psubs(el, rde2);
+				const uint32_t hu_o = psubs(hp, rfoe), fu_e = psubs(fp, rfee);
+				const uint32_t e = pmax(hl_o, el_e);
+				const uint32_t f = pmax(hu_o, fu_e);
+				const uint32_t h = pmax(pmax(d, e), f);
+				uint32_t tb = pmin(xrc, one2);                        // TB_MM
+				tb = (tb << 1) | pne(hl_o, e, one2);                   // TB_EONE
+				tb = (tb << 1) | pne(hu_o, f, one2);                   // TB_FONE
+				tb = (tb << 1) | pne(f, h, one2);                      // TB_FNE
+				tb = (tb << 1) | pne(d, h, one2);                      // TB_DNE
+				if(__builtin_expect(st + 1 >= rmin, 0)) {
+					lra = (st == rl - 1) ? (int)(h & 0xffu) : lra;
+					lrb = (st == rl) ? (int)((h >> 16) & 0xffu) : lrb;
+				}
+				if(st >= 1) {
+					const int pb = (st - 1) >> 2, pr = (st - 1) & 3;
+					const uint32_t selh = (0x03020100u & ~(0xffu << (8 * pr))) | (6u << (8 * pr));
+					Hs[pb] = perm(h, Hs[pb], selh);
+					Es[pb] = perm(e, Es[pb], selh);
+				}
+				// stores: the owner's steps only (A's extra step b is B's first)
+				if(!lastA) {
+					if(st & 1) {
+						__builtin_amdgcn_raw_buffer_store_b32(perm(tb, tbacc, 0x06040200u), dirsrc, lane * 4,
+						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
+					} else {
+						tbacc = tb;
+						if(__builtin_expect(st == shi, 0))
+							__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, lane * 4,
+							                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
+					}
+				}
+				hlp = hl; hp = h; fp = f; ep = e;
+				}
+			}
+			cur_iv = cur_iw; cur_iw = nxt_iw;
+			// A: T1 is its outputs after step b-1, the last step of the block before b
+			if(isA && b4 + 4 == b) { t1h = hp; t1f = fp; t1e = ep; t1hl = hlp; }
+			// B: its state dword of block b/4 for A's next pair
+			if(__builtin_expect((b4 >> 2) == pubblk, 0)) {
+				const int sb = pubsrc < kRowWords ? pubsrc : kRowWords - 1;
+				// (compile-time index: pubsrc is b4/4 or b4/4 - 1)
+				const uint32_t xh = ((b4 >> 2) == pubsrc) ? Hs[b4 >> 2 < kRowWords ? b4 >> 2 : kRowWords - 1]
+				                                            : Hs[(b4 >> 2) >= 1 ? (b4 >> 2) - 1 : 0];
+				const uint32_t xe = ((b4 >> 2) == pubsrc) ? Es[b4 >> 2 < kRowWords ? b4 >> 2 : kRowWords - 1]
+				                                            : Es[(b4 >> 2) >= 1 ? (b4 >> 2) - 1 : 0];
+				(void)sb;
+				t2buf[pp & 1][0][lane] = xh;
+				t2buf[pp & 1][1][lane] = xe;
+				flag_set(&flags[2], pp + 1, lane);
+			}
+			}
+			}
+			}
+			if(isA) {                                   // T1 for B (zeros: A computed nothing)
+				if(pp >= 2) flag_wait(&flags[1], pp - 1);
+				t1buf[pp & 1][0][lane] = t1h; t1buf[pp & 1][1][lane] = t1f;
+				t1buf[pp & 1][2][lane] = t1e; t1buf[pp & 1][3][lane] = t1hl;
+				flag_set(&flags[0], pp + 1, lane);
+			}
+			// last rows: the owner of row R-1 at this pair supplies both of its columns
+			const bool own = isA ? (R - 1 < b) : (R - 1 >= b);
+			if(own && active) {
+				if(j0 < C) {
+					lastrow[(size_t)j0 * 64 + lane] = (uint8_t)lra;
+					lrmax = imax(lrmax, lra);
+					ncand += (lra >= thr);
+				}
+				if(j0 + 1 < C) {
+					lastrow[(size_t)(j0 + 1) * 64 + lane] = (uint8_t)lrb;
+					lrmax = imax(lrmax, lrb);
+					ncand += (lrb >= thr);
+				}
+			}
+			bprev = b; bexec_prev = execB ? 1 : 0;
+		}
+		xlr[wv][lane] = lrmax;
+		xnc[wv][lane] = ncand;
+		__threadfence_block();
+		__syncthreads();
+		// ------------- verdict, candidate order and walk: wave w takes lanes 32w .. 32w+31
+		const bool mine = (lane >> 5) == wv;
+		lrmax = imax(xlr[0][lane], xlr[1][lane]);
+		ncand = xnc[0][lane] + xnc[1][lane];
+		if(active && mine) {
+			st_cells += (unsigned long long)R * C;
+			st_cols += C;
+			bt2x_dp_out o;
+			o.nrec = 0; o.rec_off = 0;
+			int status = 0, best = 0;
+			dp_verdict(false, lrmax, p.minsc, ncand, status, best);
+			if(refused) { status = -1; best = 0; atomicAdd(&a.counters[3], 1u); }
+			o.status = status; o.best = best; o.ncand = status > 0 ? (uint16_t)ncand : (uint16_t)0;
+			a.out[pi] = o;
+			if(status == 0 && a.fail_list && a.band) a.fail_list[atomicAdd(&a.counters[2], 1u)] = pi;
+			if(status > 0) {
+				// candidate order (DpBtCandidate: score desc, col desc), as dp_fill_kernel's u8 path
+				const int nw = (Cmax + 3) >> 2;
+				for(int q = 0; q < nw; q++) {
+					uint32_t w4 = 0;
+					for(int r = 0; r < 4; r++) {
+						const int j = q * 4 + r;
+						if(j < C) w4 |= (uint32_t)lastrow[(size_t)j * 64 + lane] << (8 * r);
+					}
+					lds[q * 64 + lane] = w4;
+				}
+				uint8_t* cands = gslot + kCandOff;
+				int cur_key = 0xffff;
+				for(int k = 0; k < ncand; k++) {
+					const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
+					uint32_t best2 = 0;
+#pragma unroll 2
+					for(int q = 0; q < nw; q++) {
+						const uint32_t w4 = lds[q * 64 + lane];
+						const uint32_t cq = (uint32_t)q * 0x40004u + 0x10000u;
+						const uint32_t ka = perm(cq, w4, 0x01060004u);
+						const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);
+						best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
+						best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
+					}
+					const int bk = (int)max(best2 & 0xffffu, best2 >> 16);
+					cur_key = bk;
+					cands[(size_t)k * 64 + lane] = (uint8_t)(bk & 0xff);
+				}
+				uint8_t* wslot = gslot + kGroupBytes;
+				walk_problem<64, kPairWords>(sc, pen_lds, a, pi, lane, lane, gslot + kDirOff, kDirBytesLane * 64u, cands,
+				                             reinterpret_cast<uint32_t*>(wslot + kEditOff), reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff),
+				                             st_bt, refN != 0, lds, false, st_d0, st_d1);
+			}
+		}
+	}
+	if(a.stats) {
+		for(int d = 32; d > 0; d >>= 1) {
+			st_cells += __shfl_xor(st_cells, d);
+			st_cols += __shfl_xor(st_cols, d);
+			st_bt += __shfl_xor(st_bt, d);
+			st_comp += __shfl_xor(st_comp, d);
+		}
+		if(lane == 0) {
+			atomicAdd(&a.stats[0], st_cells);
+			atomicAdd(&a.stats[1], st_cols);
+			atomicAdd(&a.stats[2], st_bt);
+			atomicAdd(&a.stats[3], st_comp);
+		}
+	}
+}
+
 // ------------------------------------------------------------------ walk kernel
 // SwAligner::nextAlignment until done(): per problem, its candidates in order, each
 // not already reportedThrough backtraced over the fill's traceback bytes.  Low VGPR use
@@ -2018,9 +2400,9 @@ dp_walk_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 
 } // namespace
 
-static int blocks_per_cu(const void* fn) {
+static int blocks_per_cu(const void* fn, int threads = 64) {
 	int nb = 0;
-	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64, 0) != hipSuccess || nb < 1) nb = 2;
+	if(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, 0) != hipSuccess || nb < 1) nb = 2;
 	return nb;
 }
 
@@ -2030,7 +2412,7 @@ namespace {
 struct DpOccupancy {
 	int fused[2][2];                // [debug][wide]
 	int fill[2][2];                 // split-mode fill kernels
-	int walk, wave, duo;
+	int walk, wave, duo, split;
 	DpOccupancy() {
 		fused[0][0] = blocks_per_cu((const void*)dp_fill_kernel<false, true, false>);
 		fused[1][0] = blocks_per_cu((const void*)dp_fill_kernel<true, true, false>);
@@ -2043,6 +2425,7 @@ struct DpOccupancy {
 		walk = blocks_per_cu((const void*)dp_walk_kernel);
 		wave = blocks_per_cu((const void*)dp_wave_kernel<1>);
 		duo = blocks_per_cu((const void*)dp_duo_kernel);
+		split = blocks_per_cu((const void*)dp_split_kernel, 64 * kSplitW);
 	}
 };
 const DpOccupancy& occupancy() { static const DpOccupancy o; return o; }
@@ -2079,6 +2462,19 @@ bool dp_duo(uint32_t n) {
 	return n <= (x ? (uint32_t)atoll(x) : 65536u);
 }
 
+// The two-wave split fill (dp_split_kernel) for banded u8 launches of at most
+// BT2X_DP_SPLIT_MAX problems (default 131072: up to about two 64-problem groups per SIMD,
+// where one wave's serial sweep of a group is the launch's latency; above it the lane
+// kernel's waves fill the SIMDs).  BT2X_DP_SPLIT=0: never, =1: always.  It takes
+// precedence over the duo fill.  Read per launch (tests switch it).
+bool dp_split(uint32_t n) {
+	const char* e = getenv("BT2X_DP_SPLIT");
+	if(e && e[0] == '0') return false;
+	if(e && e[0] == '1') return true;
+	const char* x = getenv("BT2X_DP_SPLIT_MAX");
+	return n <= (x ? (uint32_t)atoll(x) : 131072u);
+}
+
 uint32_t dp_wave_max() {                        // read per launch (tests switch modes)
 	const char* w = getenv("BT2X_DP_WAVE");
 	const char* x = getenv("BT2X_DP_WAVE_MAX");
@@ -2101,7 +2497,7 @@ size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups) {
 	if(!dp_split_mode()) {
 		int nb = 0;
 		for(int d = 0; d < 2; d++) for(int w = 0; w < 2; w++) nb = max(nb, o.fused[d][w]);
-		nb = max(nb, o.duo);
+		nb = max(nb, max(o.duo, o.split));
 		return (size_t)ncu * nb * (kGroupBytes + kWalkSlotBytes);
 	}
 	return (size_t)chunk_groups * kGroupBytes + (size_t)ncu * o.walk * kWalkSlotBytes;
@@ -2126,7 +2522,11 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		else hipLaunchKernelGGL((dp_wave_kernel<0, false>), dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}
-	if(!dbg && !wide && a0.band && !dp_split_mode() && dp_duo(a0.n)) {
+	if(!dbg && !wide && a0.band && !dp_split_mode() && dp_split(a0.n)) {
+		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.split;
+		if(fb > groups_all) fb = groups_all;
+		hipLaunchKernelGGL(dp_split_kernel, dim3(fb), dim3(64 * kSplitW), 0, s, sc, a, a0.n);
+	} else if(!dbg && !wide && a0.band && !dp_split_mode() && dp_duo(a0.n)) {
 		const uint32_t groups = (a0.n + kDuoG - 1) / kDuoG;
 		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.duo;
 		if(fb > groups) fb = groups;
