@@ -34,6 +34,25 @@
 
 namespace {
 
+// Development ablations of the u8 lane fills (variant libraries only, BT2X_LIB; outputs
+// invalid): -DBT2X_PROF_NOSTORE drops the traceback stores, -DBT2X_PROF_NOWINDOW the
+// reference-window loads.
+#ifdef BT2X_PROF_NOSTORE
+constexpr bool kProfStores = false;
+#else
+constexpr bool kProfStores = true;
+#endif
+// cache-policy bits of the fill's traceback stores (buffer instruction aux: sc0 1, nt 2, sc1 16)
+#ifndef BT2X_TB_STORE_AUX
+#define BT2X_TB_STORE_AUX 0
+#endif
+constexpr int kTbStoreAux = BT2X_TB_STORE_AUX;
+#ifdef BT2X_PROF_NOWINDOW
+constexpr bool kProfWindow = false;
+#else
+constexpr bool kProfWindow = true;
+#endif
+
 constexpr int kRows = BT2X_MAX_ROWS;          // 160
 constexpr int kRowWords = kRows / 4;          // state dwords (4 rows each)
 constexpr int kCols = BT2X_MAX_COLS;          // 200
@@ -1286,7 +1305,7 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			// row-info loads stay inside the pair (hoisted out of it they would hold all 40
 			// words in VGPRs)
 			asm volatile("" ::: "memory");
-			if((pp & 7) == 0) {                           // wave-uniform: the next 16 columns
+			if(kProfWindow && (pp & 7) == 0) {            // wave-uniform: the next 16 columns
 				const int w0 = pp >> 1;
 				cw0 = rfw[min(w0, lastw)]; cw1 = rfw[min(w0 + 1, lastw)];
 				cw2 = rfw[min(w0 + 2, lastw)]; cw3 = rfw[min(w0 + 3, lastw)];
@@ -1423,14 +1442,14 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 					}
 				}
 				// two steps' flags of both columns per traceback dword
-				if(st & 1) {
+				if(kProfStores && (st & 1)) {
 					__builtin_amdgcn_raw_buffer_store_b32(perm(tb, tbacc, 0x06040200u), dirsrc, lane * 4,
-					                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
+					                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), kTbStoreAux);
 				} else {
 					tbacc = tb;
 					if(__builtin_expect(st == shi, 0))
 						__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, lane * 4,
-						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
+						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), kTbStoreAux);
 				}
 				hlp = hl; hp = h; fp = f; ep = e;
 				}
@@ -1989,8 +2008,8 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 // ------------------------------------------------------------ split fill (two waves per group)
 // At the timed run's cohort launch sizes a launch holds about one 64-problem group per SIMD,
 // and a group's fill is one wave's serial sweep of the band: the launch lasts that wave's
-// dependent chain, whatever the chip's idle VALU.  Here a group has two waves (a 128-thread
-// workgroup); both own all 64 problems (lane l = problem l) and split every column pair's
+// dependent chain, whatever the chip's idle VALU.  Here a group has two waves (two of a
+// 256-thread workgroup's four, see kSplitG); both own all 64 problems (lane l = problem l) and split every column pair's
 // band window [slo, shi] at a block-aligned row b that moves down with the band:
 //  * wave A computes steps [slo, b] and owns rows < b (both columns); its step b is an
 //    extra step whose high half (row b-1 of the odd column) it needs for its own next pair
@@ -2004,10 +2023,16 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 // cell is computed differently from dp_fill_kernel (the same step code, the same band, the
 // same dead zeros), and each traceback dword is stored once, by the owner of its two steps.
 // T1 and T2 go through two-slot LDS rings with workgroup-scope flags (a pair of waves of one
-// CU; the waits are short: A needs T2 only at the end of its pair, B waits for A's pair).
+// CU, on two SIMDs; the waits are short: A needs T2 only at the end of its pair, B waits
+// for A's pair).
 // After the fill both waves combine their last-row maxima and candidate counts, and each
 // orders candidates and walks half of the group's problems (lanes 32w .. 32w+31).
 constexpr int kSplitW = 2;                                   // waves per group
+// Groups per workgroup.  A workgroup's waves are spread over the CU's SIMDs only when it
+// has four of them (measured, tools/micro/valu_chain.hip: two 2-wave workgroups' waves
+// pair up on one SIMD), so a workgroup holds two groups: waves 0 and 1 split one, 2 and 3
+// the other, and each pair synchronises through its own LDS counters, not s_barrier.
+constexpr int kSplitG = 2;
 __device__ __forceinline__ void flag_wait(const int* f, int target) {
 	while(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
 }
@@ -2016,26 +2041,43 @@ __device__ __forceinline__ void flag_set(int* f, int v, int lane) {
 	if(lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__global__ void __launch_bounds__(64 * kSplitW) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ void __launch_bounds__(64 * kSplitW * kSplitG) __attribute__((amdgpu_waves_per_eu(3)))
 dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
-	__shared__ uint32_t lds[(kCols / 4) * 64];         // row info during the fill, then keys / move logs
+	__shared__ uint32_t lds_g[kSplitG][(kCols / 4) * 64];   // row info during the fill, then keys / move logs
 	__shared__ uint32_t pen4[64];
-	__shared__ uint32_t t1buf[2][4][64];               // A -> B: h, f, e, hl after A's step b-1
-	__shared__ uint32_t t2buf[2][2][64];               // B -> A: H, E state dword of block b/4
-	__shared__ int xlr[2][64], xnc[2][64];             // per wave: last-row max, candidate count
-	__shared__ int flags[4];                           // t1_ready, t1_used, t2_ready
+	__shared__ uint32_t t1_g[kSplitG][2][4][64];             // A -> B: h, f, e, hl after A's step b-1
+	__shared__ uint32_t t2_g[kSplitG][2][2][64];             // B -> A: H, E state dword of block b/4
+	__shared__ int xlr_g[kSplitG][2][64], xnc_g[kSplitG][2][64];   // per wave: last-row max, candidate count
+	__shared__ int flags_g[kSplitG][8];                      // t1_ready, t1_used, t2_ready; [4] the pair barrier
 	const uint8_t* pen_lds = reinterpret_cast<const uint8_t*>(pen4);
 	const int lane = threadIdx.x & 63;
-	const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // 0 = A, 1 = B
+	const int wv = __builtin_amdgcn_readfirstlane((int)((threadIdx.x >> 6) & 1));   // 0 = A, 1 = B
+	const int sg = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 7));          // the workgroup's group
 	const bool isA = wv == 0;
-	if(isA) pen4[lane] = reinterpret_cast<const uint32_t*>(a.mmpen)[lane];
+	uint32_t* lds = lds_g[sg];
+	uint32_t (&t1buf)[2][4][64] = t1_g[sg];
+	uint32_t (&t2buf)[2][2][64] = t2_g[sg];
+	int (&xlr)[2][64] = xlr_g[sg];
+	int (&xnc)[2][64] = xnc_g[sg];
+	int* flags = flags_g[sg];
+	if(threadIdx.x < 64) pen4[lane] = reinterpret_cast<const uint32_t*>(a.mmpen)[lane];
+	if(threadIdx.x < kSplitG * 8) flags_g[threadIdx.x >> 3][threadIdx.x & 7] = 0;
+	__syncthreads();                                   // (the only workgroup barrier)
+	// the two waves of a group meet here (an LDS counter; the other group's waves run on)
+	int bphase = 0;
+	auto pair_bar = [&]() {
+		bphase += 2;
+		__threadfence_block();
+		if(lane == 0) __hip_atomic_fetch_add(&flags[4], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+		flag_wait(&flags[4], bphase);
+	};
 	unsigned long long st_cells = 0, st_cols = 0, st_bt = 0, st_comp = 0, st_d0 = 0, st_d1 = 0;
 	const int rdo = sc.rdo, rde = sc.rde, rfo = sc.rfo, rfe = sc.rfe, npen = sc.npen;
 	const uint32_t one2 = opaque(0x00010001u);
-	for(uint32_t grp = blockIdx.x; (uint64_t)grp * 64 < nprob; grp += gridDim.x) {
-		__syncthreads();                               // the last group's walks are done with lds
-		if(threadIdx.x < 4) flags[threadIdx.x] = 0;
-		uint8_t* gslot = a.scratch + (size_t)blockIdx.x * (kGroupBytes + kWalkSlotBytes);
+	for(uint32_t grp = blockIdx.x * kSplitG + (uint32_t)sg; (uint64_t)grp * 64 < nprob; grp += gridDim.x * kSplitG) {
+		pair_bar();                                    // the last group's walks are done with lds
+		if(isA && lane < 4) flags[lane] = 0;
+		uint8_t* gslot = a.scratch + ((size_t)blockIdx.x * kSplitG + (size_t)sg) * (kGroupBytes + kWalkSlotBytes);
 		uint32_t* dir = reinterpret_cast<uint32_t*>(gslot + kDirOff);
 		uint8_t* lastrow = gslot + kLastRowOff;
 		const uint32_t pi = grp * 64 + lane;
@@ -2056,7 +2098,7 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 		// ------------- row info, as dp_fill_kernel: the two waves build alternate 16-row blocks
 		const uint32_t kNone = row_info(7, true, npen);
 		const ByteStr rds = byte_str(rd, R > 0 ? R : 1), qus = byte_str(qu, R > 0 ? R : 1);
-		__syncthreads();                               // pen4 (first group) and the flags are set
+		pair_bar();                                    // the flags are reset
 #pragma unroll
 		for(int c16 = 0; c16 < kRows / 16; c16++) {
 			if((c16 & 1) != wv) continue;               // wave-uniform
@@ -2087,7 +2129,7 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 				for(int k = 0; k < 4; k++) lds[(4 * c16 + k) * 64 + lane] = kNone * 0x01010101u;
 			}
 		}
-		__syncthreads();
+		pair_bar();
 		// ------------- fill
 		uint32_t Hs[kRowWords], Es[kRowWords];
 #pragma unroll
@@ -2155,7 +2197,7 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 			int rmin = Rmin, rl = R;
 			asm volatile("" : "+s"(rmin), "+s"(lo), "+s"(hi), "+v"(rl));
 			asm volatile("" ::: "memory");
-			if((pp & 7) == 0) {
+			if(kProfWindow && (pp & 7) == 0) {
 				const int w0 = pp >> 1;
 				cw0 = rfw[min(w0, lastw)]; cw1 = rfw[min(w0 + 1, lastw)];
 				cw2 = rfw[min(w0 + 2, lastw)]; cw3 = rfw[min(w0 + 3, lastw)];
@@ -2243,14 +2285,14 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 				}
 				// stores: the owner's steps only (A's extra step b is B's first)
 				if(!lastA) {
-					if(st & 1) {
+					if(kProfStores && (st & 1)) {
 						__builtin_amdgcn_raw_buffer_store_b32(perm(tb, tbacc, 0x06040200u), dirsrc, lane * 4,
-						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
+						                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), kTbStoreAux);
 					} else {
 						tbacc = tb;
 						if(__builtin_expect(st == shi, 0))
 							__builtin_amdgcn_raw_buffer_store_b32(perm(0, tbacc, 0x0c0c0200u), dirsrc, lane * 4,
-							                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), 0);
+							                                      (int)(pbase + (uint32_t)(st >> 1) * 256u), kTbStoreAux);
 					}
 				}
 				hlp = hl; hp = h; fp = f; ep = e;
@@ -2299,8 +2341,7 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 		}
 		xlr[wv][lane] = lrmax;
 		xnc[wv][lane] = ncand;
-		__threadfence_block();
-		__syncthreads();
+		pair_bar();
 		// ------------- verdict, candidate order and walk: wave w takes lanes 32w .. 32w+31
 		const bool mine = (lane >> 5) == wv;
 		lrmax = imax(xlr[0][lane], xlr[1][lane]);
@@ -2425,7 +2466,7 @@ struct DpOccupancy {
 		walk = blocks_per_cu((const void*)dp_walk_kernel);
 		wave = blocks_per_cu((const void*)dp_wave_kernel<1>);
 		duo = blocks_per_cu((const void*)dp_duo_kernel);
-		split = blocks_per_cu((const void*)dp_split_kernel, 64 * kSplitW);
+		split = blocks_per_cu((const void*)dp_split_kernel, 64 * kSplitW * kSplitG);
 	}
 };
 const DpOccupancy& occupancy() { static const DpOccupancy o; return o; }
@@ -2497,7 +2538,7 @@ size_t bt2x_dp_scratch_bytes(int ncu, uint32_t chunk_groups) {
 	if(!dp_split_mode()) {
 		int nb = 0;
 		for(int d = 0; d < 2; d++) for(int w = 0; w < 2; w++) nb = max(nb, o.fused[d][w]);
-		nb = max(nb, max(o.duo, o.split));
+		nb = max(nb, max(o.duo, o.split * kSplitG));
 		return (size_t)ncu * nb * (kGroupBytes + kWalkSlotBytes);
 	}
 	return (size_t)chunk_groups * kGroupBytes + (size_t)ncu * o.walk * kWalkSlotBytes;
@@ -2524,8 +2565,8 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 	}
 	if(!dbg && !wide && a0.band && !dp_split_mode() && dp_split(a0.n)) {
 		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.split;
-		if(fb > groups_all) fb = groups_all;
-		hipLaunchKernelGGL(dp_split_kernel, dim3(fb), dim3(64 * kSplitW), 0, s, sc, a, a0.n);
+		if(fb > (groups_all + kSplitG - 1) / kSplitG) fb = (groups_all + kSplitG - 1) / kSplitG;
+		hipLaunchKernelGGL(dp_split_kernel, dim3(fb), dim3(64 * kSplitW * kSplitG), 0, s, sc, a, a0.n);
 	} else if(!dbg && !wide && a0.band && !dp_split_mode() && dp_duo(a0.n)) {
 		const uint32_t groups = (a0.n + kDuoG - 1) / kDuoG;
 		uint32_t fb = (uint32_t)a0.ncu * (uint32_t)occ.duo;

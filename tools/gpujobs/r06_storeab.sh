@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 6: cache-policy bits of the fill's traceback stores (development builds, BT2X_LIB):
+# fill only and whole DP at the timed run's cohort shapes, one-lane fill
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+T=${T:-r06f}
+out=gpurun_out/${T}_storeab.log
+: > $out
+for v in main aux1 aux2 aux3 aux17; do
+	lib=omp-bowtie2-prime_amd/bt2x/variants/libbt2x_$v.so
+	[ $v = main ] && lib=omp-bowtie2-prime_amd/bt2x/libbt2x.so
+	echo "== variant $v" >> $out
+	BT2X_LIB=$PWD/$lib timeout -k 10 400 python -u tools/dp_replay.py --slots 65536 --steps 3 \
+		BT2X_DP_SPLIT=0,BT2X_DP_DUO=0,BT2X_DP_ABLATE=1 BT2X_DP_SPLIT=0,BT2X_DP_DUO=0 >> $out 2>&1
+	rc=$?; echo "variant $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+grep -E "^== |^config" $out
