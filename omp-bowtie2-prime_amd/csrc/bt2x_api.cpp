@@ -627,7 +627,7 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 	// its window as aligned dwords, 16 columns per load
 	if((launch_flags & BT2X_DPL_REF_TEXT) && (!c->ix.text || !c->ix.rstarts)) return BT2X_E_ARG;
 	if((rc = c->b_in2.ensure(sizeof(bt2x_dp_in) * (size_t)(n ? n : 1))) ||
-	   (rc = c->b_win.ensure((size_t)BT2X_MAX_COLS * (n ? n : 1))))
+	   (rc = c->b_win.ensure((size_t)kWinSlot * (n ? n : 1) + 64)))
 		return rc;
 	if((rc = bt2x_launch_windows(c->ix, d_in, n, d_refs, (bt2x_dp_in*)c->b_in2.p, (uint8_t*)c->b_win.p, s))) return rc;
 	a.in = (const bt2x_dp_in*)c->b_in2.p;

@@ -37,6 +37,9 @@ struct DevIndex {
 // could not cut the problem's BT2X_DP_REF_TEXT window (no resident text, or a text id out
 // of range), so the DP kernels refuse it (status -1, counters[3]) instead of reading it.
 constexpr uint8_t kDpBadWindow = 0x80u;
+// DP windows (window_kernel): one slot per problem, BT2X_MAX_COLS bytes rounded up to 16
+// so the fill's 16-byte LDS-DMA chunks are aligned; the buffer has a 64-byte tail.
+constexpr uint32_t kWinSlot = (BT2X_MAX_COLS + 15) & ~15u;
 
 struct DevScoring {
 	int32_t rdo, rde, rfo, rfe;   // read/ref gap open (const+linear) and extend (linear)

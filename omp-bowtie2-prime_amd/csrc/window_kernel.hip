@@ -10,7 +10,7 @@
 // never touches the 0.8 GB packed text and the windows never cross PCIe.
 //
 // One wave per problem, one output byte per lane and step; every problem's window goes to
-// its slot of BT2X_MAX_COLS bytes in `win`, and its dp_in to `out` with ref_off = the
+// its slot of kWinSlot bytes in `win`, and its dp_in to `out` with ref_off = the
 // slot (unflagged problems are copied from `refs`), so the DP kernels run unchanged.
 // HBM-bound: per problem ~ncol/4 bytes of packed text read, ncol bytes written.
 #include <hip/hip_runtime.h>
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) window_kernel(DevIndex ix, const bt2x_dp_
 	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
 	if(i >= n) return;
 	bt2x_dp_in p = in[i];
-	uint8_t* w = win + (size_t)i * BT2X_MAX_COLS;
+	uint8_t* w = win + (size_t)i * kWinSlot;
 	const uint32_t ncol = p.ncol;
 	const bool named = (p.flags & BT2X_DP_REF_TEXT) != 0;
 	if(named && (!ix.text || !ix.rstarts || p.ref_off >= ix.npat)) {
@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(256) window_kernel(DevIndex ix, const bt2x_dp_
 		for(uint32_t c = lane; c < ncol; c += 64u) w[c] = refs[p.ref_off + c];
 	}
 	if(lane == 0) {
-		p.ref_off = (uint64_t)i * BT2X_MAX_COLS;
+		p.ref_off = (uint64_t)i * kWinSlot;
 		p.flags &= (uint8_t)~BT2X_DP_REF_TEXT;
 		out[i] = p;
 	}

@@ -52,7 +52,7 @@ SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
 # (lane-per-problem banded kernel above BT2X_DP_WAVE_MAX problems, wave per problem
 # below), and each kernel forced for every launch
 DP_MODES = {"default": None, "lane": "0", "wave": "1", "hostwin": "host", "handover": "handover", "parwave": "parwave",
-            "stream2": "stream2", "lane1": "lane1", "duo": "duo", "nostore": "nostore"}
+            "stream2": "stream2", "lane1": "lane1", "split": "split", "nostore": "nostore"}
 MD5 = os.path.join(g.GOLDEN, "e2e_md5.json")
 SUMMARY = os.path.join(g.GOLDEN, "e2e_summary.json")
 
@@ -176,7 +176,7 @@ def test_host_driver_slot_count_invariance(fixtures):
 GPU_CASES = [(s, m) for s in SETS for m in DP_MODES
              if m == "default" or (m in ("hostwin", "handover") and s[0] in ("e2e_rep", "e2e_rep_i16_mix"))
              or (m == "parwave" and s[0] in ("e2e_rep", "e2e_tandem", "e2e_tandem_i16", "e2e_rep_i16_mix"))
-             or (m in ("lane1", "duo") and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem"))
+             or (m in ("lane1", "split") and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem"))
              or (m in ("nostore", "stream2") and s[0] in ("e2e_rep", "e2e_rep_i16_mix"))
              or (m in ("lane", "wave") and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem", "e2e_rep_i16",
                                                     "e2e_tandem_i16", "e2e_rep_i16_mix"))]
@@ -186,10 +186,10 @@ GPU_CASES = [(s, m) for s in SETS for m in DP_MODES
 @pytest.mark.parametrize("case,mode", GPU_CASES, ids=[f"{c[0]}-{m}" for c, m in GPU_CASES])
 def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     """The product binary (kernels on the MI355X) == the reference's SAM, through each DP
-    kernel: the launcher's choice (the two-wave split fill below BT2X_DP_SPLIT_MAX
-    problems), the banded lane kernels (lane: the launcher's lane choice; lane1: one lane
-    per problem; duo: two lanes per problem) / the wave kernel forced, and the lane kernel
-    handing nearly every walk over to the wave kernel (a 2-step budget)."""
+    kernel: the launcher's choice, the banded lane kernels (lane: the launcher's lane
+    choice; lane1: one lane per problem; split: the two-wave split fill) / the wave kernel
+    forced, and the lane kernel handing nearly every walk over to the wave kernel (a 2-step
+    budget)."""
     name, idx, fq, opts = case
     env = dict(os.environ)
     env.pop("BT2X_DP_WAVE", None)
@@ -209,12 +209,10 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
         env["BT2X_DP_PARWALK"] = "2"
     elif DP_MODES[mode] == "lane1":               # lane kernels, one lane per problem (dp_fill_kernel)
         env["BT2X_DP_WAVE"] = "0"
-        env["BT2X_DP_SPLIT"] = "0"
         env["BT2X_DP_DUO"] = "0"
-    elif DP_MODES[mode] == "duo":                 # lane kernels, two lanes per problem (dp_duo_kernel)
+    elif DP_MODES[mode] == "split":               # lane kernels: the two-wave split fill (dp_split_kernel)
         env["BT2X_DP_WAVE"] = "0"
-        env["BT2X_DP_SPLIT"] = "0"
-        env["BT2X_DP_DUO"] = "1"
+        env["BT2X_DP_SPLIT"] = "1"
     elif DP_MODES[mode] == "nostore":             # reads sent with every request (no read store)
         env["BT2X_READ_STORE"] = "0"
     elif DP_MODES[mode] not in (None, "stream2"):

@@ -144,12 +144,13 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     fields = ["ntries", "ok", "score", "ns", "gaps", "nedit", "bases_aligned", "refns", "refoff", "nbuf"]
     # (and every successful walk handed to the wave kernel's parallel walk; the wave mode
     # with the parallel walk)
-    # (the u8 lane launches run the two-wave split fill, dp_split_kernel; BT2X_DP_SPLIT=0
-    # the two-lanes-per-problem fill, dp_duo_kernel, and with BT2X_DP_DUO=0 dp_fill_kernel)
+    # (the u8 lane launches: the two-lanes-per-problem fill, dp_duo_kernel, below 65,536
+    # problems; BT2X_DP_DUO=0 the one-lane dp_fill_kernel; BT2X_DP_SPLIT=1 the two-wave
+    # split fill, dp_split_kernel)
     for wave, env in (("0", {}), ("1", {}), ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"}),
-                      ("0", {"BT2X_DP_SPLIT": "0"}), ("0", {"BT2X_DP_SPLIT": "0", "BT2X_DP_HEAVY": "1"}),
-                      ("0", {"BT2X_DP_SPLIT": "0", "BT2X_DP_DUO": "0"}),
-                      ("0", {"BT2X_DP_SPLIT": "0", "BT2X_DP_DUO": "0", "BT2X_DP_HEAVY": "1"})):
+                      ("0", {"BT2X_DP_SPLIT": "1"}), ("0", {"BT2X_DP_SPLIT": "1", "BT2X_DP_HEAVY": "1"}),
+                      ("0", {"BT2X_DP_DUO": "0"}),
+                      ("0", {"BT2X_DP_DUO": "0", "BT2X_DP_HEAVY": "1"})):
         os.environ["BT2X_DP_WAVE"] = wave
         os.environ.update(env)
         try:
@@ -367,7 +368,7 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=True):
     (False, "0", "1", 0.0, "1", "0", None), (False, "1", "1", 0.0, None, "2", None), (False, "1", "1", 1.0, None, "2", None),
     (False, "1", "1", 0.3, None, "2", None),
     (False, "0", "1", 0.0, None, None, "0"), (False, "0", "1", 0.0, "0", None, "0"), (False, "0", "1", 0.0, "1", None, "0"),
-    (False, "0", "1", 0.0, None, None, "1"), (False, "0", "1", 0.0, "1", None, "1"),
+    (False, "0", "1", 0.0, None, None, "split"), (False, "0", "1", 0.0, "1", None, "split"),
     (False, "0", "1", 0.0, "2", None, None)])
 def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, parwalk, duo, monkeypatch):
     """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
@@ -378,14 +379,15 @@ def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, pa
     past which the lane kernel drops a problem for the wave kernel to redo (0: never; 1 and 2:
     nearly every successful problem, mid-walk; default 800).  parwalk: BT2X_DP_PARWALK, the
     wave kernel's nextAlignment sequence on all lanes (walk_wave_par; default: for the walks
-    handed over, 2: the small-launch mode too, 0: lane 0 everywhere).  duo: None for the
-    banded u8 lane launches' default (the two-wave split fill, dp_split_kernel), else
-    BT2X_DP_SPLIT=0 and BT2X_DP_DUO=duo: two lanes per problem (1: dp_duo_kernel) or one
-    (0: dp_fill_kernel)."""
+    handed over, 2: the small-launch mode too, 0: lane 0 everywhere).  duo: the banded u8
+    lane launches' fill -- None: the launcher's default (dp_duo_kernel at these sizes);
+    "1" / "0": BT2X_DP_DUO, two lanes per problem (dp_duo_kernel) or one (dp_fill_kernel);
+    "split": BT2X_DP_SPLIT=1, the two-wave split fill (dp_split_kernel)."""
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     monkeypatch.setenv("BT2X_DP_BAND", band)
-    if duo is not None:
-        monkeypatch.setenv("BT2X_DP_SPLIT", "0")
+    if duo == "split":
+        monkeypatch.setenv("BT2X_DP_SPLIT", "1")
+    elif duo is not None:
         monkeypatch.setenv("BT2X_DP_DUO", duo)
     if heavy is not None:
         monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
@@ -426,7 +428,7 @@ def test_dp_exact_best_option(ctxs, monkeypatch):
 @pytest.mark.parametrize("wave,heavy,parwalk,duo", [("0", None, None, None), ("1", None, None, None),
                                                     ("0", "1", None, None), ("1", None, "2", None),
                                                     ("0", "1", "0", None), ("0", None, None, "0"),
-                                                    ("0", "1", None, "0"), ("0", None, None, "1")])
+                                                    ("0", "1", None, "0"), ("0", None, None, "split")])
 def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, duo, gold, monkeypatch):
     """The production (non-debug) kernel, in both modes and with walks handed to the wave
     kernel (its parallel walk, and lane 0's), reproduces the reference records of the golden
@@ -436,8 +438,9 @@ def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, duo, gold, m
         monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
     if parwalk is not None:
         monkeypatch.setenv("BT2X_DP_PARWALK", parwalk)
-    if duo is not None:                          # (None: the split fill; else duo / one lane)
-        monkeypatch.setenv("BT2X_DP_SPLIT", "0")
+    if duo == "split":                           # the two-wave split fill
+        monkeypatch.setenv("BT2X_DP_SPLIT", "1")
+    elif duo is not None:
         monkeypatch.setenv("BT2X_DP_DUO", duo)
     case = g.DpCase(os.path.join(g.GOLDEN, gold))
     ctx = ctxs["rep"][0]
