@@ -36,7 +36,9 @@ namespace {
 
 // Development ablations of the u8 lane fills (variant libraries only, BT2X_LIB; outputs
 // invalid): -DBT2X_PROF_NOSTORE drops the traceback stores, -DBT2X_PROF_NOWINDOW the
-// reference-window loads.
+// reference-window loads (which also changes every cell's value and so the candidates:
+// its gain is mostly a shorter candidate ordering, not the loads' waits -- an LDS-DMA
+// window ring that removed those waits measured neutral).
 #ifdef BT2X_PROF_NOSTORE
 constexpr bool kProfStores = false;
 #else
@@ -105,38 +107,6 @@ constexpr int kWaitVm0 = 0x0f70;
 // 8-bit values and re-extend with copies that wait for the loads.  Users test low bits only.
 __device__ __forceinline__ uint32_t tb_load4(__amdgpu_buffer_rsrc_t src, uint32_t off) {
 	return __builtin_amdgcn_raw_buffer_load_b32(src, (int)off, 0, 0);
-}
-
-// The fill's reference window, 16 columns per lane at a time, comes into an LDS ring by
-// LDS-DMA (global_load_lds_dwordx4) issued 8 column pairs ahead.  A plain load's wait is
-// s_waitcnt vmcnt(0), which also waits for every traceback store issued before it (vmcnt
-// retires in order): about 13 us a time at cohort shapes, 8 ms per replay step (the
-// BT2X_PROF_NOWINDOW build).  The chunk is read 8 pairs later, after `nst` of this wave's
-// stores: when nst >= 63 it has retired without any wait (at most 63 VMEM operations are
-// ever outstanding), else vmcnt(32) or vmcnt(0) as nst allows.  Both the DMA and the read
-// are asm: the compiler would wait vmcnt(0) before any LDS access that may alias a DMA
-// target (the row information shares the array), and an untracked DMA only makes its own
-// counted waits stricter.  Window slots are kWinSlot bytes: a chunk never leaves its slot.
-constexpr int kWaitVm32 = 0x8f70;                 // s_waitcnt vmcnt(32)
-__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
-	return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
-}
-__device__ __forceinline__ void win_issue(const uint32_t* rfw, int c, uint32_t* ring) {
-	const uint32_t* src = rfw + 4 * c;
-	const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(ring + (c & 1) * 256));
-	uint32_t keep;
-	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-	             : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-}
-__device__ __forceinline__ void win_take(int c, int nst, const uint32_t* ring, int lane,
-                                         uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3) {
-	if(nst < 32) __builtin_amdgcn_s_waitcnt(kWaitVm0);
-	else if(nst < 63) __builtin_amdgcn_s_waitcnt(kWaitVm32);
-	const uint32_t addr = lds_addr(ring + (c & 1) * 256 + 4 * lane);
-	typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-	u32x4 v;
-	asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-	w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
 }
 
 // 1 in the lowest active lane, else 0 (summed over lanes: wave iterations)
@@ -1319,11 +1289,9 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 		// BT2X_MAX_COLS-byte slots (the window pass), so the dwords are aligned; loads are
 		// clamped to the window's last dword.
 		const uint32_t* rfw = reinterpret_cast<const uint32_t*>(rf);
+		const int lastw = ((C > 0 ? C : 1) - 1) >> 2;
 		uint32_t cw0 = 0, cw1 = 0, cw2 = 0, cw3 = 0;
 		uint32_t refN = 0;                              // an N in the window's columns [0, C)
-		uint32_t* wring = lds + kRowWords * 64;         // two chunks past the row info (win_issue)
-		int nst = 0;                                    // this wave's stores since the chunk's issue
-		if(kProfWindow) win_issue(rfw, 0, wring);
 		for(int pp = 0; pp < npairs; pp++) {
 			const int j0 = 2 * pp;
 			// opaque per pair: keeps the per-step guards and last-row compares from being
@@ -1340,12 +1308,13 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 			// words in VGPRs)
 			asm volatile("" ::: "memory");
 			if(kProfWindow && (pp & 7) == 0) {            // wave-uniform: the next 16 columns
-				const int c = pp >> 3;
-				win_take(c, c == 0 ? 0 : nst, wring, lane, cw0, cw1, cw2, cw3);
-				nst = 0;
-				if(8 * (c + 1) < npairs) win_issue(rfw, c + 1, wring);
+				const int w0 = pp >> 1;
+				cw0 = rfw[min(w0, lastw)]; cw1 = rfw[min(w0 + 1, lastw)];
+				cw2 = rfw[min(w0 + 2, lastw)]; cw3 = rfw[min(w0 + 3, lastw)];
+				// consumed here, so the wait for them stays inside this branch (at the join it
+				// would run at every pair)
+				asm volatile("" : "+v"(cw0), "+v"(cw1), "+v"(cw2), "+v"(cw3));
 			}
-			if(shi >= slo) nst += (shi - slo + 1) >> 1;   // the pair's traceback stores
 			const uint32_t wsel = (pp & 4) ? ((pp & 2) ? cw3 : cw2) : ((pp & 2) ? cw1 : cw0);
 			const uint32_t wsh = (uint32_t)(pp & 1) * 16u;
 			const int ca = (j0 < C) ? (int)((wsel >> wsh) & 0xffu) : 4;
@@ -2076,7 +2045,7 @@ __device__ __forceinline__ void flag_set(int* f, int v, int lane) {
 
 __global__ void __launch_bounds__(64 * kSplitW * kSplitG) __attribute__((amdgpu_waves_per_eu(3)))
 dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
-	__shared__ uint32_t lds_g[kSplitG][kRowWords * 64 + 2 * 512 > (kCols / 4) * 64 ? kRowWords * 64 + 2 * 512 : (kCols / 4) * 64];   // row info + window rings during the fill, then keys / move logs
+	__shared__ uint32_t lds_g[kSplitG][(kCols / 4) * 64];   // row info during the fill, then keys / move logs   // row info + window rings during the fill, then keys / move logs
 	__shared__ uint32_t pen4[64];
 	__shared__ uint32_t t1_g[kSplitG][2][4][64];             // A -> B: h, f, e, hl after A's step b-1
 	__shared__ uint32_t t2_g[kSplitG][2][2][64];             // B -> A: H, E state dword of block b/4
@@ -2205,13 +2174,10 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 		const __amdgpu_buffer_rsrc_t dirsrc =
 			__builtin_amdgcn_make_buffer_rsrc(dir, 0, (int)(kDirBytesLane * 64u), 0x00020000);
 		const uint32_t* rfw = reinterpret_cast<const uint32_t*>(rf);
+		const int lastw = ((C > 0 ? C : 1) - 1) >> 2;
 		uint32_t cw0 = 0, cw1 = 0, cw2 = 0, cw3 = 0;
 		uint32_t refN = 0;
 		int bprev = 0, bexec_prev = 0;                    // the last pair's split; whether B ran it
-		// each wave its own window ring (win_issue), past the group's row info
-		uint32_t* wring = lds + kRowWords * 64 + wv * 512;
-		int nst = 0;
-		if(kProfWindow) win_issue(rfw, 0, wring);
 		for(int pp = 0; pp < npairs; pp++) {
 			const int j0 = 2 * pp;
 			int slo, shi, b;
@@ -2234,12 +2200,11 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 			asm volatile("" : "+s"(rmin), "+s"(lo), "+s"(hi), "+v"(rl));
 			asm volatile("" ::: "memory");
 			if(kProfWindow && (pp & 7) == 0) {
-				const int c = pp >> 3;
-				win_take(c, c == 0 ? 0 : nst, wring, lane, cw0, cw1, cw2, cw3);
-				nst = 0;
-				if(8 * (c + 1) < npairs) win_issue(rfw, c + 1, wring);
+				const int w0 = pp >> 1;
+				cw0 = rfw[min(w0, lastw)]; cw1 = rfw[min(w0 + 1, lastw)];
+				cw2 = rfw[min(w0 + 2, lastw)]; cw3 = rfw[min(w0 + 3, lastw)];
+				asm volatile("" : "+v"(cw0), "+v"(cw1), "+v"(cw2), "+v"(cw3));
 			}
-			if(exec) nst += isA ? (b - slo) >> 1 : (shi - b + 1) >> 1;
 			const uint32_t wsel = (pp & 4) ? ((pp & 2) ? cw3 : cw2) : ((pp & 2) ? cw1 : cw0);
 			const uint32_t wsh = (uint32_t)(pp & 1) * 16u;
 			const int ca = (j0 < C) ? (int)((wsel >> wsh) & 0xffu) : 4;
