@@ -618,6 +618,10 @@ extern "C" int bt2x_dp_align_dev(bt2x_ctx* c, const uint8_t* d_reads, const uint
 			a.heavy_list = (uint32_t*)c->b_heavy.p;
 			HIPCHK(hipMemsetAsync(a.heavy_list, 0, sizeof(uint32_t), s));
 		}
+		// the wave kernel's walks of many candidates go to the wave-parallel walk
+		// (BT2X_DP_WAVE_HAND candidates, default 16; 0: never); read per launch
+		const char* wh = getenv("BT2X_DP_WAVE_HAND");
+		a.wave_hand = wh ? (uint32_t)atol(wh) : 16u;
 	}
 	static const bool prof = [] { const char* e = getenv("BT2X_DP_PROF"); return e && e[0] == '1'; }();
 	if(prof) { a.prof = c->d_stats + 16; HIPCHK(hipMemsetAsync(a.prof, 0, 14 * sizeof(unsigned long long), s)); }

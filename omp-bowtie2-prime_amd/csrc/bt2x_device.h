@@ -123,6 +123,9 @@ struct DpLaunch {
 	uint32_t* heavy_list;          // [0]: count, then problem indices: problems whose walk the lane
 	                               // kernel hands to the wave kernel (more than `heavy` candidates)
 	uint32_t heavy;
+	uint32_t wave_hand;            // small-launch wave kernel (banded layout): a problem with at least
+	                               // this many candidates goes to heavy_list for the wave-parallel
+	                               // walk of dp_wave_kernel<2> (0: never)
 	unsigned long long* prof;      // development (BT2X_DP_PROF=1): lane-kernel fill cycles, walk
 	                               // cycles, walk wave-steps, candidate wave-iterations, groups
 	const uint8_t* mmpen;          // DevScoring::mmpen in HBM (256 B): the kernels index it per lane,

@@ -607,16 +607,49 @@ if(aborted) break;
 // The aligner's DP rounds end in a tail of small launches (the few reads that need many
 // rounds): there one lane per problem leaves the chip idle and a launch still costs the
 // R x C serial cell updates of one lane, ~1.5-6 ms.  This mode gives each problem a whole
-// wave.  Lane l owns rows 4l .. 4l+3 and the wave sweeps anti-diagonals: at time t lane l
-// computes column t - l, taking the H and F of the row above from lane l-1 (one DPP
-// wave_shr), so a problem takes C + R/4 steps.  Values and flags are the lane kernel's
+// wave.  Lane l owns rows rpl*l .. rpl*l + rpl - 1 (rpl = 1..4 rows a lane, the fewest
+// that fit; 4 until round 6) and the wave sweeps anti-diagonals: at time t lane l computes
+// column t - l, taking the H and F of the row above from lane l-1 (one DPP wave_shr), so a
+// problem takes C + R/rpl - 1 steps of rpl cells.  Values and flags are the lane kernel's
 // (same recurrence and traceback byte); the traceback bytes stay in LDS, column-major with
-// a lane's 4 rows in one dword, and the walk (lane 0) reads and marks them at LDS latency.
+// a lane's rows in one dword (or banded, below), and the walk reads and marks them at LDS
+// latency.
 // Cells are plain u32 here, so one body serves both value domains: u8 (top 0xff) and
 // i16 (the int16 range shifted to [0, 0xffff]: top 0xffff = score 0, floor 0 = -65535);
 // barred gap terms subtract 0x10000, which floors either domain.
 constexpr int kWaveTbWords = kCols * kRows / 4;              // 8000 dwords = 31.25 KiB
 constexpr size_t kWaveRecStageBytes = (size_t)kRecStage * sizeof(bt2x_aln_rec);
+// Banded traceback in LDS (round 6).  Every walk stays inside the diagonal band of
+// dp_fill_kernel (a path scoring >= minsc pays for at most G gap positions), so the wave
+// kernel keeps only the band's bytes: lane l's rows over its window of columns
+// [ws(l), ws(l) + P) with ws(l) = max(0, rpl*l - dl), P dwords a lane (lane-major).  The
+// values are still the whole rectangle's (every cell is computed), only the bytes no walk
+// can reach are not stored.  19 KiB holds the 150 bp / --dpad 12 band at 3 rows a lane
+// (50 lanes x 97 dwords) and whole short-read rectangles (lanes x ncol <= 4864); the
+// kernel's LDS then fits 7 waves per CU instead of 4.  A problem whose window does not fit
+// goes to the full-rectangle pass (dp_wave_kernel<2>).
+constexpr int kWaveBandWords = 4864;                          // 19 KiB
+
+// Traceback byte offsets in LDS: full rectangle (column-major, S bytes a column, a lane's 4
+// rows in one dword) or the banded layout above (P4 = 4P bytes a lane).
+template<bool kBand> struct TbMap;
+// Lane l holds rows [rpl*l, rpl*l + rpl) (row / rpl by a multiply: mul = ceil(2^16 / rpl),
+// exact for rows < 192).
+template<> struct TbMap<false> {
+	int S, rpl, mul;
+	__device__ __forceinline__ int operator()(int row, int col) const {
+		const int l = (row * mul) >> 16;
+		return col * S + 4 * l + (row - l * rpl);
+	}
+};
+template<> struct TbMap<true> {
+	int P4, dl, rpl, mul;
+	__device__ __forceinline__ int operator()(int row, int col) const {
+		const int l = (row * mul) >> 16;
+		const int ws = rpl * l - dl > 0 ? rpl * l - dl : 0;
+		return l * P4 + ((col - ws) << 2) + (row - l * rpl);
+	}
+};
 
 __device__ __forceinline__ uint32_t subs(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
 
@@ -660,8 +693,9 @@ __device__ __forceinline__ int wave_sum(int v) {
 	return v;
 }
 
+template<class TbM>
 __device__ __forceinline__ void walk_wave_par(const DevScoring& sc, const DpLaunch& a, const bt2x_dp_in& p,
-                                              bt2x_dp_out& o, int lane, uint8_t* tbb, int S, const uint8_t* cands,
+                                              bt2x_dp_out& o, int lane, uint8_t* tbb, const TbM& tm, const uint8_t* cands,
                                               const uint8_t* rdw, const uint16_t* penw, const uint8_t* refw,
                                               uint32_t* stage_ed, bt2x_aln_rec* stage_rec, uint16_t* path,
                                               uint16_t* plen, unsigned long long& st_bt) {
@@ -681,7 +715,7 @@ __device__ __forceinline__ void walk_wave_par(const DevScoring& sc, const DpLaun
 					int row = row0, col = cands[k + lane], ct = 2, n = 0;
 					uint16_t* pp = path + lane * kPathStride;
 					while(true) {
-						const uint32_t tb = tbb[col * S + row];
+						const uint32_t tb = tbb[tm(row, col)];
 						pp[n++] = (uint16_t)(row | (col << 8));
 						if((tb & TB_MARK) || row == 0) break;
 						const uint32_t dne = tb & TB_DNE, fne = (tb >> 1) & 1u;
@@ -701,7 +735,7 @@ __device__ __forceinline__ void walk_wave_par(const DevScoring& sc, const DpLaun
 			const int len = (int)uni(plen[k - b0]);
 			const uint16_t* pk = path + (k - b0) * kPathStride;
 			if(a.ablate == 2) {                                   // profiling: no backtrace walks
-				if(!(uni(tbb[(pk[0] >> 8) * S + (pk[0] & 0xff)]) & TB_MARK)) ntries++;
+				if(!(uni(tbb[tm(pk[0] & 0xff, pk[0] >> 8)]) & TB_MARK)) ntries++;
 				continue;
 			}
 			// ---- validation: attempt k over its path, 64 cells per round
@@ -714,7 +748,7 @@ __device__ __forceinline__ void walk_wave_par(const DevScoring& sc, const DpLaun
 				const bool v = idx < len;
 				const uint32_t cell = v ? pk[idx] : 0u;
 				const int row = (int)(cell & 0xffu), col = (int)(cell >> 8);
-				const int off = col * S + row;
+				const int off = v ? tm(row, col) : 0;
 				const uint32_t tb = v ? tbb[off] : 0u;
 				const uint64_t mk = __builtin_amdgcn_ballot_w64(v && (tb & TB_MARK));
 				if(c0 == 0 && (mk & 1ull)) { skip = true; break; }      // start cell reportedThrough
@@ -855,11 +889,14 @@ __device__ __forceinline__ void walk_wave_par(const DevScoring& sc, const DpLaun
 // rectangle's last-row maximum, nothing else.  kMode 2: the problems the lane kernel handed
 // over after its fill (a.heavy_list): the whole call, their walks at LDS latency.
 // kPar: the nextAlignment sequence with every lane (walk_wave_par) instead of lane 0.
-template<int kMode, bool kPar = false>
+// kBandTb (mode 0): the banded traceback layout (kWaveBandWords); a problem whose band
+// window does not fit is queued on a.heavy_list for dp_wave_kernel<2>.
+template<int kMode, bool kPar = false, bool kBandTb = false>
 __global__ void __launch_bounds__(64)
 dp_wave_kernel(DevScoring sc, DpLaunch a) {
 	constexpr bool kBestOnly = kMode == 1;
-	__shared__ uint32_t tbw[kBestOnly ? 1 : kWaveTbWords];
+	static_assert(!kBandTb || kMode == 0, "banded traceback: mode 0 only");
+	__shared__ uint32_t tbw[kBestOnly ? 1 : (kBandTb ? kWaveBandWords : kWaveTbWords)];
 	__shared__ uint16_t pathw[kPar ? kParBatch * kPathStride : 1];
 	__shared__ uint16_t plenw[kPar ? kParBatch : 1];
 	__shared__ uint8_t refw[kCols], cands[kCols];
@@ -892,8 +929,42 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 		const uint8_t* rd = a.reads + p.read_off;
 		const uint8_t* qu = a.quals + p.qual_off;
 		const uint8_t* rf = a.refs + p.ref_off;
-		const int L = (R + 3) >> 2;                 // lanes holding rows
-		const int S = 4 * L;                        // bytes per traceback column
+		// Rows per lane: the fewest that fit 64 lanes (3 at 150 bp, 2 at 100 bp: a problem takes
+		// C + R/rpl - 1 steps of rpl cells, so fewer rows per lane shorten its chain) and whose
+		// traceback fits the LDS layout; else the next.  Lane l holds rows [rpl*l, rpl*l + rpl),
+		// their bytes in the low rpl bytes of its dword.
+		int rpl = (R + 63) >> 6;
+		rpl = rpl < 1 ? 1 : rpl;
+		int P = 0, dlw = 0, dhw = 0;                // banded layout: window P dwords a lane
+		if(kBandTb) {
+			// dp_fill_kernel's band (diagonals [-dl, dh])
+			const int mo = imax(1, (int)(rdo < rfo ? rdo : rfo));
+			int me = (int)(rde < rfe ? rde : rfe);
+			me = me < mo ? me : mo;
+			const int budget = -(int)p.minsc;
+			int G = (me <= 0) ? (1 << 16) : (budget < mo ? 0 : 1 + (budget - mo) / me);
+			G = G > (1 << 16) ? (1 << 16) : G;
+			dhw = (C - R) + G + 2;
+			dlw = G + 4;
+		}
+		for(; rpl <= 4; rpl++) {
+			const int Lr = (R + rpl - 1) / rpl;
+			if(kBestOnly) break;
+			if(!kBandTb) { if(Lr * C <= kWaveTbWords) break; continue; }
+			int wc = dhw + dlw + rpl;               // columns of lane l's rows: [rpl*l - dl, rpl*l + rpl - 1 + dh]
+			wc = wc < C ? wc : C;
+			P = wc + ((wc ^ rpl) & 1);              // P = rpl mod 2: conflict-free fill stores (stride P - 1 - rpl)
+			if(Lr * P <= kWaveBandWords) break;
+		}
+		if(kBandTb && rpl > 4) {                    // does not fit: the full-rectangle pass
+			if(lane == 0) {
+				a.heavy_list[1 + atomicAdd(&a.heavy_list[0], 1u)] = pi;
+				if(a.stats) { st_cells += (unsigned long long)R * C; st_cols += C; }
+			}
+			continue;
+		}
+		const int L = (R + rpl - 1) / rpl;          // lanes holding rows
+		const int S = 4 * L;                        // bytes per traceback column (full layout)
 		for(int j = lane; j < C; j += 64) refw[j] = rf[j];
 		if(!kBestOnly)
 			for(int i = lane; i < R; i += 64) {
@@ -905,10 +976,10 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 		uint32_t rc[4], mm[4], rdoe[4], rfoe[4], rfee[4];
 #pragma unroll
 		for(int r = 0; r < 4; r++) {
-			const int i = 4 * lane + r;
+			const int i = rpl * lane + r;
 			uint32_t c = 7, m = npen;
 			bool gbar = true;
-			if(i < R) {
+			if(r < rpl && i < R) {
 				int q = (int)qu[i] - 33;
 				q = q < 0 ? 0 : (q > 255 ? 255 : q);
 				gbar = (i < sc.gapbar) || (R - 1 - i < sc.gapbar);
@@ -922,9 +993,10 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 		__syncthreads();
 		// ---- fill: H/E of the previous column for my rows; H[i][-1] = E = floor, H[-1][*] = top
 		uint32_t Hp0 = 0, Hp1 = 0, Hp2 = 0, Hp3 = 0, Ep0 = 0, Ep1 = 0, Ep2 = 0, Ep3 = 0;
-		uint32_t hupPrev = lane == 0 ? top : 0u;    // H[4l-1][j-1]
+		uint32_t hupPrev = lane == 0 ? top : 0u;    // H[rpl*l-1][j-1]
 		uint32_t bot = 0;                           // my bottom row's H | F << 16, last column
-		const int lastLane = (R - 1) >> 2, lastR = (R - 1) & 3;
+		const int lastLane = (R - 1) / rpl, lastR = (R - 1) - lastLane * rpl;
+		const int wsl = imax(0, rpl * lane - dlw);  // banded layout: my window's first column
 		const int T = C + L - 1;
 		for(int t = 0; t < T; t++) {
 			const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bot, 0x138, 0xf, 0xf, false);
@@ -953,12 +1025,16 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 					}                                                                           \
 					hdiag = HP; HP = h; EP = e; hu = h; fu = f;                                 \
 				}
+				// (rpl is wave-uniform: scalar branches)
 				BT2X_WAVE_CELL(0, Hp0, Ep0)
-				BT2X_WAVE_CELL(1, Hp1, Ep1)
-				BT2X_WAVE_CELL(2, Hp2, Ep2)
-				BT2X_WAVE_CELL(3, Hp3, Ep3)
+				if(rpl > 1) BT2X_WAVE_CELL(1, Hp1, Ep1)
+				if(rpl > 2) BT2X_WAVE_CELL(2, Hp2, Ep2)
+				if(rpl > 3) BT2X_WAVE_CELL(3, Hp3, Ep3)
 #undef BT2X_WAVE_CELL
-				if(!kBestOnly) tbw[j * L + lane] = tbv;
+				if(kBandTb) {
+					const int w = j - wsl;
+					if((unsigned)w < (unsigned)P) tbw[lane * P + w] = tbv;
+				} else if(!kBestOnly) tbw[j * L + lane] = tbv;
 				bot = hu | (fu << 16);
 				if(lane == lastLane)
 					lastrow[j] = (uint16_t)(lastR == 0 ? Hp0 : lastR == 1 ? Hp1 : lastR == 2 ? Hp2 : Hp3);
@@ -979,6 +1055,14 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			continue;
 		}
 		if(kMode == 0) { st_cells += (unsigned long long)R * C; st_cols += C; }   // (mode 2: the lane kernel counted them)
+		// banded layout, lane-0 walk: a problem of many candidates (a repeat's: their walks
+		// one after another, 2.4 ms for one such launch of 1,025 problems) is redone by
+		// dp_wave_kernel<2>, whose walk runs on every lane (0.37 ms; round 6)
+		if(kBandTb && !kPar && status && a.wave_hand && (uint32_t)nc >= a.wave_hand && a.ablate != 1) {
+			if(lane == 0) a.heavy_list[1 + atomicAdd(&a.heavy_list[0], 1u)] = pi;
+			__syncthreads();
+			continue;
+		}
 		bt2x_dp_out o;
 		o.nrec = 0; o.rec_off = 0;
 		o.status = status; o.best = best; o.ncand = status ? (uint16_t)nc : (uint16_t)0;
@@ -996,9 +1080,12 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			cands[rank] = (uint8_t)j;
 		}
 		__syncthreads();
+		TbMap<kBandTb> tm;
+		if constexpr(kBandTb) { tm.P4 = 4 * P; tm.dl = dlw; } else { tm.S = S; }
+		tm.rpl = rpl; tm.mul = (65536 + rpl - 1) / rpl;
 		if(kPar) {
 			if(o.status != 0 && o.ncand > 0 && a.ablate != 1)
-				walk_wave_par(sc, a, p, o, lane, tbb, S, cands, rdw, penw, refw, stage_ed, stage_rec, pathw, plenw, st_bt);
+				walk_wave_par(sc, a, p, o, lane, tbb, tm, cands, rdw, penw, refw, stage_ed, stage_rec, pathw, plenw, st_bt);
 			if(lane == 0) a.out[pi] = o;
 			__syncthreads();
 			continue;
@@ -1017,13 +1104,13 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 					while(ndone < ncand) {
 						const int col0 = (int)uni(cands[ndone]);
 						ndone++;
-						if(uni(tbb[col0 * S + row0]) & TB_MARK) continue;
+						if(uni(tbb[tm(row0, col0)]) & TB_MARK) continue;
 						ntries++;
 						if(a.ablate == 2) continue;
 						int row = row0, col = col0, ct = 2, bscore = 0, ns = 0, gaps = 0, ne = 0;
 						bool over_core = false, ok = true;
 						uint32_t tb_end = 0;
-						int bo = col * S + row;
+						int bo = tm(row, col);
 						uint32_t tb = uni(tbb[bo]);
 						while(true) {
 							st_bt++;
@@ -1038,9 +1125,9 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 							const bool isF = (ct == 1) || (inH && dne && !fne);
 							const int nct = isD ? 2 : isF ? (fext ? 1 : 2) : (eext ? 0 : 2);
 							const int cbo = bo;
-							bo += isD ? -(S + 1) : isF ? -1 : -S;
 							const int crow = row, ccol = col;
 							row -= (isD || isF) ? 1 : 0; col -= isF ? 0 : 1; ct = nct;
+							bo = tm(row, col);
 							const uint32_t ctb = tb;
 							tb = uni(tbb[bo]);
 							tbb[cbo] = (uint8_t)TB_MARK;               // setReportedThrough
@@ -2456,7 +2543,10 @@ struct DpOccupancy {
 	int fused[2][2];                // [debug][wide]
 	int fill[2][2];                 // split-mode fill kernels
 	int walk, wave, duo, split;
+	int wave_band[2];               // dp_wave_kernel<0, kPar, true>, [kPar]
 	DpOccupancy() {
+		wave_band[0] = blocks_per_cu((const void*)dp_wave_kernel<0, false, true>);
+		wave_band[1] = blocks_per_cu((const void*)dp_wave_kernel<0, true, true>);
 		fused[0][0] = blocks_per_cu((const void*)dp_fill_kernel<false, true, false>);
 		fused[1][0] = blocks_per_cu((const void*)dp_fill_kernel<true, true, false>);
 		fused[0][1] = blocks_per_cu((const void*)dp_fill_kernel<false, true, true>);
@@ -2518,6 +2608,14 @@ bool dp_split(uint32_t n) {
 	return n <= (x ? (uint32_t)atoll(x) : 131072u);
 }
 
+// The banded traceback layout of the small-launch wave kernel (default on; needs the
+// hand-over list, i.e. BT2X_DP_HEAVY != 0; BT2X_DP_WAVE_BAND=0: whole rectangles in LDS).
+// Read per launch (tests switch it).
+bool dp_wave_band() {
+	const char* e = getenv("BT2X_DP_WAVE_BAND");
+	return !(e && e[0] == '0');
+}
+
 uint32_t dp_wave_max() {                        // read per launch (tests switch modes)
 	const char* w = getenv("BT2X_DP_WAVE");
 	const char* x = getenv("BT2X_DP_WAVE_MAX");
@@ -2555,13 +2653,25 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 	DpLaunch a = a0;
 	const uint32_t groups_all = (a0.n + 63) / 64;
 	if(!dbg && a0.n <= dp_wave_max()) {
-		// small launch: one wave per problem (persistent, 4 waves per CU by LDS); it fills
-		// whole rectangles, so every best is exact
-		uint32_t wb = (uint32_t)a0.ncu * 4u;
+		// small launch: one wave per problem (persistent; 4 waves per CU with whole
+		// rectangles in LDS, 8 with the banded layout); it fills whole rectangles, so every
+		// best is exact
+		const bool band = a0.heavy_list != nullptr && dp_wave_band();
+		const bool par = dp_parwalk() >= 2;
 		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
+		uint32_t wb = (uint32_t)a0.ncu * (band ? (uint32_t)occ.wave_band[par ? 1 : 0] : 4u);
 		if(wb > slots) wb = (uint32_t)slots;
 		if(wb > a0.n) wb = a0.n;
-		if(dp_parwalk() >= 2) hipLaunchKernelGGL((dp_wave_kernel<0, true>), dim3(wb), dim3(64), 0, s, sc, a);
+		if(band) {
+			if(par) hipLaunchKernelGGL((dp_wave_kernel<0, true, true>), dim3(wb), dim3(64), 0, s, sc, a);
+			else hipLaunchKernelGGL((dp_wave_kernel<0, false, true>), dim3(wb), dim3(64), 0, s, sc, a);
+			// the problems whose band window did not fit: whole rectangles
+			uint32_t wb2 = (uint32_t)a0.ncu * 4u;
+			if(wb2 > slots) wb2 = (uint32_t)slots;
+			if(wb2 > a0.n) wb2 = a0.n;
+			if(dp_parwalk() >= 1) hipLaunchKernelGGL((dp_wave_kernel<2, true>), dim3(wb2), dim3(64), 0, s, sc, a);
+			else hipLaunchKernelGGL((dp_wave_kernel<2, false>), dim3(wb2), dim3(64), 0, s, sc, a);
+		} else if(par) hipLaunchKernelGGL((dp_wave_kernel<0, true>), dim3(wb), dim3(64), 0, s, sc, a);
 		else hipLaunchKernelGGL((dp_wave_kernel<0, false>), dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 	}

@@ -147,7 +147,7 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     # (the u8 lane launches: the two-lanes-per-problem fill, dp_duo_kernel, below 65,536
     # problems; BT2X_DP_DUO=0 the one-lane dp_fill_kernel; BT2X_DP_SPLIT=1 the two-wave
     # split fill, dp_split_kernel)
-    for wave, env in (("0", {}), ("1", {}), ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"}),
+    for wave, env in (("0", {}), ("1", {}), ("1", {"BT2X_DP_WAVE_BAND": "0"}), ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"}),
                       ("0", {"BT2X_DP_SPLIT": "1"}), ("0", {"BT2X_DP_SPLIT": "1", "BT2X_DP_HEAVY": "1"}),
                       ("0", {"BT2X_DP_DUO": "0"}),
                       ("0", {"BT2X_DP_DUO": "0", "BT2X_DP_HEAVY": "1"})):
@@ -369,7 +369,9 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=True):
     (False, "1", "1", 0.3, None, "2", None),
     (False, "0", "1", 0.0, None, None, "0"), (False, "0", "1", 0.0, "0", None, "0"), (False, "0", "1", 0.0, "1", None, "0"),
     (False, "0", "1", 0.0, None, None, "split"), (False, "0", "1", 0.0, "1", None, "split"),
-    (False, "0", "1", 0.0, "2", None, None)])
+    (False, "0", "1", 0.0, "2", None, None),
+    (False, "1f", "1", 0.0, None, None, None), (False, "1f", "1", 1.0, None, None, None),
+    (False, "1f", "1", 0.3, None, "2", None), (False, "1", "1", 0.3, "0", None, None)])
 def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, parwalk, duo, monkeypatch):
     """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
     wave-per-problem mode) and debug kernels on random shapes/penalty thresholds at the ABI
@@ -382,7 +384,13 @@ def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, pa
     handed over, 2: the small-launch mode too, 0: lane 0 everywhere).  duo: the banded u8
     lane launches' fill -- None: the launcher's default (dp_duo_kernel at these sizes);
     "1" / "0": BT2X_DP_DUO, two lanes per problem (dp_duo_kernel) or one (dp_fill_kernel);
-    "split": BT2X_DP_SPLIT=1, the two-wave split fill (dp_split_kernel)."""
+    "split": BT2X_DP_SPLIT=1, the two-wave split fill (dp_split_kernel).  wave "1" runs the
+    wave kernel with its banded traceback layout (problems whose band window does not fit
+    go to the whole-rectangle pass; with heavy "0" there is no hand-over list and the whole
+    rectangle is kept), "1f" with whole rectangles in LDS (BT2X_DP_WAVE_BAND=0)."""
+    if wave.endswith("f"):
+        wave = wave[:-1]
+        monkeypatch.setenv("BT2X_DP_WAVE_BAND", "0")
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     monkeypatch.setenv("BT2X_DP_BAND", band)
     if duo == "split":
@@ -428,11 +436,16 @@ def test_dp_exact_best_option(ctxs, monkeypatch):
 @pytest.mark.parametrize("wave,heavy,parwalk,duo", [("0", None, None, None), ("1", None, None, None),
                                                     ("0", "1", None, None), ("1", None, "2", None),
                                                     ("0", "1", "0", None), ("0", None, None, "0"),
-                                                    ("0", "1", None, "0"), ("0", None, None, "split")])
+                                                    ("0", "1", None, "0"), ("0", None, None, "split"),
+                                                    ("1f", None, None, None)])
 def test_dp_production_kernel_on_golden(ctxs, wave, heavy, parwalk, duo, gold, monkeypatch):
     """The production (non-debug) kernel, in both modes and with walks handed to the wave
     kernel (its parallel walk, and lane 0's), reproduces the reference records of the golden
-    set (oracle-checked, then against the golden itself)."""
+    set (oracle-checked, then against the golden itself).  wave "1f": the wave kernel with
+    whole rectangles in LDS (BT2X_DP_WAVE_BAND=0; "1" is its banded layout)."""
+    if wave.endswith("f"):
+        wave = wave[:-1]
+        monkeypatch.setenv("BT2X_DP_WAVE_BAND", "0")
     monkeypatch.setenv("BT2X_DP_WAVE", wave)
     if heavy is not None:
         monkeypatch.setenv("BT2X_DP_HEAVY", heavy)
