@@ -889,14 +889,17 @@ __device__ __forceinline__ void walk_wave_par(const DevScoring& sc, const DpLaun
 // rectangle's last-row maximum, nothing else.  kMode 2: the problems the lane kernel handed
 // over after its fill (a.heavy_list): the whole call, their walks at LDS latency.
 // kPar: the nextAlignment sequence with every lane (walk_wave_par) instead of lane 0.
-// kBandTb (mode 0): the banded traceback layout (kWaveBandWords); a problem whose band
-// window does not fit is queued on a.heavy_list for dp_wave_kernel<2>.
+// kBandTb (modes 0 and 2): the banded traceback layout; in mode 0 within kWaveBandWords (a
+// problem whose window does not fit goes to mode 2), in mode 2 within kWaveTbWords, which
+// holds any problem (at worst the whole rectangle, lane-major, 4 rows a lane).  Mode 0 hands
+// problems over on a.heavy_list; it must be followed by the mode-2 pass.
 template<int kMode, bool kPar = false, bool kBandTb = false>
 __global__ void __launch_bounds__(64)
 dp_wave_kernel(DevScoring sc, DpLaunch a) {
 	constexpr bool kBestOnly = kMode == 1;
-	static_assert(!kBandTb || kMode == 0, "banded traceback: mode 0 only");
-	__shared__ uint32_t tbw[kBestOnly ? 1 : (kBandTb ? kWaveBandWords : kWaveTbWords)];
+	static_assert(!kBandTb || kMode != 1, "banded traceback: modes 0 and 2");
+	constexpr int kTbWords = (kBandTb && kMode == 0) ? kWaveBandWords : kWaveTbWords;
+	__shared__ uint32_t tbw[kBestOnly ? 1 : kTbWords];
 	__shared__ uint16_t pathw[kPar ? kParBatch * kPathStride : 1];
 	__shared__ uint16_t plenw[kPar ? kParBatch : 1];
 	__shared__ uint8_t refw[kCols], cands[kCols];
@@ -954,9 +957,9 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 			int wc = dhw + dlw + rpl;               // columns of lane l's rows: [rpl*l - dl, rpl*l + rpl - 1 + dh]
 			wc = wc < C ? wc : C;
 			P = wc + ((wc ^ rpl) & 1);              // P = rpl mod 2: conflict-free fill stores (stride P - 1 - rpl)
-			if(Lr * P <= kWaveBandWords) break;
+			if(Lr * P <= kTbWords) break;
 		}
-		if(kBandTb && rpl > 4) {                    // does not fit: the full-rectangle pass
+		if(kBandTb && kMode == 0 && rpl > 4) {      // does not fit: the full-rectangle pass
 			if(lane == 0) {
 				a.heavy_list[1 + atomicAdd(&a.heavy_list[0], 1u)] = pi;
 				if(a.stats) { st_cells += (unsigned long long)R * C; st_cols += C; }
@@ -1058,7 +1061,7 @@ dp_wave_kernel(DevScoring sc, DpLaunch a) {
 		// banded layout, lane-0 walk: a problem of many candidates (a repeat's: their walks
 		// one after another, 2.4 ms for one such launch of 1,025 problems) is redone by
 		// dp_wave_kernel<2>, whose walk runs on every lane (0.37 ms; round 6)
-		if(kBandTb && !kPar && status && a.wave_hand && (uint32_t)nc >= a.wave_hand && a.ablate != 1) {
+		if(kMode == 0 && kBandTb && !kPar && status && a.wave_hand && (uint32_t)nc >= a.wave_hand && a.ablate != 1) {
 			if(lane == 0) a.heavy_list[1 + atomicAdd(&a.heavy_list[0], 1u)] = pi;
 			__syncthreads();
 			continue;
@@ -2608,8 +2611,9 @@ bool dp_split(uint32_t n) {
 	return n <= (x ? (uint32_t)atoll(x) : 131072u);
 }
 
-// The banded traceback layout of the small-launch wave kernel (default on; needs the
-// hand-over list, i.e. BT2X_DP_HEAVY != 0; BT2X_DP_WAVE_BAND=0: whole rectangles in LDS).
+// The banded traceback layout of the wave kernels (default on; in the small-launch mode it
+// needs the hand-over list, i.e. BT2X_DP_HEAVY != 0; BT2X_DP_WAVE_BAND=0: whole rectangles
+// in LDS, column-major, 4 rows a lane, as up to round 5).
 // Read per launch (tests switch it).
 bool dp_wave_band() {
 	const char* e = getenv("BT2X_DP_WAVE_BAND");
@@ -2665,12 +2669,12 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		if(band) {
 			if(par) hipLaunchKernelGGL((dp_wave_kernel<0, true, true>), dim3(wb), dim3(64), 0, s, sc, a);
 			else hipLaunchKernelGGL((dp_wave_kernel<0, false, true>), dim3(wb), dim3(64), 0, s, sc, a);
-			// the problems whose band window did not fit: whole rectangles
+			// the problems handed over: band window too wide, or many candidates
 			uint32_t wb2 = (uint32_t)a0.ncu * 4u;
 			if(wb2 > slots) wb2 = (uint32_t)slots;
 			if(wb2 > a0.n) wb2 = a0.n;
-			if(dp_parwalk() >= 1) hipLaunchKernelGGL((dp_wave_kernel<2, true>), dim3(wb2), dim3(64), 0, s, sc, a);
-			else hipLaunchKernelGGL((dp_wave_kernel<2, false>), dim3(wb2), dim3(64), 0, s, sc, a);
+			if(dp_parwalk() >= 1) hipLaunchKernelGGL((dp_wave_kernel<2, true, true>), dim3(wb2), dim3(64), 0, s, sc, a);
+			else hipLaunchKernelGGL((dp_wave_kernel<2, false, true>), dim3(wb2), dim3(64), 0, s, sc, a);
 		} else if(par) hipLaunchKernelGGL((dp_wave_kernel<0, true>), dim3(wb), dim3(64), 0, s, sc, a);
 		else hipLaunchKernelGGL((dp_wave_kernel<0, false>), dim3(wb), dim3(64), 0, s, sc, a);
 		return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
@@ -2716,8 +2720,14 @@ int bt2x_launch_dp(const DevScoring& sc, const DpLaunch& a0, void* stream) {
 		uint32_t wb = (uint32_t)a0.ncu * 4u;
 		const size_t slots = bt2x_dp_scratch_bytes(a0.ncu, a0.chunk_groups) / kWaveRecStageBytes;
 		if(wb > slots) wb = (uint32_t)slots;
-		if(dp_parwalk() >= 1) hipLaunchKernelGGL((dp_wave_kernel<2, true>), dim3(wb), dim3(64), 0, s, sc, a);
-		else hipLaunchKernelGGL((dp_wave_kernel<2, false>), dim3(wb), dim3(64), 0, s, sc, a);
+		const bool band = dp_wave_band();
+		if(dp_parwalk() >= 1) {
+			if(band) hipLaunchKernelGGL((dp_wave_kernel<2, true, true>), dim3(wb), dim3(64), 0, s, sc, a);
+			else hipLaunchKernelGGL((dp_wave_kernel<2, true>), dim3(wb), dim3(64), 0, s, sc, a);
+		} else {
+			if(band) hipLaunchKernelGGL((dp_wave_kernel<2, false, true>), dim3(wb), dim3(64), 0, s, sc, a);
+			else hipLaunchKernelGGL((dp_wave_kernel<2, false>), dim3(wb), dim3(64), 0, s, sc, a);
+		}
 	}
 	return hipGetLastError() == hipSuccess ? 0 : BT2X_E_NODEVICE;
 }

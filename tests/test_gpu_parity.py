@@ -147,7 +147,12 @@ def test_dp_kernel_matches_oracle_at_scale(ctxs):
     # (the u8 lane launches: the two-lanes-per-problem fill, dp_duo_kernel, below 65,536
     # problems; BT2X_DP_DUO=0 the one-lane dp_fill_kernel; BT2X_DP_SPLIT=1 the two-wave
     # split fill, dp_split_kernel)
-    for wave, env in (("0", {}), ("1", {}), ("1", {"BT2X_DP_WAVE_BAND": "0"}), ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"}),
+    # (the wave kernel: its banded layout, whole rectangles, every problem with a candidate
+    # or none handed to the wave-parallel walk; the lane kernel's hand-over pass with whole
+    # rectangles)
+    for wave, env in (("0", {}), ("1", {}), ("1", {"BT2X_DP_WAVE_BAND": "0"}), ("1", {"BT2X_DP_WAVE_HAND": "1"}),
+                      ("1", {"BT2X_DP_WAVE_HAND": "0"}), ("0", {"BT2X_DP_HEAVY": "1", "BT2X_DP_WAVE_BAND": "0"}),
+                      ("0", {"BT2X_DP_HEAVY": "1"}), ("1", {"BT2X_DP_PARWALK": "2"}),
                       ("0", {"BT2X_DP_SPLIT": "1"}), ("0", {"BT2X_DP_SPLIT": "1", "BT2X_DP_HEAVY": "1"}),
                       ("0", {"BT2X_DP_DUO": "0"}),
                       ("0", {"BT2X_DP_DUO": "0", "BT2X_DP_HEAVY": "1"})):
@@ -371,7 +376,8 @@ def _compare_dp(out, recs, edits, eo, erecs, eedits, inp, exact_best=True):
     (False, "0", "1", 0.0, None, None, "split"), (False, "0", "1", 0.0, "1", None, "split"),
     (False, "0", "1", 0.0, "2", None, None),
     (False, "1f", "1", 0.0, None, None, None), (False, "1f", "1", 1.0, None, None, None),
-    (False, "1f", "1", 0.3, None, "2", None), (False, "1", "1", 0.3, "0", None, None)])
+    (False, "1f", "1", 0.3, None, "2", None), (False, "1", "1", 0.3, "0", None, None),
+    (False, "0f", "1", 0.3, "1", None, None)])
 def test_dp_kernel_edge_shapes_vs_oracle(ctxs, debug, wave, band, i16, heavy, parwalk, duo, monkeypatch):
     """Production (debug=False; lane-per-problem kernel with and without the diagonal band,
     wave-per-problem mode) and debug kernels on random shapes/penalty thresholds at the ABI
