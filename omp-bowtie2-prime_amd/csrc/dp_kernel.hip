@@ -142,6 +142,82 @@ __device__ __forceinline__ uint32_t pne(uint32_t a, uint32_t b, uint32_t one2) {
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
 __device__ __forceinline__ uint32_t opaque(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
 
+// ---------------------------------------------- candidate order (DpBtCandidate)
+// A lane's last row as byte keys in LDS (lds[q * 64 + lane], 4 columns a dword, q < nw;
+// byte 0 = below the threshold) is put in DpBtCandidate order (score desc, col desc,
+// aligner_swsse_ee_u8.cpp:519-536 + the sort of btncand_): key = score << 8 | col, 16 bits,
+// two keys per packed op; keys of non-qualifying columns (score 0) are below every
+// qualifying one and are never reached within ncand.
+//
+// keys_below: the largest key below cur (cur2 = cur in both halves) among dword q's four
+// columns, per half (0 if none).
+__device__ __forceinline__ uint32_t keys_below(uint32_t w4, uint32_t q, uint32_t cur2, uint32_t one2) {
+	const uint32_t cq = q * 0x40004u + 0x10000u;                   // cols 4q, 4q+1
+	const uint32_t ka = perm(cq, w4, 0x01060004u);                 // [4q, s0, 4q+1, s1]
+	const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);      // [4q+2, s2, 4q+3, s3]
+	return pmax(pmul_lo(pmin(psubs(cur2, ka), one2), ka), pmul_lo(pmin(psubs(cur2, kb), one2), kb));
+}
+
+// The ncand sorted keys, emit(k, key) each.  Round 6: per 16-column group the largest key
+// not yet emitted is kept (13 groups, two a register); the next candidate is the largest of
+// those, and only its group is scanned again for its next key below (every larger key of
+// the group is already out) -- ~80 instructions a candidate instead of a max-below-key scan
+// of the whole row (~11 per dword, ~500 at 181 columns).  A wave whose lanes have at most
+// two candidates keeps the plain scans (the groups' setup costs one).
+template<class Emit>
+__device__ __forceinline__ void order_candidates(const uint32_t* lds, int lane, int nw, int ncand, uint32_t one2,
+                                                 Emit&& emit) {
+	constexpr int kGroups = (kCols + 15) / 16;                     // 13
+	if(__builtin_amdgcn_ballot_w64(ncand > 2) == 0) {
+		int cur_key = 0xffff;
+		for(int k = 0; k < ncand; k++) {
+			const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
+			uint32_t best2 = 0;
+#pragma unroll 2
+			for(int q = 0; q < nw; q++) best2 = pmax(best2, keys_below(lds[q * 64 + lane], (uint32_t)q, cur2, one2));
+			cur_key = (int)max(best2 & 0xffffu, best2 >> 16);
+			emit(k, cur_key);
+		}
+		return;
+	}
+	uint32_t gm[(kGroups + 1) / 2];                                // group 2i: low half, 2i+1: high half
+#pragma unroll
+	for(int i = 0; i < (kGroups + 1) / 2; i++) gm[i] = 0;
+#pragma unroll
+	for(int g = 0; g < kGroups; g++) {
+		if(4 * g >= nw) break;                                     // (wave-uniform)
+		uint32_t m2 = 0;
+#pragma unroll
+		for(int i = 0; i < 4; i++) {
+			const int q = 4 * g + i;
+			if(q < nw) m2 = pmax(m2, keys_below(lds[q * 64 + lane], (uint32_t)q, 0xffffffffu, one2));
+		}
+		const uint32_t gmax = max(m2 & 0xffffu, m2 >> 16);
+		gm[g >> 1] |= gmax << (16 * (g & 1));
+	}
+	for(int k = 0; k < ncand; k++) {
+		uint32_t m2 = gm[0];
+#pragma unroll
+		for(int i = 1; i < (kGroups + 1) / 2; i++) m2 = pmax(m2, gm[i]);
+		const uint32_t key = max(m2 & 0xffffu, m2 >> 16);
+		emit(k, (int)key);
+		const int g = (int)(key & 0xffu) >> 4;                     // the key's column -> its group
+		const uint32_t cur2 = key * 0x10001u;
+		uint32_t b2 = 0;
+#pragma unroll
+		for(int i = 0; i < 4; i++) {
+			const int q = 4 * g + i;
+			if(q < nw) b2 = pmax(b2, keys_below(lds[q * 64 + lane], (uint32_t)q, cur2, one2));
+		}
+		const uint32_t nb = max(b2 & 0xffffu, b2 >> 16);
+#pragma unroll
+		for(int i = 0; i < (kGroups + 1) / 2; i++) {
+			const uint32_t hi = (gm[i] & 0xffffu) | (nb << 16), lo = (gm[i] & 0xffff0000u) | nb;
+			gm[i] = (g >> 1) == i ? ((g & 1) ? hi : lo) : gm[i];
+		}
+	}
+}
+
 enum { H_NONE = 0, H_DIAG = 1, H_REF_OPEN = 2, H_RFGAP_EXT = 3, H_READ_OPEN = 4, H_RDGAP_EXT = 5 };
 enum { EDIT_READ_GAP = 1, EDIT_REF_GAP = 2, EDIT_MM = 3 };
 
@@ -1611,31 +1687,14 @@ dp_fill_kernel(DevScoring sc, DpLaunch a, uint32_t base, uint32_t nprob) {
 				}
 				lds[q * 64 + lane] = w4;
 			}
-			int cur_key = 0xffff;
-			// Two columns per packed op: key = score << 8 | col in each 16-bit half; the max
-			// key below the previous one is the next candidate (keys of scores below the
-			// threshold are smaller than every qualifying key and are never reached).
-			for(int k = 0; k < ncand; k++) {
-				const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
-				uint32_t best2 = 0;
-#pragma unroll 2
-				for(int q = 0; q < nw; q++) {
-					const uint32_t w4 = lds[q * 64 + lane];
-					const uint32_t cq = (uint32_t)q * 0x40004u + 0x10000u;     // cols 4q, 4q+1
-					const uint32_t ka = perm(cq, w4, 0x01060004u);             // [4q, s0, 4q+1, s1]
-					const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);  // [4q+2, s2, 4q+3, s3]
-					best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
-					best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
-				}
-				const int bk = (int)max(best2 & 0xffffu, best2 >> 16);
-				cur_key = bk;
+			order_candidates(lds, lane, nw, ncand, one2, [&](int k, int bk) {
 				cands[(size_t)k * 64 + lane] = (uint8_t)(bk & 0xff);
 				if(kDebug && a.cands) {
 					const int score = kWide ? (bk >> 8) - 1 + thr : (bk >> 8);
 					a.cands[(size_t)pi * kCols + k] = i16 ? BT2X_CAND_PACK16(bk & 0xff, score - 0x8000)
 					                                      : BT2X_CAND_PACK(row0, bk & 0xff, score);
 				}
-			}
+			});
 		} else {
 			// an i16 problem with minsc < -254 in the wave: 32-bit keys (value << 8 | col)
 			// straight from the last row (rare: non-default --score-min)
@@ -2053,23 +2112,7 @@ dp_duo_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 			}
 			lds[qw * 64 + lane] = w4;
 		}
-		int cur_key = 0xffff;
-		for(int k = 0; k < ncand; k++) {
-			const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
-			uint32_t best2 = 0;
-#pragma unroll 2
-			for(int qw = 0; qw < nw; qw++) {
-				const uint32_t w4 = lds[qw * 64 + lane];
-				const uint32_t cq = (uint32_t)qw * 0x40004u + 0x10000u;
-				const uint32_t ka = perm(cq, w4, 0x01060004u);
-				const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);
-				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
-				best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
-			}
-			const int bk2 = (int)max(best2 & 0xffffu, best2 >> 16);
-			cur_key = bk2;
-			cands[(size_t)k * 64 + lane] = (uint8_t)(bk2 & 0xff);
-		}
+		order_candidates(lds, lane, nw, ncand, one2, [&](int k, int bk) { cands[(size_t)k * 64 + lane] = (uint8_t)(bk & 0xff); });
 		uint8_t* wslot = gslot + kGroupBytes;
 		walk_problem<kDuoG, kDuoPW>(sc, pen_lds, a, pi, lane, q, gslot + kDuoPairBytes, kDuoDirBytes - kDuoPairBytes,
 		                                cands, reinterpret_cast<uint32_t*>(wslot + kEditOff),
@@ -2461,23 +2504,7 @@ dp_split_kernel(DevScoring sc, DpLaunch a, uint32_t nprob) {
 					lds[q * 64 + lane] = w4;
 				}
 				uint8_t* cands = gslot + kCandOff;
-				int cur_key = 0xffff;
-				for(int k = 0; k < ncand; k++) {
-					const uint32_t cur2 = (uint32_t)cur_key * 0x10001u;
-					uint32_t best2 = 0;
-#pragma unroll 2
-					for(int q = 0; q < nw; q++) {
-						const uint32_t w4 = lds[q * 64 + lane];
-						const uint32_t cq = (uint32_t)q * 0x40004u + 0x10000u;
-						const uint32_t ka = perm(cq, w4, 0x01060004u);
-						const uint32_t kb = perm(cq + 0x20002u, w4, 0x03060204u);
-						best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, ka), one2), ka));
-						best2 = pmax(best2, pmul_lo(pmin(psubs(cur2, kb), one2), kb));
-					}
-					const int bk = (int)max(best2 & 0xffffu, best2 >> 16);
-					cur_key = bk;
-					cands[(size_t)k * 64 + lane] = (uint8_t)(bk & 0xff);
-				}
+				order_candidates(lds, lane, nw, ncand, one2, [&](int k, int bk) { cands[(size_t)k * 64 + lane] = (uint8_t)(bk & 0xff); });
 				uint8_t* wslot = gslot + kGroupBytes;
 				walk_problem<64, kPairWords>(sc, pen_lds, a, pi, lane, lane, gslot + kDirOff, kDirBytesLane * 64u, cands,
 				                             reinterpret_cast<uint32_t*>(wslot + kEditOff), reinterpret_cast<bt2x_aln_rec*>(wslot + kRecOff),
