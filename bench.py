@@ -827,6 +827,29 @@ def reap_children() -> list:
     return found
 
 
+def user_procs():
+    """This user's processes other than bench.py, its ancestors and its children, as
+    "pid:name:command" (the review counts one process left at the end of the driver's run;
+    this lists what is alive, under the same user, as bench.py exits)."""
+    try:
+        import psutil
+    except ImportError:
+        return []
+    me = psutil.Process()
+    skip = {me.pid} | {p.pid for p in me.parents()} | {p.pid for p in me.children(recursive=True)}
+    out = []
+    for p in psutil.process_iter(["pid", "name", "uids", "cmdline"]):
+        try:
+            if p.info["pid"] in skip or p.info["uids"] is None or p.info["uids"].real != os.getuid():
+                continue
+            if not p.info["cmdline"]:                    # kernel threads
+                continue
+            out.append(f"{p.info['pid']}:{p.info['name']}:{' '.join(p.info['cmdline'] or [])[:120]}")
+        except psutil.Error:
+            pass
+    return out
+
+
 # ------------------------------------------------------------------------ main
 
 def main():
@@ -997,6 +1020,7 @@ def main():
     if rank == 0 and world == 1 and getattr(args, "rep_leg", False):
         line.setdefault("configs_other", {})["C3_rep50"] = rep_leg(args, rdir, gpu)
     line["end_to_end"]["reaped_at_exit"] = reap_children()
+    line["end_to_end"]["user_procs_at_exit"] = user_procs()
     if dist:
         dist.barrier()
     if rank == 0:
