@@ -257,12 +257,17 @@ def kv_line(err: str, tag: str) -> dict:
     return out
 
 
+def bdist_mod():
+    from bt2x import dist
+    return dist
+
+
 def run_aligner(args, cmd, errp, what):
     """bt2x-align as a child process (this process's GPU context, if any, stays idle), with
     a host-RAM watchdog (the box caps a command's RAM) and a progress line every 30 s."""
     t0 = time.perf_counter()
     with open(errp, "w") as ferr:
-        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=ferr)
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=ferr, env=bdist_mod().malloc_thp_env())
         peak, last = 0, t0
         while p.poll() is None:
             try:
@@ -497,7 +502,8 @@ def roofline(args, rp, kernel=None):
 # ------------------------------------------------------------------------ CPU baseline
 
 def ref_run(args, base, fq, threads, sam):
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_WAIT_POLICY="ACTIVE")
+    # (the same malloc setting as bt2x-align's runs: the baseline gets huge pages too)
+    env = dict(bdist_mod().malloc_thp_env(), OMP_NUM_THREADS=str(threads), OMP_WAIT_POLICY="ACTIVE")
     t0 = time.perf_counter()
     # (the fork's -p is a tasks-per-thread multiplier, default 10: BASELINE.md runs it as is)
     r = subprocess.run([REF_ALIGN, "-x", base, "-U", fq, "-S", sam, "--dpad", str(args.dpad)],
@@ -611,7 +617,7 @@ def ref_baseline(args, binary, base, fqs, rdir, n, extra, tag):
     m = head_fastq(fqs, sample, n)
     head_fastq(fqs, one, 1)
     sam = os.path.join(rdir, f"{tag}_ref.sam")
-    env = dict(os.environ, OMP_NUM_THREADS=str(share), OMP_WAIT_POLICY="ACTIVE")
+    env = dict(bdist_mod().malloc_thp_env(), OMP_NUM_THREADS=str(share), OMP_WAIT_POLICY="ACTIVE")
     walls = []
     for fq, dst in ((one, os.devnull), (sample, sam)):
         t0 = time.perf_counter()
@@ -964,7 +970,7 @@ def main():
                                f"step = one FASTQ file of {per} reads",
                    "reads_per_gpu": args.reads, "read_len": args.read_len, "parallelism": f"dp{world} (read shards)",
                    "host_threads": args.host_threads, "host_threads_note": threads_note, "cpu_share": share,
-                   "host_cpus": host_cpus, "host_cpus_note": cpu_note or "one rank: the aligner pins itself to its GPU's NUMA node",
+                   "malloc": bdist_mod().malloc_thp_env().get("GLIBC_TUNABLES", "default") + " (bt2x-align and the reference runs)", "host_cpus": host_cpus, "host_cpus_note": cpu_note or "one rank: the aligner pins itself to its GPU's NUMA node",
                    "slots": args.slots, "key": workload_key(args)},
         "end_to_end": {"runs": [run_entry(r) for r in runs],
                        "value_is": f"the median of {len(runs)} timed runs (separate bt2x-align processes, same index "

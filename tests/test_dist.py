@@ -291,3 +291,14 @@ def test_gpu_two_rank_sharded_alignment(tmp_path):
     assert split_stderr(r.stderr)[1] == split_stderr(ref)[1]
     assert "BT2X_DIST ranks=2 reads=3560" in r.stderr
     assert not list(tmp_path.glob("dist.sam.part*"))
+
+
+def test_malloc_thp_env():
+    """Aligner children get glibc's malloc on transparent huge pages (appended to any
+    GLIBC_TUNABLES already set), unless BT2X_MALLOC_THP=0."""
+    from bt2x import dist as bd
+    assert bd.malloc_thp_env({})["GLIBC_TUNABLES"] == "glibc.malloc.hugetlb=1"
+    assert bd.malloc_thp_env({"GLIBC_TUNABLES": "glibc.malloc.arena_max=4"})["GLIBC_TUNABLES"] == \
+        "glibc.malloc.arena_max=4:glibc.malloc.hugetlb=1"
+    assert bd.malloc_thp_env({"GLIBC_TUNABLES": "glibc.malloc.hugetlb=0"})["GLIBC_TUNABLES"] == "glibc.malloc.hugetlb=0"
+    assert "GLIBC_TUNABLES" not in bd.malloc_thp_env({"BT2X_MALLOC_THP": "0"})
