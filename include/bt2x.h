@@ -37,9 +37,10 @@ extern "C" {
 #endif
 
 /* 3: bt2x_elt 8 B, bt2x_sat 4 B, bt2x_last_round_stats 4 words, bt2x_seed_round_dev's
- * d_used 4 words.  bt2x_abi_version() returns the library's value: a binding compares it
- * with the header it was written against before any other call. */
-#define BT2X_ABI_VERSION 3
+ * d_used 4 words.  4: bt2x_sam_tails[_dev] and bt2x_sam_req.  bt2x_abi_version() returns
+ * the library's value: a binding compares it with the header it was written against
+ * before any other call. */
+#define BT2X_ABI_VERSION 4
 
 enum {
 	BT2X_OK = 0,
@@ -362,6 +363,40 @@ typedef struct {
 } bt2x_store_in;
 int bt2x_store_reads(bt2x_ctx* ctx, const uint8_t* packed, uint64_t packed_bytes, const bt2x_store_in* in,
                      uint32_t n);
+
+/* SAM record tails from the read store (ABI 4, round 6).  Replaces the text the reference's
+ * AlnSinkSam::appendMate writes after an aligned read's MAPQ field (aln_sink.cpp:1889-2090,
+ * SamConfig::printAlignedOptFlags sam.cpp:121-730) for the common record whose printed
+ * edits are mismatches only (the CIGAR is one <rdlen>M run; StackedAln over such edits,
+ * aligner_result.cpp:448-770).  Per request: "CIGAR\t*\t0\t0\tSEQ\tQUAL\tAS:i:as
+ * [\tXS:i:xs]\tXN:i:xn\tXM:i:nmm\tXO:i:0\tXG:i:0\tNM:i:nmm\tMD:Z:md\tYT:Z:UU\tYF:Z:LN\n"
+ * (the leading tab before CIGAR is the caller's).  SEQ/QUAL are the store slot's patFw and
+ * qualities (fw) or patRc and reversed qualities, codes printed as ACGTN.  mm_pos are the
+ * mismatches' positions in the printed read (0-based, increasing, < rdlen), mm_chr their
+ * reference characters.  The text goes to text[text_off ..) and is at most
+ * BT2X_SAM_TAIL_MAX(rdlen, nmm) bytes; lens[i] receives its length.  The slot must hold the
+ * read the request names (put with the same rdlen). */
+#define BT2X_SAM_MAX_MM 16
+#define BT2X_SAM_TAIL_MAX(rdlen, nmm) (2u * (rdlen) + 200u + 4u * (nmm))
+typedef struct {
+	uint32_t slot;
+	uint16_t rdlen;          /* 1..BT2X_STORE_MAX_LEN */
+	uint8_t fw;              /* 1: patFw + qualities; 0: patRc + reversed qualities */
+	uint8_t nmm;             /* 0..BT2X_SAM_MAX_MM */
+	int32_t as;              /* AS:i */
+	int32_t xs;              /* XS:i, printed when has_xs */
+	uint32_t xn;             /* XN:i */
+	uint32_t has_xs;
+	uint64_t text_off;
+	uint16_t mm_pos[BT2X_SAM_MAX_MM];
+	uint8_t mm_chr[BT2X_SAM_MAX_MM];
+} bt2x_sam_req;
+/* host buffers: text holds text_bytes bytes (every request's text_off + its bound) */
+int bt2x_sam_tails(bt2x_ctx* ctx, const bt2x_sam_req* req, uint32_t n, char* text, uint64_t text_bytes,
+                   uint16_t* lens);
+/* HBM buffers, async on `stream` (NULL: the context's stream) */
+int bt2x_sam_tails_dev(bt2x_ctx* ctx, const bt2x_sam_req* d_req, uint32_t n, char* d_text, uint16_t* d_lens,
+                       void* stream);
 
 /* Context options.  BT2X_OPT_EXACT_BEST (default 1): bt2x_dp_align reports the exact
  * best of failed problems (one extra unbanded pass over them); 0 when the caller never

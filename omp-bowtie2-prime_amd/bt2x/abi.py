@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import numpy as np
 
-ABI_VERSION = 3             # BT2X_ABI_VERSION of the bt2x.h these mirrors follow
+ABI_VERSION = 4             # BT2X_ABI_VERSION of the bt2x.h these mirrors follow
 
 SEED_IN = np.dtype([("read_off", "<u8"), ("seed_off", "u1"), ("seed_len", "u1"),
                     ("pad", "u1", 6)], align=True)
@@ -36,6 +36,15 @@ NO_TIDX = 0xFFFFFFFF
 ELT = np.dtype([("v", "<u8")])   # bt2x_elt: toff bits 0-38, straddled bit 39, tidx bits 40-63
 STORE_IN = np.dtype([("off", "<u8"), ("slot", "<u4"), ("len", "<u2"), ("pad", "<u2")], align=True)   # bt2x_store_in
 STORE_SLOT_BYTES = 1024
+SAM_MAX_MM = 16
+SAM_REQ = np.dtype([("slot", "<u4"), ("rdlen", "<u2"), ("fw", "u1"), ("nmm", "u1"), ("as_", "<i4"), ("xs", "<i4"),
+                    ("xn", "<u4"), ("has_xs", "<u4"), ("text_off", "<u8"), ("mm_pos", "<u2", (SAM_MAX_MM,)),
+                    ("mm_chr", "u1", (SAM_MAX_MM,))], align=True)   # bt2x_sam_req
+
+
+def sam_tail_max(rdlen, nmm):
+    """BT2X_SAM_TAIL_MAX"""
+    return 2 * rdlen + 200 + 4 * nmm
 ROUND_IN = np.dtype([("read_off", "<u8"), ("seed0", "<u8"), ("rnd_last", "<u4"), ("rnd_lastoff", "<i4"),
                      ("exr0", "<u4"), ("nexr", "<u2"), ("nseeds", "<u2"), ("num_offs", "<u2"),
                      ("rdlen", "<u2"), ("interval", "<u2"), ("offset", "<u2"), ("seedlen", "<u2"),

@@ -64,6 +64,10 @@ FUNCS = {
                                            ctypes.c_void_p]),
     "bt2x_store_reads": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_uint32]),
+    "bt2x_sam_tails": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                      ctypes.c_void_p]),
+    "bt2x_sam_tails_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
     "bt2x_version": (ctypes.c_char_p, []),
     "bt2x_abi_version": (ctypes.c_int, []),
     "bt2x_host_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
@@ -185,6 +189,18 @@ class Context:
         inp = np.ascontiguousarray(inp, dtype=abi.STORE_IN)
         check(load().bt2x_store_reads(self.h, abi.ptr(packed), packed.nbytes, abi.ptr(inp), len(inp)),
               "bt2x_store_reads")
+
+    def sam_tails(self, req):
+        """bt2x_sam_tails: the record tails (bytes) of requests req (abi.SAM_REQ; text_off is
+        filled here), from the read store."""
+        req = np.array(req, dtype=abi.SAM_REQ)
+        bound = np.array([abi.sam_tail_max(int(r["rdlen"]), int(r["nmm"])) for r in req], dtype=np.uint64)
+        req["text_off"] = np.concatenate([[0], np.cumsum(bound)[:-1]]).astype(np.uint64) if len(req) else bound
+        text = np.zeros(int(bound.sum()) if len(req) else 1, dtype=np.uint8)
+        lens = np.zeros(max(1, len(req)), dtype=np.uint16)
+        check(load().bt2x_sam_tails(self.h, abi.ptr(req), len(req), abi.ptr(text), text.nbytes, abi.ptr(lens)),
+              "bt2x_sam_tails")
+        return [text[int(r["text_off"]): int(r["text_off"]) + int(lens[i])].tobytes() for i, r in enumerate(req)]
 
     def dp_align(self, reads, quals, refs, inp, debug=False, rec_cap=None, edit_cap=None):
         """reads = quals = None: read_off / qual_off index the read store."""
@@ -351,6 +367,6 @@ def build_index_sa(fasta: str, outbase: str, sa, off_rate: int = 4, ftab_chars: 
 
 
 def abi_sizes() -> list[int]:
-    buf = (ctypes.c_uint32 * 16)()
-    n = load().bt2x_abi_sizes(buf, 16)
-    return list(buf[:n])
+    buf = (ctypes.c_uint32 * 32)()
+    n = load().bt2x_abi_sizes(buf, 32)
+    return list(buf[:min(n, 32)])

@@ -176,7 +176,7 @@ extern "C" void bt2x_host_free(void* p) {
 	if(p) (void)hipHostFree(p);
 }
 
-extern "C" const char* bt2x_version(void) { return "bt2x 0.3 (gfx950; abi 3)"; }
+extern "C" const char* bt2x_version(void) { return "bt2x 0.4 (gfx950; abi 4)"; }
 extern "C" int bt2x_abi_version(void) { return BT2X_ABI_VERSION; }
 
 // -------------------------------------------------------------------- context
@@ -219,6 +219,7 @@ struct bt2x_ctx {
 	uint64_t store_bytes = 0;   // allocated (with growth slack)
 	uint64_t store_hw = 0;      // (highest slot written + 1) * BT2X_STORE_SLOT_BYTES: requests are checked against it
 	DevBuf b_pack, b_sin, b_gseeds;                         // + seeds instantiated on the GPU
+	DevBuf b_sreq, b_stext, b_slens;                        // SAM tails (bt2x_sam_tails)
 	uint64_t npat = 0;
 	bool exact_best = true;                    // BT2X_OPT_EXACT_BEST
 	int ncu = 0;
@@ -238,7 +239,7 @@ bt2x_ctx::~bt2x_ctx() {
 	for(DevBuf* b : {&b_reads, &b_quals, &b_refs, &b_in, &b_out, &b_recs, &b_edits, &b_dbg_dig, &b_dbg_cand, &scratch, &b_fail, &b_heavy,
 	                 &b_in2, &b_win,
 	                 &b_rin, &b_exr, &b_rout, &b_sats, &b_elts, &b_exro, &b_used, &b_sout, &b_rows, &b_ws,
-	                 &b_jobs, &b_ranges, &b_rcnt, &b_pack, &b_sin, &b_gseeds})
+	                 &b_jobs, &b_ranges, &b_rcnt, &b_pack, &b_sin, &b_gseeds, &b_sreq, &b_stext, &b_slens})
 		b->release();
 	if(d_store) (void)hipFree(d_store);
 	if(!shares_index)
@@ -748,7 +749,7 @@ extern "C" int bt2x_abi_sizes(uint32_t* out, int n) {
 	                      (uint32_t)sizeof(bt2x_resolve_in), (uint32_t)sizeof(bt2x_resolve_out),
 	                      (uint32_t)sizeof(bt2x_round_in), (uint32_t)sizeof(bt2x_round_out),
 	                      (uint32_t)sizeof(bt2x_sat), (uint32_t)sizeof(bt2x_exrange), (uint32_t)sizeof(bt2x_elt),
-	                      (uint32_t)sizeof(bt2x_store_in)};
+	                      (uint32_t)sizeof(bt2x_store_in), (uint32_t)sizeof(bt2x_sam_req)};
 	const int m = (int)(sizeof s / sizeof s[0]);
 	for(int i = 0; i < n && i < m; i++) out[i] = s[i];
 	return m;
@@ -938,6 +939,43 @@ extern "C" int bt2x_store_reads(bt2x_ctx* c, const uint8_t* packed, uint64_t pac
 	if((rc = bt2x_launch_store((const uint8_t*)c->b_pack.p, (const bt2x_store_in*)c->b_sin.p, n, c->d_store, c->stream)))
 		return rc;
 	HIPCHK(stream_wait(c));                          // the caller may reuse `packed` on return
+	return BT2X_OK;
+}
+
+// ---------------------------------------------------------------- SAM tails
+extern "C" int bt2x_sam_tails_dev(bt2x_ctx* c, const bt2x_sam_req* d_req, uint32_t n, char* d_text, uint16_t* d_lens,
+                                  void* stream) {
+	if(!c || (n && (!d_req || !d_text || !d_lens))) return BT2X_E_ARG;
+	if(n == 0) return BT2X_OK;
+	if(!c->d_store) return BT2X_E_ARG;
+	HIPCHK(hipSetDevice(c->device));
+	return bt2x_launch_sam_tails(d_req, n, c->d_store, d_text, d_lens, c->ncu, stream ? stream : (void*)c->stream);
+}
+
+extern "C" int bt2x_sam_tails(bt2x_ctx* c, const bt2x_sam_req* req, uint32_t n, char* text, uint64_t text_bytes,
+                              uint16_t* lens) {
+	if(!c || (n && (!req || !text || !lens))) return BT2X_E_ARG;
+	if(n == 0) return BT2X_OK;
+	for(uint32_t i = 0; i < n; i++) {                // the kernel trusts these
+		const bt2x_sam_req& q = req[i];
+		if(q.rdlen < 1 || q.rdlen > BT2X_STORE_MAX_LEN || q.nmm > BT2X_SAM_MAX_MM) return BT2X_E_ARG;
+		if((uint64_t)(q.slot + 1) * BT2X_STORE_SLOT_BYTES > c->store_hw) return BT2X_E_ARG;
+		if(q.text_off + BT2X_SAM_TAIL_MAX(q.rdlen, q.nmm) > text_bytes) return BT2X_E_ARG;
+		for(int e = 0; e < q.nmm; e++)
+			if(q.mm_pos[e] >= q.rdlen || (e && q.mm_pos[e] <= q.mm_pos[e - 1])) return BT2X_E_ARG;
+	}
+	HIPCHK(hipSetDevice(c->device));
+	int rc;
+	if((rc = c->b_sreq.ensure(sizeof(bt2x_sam_req) * n)) || (rc = c->b_stext.ensure(text_bytes)) ||
+	   (rc = c->b_slens.ensure(sizeof(uint16_t) * n)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(c->b_sreq.p, req, sizeof(bt2x_sam_req) * n, hipMemcpyHostToDevice, c->stream));
+	if((rc = bt2x_sam_tails_dev(c, (const bt2x_sam_req*)c->b_sreq.p, n, (char*)c->b_stext.p, (uint16_t*)c->b_slens.p,
+	                            c->stream)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(lens, c->b_slens.p, sizeof(uint16_t) * n, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipMemcpyAsync(text, c->b_stext.p, text_bytes, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(stream_wait(c));
 	return BT2X_OK;
 }
 

@@ -96,6 +96,9 @@ size_t bt2x_round_range_bytes();
 uint32_t bt2x_round_lanes(int ncu);
 int bt2x_launch_round(const RoundLaunch& a, void* stream);
 // read store (bt2x_store_reads): n packed reads into their BT2X_STORE_SLOT_BYTES slots
+// SAM record tails (bt2x_sam_tails): one wave per request
+int bt2x_launch_sam_tails(const bt2x_sam_req* d_req, uint32_t n, const uint8_t* d_store, char* d_text,
+                          uint16_t* d_lens, int ncu, void* stream);
 int bt2x_launch_store(const uint8_t* d_packed, const bt2x_store_in* d_in, uint32_t n, uint8_t* d_store,
                       void* stream);
 

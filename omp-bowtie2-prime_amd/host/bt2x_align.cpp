@@ -549,6 +549,26 @@ int64_t mapq_v2(const Params& p, size_t rdlen, int64_t best, bool hasSecbest, in
 	return ret;
 }
 
+// cigar_md's fast path as a bt2x_sam_req: the printed edits (ned() order; mirrored for the
+// reverse strand) are mismatches in increasing read order, so the CIGAR is one M run and MD
+// interleaves match runs and reference characters; false otherwise (the host formats it).
+bool mm_only_tail(size_t rdlen, bool fw, const uint32_t* ned0, size_t nedn, bt2x_sam_req& q) {
+	if(rdlen == 0) return false;
+	uint32_t prev = 0;
+	for(size_t k = 0; k < nedn; k++) {
+		// invert_poss for the reverse strand: reversed order, position rdlen - pos - 1
+		const uint32_t e = fw ? ned0[k] : ned0[nedn - 1 - k];
+		if(e_type(e) != ET_MM) return false;
+		const uint32_t p = fw ? e_pos(e) : (uint32_t)(rdlen - e_pos(e) - 1);
+		if(p >= rdlen || (k && p <= prev)) return false;
+		q.mm_pos[k] = (uint16_t)p;
+		q.mm_chr[k] = (uint8_t)e_chr(e);
+		prev = p;
+	}
+	q.nmm = (uint8_t)nedn;
+	return true;
+}
+
 // isspace in the C locale (the reference's): ' ', \t, \n, \v, \f, \r
 inline bool c_space(unsigned char ch) { return ch == ' ' || (ch >= '\t' && ch <= '\r'); }
 
@@ -585,8 +605,12 @@ void append_seq(std::string& o, const std::vector<uint8_t>& s) {
 
 // AlnSinkWrap::finishRead, unpaired branch (aln_sink.cpp:643-1384) -> one SAM record in
 // `o` (AlnSinkSam::appendMate, aln_sink.cpp:1889-2090; tags per sam.cpp:121-730).
-void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, Rng& rnd,
-                 const std::vector<uint32_t>& edbuf, bool* aligned, bool* rep, std::string& o) {
+// gpu (optional): an aligned record whose printed edits are mismatches only gets its head
+// (name through MAPQ) in `o` and its tail as *gpu (bt2x_sam_tails: CIGAR, SEQ, QUAL and
+// the tags, from the read store; text_off and slot are the caller's); returns true then.
+bool finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, Rng& rnd,
+                 const std::vector<uint32_t>& edbuf, bool* aligned, bool* rep, std::string& o,
+                 bt2x_sam_req* gpu = nullptr) {
 	// ReportingState::finish + getReport
 	if(!sk.doneUnpair) {
 		sk.doneUnpair = true;
@@ -609,7 +633,7 @@ void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, 
 		o.push_back('\t');
 		if(rd.qual.empty()) o.push_back('*'); else o += rd.qual;
 		o += "\tYT:Z:UU\tYF:Z:LN\n";
-		return;
+		return false;
 	}
 	// selectByScore (aln_sink.cpp:1477-1640): sort by score desc (ties by index desc),
 	// shuffle equal-score streaks with the read's RNG
@@ -645,6 +669,23 @@ void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, 
 	const bool hasSec = buf.size() > 1;
 	const int64_t secU = hasSec ? sk.rs[buf[1].second].score : 0;
 	*aligned = true; *rep = unpairMax;
+	if(gpu && nedn <= BT2X_SAM_MAX_MM && !rd.qual.empty() && rd.length() <= BT2X_STORE_MAX_LEN &&
+	   mm_only_tail(rd.length(), r.fw, ned, nedn, *gpu)) {
+		o += r.fw ? "\t0\t" : "\t16\t";
+		append_refname(o, ref.name((size_t)r.refid));
+		o.push_back('\t');
+		append_int(o, r.refoff + 1);
+		o.push_back('\t');
+		append_int(o, mapq_v2(p, rd.length(), bestU, hasSec, secU));
+		o.push_back('\t');
+		gpu->rdlen = (uint16_t)rd.length();
+		gpu->fw = r.fw ? 1 : 0;
+		gpu->as = (int32_t)r.score;
+		gpu->has_xs = hasSec ? 1u : 0u;
+		gpu->xs = (int32_t)secU;
+		gpu->xn = (uint32_t)r.refns;
+		return true;
+	}
 	thread_local std::string cig, md;
 	cig.clear(); md.clear();
 	cigar_md(rd, r.fw, ned, nedn, cig, md);
@@ -682,6 +723,7 @@ void finish_read(const Params& p, const RefInfo& ref, const Read& rd, Sink& sk, 
 	o += "\tNM:i:"; append_int(o, nedn);
 	o += "\tMD:Z:"; o += md;
 	o += "\tYT:Z:UU\tYF:Z:LN\n";
+	return false;
 }
 
 // SwAligner::initRef's problem for key k (the window, BitPairReference::getStretch, is
@@ -1114,7 +1156,9 @@ ReadTask Aligner::align_read(ReadCtx* c) {
 		}
 	}
 	PH(5);
-	finish_read(P, ref_, rd, sink, rnd, c->edbuf, &c->aligned, &c->repetitive, c->sam);
+	c->sam_gpu = finish_read(P, ref_, rd, sink, rnd, c->edbuf, &c->aligned, &c->repetitive, c->sam,
+	                         gpu_sam_ && c->in_store ? &c->sam_req : nullptr);
+	if(c->sam_gpu) c->sam_req.slot = c->slot;
 	// the finishRead counter update (aln_sink.cpp:994-1013): rs1u_ holds every alignment found
 	c->met_kind = c->repetitive ? 3 : !c->aligned ? 0 : sink.rs.size() == 1 ? 1 : 2;
 	PH(8);
@@ -1376,7 +1420,12 @@ void Aligner::gather(Launch& L, const std::vector<ReadCtx*>& cohort) {
 // backend when there is one).
 void Aligner::execute(Launch& L) {
 	Backend& be = (be2_ && &L == &launch_[1]) ? *be2_ : be_;
-	L.t_seed = L.t_resolve = L.t_dp = L.t_round = 0;
+	L.t_seed = L.t_resolve = L.t_dp = L.t_round = L.t_sam = 0;
+	if(!L.sam_req.empty()) {                  // retired reads' record tails, before their slots are reused
+		const double t0 = now_s();
+		be.sam_tails(L.sam_req, L.sam_text, L.sam_text_bytes, L.sam_lens);
+		L.t_sam = now_s() - t0;
+	}
 	if(!L.store_in.empty()) be.store_put(L.store_packed, L.store_in);   // before the requests that read them
 	if(!L.wn.empty()) {
 		const double t0 = now_s();
@@ -1727,19 +1776,24 @@ Aligner::~Aligner() {
 // Retire the finished reads of `act` (their records go to `put`, their contexts back to
 // the pool); the others stay in `act`.  Parallel over 1024-read chunks, each with its own
 // counters; then a serial compaction.
-void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, const std::function<void(uint64_t, std::string&)>& put) {
+void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, const std::function<void(uint64_t, std::string&)>& put,
+                     Launch* defer) {
 	const long n = (long)act.size(), nch = (n + 1023) / 1024;
 	std::vector<RetireAcc> acc((size_t)nch);
 	// each chunk splits its reads into the ones still running and the finished ones (in
 	// order), so the serial part only concatenates the chunks' lists: a serial pass over
 	// the cohort's cold contexts cost ~2.5 ms per step
-	if(retire_keep_.size() < (size_t)nch) { retire_keep_.resize((size_t)nch); retire_fin_.resize((size_t)nch); }
+	if(retire_keep_.size() < (size_t)nch) {
+		retire_keep_.resize((size_t)nch); retire_fin_.resize((size_t)nch); retire_sam_.resize((size_t)nch);
+	}
 	const bool pf = host_prefetch();
+	std::vector<uint64_t> sam_bytes((size_t)nch, 0);
 	pool().parallel_for(nch, 1, [&](long ch) {
 		RetireAcc& a = acc[(size_t)ch];
 		std::vector<ReadCtx*>& keep = retire_keep_[(size_t)ch];
 		std::vector<ReadCtx*>& fin = retire_fin_[(size_t)ch];
-		keep.clear(); fin.clear();
+		std::vector<ReadCtx*>& sam = retire_sam_[(size_t)ch];
+		keep.clear(); fin.clear(); sam.clear();
 		const long e = std::min(n, (ch + 1) * 1024);
 		for(long i = ch * 1024; i < e; i++) {
 			ReadCtx* c = act[(size_t)i];
@@ -1749,7 +1803,12 @@ void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, const std::functi
 			c->task.h = nullptr;
 			a.count(c);
 			if(!c->warn.empty()) std::fputs(c->warn.c_str(), stderr);
-			put(c->rd.rdid, c->sam);
+			if(defer && c->sam_gpu) {
+				sam.push_back(c);
+				sam_bytes[(size_t)ch] += BT2X_SAM_TAIL_MAX(c->sam_req.rdlen, c->sam_req.nmm);
+			} else {
+				put(c->rd.rdid, c->sam);
+			}
 			c->done = false;
 			fin.push_back(c);
 		}
@@ -1760,6 +1819,52 @@ void Aligner::retire(std::vector<ReadCtx*>& act, RunStats& st, const std::functi
 		act.insert(act.end(), retire_keep_[(size_t)ch].begin(), retire_keep_[(size_t)ch].end());
 		free_.insert(free_.end(), retire_fin_[(size_t)ch].begin(), retire_fin_[(size_t)ch].end());
 	}
+	if(!defer) return;
+	// the deferred records: heads and requests into the launch, at each chunk's base (the
+	// contexts go back to the pool above, but no read takes them before this returns)
+	Launch& L = *defer;
+	std::vector<uint64_t> base((size_t)nch + 1, 0), tbase((size_t)nch + 1, 0);
+	base[0] = L.sam_ids.size();
+	tbase[0] = L.sam_text_bytes;
+	for(long ch = 0; ch < nch; ch++) {
+		base[(size_t)ch + 1] = base[(size_t)ch] + retire_sam_[(size_t)ch].size();
+		tbase[(size_t)ch + 1] = tbase[(size_t)ch] + sam_bytes[(size_t)ch];
+	}
+	const size_t total = base[(size_t)nch];
+	if(total == base[0]) return;
+	L.sam_ids.resize(total);
+	if(L.sam_recs.size() < total) L.sam_recs.resize(total);
+	L.sam_req.resize(total);
+	L.sam_text_bytes = tbase[(size_t)nch];
+	pool().parallel_for(nch, 1, [&](long ch) {
+		uint64_t k = base[(size_t)ch], t = tbase[(size_t)ch];
+		for(ReadCtx* c : retire_sam_[(size_t)ch]) {
+			L.sam_ids[k] = c->rd.rdid;
+			L.sam_recs[k].swap(c->sam);              // (the context keeps the old buffer's capacity)
+			c->sam.clear();
+			bt2x_sam_req& q = L.sam_req[k];
+			q = c->sam_req;
+			q.text_off = t;
+			t += BT2X_SAM_TAIL_MAX(q.rdlen, q.nmm);
+			c->sam_gpu = false;
+			k++;
+		}
+	});
+}
+
+void Aligner::flush_sam(Launch& L, RunStats& st, const std::function<void(uint64_t, std::string&)>& put) {
+	const long n = (long)L.sam_ids.size();
+	if(!n) return;
+	st.sam_gpu += (uint64_t)n;
+	st.t_sam += L.t_sam;
+	pool().parallel_for(n, 256, [&](long i) {
+		std::string& r = L.sam_recs[(size_t)i];
+		r.append(L.sam_text.data() + L.sam_req[(size_t)i].text_off, L.sam_lens[(size_t)i]);
+		put(L.sam_ids[(size_t)i], r);
+	});
+	L.sam_ids.clear();
+	L.sam_req.clear();
+	L.sam_text_bytes = 0;
 }
 
 namespace {
@@ -1798,6 +1903,9 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 	RunStats st;
 	use_threads(threads);
 	dseeds_ = be_.device_seeds();
+	// record tails on the GPU: pipelined runs (a launch per cohort to carry the requests)
+	// whose backends keep the reads in a store and can format them
+	gpu_sam_ = pipeline_ && be_.sam_tails_ok() && (!be2_ || be2_->sam_tails_ok());
 	const double t_start = now_s();
 	if(header_on_) {
 		const std::string hdr = header();
@@ -1899,9 +2007,9 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		st.t_host += now_s() - t0;
 		co.insert(co.end(), fresh.begin(), fresh.end());
 	};
-	auto retire_write = [&](std::vector<ReadCtx*>& co) {
+	auto retire_write = [&](std::vector<ReadCtx*>& co, Launch* defer) {
 		const double t0 = now_s();
-		retire(co, st, put);
+		retire(co, st, put, defer);
 		const double t1 = now_s();
 		writer.kick();
 		st.t_io += now_s() - t0;
@@ -1915,7 +2023,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			const double t0 = now_s();
 			step(act, st);
 			st.t_step += now_s() - t0;
-			retire_write(act);
+			retire_write(act, nullptr);
 		}
 	} else {
 		// Two cohorts of up to slots/2 reads alternate: while the GPU thread runs one
@@ -1925,7 +2033,9 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 		// is gathered, alongside the other cohort's launch still on the GPU.
 		std::vector<ReadCtx*> co[2];
 		const size_t cap = slots / 2;
-		auto empty = [](const Launch& L) { return L.ws.empty() && L.wr.empty() && L.wd.empty() && L.wn.empty(); };
+		auto empty = [](const Launch& L) {
+			return L.ws.empty() && L.wr.empty() && L.wd.empty() && L.wn.empty() && L.sam_req.empty();
+		};
 		// A backend error on a GPU thread is carried over to this one and rethrown after the
 		// join; unwinding on either side joins the threads first (a joinable std::thread must
 		// not be destroyed).
@@ -1958,8 +2068,9 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 			const int b = 1 - a;
 			if(!two) start(b);
 			const double t1 = now_s();
+			flush_sam(launch_[a], st, put);              // the tails this launch formatted
 			scatter_resume(launch_[a], st);
-			retire_write(co[a]);
+			retire_write(co[a], gpu_sam_ ? &launch_[a] : nullptr);
 			refill(co[a], cap);
 			gather(launch_[a], co[a]);
 			st.t_step += now_s() - t1;
@@ -1982,6 +2093,7 @@ RunStats Aligner::run(FastqReader& fq, std::FILE* out, size_t slots, int threads
 
 std::string Aligner::align_all(std::vector<Read>& reads, size_t slots, int threads, RunStats* stp) {
 	RunStats st;
+	gpu_sam_ = false;                              // (records formatted here, in step())
 	use_threads(threads);
 	dseeds_ = be_.device_seeds();
 	std::vector<ReadCtx*> act, fresh;

@@ -1027,7 +1027,10 @@ struct ReadCtx {
 	RedundantAlns redAnchor;
 	Sink sink;
 	std::vector<uint32_t> edbuf;         // SwDriver::resGap_.alres.ned_ storage
-	std::string sam;                     // the finished record
+	std::string sam;                     // the finished record (sam_gpu: its head; the tail comes
+	                                     // from bt2x_sam_tails with the cohort's next launch)
+	bool sam_gpu = false;
+	bt2x_sam_req sam_req;
 	ReadTask task;
 	// statistics for the run summary
 	bool aligned = false, repetitive = false;
@@ -1081,6 +1084,11 @@ public:
 	// instantiates them, round_in's seed0 / nseeds / seedflags as the driver set them)
 	virtual bool device_seeds() const { return false; }
 	virtual void store_put(const HostVec<uint8_t>& packed, const HostVec<bt2x_store_in>& in) { (void)packed; (void)in; }
+	// true: sam_tails formats aligned records' tails from the read store (bt2x_sam_tails);
+	// text holds text_bytes (every request's text_off + its bound), lens gets the lengths
+	virtual bool sam_tails_ok() const { return false; }
+	virtual void sam_tails(const HostVec<bt2x_sam_req>& req, HostVec<char>& text, uint64_t text_bytes,
+	                       HostVec<uint16_t>& lens) { (void)req; (void)text; (void)text_bytes; (void)lens; }
 };
 
 // -------------------------------------------------------------------- driver
@@ -1106,6 +1114,8 @@ struct RunStats {
 	uint64_t seeds = 0, resolves = 0, dps = 0, dps_used = 0, tight_recs = 0;
 	uint64_t round_launches = 0, rounds = 0, round_redo = 0;
 	uint64_t dp_max_launch = 0;     // problems in the largest DP launch
+	uint64_t sam_gpu = 0;           // records whose tail bt2x_sam_tails formatted
+	double t_sam = 0;
 	ReportingMetrics met;
 	std::vector<double> t_files;    // when each input file's last record was written
 	double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_host = 0, t_io = 0, t_alloc = 0, t_step = 0, t_backend = 0,
@@ -1165,6 +1175,15 @@ private:
 		uint64_t n_round_seeds = 0;                      // the round's seeds (sent or instantiated on the GPU)
 		HostVec<uint8_t> store_packed;                   // the launch's new reads for the read store
 		HostVec<bt2x_store_in> store_in;
+		// record tails formatted on the GPU (before the launch's store puts reuse the slots):
+		// the retired reads' ids, record heads, requests, and the returned text
+		std::vector<uint64_t> sam_ids;
+		std::vector<std::string> sam_recs;
+		HostVec<bt2x_sam_req> sam_req;
+		HostVec<char> sam_text;
+		HostVec<uint16_t> sam_lens;
+		uint64_t sam_text_bytes = 0;
+		double t_sam = 0;
 		double t_seed = 0, t_resolve = 0, t_dp = 0, t_round = 0, t_gather = 0;
 		// gather's per-chunk lists, sizes and bases
 		struct Chunk {
@@ -1187,11 +1206,18 @@ private:
 	ReadCtx* take_ctx();
 	// put(id, record) takes a finished read's SAM record; it is called from the pool's
 	// threads, for distinct ids
-	void retire(std::vector<ReadCtx*>& act, RunStats& st, const std::function<void(uint64_t, std::string&)>& put);
+	// With `defer`, reads whose record tail is formatted on the GPU (sam_gpu) go to that
+	// launch's tail requests instead of `put`.
+	void retire(std::vector<ReadCtx*>& act, RunStats& st, const std::function<void(uint64_t, std::string&)>& put,
+	            Launch* defer = nullptr);
+	// the tails of launch L's deferred records (L executed): heads + tails to `put`
+	void flush_sam(Launch& L, RunStats& st, const std::function<void(uint64_t, std::string&)>& put);
+	bool gpu_sam_ = false;                // record tails on the GPU (pipelined run, backend able)
 	// pooled read contexts (kept across runs; released by the destructor)
 	std::vector<std::unique_ptr<ReadCtx>> ctxs_;
 	std::vector<ReadCtx*> free_;
 	std::vector<std::vector<ReadCtx*>> retire_keep_, retire_fin_;   // retire()'s per-chunk lists
+	std::vector<std::vector<ReadCtx*>> retire_sam_;                  // and the reads it defers
 	std::vector<std::string> sam_ring_;   // the SAM writer's ring of record buffers (kept across runs)
 	// host threads for the parallel loops over reads
 	std::unique_ptr<WorkPool> pool_;

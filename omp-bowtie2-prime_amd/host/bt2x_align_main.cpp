@@ -89,6 +89,23 @@ public:
 		store_ = !(st && st[0] == '0');
 		const char* hs = std::getenv("BT2X_HOST_SEEDS");          // 1: the driver's seed lists are sent
 		dseeds_ = !(hs && hs[0] == '1');
+		// 1: mismatch-only records' tails formatted by bt2x_sam_tails (off by default: measured
+		// slower end to end, DESIGN.md §3 round 6 -- the host still copies every tail once more
+		// out of the page-locked buffer, and that costs what formatting it saved)
+		const char* gs_ = std::getenv("BT2X_GPU_SAM");
+		gpu_sam_ = store_ && gs_ && gs_[0] == '1';
+	}
+	bool sam_tails_ok() const override { return gpu_sam_; }
+	void sam_tails(const HostVec<bt2x_sam_req>& req, HostVec<char>& text, uint64_t text_bytes,
+	               HostVec<uint16_t>& lens) override {
+		const auto t0 = std::chrono::steady_clock::now();
+		text.resize(text_bytes);
+		lens.resize(req.size());
+		bt2x::check(bt2x_sam_tails(ctx_, req.data(), (uint32_t)req.size(), text.data(), text_bytes, lens.data()),
+		            "bt2x_sam_tails");
+		gs.sam_h2d += req.size() * sizeof(bt2x_sam_req);
+		gs.sam_d2h += text_bytes + req.size() * sizeof(uint16_t);
+		gs.t_sam_call += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 	}
 	bool read_store() const override { return store_; }
 	bool device_seeds() const override { return dseeds_; }
@@ -183,10 +200,12 @@ public:
 	struct GpuStats {                      // kernel time and bytes over PCIe, per request kind
 		double k_round_ms = 0, k_dp_ms = 0, t_round_call = 0, t_dp_call = 0;
 		uint64_t round_h2d = 0, round_d2h = 0, dp_h2d = 0, dp_d2h = 0, store_h2d = 0, retries = 0;
+		uint64_t sam_h2d = 0, sam_d2h = 0;
+		double t_sam_call = 0;
 	} gs;
 private:
 	bt2x_ctx* ctx_;
-	bool ref_text_ = false, store_ = true, dseeds_ = true;
+	bool ref_text_ = false, store_ = true, dseeds_ = true, gpu_sam_ = false;
 	double sat_per_read_ = 16, elt_per_read_ = 64;
 };
 
@@ -485,12 +504,15 @@ int main(int argc, char** argv) {
 				g.k_round_ms += h.k_round_ms; g.k_dp_ms += h.k_dp_ms; g.t_round_call += h.t_round_call;
 				g.t_dp_call += h.t_dp_call; g.round_h2d += h.round_h2d; g.round_d2h += h.round_d2h;
 				g.dp_h2d += h.dp_h2d; g.dp_d2h += h.dp_d2h; g.store_h2d += h.store_h2d; g.retries += h.retries;
+				g.sam_h2d += h.sam_h2d; g.sam_d2h += h.sam_d2h; g.t_sam_call += h.t_sam_call;
 			}
 			std::fprintf(stderr, "BT2X_GPU k_round=%.4f t_round_call=%.4f round_h2d_mib=%.1f round_d2h_mib=%.1f "
-			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f store_h2d_mib=%.1f retries=%llu\n",
+			             "k_dp=%.4f t_dp_call=%.4f dp_h2d_mib=%.1f dp_d2h_mib=%.1f store_h2d_mib=%.1f retries=%llu "
+			             "sam_h2d_mib=%.1f sam_d2h_mib=%.1f t_sam_call=%.4f sam_gpu=%llu\n",
 			             g.k_round_ms * 1e-3, g.t_round_call, g.round_h2d / 1048576.0, g.round_d2h / 1048576.0, g.k_dp_ms * 1e-3,
 			             g.t_dp_call, g.dp_h2d / 1048576.0, g.dp_d2h / 1048576.0, g.store_h2d / 1048576.0,
-			             (unsigned long long)g.retries);
+			             (unsigned long long)g.retries, g.sam_h2d / 1048576.0, g.sam_d2h / 1048576.0, g.t_sam_call,
+			             (unsigned long long)st.sam_gpu);
 		}
 	} catch(const std::exception& e) {
 		std::fprintf(stderr, "bt2x-align: %s\n", e.what());

@@ -41,6 +41,7 @@ def test_struct_sizes_match_numpy_mirrors():
     assert s[10:14] == [abi.ROUND_IN.itemsize, abi.ROUND_OUT.itemsize, abi.SAT.itemsize, abi.EXRANGE.itemsize]
     assert s[14] == abi.ELT.itemsize == 8
     assert s[15] == abi.STORE_IN.itemsize == 16
+    assert s[16] == abi.SAM_REQ.itemsize == 80
 
 
 def test_scoring_tables_match_oracle():

@@ -52,7 +52,7 @@ SETS = [("e2e_lambda", "lambda_virus", "lambda_longreads.fq", []),
 # (lane-per-problem banded kernel above BT2X_DP_WAVE_MAX problems, wave per problem
 # below), and each kernel forced for every launch
 DP_MODES = {"default": None, "lane": "0", "wave": "1", "hostwin": "host", "handover": "handover", "parwave": "parwave",
-            "stream2": "stream2", "lane1": "lane1", "split": "split", "nostore": "nostore", "wavefull": "wavefull"}
+            "stream2": "stream2", "lane1": "lane1", "split": "split", "nostore": "nostore", "wavefull": "wavefull", "gpusam": "gpusam"}
 MD5 = os.path.join(g.GOLDEN, "e2e_md5.json")
 SUMMARY = os.path.join(g.GOLDEN, "e2e_summary.json")
 
@@ -177,7 +177,7 @@ GPU_CASES = [(s, m) for s in SETS for m in DP_MODES
              if m == "default" or (m in ("hostwin", "handover") and s[0] in ("e2e_rep", "e2e_rep_i16_mix"))
              or (m == "parwave" and s[0] in ("e2e_rep", "e2e_tandem", "e2e_tandem_i16", "e2e_rep_i16_mix"))
              or (m in ("lane1", "split") and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem"))
-             or (m in ("nostore", "stream2") and s[0] in ("e2e_rep", "e2e_rep_i16_mix"))
+             or (m in ("nostore", "stream2", "gpusam") and s[0] in ("e2e_rep", "e2e_rep_i16_mix", "e2e_tandem"))
              or (m == "wavefull" and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem_i16"))
              or (m in ("lane", "wave") and s[0] in ("e2e_rep", "e2e_rep_dpad12", "e2e_tandem", "e2e_rep_i16",
                                                     "e2e_tandem_i16", "e2e_rep_i16_mix"))]
@@ -189,7 +189,9 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     """The product binary (kernels on the MI355X) == the reference's SAM, through each DP
     kernel: the launcher's choice, the banded lane kernels (lane: the launcher's lane
     choice; lane1: one lane per problem; split: the two-wave split fill) / the wave kernel
-    forced (wave: its banded traceback layout, the default; wavefull: whole rectangles), and the lane kernel handing nearly every walk over to the wave kernel (a 2-step
+    forced (wave: its banded traceback layout, the default; wavefull: whole rectangles), the
+    mismatch-only records' tails formatted on the GPU (gpusam: bt2x_sam_tails; by default the
+    host formats every record), and the lane kernel handing nearly every walk over to the wave kernel (a 2-step
     budget)."""
     name, idx, fq, opts = case
     env = dict(os.environ)
@@ -201,6 +203,7 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     env.pop("BT2X_DP_SPLIT", None)
     env.pop("BT2X_READ_STORE", None)
     env.pop("BT2X_DP_WAVE_BAND", None)
+    env.pop("BT2X_GPU_SAM", None)
     if DP_MODES[mode] == "host":
         env["BT2X_HOST_WINDOWS"] = "1"          # DP windows cut on the host (RefInfo::stretch)
     elif DP_MODES[mode] == "handover":
@@ -218,6 +221,8 @@ def test_bt2x_align_vs_reference_sam(fixtures, case, mode):
     elif DP_MODES[mode] == "wavefull":            # wave per problem, whole rectangles in LDS
         env["BT2X_DP_WAVE"] = "1"
         env["BT2X_DP_WAVE_BAND"] = "0"
+    elif DP_MODES[mode] == "gpusam":              # mismatch-only records' tails from bt2x_sam_tails
+        env["BT2X_GPU_SAM"] = "1"
     elif DP_MODES[mode] == "nostore":             # reads sent with every request (no read store)
         env["BT2X_READ_STORE"] = "0"
     elif DP_MODES[mode] not in (None, "stream2"):

@@ -499,6 +499,86 @@ def test_dp_from_read_store_matches_uploaded_reads(ctxs):
     _compare_dp(*got, *ref, case.inp)                    # (record arena offsets come from atomics)
 
 
+def _sam_tail_py(r, codes, quals):
+    """The record tail bt2x_sam_tails writes (restated from the host driver's formatting of a
+    mismatch-only record, host/bt2x_align.cpp cigar_md + finish_read)."""
+    R = int(r["rdlen"])
+    out = f"{R}M\t*\t0\t0\t" + "".join("ACGTN"[min(int(c), 4)] for c in codes) + "\t" + bytes(quals).decode()
+    out += f"\tAS:i:{int(r['as_'])}" + (f"\tXS:i:{int(r['xs'])}" if r["has_xs"] else "") + f"\tXN:i:{int(r['xn'])}"
+    n = int(r["nmm"])
+    out += f"\tXM:i:{n}\tXO:i:0\tXG:i:0\tNM:i:{n}\tMD:Z:"
+    prev, mm_last, first = 0, False, True
+    for e in range(n):
+        p = int(r["mm_pos"][e])
+        if p > prev:
+            out += str(p - prev)
+            mm_last = first = False
+        if mm_last or first:
+            out += "0"
+        out += chr(int(r["mm_chr"][e]))
+        mm_last, first, prev = True, False, p + 1
+    if R > prev:
+        out += str(R - prev)
+    elif mm_last:
+        out += "0"
+    return (out + "\tYT:Z:UU\tYF:Z:LN\n").encode()
+
+
+def test_sam_tails_from_read_store(ctxs):
+    """bt2x_sam_tails: record tails of aligned reads (either strand, 0-16 mismatches at the
+    read's ends and anywhere, lengths 1-256, N codes, optional XS) from store slots equal the
+    host driver's formatting; malformed requests are refused."""
+    ctx = ctxs["rep"][0]
+    rng = np.random.default_rng(11)
+    comp = np.array([3, 2, 1, 0, 4], np.uint8)
+    n = 3000
+    lens = rng.integers(1, 257, n)
+    lens[:8] = [1, 9, 10, 99, 100, 150, 255, 256]
+    packed, sin, reads, off = [], np.zeros(n, dtype=abi.STORE_IN), [], 0
+    for i in range(n):
+        L = int(lens[i])
+        codes = rng.choice(5, L, p=[0.24, 0.24, 0.24, 0.24, 0.04]).astype(np.uint8)
+        quals = rng.integers(33, 75, L).astype(np.uint8)
+        packed += [codes, quals]
+        sin[i] = (off, 2 * i + 1, L, 0)
+        off += 2 * L
+        reads.append((codes, quals))
+    ctx.store_reads(np.concatenate(packed), sin)
+    req = np.zeros(n, dtype=abi.SAM_REQ)
+    for i in range(n):
+        L = int(lens[i])
+        req[i]["slot"], req[i]["rdlen"], req[i]["fw"] = 2 * i + 1, L, i % 2
+        k = int(rng.integers(0, min(abi.SAM_MAX_MM, L) + 1))
+        pos = np.sort(rng.choice(L, k, replace=False))
+        if k and i % 7 == 0:
+            pos[0] = 0
+        if k and i % 5 == 0:
+            pos[-1] = L - 1 if k == 1 or pos[-2] < L - 1 else pos[-1]
+        req[i]["nmm"] = k
+        req[i]["mm_pos"][:k] = pos
+        req[i]["mm_chr"][:k] = rng.choice(np.frombuffer(b"ACGTN", np.uint8), k)
+        req[i]["as_"] = -int(rng.integers(0, 300))
+        req[i]["has_xs"] = i % 3 == 0
+        req[i]["xs"] = -int(rng.integers(0, 300))
+        req[i]["xn"] = int(rng.integers(0, 4))
+    got = ctx.sam_tails(req)
+    for i in range(n):
+        codes, quals = reads[i]
+        if req[i]["fw"] == 0:
+            codes, quals = comp[codes[::-1]], quals[::-1]
+        assert got[i] == _sam_tail_py(req[i], codes, quals), i
+    for bad in ({"nmm": abi.SAM_MAX_MM + 1}, {"slot": 2 * n + 5}, {"rdlen": 0}):
+        r = req[:4].copy()
+        for k, v in bad.items():
+            r[1][k] = v
+        with pytest.raises(lib.Bt2xError):
+            ctx.sam_tails(r)
+    r = req[req["nmm"] >= 2][:1].copy()
+    r[0]["mm_pos"][1] = r[0]["mm_pos"][0]                # not increasing
+    with pytest.raises(lib.Bt2xError):
+        ctx.sam_tails(r)
+
+
 def test_empty_batches(ctxs):
     ctx = ctxs["rep"][0]
     out = ctx.seed_search(np.zeros(16, np.uint8), np.zeros(0, dtype=abi.SEED_IN), do_extend=True)
