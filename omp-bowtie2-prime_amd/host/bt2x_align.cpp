@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <cctype>
+#include <cerrno>
 #include <charconv>
 #include <chrono>
 #include <condition_variable>
@@ -1630,6 +1631,7 @@ public:
 		ready_.reset(new std::atomic<uint8_t>[cap]);
 		for(size_t i = 0; i < cap; i++) ready_[i].store(0, std::memory_order_relaxed);
 		cap_ = cap;
+		std::fflush(f_);                                  // (the header) before the raw writes
 		th_ = std::thread([this] { loop(); });
 	}
 	~OrderedSamWriter() {
@@ -1706,12 +1708,25 @@ private:
 			do {
 				full = drain(chunk);
 				if(full || (stop && !chunk.empty())) {
-					std::fwrite(chunk.data(), 1, chunk.size(), f_);
+					put_chunk(chunk);
 					chunk.clear();
 				}
 			} while(full);
 			if(stop) return;
 		}
+	}
+	// the chunk straight to the file descriptor (the FILE's buffer, flushed when the writer
+	// starts, would copy every byte once more); fwrite if the stream has no descriptor
+	void put_chunk(const std::string& c) {
+		const int fd = ::fileno(f_);
+		size_t o = 0;
+		while(fd >= 0 && o < c.size()) {
+			const ssize_t w = ::write(fd, c.data() + o, c.size() - o);
+			if(w < 0 && errno == EINTR) continue;
+			if(w <= 0) break;                            // (as an unchecked fwrite: the run's output is short)
+			o += (size_t)w;
+		}
+		if(fd < 0) std::fwrite(c.data(), 1, c.size(), f_);
 	}
 	std::FILE* f_;
 	std::vector<std::string>& store_;
