@@ -556,11 +556,23 @@ def cpu_baseline(args, base, fqs, rdir):
     head_fastq(fqs, one, 1)
     sam = os.path.join(rdir, "ref.sam")
     load = {}
+    # the reference's own run-to-run agreement on the sample (its F11 edit-buffer reads can
+    # reach bytes past a read's end that depend on what its thread aligned before): every
+    # sample run's records against the first one's
+    first, rdiff, rex = [], [], []
 
     def rate(threads, fqp, reads):
         if threads not in load:
             load[threads] = ref_run(args, base, one, threads, os.devnull)[0]
         wall, timers = ref_run(args, base, fqp, threads, sam if fqp == sample else os.devnull)
+        if fqp == sample:
+            recs = set(sam_records(sam))
+            if not first:
+                first.append(recs)
+            else:
+                d = first[0] ^ recs
+                rdiff.append(len(first[0] - recs))
+                rex.extend(r.decode(errors="replace")[:600] for r in sorted(d)[:4 - len(rex)] if len(rex) < 4)
         return reads / max(wall - load[threads], 1e-6), wall, timers
 
     runs = {}
@@ -582,6 +594,7 @@ def cpu_baseline(args, base, fqs, rdir):
                       f"1-read run (index load {load[best]:.2f} s)",
             "runs": {str(t): [round(r[0], 1) for r in v] for t, v in runs.items()},
             "one_thread": {"value": round(one_t[0] / 1e6, 6), "reads": m1},
+            "reference_runs_differ": rdiff, "reference_runs_examples": rex,
             "timer_sums_s": med[2], "cpu_share": n}, sam
 
 
@@ -787,9 +800,14 @@ def parity(ours_sam, ref_sam, n) -> dict:
     the reference aligner's records for the same n reads, compared sorted."""
     ours, theirs = sam_records(ours_sam, n), sam_records(ref_sam)
     diff = sum(1 for a, b in zip(ours, theirs) if a != b) + abs(len(ours) - len(theirs))
-    return {"sample_reads": n, "records_ours": len(ours), "records_reference": len(theirs), "records_differ": diff,
-            "what": "sorted SAM records of the timed run's first sample_reads reads vs the reference "
-                    "aligner's on the same reads"}
+    out = {"sample_reads": n, "records_ours": len(ours), "records_reference": len(theirs), "records_differ": diff,
+           "what": "sorted SAM records of the timed run's first sample_reads reads vs the reference "
+                   "aligner's on the same reads"}
+    if diff:                                     # (the first few, for the record)
+        a, b = set(ours), set(theirs)
+        out["examples_ours"] = [r.decode(errors="replace")[:600] for r in sorted(a - b)[:4]]
+        out["examples_reference"] = [r.decode(errors="replace")[:600] for r in sorted(b - a)[:4]]
+    return out
 
 
 def host_threads(args, share: int, world: int) -> tuple[int, str]:
