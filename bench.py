@@ -66,6 +66,10 @@ def parse(argv=None):
     ap.add_argument("--genome-mb", type=float, default=3100.0)
     ap.add_argument("--genome-seed", type=int, default=2024)
     ap.add_argument("--host-threads", type=int, default=0, help="bt2x-align -p (0: the rank's CPU share)")
+    # (131,072: two cohorts of 65,536.  Round 6 measured 262,144 with malloc on huge pages: DP
+    # launches twice as large put the DP at 0.387 of its roofline instead of 0.296 and C2's
+    # i16 at 0.382, but the host-bound end-to-end rate fell 4.6 % over four interleaved pairs
+    # and the repeat-heavy leg 14 %: profiles/r06s3_slots/, r06s4_slots/, r06b1_slots262144/)
     ap.add_argument("--slots", type=int, default=1 << 17, help="bt2x-align --slots (reads in flight)")
     ap.add_argument("--replay-reads", type=int, default=1 << 20, help="reads whose GPU launches are replayed")
     ap.add_argument("--replay-steps", type=int, default=3)

@@ -316,7 +316,7 @@ int main(int argc, char** argv) {
 	std::string idx, fq, outp, mate1, mate2;
 	Params p;
 	int threads = 16, device = 0;
-	size_t slots = 1 << 17;
+	size_t slots = 1 << 17;                             // reads in flight: two cohorts of 65,536
 	bool stats = false, pipeline = true, gpu_round = true, hd = true, metrics = false;
 	// --streams 2: the second cohort on a second context (bt2x_open_shared).  One is the
 	// default: the run is host-bound, and two contexts' concurrent launches each take longer
