@@ -290,6 +290,23 @@ std::string pin_to_gpu_node(int device, int threads) {
 		for(long c = a; c <= b && c < CPU_SETSIZE; c++) if(CPU_ISSET(c, &cur)) CPU_SET(c, &want);
 		p = (*q == ',') ? q + 1 : q;
 	}
+	// BT2X_NUMA_CORES=1: one hardware thread per physical core of the node (its first SMT
+	// sibling), when that still leaves a CPU per worker thread
+	const char* oc = std::getenv("BT2X_NUMA_CORES");
+	if(oc && oc[0] == '1') {
+		cpu_set_t first;
+		CPU_ZERO(&first);
+		for(int c = 0; c < CPU_SETSIZE; c++) {
+			if(!CPU_ISSET(c, &want)) continue;
+			char sp[128];
+			std::snprintf(sp, sizeof sp, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c);
+			std::FILE* sf = std::fopen(sp, "r");
+			long lo = c;
+			if(sf) { if(std::fscanf(sf, "%ld", &lo) != 1) lo = c; std::fclose(sf); }
+			if(lo == c) CPU_SET(c, &first);
+		}
+		if(CPU_COUNT(&first) >= threads) want = first;
+	}
 	const int have = CPU_COUNT(&want);
 	char note[64];
 	if(have >= 4 && have >= threads && sched_setaffinity(0, sizeof want, &want) == 0)
