@@ -974,6 +974,9 @@ def main():
              "t_align_max_s": round(r["t_max"], 3), "peak_rss_mib": r["peak"]}
         if ru and r["met"]["nread"]:
             e["host_cpu_us_per_read"] = round((float(ru.get("user", 0)) + float(ru.get("sys", 0))) / r["met"]["nread"] * 1e6, 3)
+            # (each run's own split: a slow run's extra CPU shows as user or sys time, and
+            # faults / preemptions, e.g. huge-page compaction or a busy node)
+            e["rusage"] = {k: ru.get(k) for k in ("user", "sys", "minflt", "vcsw", "ivcsw")}
         g = kv_line(r["err"], "BT2X_GPU")
         if g:
             e["k_dp_s"], e["k_round_s"] = g.get("k_dp"), g.get("k_round")
